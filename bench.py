@@ -1,0 +1,286 @@
+#!/usr/bin/env python3
+"""Headline benchmark: GCN copy_u_sum (g-SpMM) on a 100M-edge RMAT graph.
+
+Metric (BASELINE.json): edges/sec + achieved HBM GB/s, GCN copy_u_sum on a
+100M-edge graph, 1/2/4/8 MI355X.
+
+Workload M1: RMAT (a,b,c,d) = (0.57, 0.19, 0.19, 0.05),
+scale 23 (N = 8,388,608), E = 100,000,000, vertex ids randomly permuted,
+duplicates and self-loops kept, X ~ U(-1, 1) of shape (N, 64) fp32, int32
+dst-major CSR.  Generated on the GPU (seeded), CSRs built on the GPU.
+
+A step = one copy_u_sum pass (DGLGraph.update_all(copy_u, sum) lowers to
+exactly this call) over the resident graph: out[v] = sum_{u->v} X[u].
+
+Multi-GPU (torchrun, one process per GPU): weak scaling.  The global graph
+has N x 100M edges (RMAT scale 23 + log2 N); every rank owns a contiguous
+block of destination rows with all their in-edges (1-D row partition, the
+halo-subgraph semantics of graph_op.cc:403-509 with num_hops = 1) and holds
+the source features replicated (DESIGN.md "Multi-GPU"), so the timed SpMM
+has no data-path collective.  `value` = all ranks' edges / max-over-ranks time.
+
+cpu_baseline: the reference's CPU algorithm (out-CSR traversal, OpenMP over
+source rows, `omp atomic` scatter; oracle/dgl_ref.c) on a bounded sample of
+the same graph, rank 0 at N = 1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(ROOT, "dgl-hack_amd"), ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch as th  # noqa: E402
+
+RMAT = (0.57, 0.19, 0.19, 0.05)
+SCALE = 23
+EDGES_PER_GPU = 100_000_000
+FEAT = 64
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def rmat_edges(scale, num_edges, seed, device, chunk=25_000_000):
+    """RMAT edge list on the GPU (int32 src, dst), unpermuted ids."""
+    a, b, c, _ = RMAT
+    gen = th.Generator(device=device)
+    gen.manual_seed(seed)
+    srcs, dsts = [], []
+    done = 0
+    while done < num_edges:
+        cnt = min(chunk, num_edges - done)
+        s = th.zeros(cnt, dtype=th.int32, device=device)
+        d = th.zeros(cnt, dtype=th.int32, device=device)
+        for lvl in range(scale):
+            r = th.rand(cnt, generator=gen, device=device)
+            sb = r > (a + b)
+            db = ((r > a) & (r <= a + b)) | (r > a + b + c)
+            s |= sb.to(th.int32) << lvl
+            d |= db.to(th.int32) << lvl
+        srcs.append(s)
+        dsts.append(d)
+        done += cnt
+    return th.cat(srcs), th.cat(dsts)
+
+
+def build_workload(world, rank, device):
+    scale = SCALE + int(round(math.log2(world)))
+    n = 1 << scale
+    m = EDGES_PER_GPU * world
+    t0 = time.time()
+    src, dst = rmat_edges(scale, m, seed=1234, device=device)
+    gp = th.Generator(device=device)
+    gp.manual_seed(1)
+    perm = th.randperm(n, generator=gp, device=device).to(th.int32)
+    src = perm[src.long()]
+    dst = perm[dst.long()]
+    del perm
+    lo = n * rank // world
+    hi = n * (rank + 1) // world
+    if world > 1:
+        keep = (dst >= lo) & (dst < hi)
+        src, dst = src[keep], dst[keep] - lo
+    gx = th.Generator(device=device)
+    gx.manual_seed(2)
+    x = th.rand(n, FEAT, generator=gx, device=device) * 2 - 1
+    th.cuda.synchronize()
+    log("graph generated: scale %d, %d edges total, rank rows [%d, %d), %d local edges (%.1fs)"
+        % (scale, m, lo, hi, src.shape[0], time.time() - t0))
+    return n, hi - lo, src.contiguous(), dst.contiguous(), x
+
+
+def make_local_graph(n_src, n_dst, src, dst, device):
+    """Local in-CSR (rows = owned dst, cols = global src) built on the GPU."""
+    from dgl.graph_index import (DeviceCSR, ImmutableGraphIndex, device_coo_to_csr,
+                                 device_expand_rows)
+    nodes = max(n_src, n_dst)
+    # out-CSR (rows = src) then in-CSR = stable re-sort by dst == CSRTranspose(out-CSR)
+    o_ptr, o_idx, o_dat = device_coo_to_csr(nodes, src, dst)
+    o_rows = device_expand_rows(o_ptr, src.shape[0])
+    i_ptr, i_idx, i_dat = device_coo_to_csr(n_dst, o_idx, o_rows, o_dat)
+    i_rows = device_expand_rows(i_ptr, src.shape[0])
+    in_csr = DeviceCSR(i_ptr, i_idx, i_dat, i_rows, n_src)
+    out_csr = DeviceCSR(o_ptr, o_idx, o_dat, o_rows, n_dst)
+    return ImmutableGraphIndex(in_csr, out_csr, n_src, n_dst, th.device(device)), (o_ptr, o_idx)
+
+
+def cpu_baseline(o_ptr, o_idx, x, n_dst, budget_s=20.0, sample_edges=None):
+    """Reference CPU algorithm on the M1 graph (or its leading source rows when
+    `sample_edges` is given), passes repeated until `budget_s` is spent (>= 1 pass)."""
+    from oracle import oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or O.max_threads()
+    ptr = o_ptr.cpu().numpy()
+    rows = ptr.shape[0] - 1
+    if sample_edges is not None:
+        rows = max(1, min(rows, int(np.searchsorted(ptr, sample_edges, side="right")) - 1))
+    e = int(ptr[rows])
+    idx = o_idx[:e].cpu().numpy().astype(np.int32)
+    xs = np.ascontiguousarray(x[:rows].cpu().numpy())  # features of the sampled source rows
+    ptr_s = ptr[:rows + 1].astype(np.int32)
+    times = []
+    t_start = time.time()
+    for it in range(5):
+        t0 = time.time()
+        O.copy_src_sum_i32(rows, ptr_s, idx, xs, n_dst, threads)
+        times.append(time.time() - t0)
+        if time.time() - t_start > budget_s:
+            break
+    t = float(np.median(times))
+    return {"value": e / t, "unit": "edges/s", "cores": threads, "kind": "port",
+            "sample": "reference CPU algorithm (oracle/dgl_ref.c ref_copy_src_sum_i32: out-CSR, "
+                      "OpenMP over src rows, omp-atomic scatter, zero fill of all %d dst rows) on "
+                      "%d source rows (%d edges) of the M1 graph, F=%d, median of %d pass(es), "
+                      "%d OpenMP threads" % (n_dst, rows, e, FEAT, len(times), threads),
+            "seconds_per_pass": t}
+
+
+def load_pmc_traffic():
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if present."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        return json.load(open(path)).get("bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    th.cuda.set_device(local)
+    device = "cuda:%d" % local
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=th.device(device))
+
+    import dgl  # noqa: F401
+    from dgl import kernel as K
+
+    n, n_dst, src, dst, x = build_workload(world, rank, device)
+    t0 = time.time()
+    gidx, (o_ptr, o_idx) = make_local_graph(n, n_dst, src, dst, device)
+    m_local = src.shape[0]
+    del src, dst
+    th.cuda.synchronize()
+    log("CSRs built on device in %.2fs" % (time.time() - t0))
+
+    out = th.empty(n_dst, FEAT, device=device)
+
+    def step():
+        K.copy_reduce("sum", gidx, 0, x, out)
+
+    # correctness spot check on the resident workload: a checksum of checksums is
+    # order-independent up to fp32 rounding (sum over rows of out == sum_u outdeg(u) * X[u])
+    step()
+    th.cuda.synchronize()
+    outdeg = th.bincount(gidx.in_csr.indices.long(), minlength=n).double()
+    expect = (outdeg[:, None] * x.double()).sum(0)
+    got = out.double().sum(0)
+    rel = float(((got - expect).abs().max() / expect.abs().max().clamp(min=1)).item())
+    log("checksum-of-checksums rel err %.2e" % rel)
+    if rel > 1e-3:
+        raise SystemExit("copy_u_sum checksum mismatch: %g" % rel)
+    del outdeg, expect, got
+
+    for _ in range(args.warmup):
+        step()
+    stream = th.cuda.current_stream()
+    ev = [(th.cuda.Event(enable_timing=True), th.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    if dist is not None:
+        dist.barrier()
+    th.cuda.synchronize()
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    th.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    th.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    edges_total = m_local
+    if dist is not None:
+        t = th.tensor([elapsed], device=device, dtype=th.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        k = th.tensor([kernel_ms], device=device, dtype=th.float64)
+        dist.all_reduce(k, op=dist.ReduceOp.MAX)
+        kernel_ms = float(k.item())
+        e = th.tensor([m_local], device=device, dtype=th.float64)
+        dist.all_reduce(e)
+        edges_total = int(e.item())
+
+    ms_per_step = elapsed * 1000.0 / args.steps
+    value = edges_total * args.steps / elapsed
+    # algorithmic bytes per launch (per rank): indptr + indices + one
+    # gathered 4F-byte source row per edge + one 4F-byte output row per destination
+    alg_bytes = 4 * (n_dst + 1) + 4 * m_local + 4 * FEAT * m_local + 4 * FEAT * n_dst
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    compulsory = 4 * (n_dst + 1) + 4 * m_local + 4 * FEAT * n + 4 * FEAT * n_dst
+    pmc = load_pmc_traffic()
+    res = {
+        "metric": "edges/sec + achieved HBM GB/s, GCN copy_u_sum on 100M-edge graph, 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "edges/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic RMAT(0.57,0.19,0.19,0.05) generated on device, ids permuted, "
+                "X~U(-1,1) seed 2",
+        "config": {"workload": "M1 copy_u_sum: RMAT scale %d, %d edges, feat %d, int32 in-CSR%s"
+                               % (SCALE + int(round(math.log2(world))), EDGES_PER_GPU * world, FEAT,
+                                  "" if world == 1 else ", %d-way dst-row partition, X replicated" % world),
+                   "nodes": n, "edges": EDGES_PER_GPU * world, "feat": FEAT,
+                   "parallelism": "dst-row partition x%d" % world if world > 1 else "single"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": pmc,
+                     "kernel": "k_chunk_reduce + k_chunk_fixup (one copy_u_sum launch pair)",
+                     "kernel_ms": kernel_ms, "alg_bytes_per_launch": alg_bytes,
+                     "compulsory_bytes_per_launch": compulsory},
+        "hbm_gbps_achieved": achieved,
+        "edges_per_sec_per_gpu": value / world,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            res["cpu_baseline"] = cpu_baseline(o_ptr, o_idx, x, n_dst)
+        except Exception as exc:  # the baseline must never take the GPU line down
+            res["cpu_baseline"] = {"value": None, "error": repr(exc)}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

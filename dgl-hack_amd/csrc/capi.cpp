@@ -1,0 +1,592 @@
+// C ABI of the engine: validation, shape / broadcast inference, target -> role
+// resolution and kernel dispatch.  Mirrors the reference dispatcher
+// src/kernel/binary_reduce.cc (BinaryOpReduce :295-336, the Backward*
+// variants :452-626, CopyReduce :628-716) and the device-agnostic drivers of
+// src/kernel/binary_reduce_impl.h, with the reference's CHECK/LOG(FATAL)
+// failures turned into -1 + DGLMIGetLastError() (runtime_base.h:13-32).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "internal.h"
+
+using namespace dglmi;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct Error : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+#define DGLMI_CHECK(cond, msg)                                                     \
+  do {                                                                             \
+    if (!(cond)) throw Error(std::string("Check failed: " #cond ": ") + (msg));   \
+  } while (0)
+
+#define API_BEGIN() try {
+#define API_END()                                 \
+  }                                               \
+  catch (const std::exception& e) {               \
+    g_last_error = e.what();                      \
+    return -1;                                    \
+  }                                               \
+  return 0;
+
+void check_hip(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw Error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    check_hip(hipGetDevice(&prev), "hipGetDevice");
+    if (prev != dev) check_hip(hipSetDevice(dev), "hipSetDevice");
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur != prev && prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+int parse_reducer(const char* s) {
+  DGLMI_CHECK(s != nullptr, "null reducer");
+  const std::string r(s);
+  if (r == "sum") return RED_SUM;
+  if (r == "max") return RED_MAX;
+  if (r == "min") return RED_MIN;
+  if (r == "prod") return RED_PROD;
+  if (r == "none") return RED_NONE;
+  if (r == "mean") throw Error("reduce mean is not supported.");  // binary_reduce_impl.h:95-98
+  throw Error("Unsupported reducer: " + r);
+}
+
+int parse_op(const char* s) {
+  DGLMI_CHECK(s != nullptr, "null op");
+  const std::string o(s);
+  if (o == "add") return OP_ADD;
+  if (o == "sub") return OP_SUB;
+  if (o == "mul") return OP_MUL;
+  if (o == "div") return OP_DIV;
+  if (o == "dot") return OP_DOT;
+  if (o == "use_lhs") return OP_USE_LHS;
+  throw Error("Unsupported binary op: " + o);
+}
+
+std::string shape_str(const DGLMIArray* a) {
+  std::string s = "(";
+  for (int i = 1; i < a->ndim; ++i) {
+    s += std::to_string(a->shape[i]);
+    if (i + 1 < a->ndim) s += ",";
+  }
+  return s + ")";
+}
+
+int64_t feat_numel(const DGLMIArray* a) {
+  int64_t n = 1;
+  for (int i = 1; i < a->ndim; ++i) n *= a->shape[i];
+  return n;
+}
+
+void check_array(const DGLMIArray* a, const char* name) {
+  if (a == nullptr) throw Error(std::string("null array: ") + name);
+  if (a->ndim < 1 || a->ndim > DGLMI_MAX_NDIM + 1)
+    throw Error(std::string("bad ndim for ") + name);
+  int64_t n = 1;
+  for (int i = 0; i < a->ndim; ++i) {
+    if (a->shape[i] < 0) throw Error(std::string("negative dim in ") + name);
+    n *= a->shape[i];
+  }
+  if (n > 0 && a->data == nullptr) throw Error(std::string("null data pointer for ") + name);
+}
+
+// binary_reduce.cc:54-66
+bool valid_elementwise(const DGLMIArray* l, const DGLMIArray* r) {
+  if (l->ndim != r->ndim) return false;
+  for (int i = 1; i < l->ndim; ++i)
+    if (l->shape[i] != r->shape[i]) return false;
+  return true;
+}
+// binary_reduce.cc:73-84
+bool has_bcast(const DGLMIArray* l, const DGLMIArray* r) { return !valid_elementwise(l, r); }
+
+// CalcBcastInfo (binary_reduce.cc:96-155).  real_out receives the feature
+// shape the op produces (dot: including the vector length as the last dim).
+Bcast calc_bcast(int op, const DGLMIArray* lhs, const DGLMIArray* rhs, std::vector<int64_t>* real_out) {
+  Bcast b;
+  std::memset(&b, 0, sizeof(b));
+  std::vector<int64_t> ls, rs, os, ro;
+  const int max_ndim = std::max(lhs->ndim, rhs->ndim) - 1;
+  int64_t accum = 0;
+  int j = 0;
+  if (op == OP_DOT) {
+    b.data_len = lhs->shape[lhs->ndim - 1];
+    DGLMI_CHECK(rhs->shape[rhs->ndim - 1] == b.data_len, "dot operands differ in vector length");
+    ++j;
+    ro.push_back(b.data_len);
+  } else {
+    b.data_len = 1;
+  }
+  for (; j < max_ndim; ++j) {
+    const int64_t dl = (lhs->ndim - 1 - j < 1) ? 1 : lhs->shape[lhs->ndim - 1 - j];
+    const int64_t dr = (rhs->ndim - 1 - j < 1) ? 1 : rhs->shape[rhs->ndim - 1 - j];
+    if (dl != dr) {
+      if (dl != 1 && dr != 1)
+        throw Error("Invalid broadcasting between feature shapes " + shape_str(lhs) + " and " +
+                    shape_str(rhs));
+      if (accum != 0) {
+        ls.push_back(accum);
+        rs.push_back(accum);
+        os.push_back(accum);
+        accum = 0;
+      }
+      ls.push_back(dl);
+      rs.push_back(dr);
+      os.push_back(std::max(dl, dr));
+    } else {
+      accum = accum == 0 ? dl : accum * dl;
+    }
+    ro.push_back(std::max(dl, dr));
+  }
+  if (accum != 0) {
+    ls.push_back(accum);
+    rs.push_back(accum);
+    os.push_back(accum);
+  }
+  if (os.size() > static_cast<size_t>(kMaxDim)) throw Error("Too many broadcasting dimensions.");
+  std::reverse(ro.begin(), ro.end());
+  std::reverse(ls.begin(), ls.end());
+  std::reverse(rs.begin(), rs.end());
+  std::reverse(os.begin(), os.end());
+  b.ndim = static_cast<int>(os.size());
+  b.lhs_len = b.rhs_len = b.out_len = 1;
+  for (int d = b.ndim - 1; d >= 0; --d) {
+    b.lhs_shape[d] = ls[d];
+    b.rhs_shape[d] = rs[d];
+    b.out_shape[d] = os[d];
+    b.lhs_stride[d] = (d == b.ndim - 1) ? 1 : b.lhs_stride[d + 1] * ls[d + 1];
+    b.rhs_stride[d] = (d == b.ndim - 1) ? 1 : b.rhs_stride[d + 1] * rs[d + 1];
+    b.out_stride[d] = (d == b.ndim - 1) ? 1 : b.out_stride[d + 1] * os[d + 1];
+    b.lhs_len *= ls[d];
+    b.rhs_len *= rs[d];
+    b.out_len *= os[d];
+  }
+  if (real_out) *real_out = ro;
+  return b;
+}
+
+void check_graph(const DGLMIGraph* g) {
+  DGLMI_CHECK(g != nullptr, "null graph");
+  if (g->num_bits != 32)
+    throw Error("Unsupported idx bits: " + std::to_string(g->num_bits));  // common.h:62-69
+}
+
+void check_csr(const DGLMICsr& c, const char* which, bool need_rows) {
+  if (c.num_rows < 0 || c.nnz < 0) throw Error(std::string("bad CSR sizes: ") + which);
+  if (c.indptr == nullptr) throw Error(std::string("null indptr: ") + which);
+  if (c.nnz > 0 && (c.indices == nullptr || c.data == nullptr))
+    throw Error(std::string("null CSR arrays: ") + which);
+  if (need_rows && c.nnz > 0 && c.rows == nullptr)
+    throw Error(std::string("CSR row ids (rows) required: ") + which);
+  if (c.nnz > INT32_MAX || c.num_rows > INT32_MAX) throw Error("graph exceeds int32 indexing");
+}
+
+int role_of(int target, bool walk_in) {
+  // in-CSR: row = dst, col = src ; out-CSR: row = src, col = dst
+  switch (target) {
+    case DGLMI_TARGET_SRC: return walk_in ? ROLE_COL : ROLE_ROW;
+    case DGLMI_TARGET_DST: return walk_in ? ROLE_ROW : ROLE_COL;
+    case DGLMI_TARGET_EDGE: return ROLE_EDGE;
+    default: return ROLE_NONE;
+  }
+}
+
+float identity_of(int red) {
+  switch (red) {
+    case RED_MAX: return -3.402823466e+38f;
+    case RED_MIN: return 3.402823466e+38f;
+    case RED_PROD: return 1.0f;
+    default: return 0.0f;
+  }
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// Scratch for the load-balanced path: the caller's workspace, or a
+// stream-ordered allocation released on the same stream.
+struct Scratch {
+  void* ptr = nullptr;
+  bool owned = false;
+  hipStream_t s = nullptr;
+  Scratch(const DGLMIGraph* g, int64_t bytes, hipStream_t stream) : s(stream) {
+    if (bytes <= 0) return;
+    if (g->workspace != nullptr && g->workspace_bytes >= bytes) {
+      ptr = g->workspace;
+    } else {
+      check_hip(hipMallocAsync(&ptr, static_cast<size_t>(bytes), stream), "hipMallocAsync");
+      owned = true;
+    }
+  }
+  ~Scratch() {
+    if (owned && ptr) (void)hipFreeAsync(ptr, s);
+  }
+};
+
+// Run a reduce-to-row on the load-balanced kernels.  `walk` is the CSR whose
+// rows own the output; out has `walk.num_rows` rows of F floats.
+void run_fast(const DGLMIGraph* g, const DGLMICsr& walk, int kind, int red, const float* x,
+              const int32_t* x_map, const float* w, const int32_t* w_map, float* out, int64_t F,
+              int64_t head_dim, hipStream_t s) {
+  if (walk.nnz == 0) {
+    launch_fill(out, walk.num_rows * F, identity_of(red), s);
+    return;
+  }
+  FastArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.indptr = walk.indptr;
+  a.rows = walk.rows;
+  a.indices = walk.indices;
+  a.eids = walk.data;
+  a.nnz = walk.nnz;
+  a.num_rows = walk.num_rows;
+  a.x = x;
+  a.w = w;
+  a.x_map = x_map;
+  a.w_map = w_map;
+  a.out = out;
+  a.F = F;
+  a.head_dim = head_dim;
+  a.chunk = fast_chunk_edges(walk.nnz, F);
+  Scratch carry(g, fast_workspace_bytes(walk.nnz, F), s);
+  a.carry = static_cast<float*>(carry.ptr);
+  launch_fast_reduce(kind, red, a, s);
+  check_hip(hipGetLastError(), "fast reduce launch");
+}
+
+EdgeArgs base_args(const DGLMICsr& walk) {
+  EdgeArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.indptr = walk.indptr;
+  a.indices = walk.indices;
+  a.eids = walk.data;
+  a.rows = walk.rows;
+  a.num_rows = walk.num_rows;
+  a.nnz = walk.nnz;
+  a.len = 1;
+  return a;
+}
+
+// ---------------------------------------------------------------------------
+// Forward: BinaryOpReduce / CopyReduce
+// ---------------------------------------------------------------------------
+void forward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const DGLMIArray* lhs,
+             const DGLMIArray* rhs, DGLMIArray* out, const int32_t* lhs_map,
+             const int32_t* rhs_map, const int32_t* out_map, hipStream_t s) {
+  check_graph(g);
+  check_array(lhs, "lhs");
+  check_array(out, "out");
+  DGLMI_CHECK(lhs_t >= 0 && lhs_t <= 2, "bad lhs target");
+  if (op != OP_USE_LHS) {
+    check_array(rhs, "rhs");
+    DGLMI_CHECK(rhs_t >= 0 && rhs_t <= 2, "bad rhs target");
+    DGLMI_CHECK(lhs_t != rhs_t, "lhs and rhs targets must differ");  // binary_reduce.cc:216
+    if ((op == OP_ADD || op == OP_MUL) && lhs_t > rhs_t) {  // NeedSwitchOrder :214-219
+      std::swap(lhs_t, rhs_t);
+      std::swap(lhs, rhs);
+      std::swap(lhs_map, rhs_map);
+    }
+  }
+  const DGLMICsr& walk = g->in_csr;  // reductions go to dst; edges enumerated on the in-CSR
+  check_csr(walk, "in_csr", red == RED_NONE || true);
+
+  bool bc = false;
+  Bcast binfo;
+  std::memset(&binfo, 0, sizeof(binfo));
+  int64_t D, len = 1;
+  if (op == OP_USE_LHS) {
+    D = feat_numel(lhs);
+  } else if (has_bcast(lhs, rhs)) {
+    bc = true;
+    binfo = calc_bcast(op, lhs, rhs, nullptr);
+    D = binfo.out_len;
+    len = binfo.data_len;
+  } else {
+    if (!valid_elementwise(lhs, rhs))
+      throw Error("Cannot compute binary operation between feature shapes " + shape_str(lhs) +
+                  " and " + shape_str(rhs));
+    if (op == OP_DOT) {
+      len = lhs->shape[lhs->ndim - 1];
+      D = feat_numel(lhs) / std::max<int64_t>(len, 1);
+      if (len == 0) D = 0;
+    } else {
+      D = feat_numel(lhs);
+    }
+  }
+  DGLMI_CHECK(feat_numel(out) == D, "out feature size " + std::to_string(feat_numel(out)) +
+                                        " != expected " + std::to_string(D));
+  const int64_t out_rows = out->shape[0];
+  const int64_t expect_rows = red == RED_NONE ? walk.nnz : walk.num_rows;
+  const bool need_fill = out_map != nullptr || out_rows != expect_rows;
+  if (!out_map) DGLMI_CHECK(out_rows >= expect_rows, "out has too few rows");
+  if (out_rows * D == 0) return;
+
+  // ---- load-balanced path for the hot reduce-to-dst message functions ----
+  if (red != RED_NONE && out_map == nullptr && out_rows == walk.num_rows && red != RED_PROD &&
+      aligned16(out->data) && aligned16(lhs->data)) {
+    int kind = -1;
+    int64_t head_dim = 1;
+    if (op == OP_USE_LHS && lhs_t == DGLMI_TARGET_SRC) kind = FAST_COPY_COL;
+    else if (op == OP_USE_LHS && lhs_t == DGLMI_TARGET_EDGE) kind = FAST_COPY_EDGE;
+    else if (op == OP_MUL && red == RED_SUM && lhs_t == DGLMI_TARGET_SRC &&
+             rhs_t == DGLMI_TARGET_EDGE && aligned16(rhs->data)) {
+      if (!bc) {
+        kind = FAST_COL_MUL_EDGE;
+      } else if (binfo.ndim == 2 && binfo.rhs_shape[1] == 1 && binfo.lhs_shape[0] == binfo.rhs_shape[0] &&
+                 binfo.lhs_shape[1] == binfo.out_shape[1]) {
+        kind = FAST_COL_MUL_EDGE_BCAST;  // (N, H, D) x (E, H, 1): GAT aggregation
+        head_dim = binfo.lhs_shape[1];
+      } else if (binfo.ndim == 1 && binfo.rhs_shape[0] == 1) {
+        kind = FAST_COL_MUL_EDGE_BCAST;  // (N, D) x (E, 1)
+        head_dim = binfo.lhs_shape[0];
+      }
+    }
+    if (kind >= 0 && fast_supported(kind, D, head_dim) && walk.rows != nullptr) {
+      const float* w = (kind == FAST_COL_MUL_EDGE || kind == FAST_COL_MUL_EDGE_BCAST) ? rhs->data : nullptr;
+      run_fast(g, walk, kind, red, lhs->data, lhs_map, w, rhs_map, out->data, D, head_dim, s);
+      return;
+    }
+  }
+
+  // ---- generic path ----
+  EdgeArgs a = base_args(walk);
+  a.lhs = Operand{lhs->data, lhs_map, role_of(lhs_t, true)};
+  if (op == OP_USE_LHS) a.rhs = Operand{nullptr, nullptr, ROLE_NONE};
+  else a.rhs = Operand{rhs->data, rhs_map, role_of(rhs_t, true)};
+  a.out = out->data;
+  a.out_map = out_map;
+  a.out_role = red == RED_NONE ? ROLE_EDGE : ROLE_ROW;
+  a.D = D;
+  a.len = len;
+  a.out_rows = out_rows;
+  a.bc = binfo;
+  if (need_fill) launch_fill(out->data, out_rows * D, identity_of(red), s);
+  if (red == RED_NONE && walk.nnz > 0) DGLMI_CHECK(walk.rows != nullptr, "in_csr.rows required");
+  launch_generic_forward(op, red, bc, a, s);
+  check_hip(hipGetLastError(), "generic forward launch");
+}
+
+// ---------------------------------------------------------------------------
+// Backward: Backward{Lhs,Rhs}BinaryOpReduce / BackwardCopyReduce
+// ---------------------------------------------------------------------------
+void backward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const int32_t* lhs_map,
+              const int32_t* rhs_map, const int32_t* out_map, const DGLMIArray* lhs,
+              const DGLMIArray* rhs, const DGLMIArray* out, const DGLMIArray* grad_out,
+              DGLMIArray* grad, int want, hipStream_t s) {
+  check_graph(g);
+  check_array(lhs, "lhs");
+  check_array(out, "out");
+  check_array(grad_out, "grad_out");
+  check_array(grad, "grad");
+  DGLMI_CHECK(lhs_t >= 0 && lhs_t <= 2, "bad lhs target");
+  if (op != OP_USE_LHS) {
+    check_array(rhs, "rhs");
+    DGLMI_CHECK(rhs_t >= 0 && rhs_t <= 2, "bad rhs target");
+    DGLMI_CHECK(lhs_t != rhs_t, "lhs and rhs targets must differ");
+    if ((op == OP_ADD || op == OP_MUL) && lhs_t > rhs_t) {  // binary_reduce.cc:470-476, 571-577
+      std::swap(lhs_t, rhs_t);
+      std::swap(lhs, rhs);
+      std::swap(lhs_map, rhs_map);
+      want = 1 - want;
+    }
+  } else {
+    DGLMI_CHECK(want == 0, "copy reduce has no rhs gradient");
+  }
+  const int x_t = want == 0 ? lhs_t : rhs_t;
+  const bool walk_in = x_t != DGLMI_TARGET_SRC;  // src grads are owned by out-CSR rows
+  const DGLMICsr& walk = walk_in ? g->in_csr : g->out_csr;
+  check_csr(walk, walk_in ? "in_csr" : "out_csr", x_t == DGLMI_TARGET_EDGE);
+
+  bool bc = false;
+  Bcast binfo;
+  std::memset(&binfo, 0, sizeof(binfo));
+  int64_t D, len = 1;
+  if (op == OP_USE_LHS) {
+    D = feat_numel(lhs);
+  } else if (has_bcast(lhs, rhs)) {
+    bc = true;
+    binfo = calc_bcast(op, lhs, rhs, nullptr);
+    D = binfo.out_len;
+    len = binfo.data_len;
+  } else {
+    if (!valid_elementwise(lhs, rhs))
+      throw Error("Cannot compute binary operation between feature shapes " + shape_str(lhs) +
+                  " and " + shape_str(rhs));
+    len = op == OP_DOT ? lhs->shape[lhs->ndim - 1] : 1;
+    D = op == OP_DOT ? (len ? feat_numel(lhs) / len : 0) : feat_numel(lhs);
+  }
+  DGLMI_CHECK(feat_numel(out) == D && feat_numel(grad_out) == D, "out / grad_out feature size mismatch");
+  const int64_t Dg = D * len;
+  DGLMI_CHECK(feat_numel(grad) == Dg, "grad feature size " + std::to_string(feat_numel(grad)) +
+                                          " != expected " + std::to_string(Dg));
+  const int64_t grad_rows = grad->shape[0];
+  if (grad_rows * Dg == 0) return;
+  const int32_t* x_map = want == 0 ? lhs_map : rhs_map;
+  const int64_t expect_rows = x_t == DGLMI_TARGET_EDGE ? walk.nnz : walk.num_rows;
+  if (!x_map) DGLMI_CHECK(grad_rows >= expect_rows, "grad has too few rows");
+  const bool need_fill = x_map != nullptr || grad_rows != expect_rows;
+
+  // ---- load-balanced path: gradients that are themselves a reduce-to-row ----
+  // copy_u_sum:  grad_u[src] = sum_{dst in out(src)} grad_out[dst]
+  // u_mul_e_sum: grad_u[src] = sum grad_out[dst] * e[eid]  (the reference's
+  // csrmm2-on-out-CSR specialisation, binary_reduce_sum.cu:262-292).
+  if (red == RED_SUM && x_t == DGLMI_TARGET_SRC && !need_fill && out_map == nullptr &&
+      walk.rows != nullptr && aligned16(grad->data) && aligned16(grad_out->data)) {
+    int kind = -1;
+    int64_t head_dim = 1;
+    const float* w = nullptr;
+    const int32_t* w_map = nullptr;
+    if (op == OP_USE_LHS) {
+      kind = FAST_COPY_COL;
+    } else if (op == OP_MUL && want == 0 && rhs_t == DGLMI_TARGET_EDGE && aligned16(rhs->data)) {
+      w = rhs->data;
+      w_map = rhs_map;
+      if (!bc) {
+        kind = FAST_COL_MUL_EDGE;
+      } else if (binfo.ndim == 2 && binfo.rhs_shape[1] == 1 && binfo.lhs_shape[0] == binfo.rhs_shape[0] &&
+                 binfo.lhs_shape[1] == binfo.out_shape[1]) {
+        kind = FAST_COL_MUL_EDGE_BCAST;
+        head_dim = binfo.lhs_shape[1];
+      } else if (binfo.ndim == 1 && binfo.rhs_shape[0] == 1) {
+        kind = FAST_COL_MUL_EDGE_BCAST;
+        head_dim = binfo.lhs_shape[0];
+      }
+    }
+    if (kind >= 0 && fast_supported(kind, D, head_dim)) {
+      run_fast(g, walk, kind, RED_SUM, grad_out->data, nullptr, w, w_map, grad->data, D, head_dim, s);
+      return;
+    }
+  }
+
+  EdgeArgs a = base_args(walk);
+  a.lhs = Operand{lhs->data, lhs_map, role_of(lhs_t, walk_in)};
+  if (op == OP_USE_LHS) a.rhs = Operand{nullptr, nullptr, ROLE_NONE};
+  else a.rhs = Operand{rhs->data, rhs_map, role_of(rhs_t, walk_in)};
+  a.out = grad->data;
+  a.out_role = x_t == DGLMI_TARGET_EDGE ? ROLE_EDGE : ROLE_ROW;
+  a.D = D;
+  a.len = len;
+  a.out_rows = grad_rows;
+  a.fwd_out = out->data;
+  a.grad_out = grad_out->data;
+  a.fo_map = out_map;
+  a.fo_role = red == RED_NONE ? ROLE_EDGE : role_of(DGLMI_TARGET_DST, walk_in);
+  a.want = want;
+  a.bc = binfo;
+  if (need_fill) launch_fill(grad->data, grad_rows * Dg, 0.0f, s);
+  launch_generic_backward(op, red, bc, a, s);
+  check_hip(hipGetLastError(), "generic backward launch");
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* DGLMIGetLastError(void) { return g_last_error.c_str(); }
+
+const char* DGLMIVersion(void) { return "0.4-mi355x"; }
+
+int DGLMIKernelInferBinaryFeatureShape(const char* op, const DGLMIArray* lhs,
+                                       const DGLMIArray* rhs, int64_t* out_shape,
+                                       int32_t* out_ndim) {
+  API_BEGIN();
+  DGLMI_CHECK(lhs && rhs && out_shape && out_ndim, "null argument");
+  std::vector<int64_t> ro;
+  calc_bcast(parse_op(op), lhs, rhs, &ro);
+  *out_ndim = static_cast<int32_t>(ro.size());
+  for (size_t i = 0; i < ro.size(); ++i) out_shape[i] = ro[i];
+  API_END();
+}
+
+int DGLMIKernelBinaryOpReduce(const char* reducer, const char* op, const DGLMIGraph* graph,
+                              int32_t lhs_target, int32_t rhs_target, const DGLMIArray* lhs,
+                              const DGLMIArray* rhs, DGLMIArray* out,
+                              const int32_t* lhs_mapping, const int32_t* rhs_mapping,
+                              const int32_t* out_mapping, void* stream) {
+  API_BEGIN();
+  const int red = parse_reducer(reducer);
+  const int o = parse_op(op);
+  check_graph(graph);
+  DeviceGuard guard(graph->device);
+  forward(red, o, graph, lhs_target, rhs_target, lhs, rhs, out, lhs_mapping, rhs_mapping,
+          out_mapping, static_cast<hipStream_t>(stream));
+  API_END();
+}
+
+int DGLMIKernelBackwardLhsBinaryOpReduce(
+    const char* reducer, const char* op, const DGLMIGraph* graph, int32_t lhs_target,
+    int32_t rhs_target, const int32_t* lhs_mapping, const int32_t* rhs_mapping,
+    const int32_t* out_mapping, const DGLMIArray* lhs, const DGLMIArray* rhs,
+    const DGLMIArray* out, const DGLMIArray* grad_out, DGLMIArray* grad_lhs, void* stream) {
+  API_BEGIN();
+  const int red = parse_reducer(reducer);
+  const int o = parse_op(op);
+  check_graph(graph);
+  DeviceGuard guard(graph->device);
+  backward(red, o, graph, lhs_target, rhs_target, lhs_mapping, rhs_mapping, out_mapping, lhs, rhs,
+           out, grad_out, grad_lhs, 0, static_cast<hipStream_t>(stream));
+  API_END();
+}
+
+int DGLMIKernelBackwardRhsBinaryOpReduce(
+    const char* reducer, const char* op, const DGLMIGraph* graph, int32_t lhs_target,
+    int32_t rhs_target, const int32_t* lhs_mapping, const int32_t* rhs_mapping,
+    const int32_t* out_mapping, const DGLMIArray* lhs, const DGLMIArray* rhs,
+    const DGLMIArray* out, const DGLMIArray* grad_out, DGLMIArray* grad_rhs, void* stream) {
+  API_BEGIN();
+  const int red = parse_reducer(reducer);
+  const int o = parse_op(op);
+  check_graph(graph);
+  DeviceGuard guard(graph->device);
+  backward(red, o, graph, lhs_target, rhs_target, lhs_mapping, rhs_mapping, out_mapping, lhs, rhs,
+           out, grad_out, grad_rhs, 1, static_cast<hipStream_t>(stream));
+  API_END();
+}
+
+int DGLMIKernelCopyReduce(const char* reducer, const DGLMIGraph* graph, int32_t target,
+                          const DGLMIArray* in, DGLMIArray* out, const int32_t* in_mapping,
+                          const int32_t* out_mapping, void* stream) {
+  API_BEGIN();
+  const int red = parse_reducer(reducer);
+  check_graph(graph);
+  DeviceGuard guard(graph->device);
+  forward(red, OP_USE_LHS, graph, target, DGLMI_TARGET_NONE, in, nullptr, out, in_mapping,
+          nullptr, out_mapping, static_cast<hipStream_t>(stream));
+  API_END();
+}
+
+int DGLMIKernelBackwardCopyReduce(const char* reducer, const DGLMIGraph* graph, int32_t target,
+                                  const DGLMIArray* in, const DGLMIArray* out,
+                                  const DGLMIArray* grad_out, DGLMIArray* grad_in,
+                                  const int32_t* in_mapping, const int32_t* out_mapping,
+                                  void* stream) {
+  API_BEGIN();
+  const int red = parse_reducer(reducer);
+  check_graph(graph);
+  DeviceGuard guard(graph->device);
+  backward(red, OP_USE_LHS, graph, target, DGLMI_TARGET_NONE, in_mapping, nullptr, out_mapping, in,
+           nullptr, out, grad_out, grad_in, 0, static_cast<hipStream_t>(stream));
+  API_END();
+}
+
+int64_t DGLMIKernelWorkspaceBytes(const DGLMICsr* csr, int64_t feat_len) {
+  if (csr == nullptr || csr->nnz <= 0 || feat_len <= 0) return 0;
+  return fast_workspace_bytes(csr->nnz, feat_len);
+}
+
+}  // extern "C"

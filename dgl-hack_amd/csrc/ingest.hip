@@ -1,0 +1,221 @@
+// Graph ingestion: COO -> CSR, CSR transpose, CSR row expansion.
+//
+// Host versions restate aten::COOToCSR (array/cpu/spmat_op_impl_coo.cc:230-283)
+// and aten::CSRTranspose (array/cpu/spmat_op_impl.cc:323-369): stable counting
+// sorts, so the resulting arrays are bit-identical to the reference's.
+// The device version builds the same arrays on the GPU with a stable LSD
+// radix sort of (row, position) pairs -- stability gives the identical
+// within-row order -- so a multi-hundred-million-edge graph never needs a
+// CPU CSR build and a host-to-device copy (the reference builds on the CPU
+// and copies, immutable_graph.cc:548-559).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "internal.h"
+
+namespace {
+
+template <typename I>
+void coo_to_csr(int64_t n, int64_t nnz, const I* row, const I* col, const I* data, I* bp, I* bi,
+                I* bx) {
+  std::fill(bp, bp + n, I(0));
+  for (int64_t i = 0; i < nnz; ++i) bp[row[i]]++;
+  I cum = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const I t = bp[i];
+    bp[i] = cum;
+    cum += t;
+  }
+  bp[n] = static_cast<I>(nnz);
+  for (int64_t i = 0; i < nnz; ++i) {
+    const I r = row[i];
+    bi[bp[r]] = col[i];
+    bx[bp[r]] = data ? data[i] : static_cast<I>(i);
+    bp[r]++;
+  }
+  I last = 0;
+  for (int64_t i = 0; i <= n; ++i) {
+    const I t = bp[i];
+    bp[i] = last;
+    last = t;
+  }
+}
+
+template <typename I>
+void csr_transpose(int64_t n, int64_t m, const I* ap, const I* aj, const I* ax, I* bp, I* bi,
+                   I* bx) {
+  const int64_t nnz = ap[n];
+  std::fill(bp, bp + m, I(0));
+  for (int64_t j = 0; j < nnz; ++j) bp[aj[j]]++;
+  I cum = 0;
+  for (int64_t i = 0; i < m; ++i) {
+    const I t = bp[i];
+    bp[i] = cum;
+    cum += t;
+  }
+  bp[m] = static_cast<I>(nnz);
+  for (int64_t i = 0; i < n; ++i) {
+    for (I j = ap[i]; j < ap[i + 1]; ++j) {
+      const I d = aj[j];
+      bi[bp[d]] = static_cast<I>(i);
+      bx[bp[d]] = ax ? ax[j] : j;
+      bp[d]++;
+    }
+  }
+  I last = 0;
+  for (int64_t i = 0; i <= m; ++i) {
+    const I t = bp[i];
+    bp[i] = last;
+    last = t;
+  }
+}
+
+__global__ void k_iota(int32_t* __restrict__ out, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    out[i] = static_cast<int32_t>(i);
+}
+
+__global__ void k_gather_cols(const int32_t* __restrict__ perm, const int32_t* __restrict__ col,
+                              const int32_t* __restrict__ data, int32_t* __restrict__ indices,
+                              int32_t* __restrict__ out_data, int64_t nnz) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nnz; i += stride) {
+    const int32_t p = perm[i];
+    indices[i] = col[p];
+    out_data[i] = data ? data[p] : p;
+  }
+}
+
+// indptr from the sorted row keys: position i opens every row in (key[i-1], key[i]].
+__global__ void k_indptr_from_sorted(const int32_t* __restrict__ key, int64_t nnz, int64_t n,
+                                     int32_t* __restrict__ indptr) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= nnz; i += stride) {
+    const int64_t lo = i == 0 ? 0 : (int64_t)key[i - 1] + 1;
+    const int64_t hi = i == nnz ? n : (int64_t)key[i];
+    for (int64_t r = lo; r <= hi; ++r) indptr[r] = static_cast<int32_t>(i);
+  }
+}
+
+__global__ void k_mark_row_starts(const int32_t* __restrict__ indptr, int64_t n,
+                                  int32_t* __restrict__ rows) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += stride)
+    if (indptr[r + 1] > indptr[r]) rows[indptr[r]] = static_cast<int32_t>(r);
+}
+
+struct MaxOp {
+  __device__ __forceinline__ int32_t operator()(int32_t a, int32_t b) const { return a > b ? a : b; }
+};
+
+unsigned grid_of(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  if (b > 16384) b = 16384;
+  if (b < 1) b = 1;
+  return static_cast<unsigned>(b);
+}
+
+int bits_for(int64_t n) {
+  int b = 1;
+  while ((int64_t(1) << b) < n && b < 31) ++b;
+  return b;
+}
+
+size_t sort_temp_bytes(int64_t n, int64_t nnz) {
+  size_t bytes = 0;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, static_cast<const int32_t*>(nullptr),
+                                     static_cast<int32_t*>(nullptr),
+                                     static_cast<const int32_t*>(nullptr),
+                                     static_cast<int32_t*>(nullptr), static_cast<int>(nnz), 0,
+                                     bits_for(n));
+  return bytes;
+}
+
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+thread_local std::string g_ingest_error;
+
+}  // namespace
+
+extern "C" {
+
+int DGLMICOOToCSR(int64_t num_rows, int64_t nnz, const int64_t* row, const int64_t* col,
+                  const int64_t* data, int64_t* indptr, int64_t* indices, int64_t* out_data) {
+  if (num_rows < 0 || nnz < 0 || indptr == nullptr) return -1;
+  for (int64_t i = 0; i < nnz; ++i)
+    if (row[i] < 0 || row[i] >= num_rows) return -1;
+  coo_to_csr<int64_t>(num_rows, nnz, row, col, data, indptr, indices, out_data);
+  return 0;
+}
+
+int DGLMICSRTranspose(int64_t num_rows, int64_t num_cols, const int64_t* indptr,
+                      const int64_t* indices, const int64_t* data, int64_t* t_indptr,
+                      int64_t* t_indices, int64_t* t_data) {
+  if (num_rows < 0 || num_cols < 0 || indptr == nullptr || t_indptr == nullptr) return -1;
+  for (int64_t j = 0; j < indptr[num_rows]; ++j)
+    if (indices[j] < 0 || indices[j] >= num_cols) return -1;
+  csr_transpose<int64_t>(num_rows, num_cols, indptr, indices, data, t_indptr, t_indices, t_data);
+  return 0;
+}
+
+int64_t DGLMICOOToCSRDeviceWorkspaceBytes(int64_t num_rows, int64_t nnz) {
+  if (nnz <= 0) return 256;
+  return static_cast<int64_t>(3 * align256(nnz * sizeof(int32_t)) +
+                              align256(sort_temp_bytes(num_rows, nnz)));
+}
+
+int DGLMICOOToCSRDevice(int64_t num_rows, int64_t nnz, const int32_t* row, const int32_t* col,
+                        const int32_t* data, int32_t* indptr, int32_t* indices, int32_t* out_data,
+                        void* workspace, int64_t workspace_bytes, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (num_rows < 0 || nnz < 0 || nnz > INT32_MAX || num_rows >= INT32_MAX) return -1;
+  if (nnz == 0) {
+    dglmi::launch_fill_i32(indptr, num_rows + 1, 0, s);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+  if (workspace_bytes < DGLMICOOToCSRDeviceWorkspaceBytes(num_rows, nnz)) return -1;
+  char* ws = static_cast<char*>(workspace);
+  const size_t seg = align256(nnz * sizeof(int32_t));
+  int32_t* keys_out = reinterpret_cast<int32_t*>(ws);
+  int32_t* perm_in = reinterpret_cast<int32_t*>(ws + seg);
+  int32_t* perm_out = reinterpret_cast<int32_t*>(ws + 2 * seg);
+  void* temp = ws + 3 * seg;
+  size_t temp_bytes = sort_temp_bytes(num_rows, nnz);
+  hipLaunchKernelGGL(k_iota, dim3(grid_of(nnz)), dim3(256), 0, s, perm_in, nnz);
+  if (hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, row, keys_out, perm_in, perm_out,
+                                         static_cast<int>(nnz), 0, bits_for(num_rows), s) !=
+      hipSuccess)
+    return -1;
+  hipLaunchKernelGGL(k_gather_cols, dim3(grid_of(nnz)), dim3(256), 0, s, perm_out, col, data,
+                     indices, out_data, nnz);
+  hipLaunchKernelGGL(k_indptr_from_sorted, dim3(grid_of(nnz + 1)), dim3(256), 0, s, keys_out, nnz,
+                     num_rows, indptr);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int DGLMICSRExpandRows(const int32_t* indptr, int64_t num_rows, int64_t nnz, int32_t* rows,
+                       void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (nnz == 0) return 0;
+  dglmi::launch_fill_i32(rows, nnz, 0, s);
+  hipLaunchKernelGGL(k_mark_row_starts, dim3(grid_of(num_rows)), dim3(256), 0, s, indptr, num_rows,
+                     rows);
+  size_t temp_bytes = 0;
+  hipcub::DeviceScan::InclusiveScan(nullptr, temp_bytes, rows, rows, MaxOp(), static_cast<int>(nnz),
+                                    s);
+  void* temp = nullptr;
+  if (hipMallocAsync(&temp, temp_bytes, s) != hipSuccess) return -1;
+  const hipError_t e = hipcub::DeviceScan::InclusiveScan(temp, temp_bytes, rows, rows, MaxOp(),
+                                                         static_cast<int>(nnz), s);
+  (void)hipFreeAsync(temp, s);
+  if (e != hipSuccess) return -1;
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // extern "C"

@@ -1,0 +1,166 @@
+// Internal definitions shared by the C-ABI layer and the gfx950 kernels.
+//
+// Roles.  The reference selects kernel operands by target (src / dst / edge,
+// binary_reduce_common.h:56-105) and swaps src and dst when it walks the
+// reverse CSR for gradients (SwitchSrcDst, :107-121).  Here every kernel walks
+// one CSR and sees operands by ROLE relative to that CSR: the row node, the
+// column node, the edge, or nothing.  The host layer maps targets to roles
+// for the CSR it picks (in-CSR: row = dst, col = src; out-CSR: row = src,
+// col = dst), which is the same switch made explicit.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/dglmi.h"
+
+namespace dglmi {
+
+enum Role : int { ROLE_ROW = 0, ROLE_COL = 1, ROLE_EDGE = 2, ROLE_NONE = 3 };
+enum Red : int { RED_SUM = 0, RED_MAX = 1, RED_MIN = 2, RED_PROD = 3, RED_NONE = 4 };
+enum Op : int { OP_ADD = 0, OP_SUB = 1, OP_MUL = 2, OP_DIV = 3, OP_DOT = 4, OP_USE_LHS = 5 };
+
+constexpr int kMaxDim = DGLMI_MAX_NDIM;
+
+// Flattened broadcast description (BcastInfo, binary_reduce.h / binary_reduce.cc:96-155).
+struct Bcast {
+  int ndim;
+  int64_t out_shape[kMaxDim], out_stride[kMaxDim];
+  int64_t lhs_shape[kMaxDim], lhs_stride[kMaxDim];
+  int64_t rhs_shape[kMaxDim], rhs_stride[kMaxDim];
+  int64_t lhs_len, rhs_len, out_len, data_len;
+};
+
+struct Operand {
+  const float* data;
+  const int32_t* map;  // node map (node id -> row) or edge map (edge id -> row)
+  int role;
+};
+
+// Everything a generic kernel needs; passed by value as the kernel argument.
+struct EdgeArgs {
+  const int32_t* indptr;   // CSR walked (rows = owners of the reduction)
+  const int32_t* indices;  // column node per position
+  const int32_t* eids;     // edge id per position
+  const int32_t* rows;     // row per position (edge-wise kernels)
+  int64_t num_rows;
+  int64_t nnz;
+  Operand lhs, rhs;
+  float* out;              // forward: out; backward: grad buffer
+  const int32_t* out_map;  // row map of `out`
+  int out_role;            // ROLE_ROW (reduce to row node) or ROLE_EDGE (per edge)
+  int64_t D;               // forward out features per row (x_len or bcast out_len)
+  int64_t len;             // dot length (1 otherwise)
+  int64_t out_rows;        // rows of `out` (bounds for the identity fill)
+  // backward only
+  const float* fwd_out;    // the forward output
+  const float* grad_out;   // its gradient
+  const int32_t* fo_map;   // row map of fwd_out/grad_out
+  int fo_role;             // ROLE_COL/ROLE_ROW (node output) or ROLE_EDGE
+  int want;                // 0 = grad wrt lhs, 1 = grad wrt rhs
+  Bcast bc;
+};
+
+// ---- device helpers ---------------------------------------------------------
+template <int RED>
+__device__ __forceinline__ float red_identity() {
+  if constexpr (RED == RED_MAX) return -3.402823466e+38f;  // numeric_limits<float>::lowest()
+  else if constexpr (RED == RED_MIN) return 3.402823466e+38f;
+  else if constexpr (RED == RED_PROD) return 1.0f;
+  else return 0.0f;
+}
+
+// cpu/functor.h:19-71 -- std::max / std::min tie and NaN behaviour kept.
+template <int RED>
+__device__ __forceinline__ float red_apply(float acc, float v) {
+  if constexpr (RED == RED_MAX) return (acc < v) ? v : acc;
+  else if constexpr (RED == RED_MIN) return (v < acc) ? v : acc;
+  else if constexpr (RED == RED_PROD) return acc * v;
+  else if constexpr (RED == RED_NONE) return v;
+  else return acc + v;
+}
+
+template <int RED>
+__device__ __forceinline__ float red_backward(float val, float accum) {
+  if constexpr (RED == RED_MAX || RED == RED_MIN) return static_cast<float>(val == accum);
+  else if constexpr (RED == RED_PROD) return accum / val;
+  else return 1.0f;
+}
+
+// binary_reduce_common.h:131-213
+template <int OP>
+__device__ __forceinline__ float op_apply(const float* l, const float* r, int64_t len) {
+  if constexpr (OP == OP_ADD) return l[0] + r[0];
+  else if constexpr (OP == OP_SUB) return l[0] - r[0];
+  else if constexpr (OP == OP_MUL) return l[0] * r[0];
+  else if constexpr (OP == OP_DIV) return l[0] / r[0];
+  else if constexpr (OP == OP_USE_LHS) return l[0];
+  else {
+    float out = 0.0f;
+    for (int64_t i = 0; i < len; ++i) out += l[i] * r[i];
+    return out;
+  }
+}
+template <int OP>
+__device__ __forceinline__ float op_grad_lhs(float l, float r) {
+  if constexpr (OP == OP_MUL || OP == OP_DOT) return r;
+  else if constexpr (OP == OP_DIV) return 1.0f / r;
+  else return 1.0f;
+}
+template <int OP>
+__device__ __forceinline__ float op_grad_rhs(float l, float r) {
+  if constexpr (OP == OP_ADD) return 1.0f;
+  else if constexpr (OP == OP_SUB) return -1.0f;
+  else if constexpr (OP == OP_MUL || OP == OP_DOT) return l;
+  else if constexpr (OP == OP_DIV) return -l / (r * r);
+  else return 0.0f;
+}
+
+__device__ __forceinline__ int64_t resolve(const Operand& o, int64_t row, int64_t col,
+                                           int64_t eid) {
+  int64_t id = o.role == ROLE_ROW ? row : (o.role == ROLE_COL ? col : (o.role == ROLE_EDGE ? eid : 0));
+  if (o.map && o.role != ROLE_NONE) id = o.map[id];
+  return id;
+}
+
+// ---- host-side launchers (defined in the .hip files) ------------------------
+void launch_fill(float* out, int64_t n, float value, hipStream_t s);
+void launch_fill_i32(int32_t* out, int64_t n, int32_t value, hipStream_t s);
+
+// Generic forward: reduce to row nodes (out_role == ROLE_ROW) or per edge.
+void launch_generic_forward(int op, int red, bool bcast, const EdgeArgs& a, hipStream_t s);
+// Generic backward for one operand (a.want), reduce to row nodes or per edge.
+void launch_generic_backward(int op, int red, bool bcast, const EdgeArgs& a, hipStream_t s);
+
+// Load-balanced reduce-to-row kernels (kernels_spmm.hip).
+enum FastKind : int {
+  FAST_COPY_COL = 0,    // v = X[col]
+  FAST_COPY_EDGE = 1,   // v = E[eid]
+  FAST_COL_MUL_EDGE = 2,        // v = X[col] * E[eid]            (same feature shape)
+  FAST_COL_MUL_EDGE_BCAST = 3,  // v = X[col, h, :] * E[eid, h]   (E broadcast over the last dim)
+};
+struct FastArgs {
+  const int32_t* indptr;
+  const int32_t* rows;
+  const int32_t* indices;
+  const int32_t* eids;
+  int64_t nnz;
+  int64_t num_rows;     // rows owned (out rows 0..num_rows-1 written)
+  const float* x;       // column-node or edge features
+  const float* w;       // edge features (mul kinds)
+  const int32_t* x_map; // optional row maps
+  const int32_t* w_map;
+  float* out;
+  int64_t F;            // features per output row
+  int64_t head_dim;     // bcast: features per head (E has F / head_dim values per edge)
+  float* carry;         // workspace: num_chunks * F floats
+  int64_t chunk;        // edges per chunk
+};
+int64_t fast_chunk_edges(int64_t nnz, int64_t F);
+int64_t fast_workspace_bytes(int64_t nnz, int64_t F);
+// Returns false if the shape is not supported by the fast path.
+bool fast_supported(int kind, int64_t F, int64_t head_dim);
+void launch_fast_reduce(int kind, int red, const FastArgs& a, hipStream_t s);  // needs a.indptr
+
+}  // namespace dglmi

@@ -1,0 +1,327 @@
+// Load-balanced g-SpMM (reduce to the row node) for gfx950.
+//
+// Covers the hot reduce-to-node message functions of GraphConv / GATConv:
+//   copy_u  -> v = X[col]              (GCN aggregation, copy_u_sum / copy_u_max)
+//   copy_e  -> v = E[eid]              (edge-softmax denominators)
+//   u_mul_e -> v = X[col] * E[eid]     (and E broadcast over the head dim, GAT)
+// folded with sum / max / min into out[row].
+//
+// Reference: the same arithmetic as cpu/binary_reduce_impl.h:29-52 with
+// ReduceSum/Max/Min (cpu/functor.h:19-48); on GPU the reference calls
+// cuSPARSE csrmm2 + a cuBLAS transpose for copy_u_sum
+// (cuda/binary_reduce_sum.cu:84-143) and a minigun edge-parallel kernel with
+// atomics otherwise (cuda/binary_reduce_impl.cuh:22-54).
+//
+// Design (MI355X-first):
+//  * Work is cut into fixed chunks of K consecutive CSR positions (merge-path
+//    style), so a power-law hub with 10^5 in-edges is spread over many chunks
+//    while ordinary rows cost one pass: every group does the same work.
+//  * A group of L lanes (L * 4 * NV >= F floats) owns a chunk; the chunk's
+//    (row, col, eid) triples are staged through LDS B at a time with coalesced
+//    loads, then each lane gathers float4 slices of U source rows at once
+//    (U * 16 B in flight per lane, whole 256-B rows per group at F = 64).
+//  * Rows are folded in registers and written once (owner computes, no
+//    atomics).  A row cut by a chunk boundary writes its head partial to out
+//    and each continuing chunk writes one partial to the carry workspace; a
+//    fixup pass folds the carries into out in chunk order, so results are
+//    deterministic and independent of scheduling.
+//  * Zero-in-degree rows get the reducer identity from the group that sees
+//    the gap in the row sequence (no separate fill pass over `out`).
+#include "internal.h"
+
+#include <climits>
+
+namespace dglmi {
+namespace {
+
+constexpr int kBlock = 256;
+
+template <int RED>
+__device__ __forceinline__ float4 red4(float4 a, float4 b) {
+  return make_float4(red_apply<RED>(a.x, b.x), red_apply<RED>(a.y, b.y),
+                     red_apply<RED>(a.z, b.z), red_apply<RED>(a.w, b.w));
+}
+template <int RED>
+__device__ __forceinline__ float4 ident4() {
+  const float v = red_identity<RED>();
+  return make_float4(v, v, v, v);
+}
+
+__device__ __forceinline__ float4 ld4(const float* p) {
+  return *reinterpret_cast<const float4*>(p);
+}
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+template <int KIND>
+constexpr bool needs_eid() {
+  return KIND != FAST_COPY_COL;
+}
+
+// Value of one edge for float4 slot f4 of the output row.
+template <int KIND>
+__device__ __forceinline__ float4 edge_value(const FastArgs& a, int32_t col, int32_t eid, int f4) {
+  if constexpr (KIND == FAST_COPY_COL) {
+    const int64_t c = a.x_map ? a.x_map[col] : col;
+    return ld4(a.x + c * a.F + 4 * f4);
+  } else if constexpr (KIND == FAST_COPY_EDGE) {
+    const int64_t e = a.x_map ? a.x_map[eid] : eid;
+    return ld4(a.x + e * a.F + 4 * f4);
+  } else if constexpr (KIND == FAST_COL_MUL_EDGE) {
+    const int64_t c = a.x_map ? a.x_map[col] : col;
+    const int64_t e = a.w_map ? a.w_map[eid] : eid;
+    const float4 x = ld4(a.x + c * a.F + 4 * f4);
+    const float4 w = ld4(a.w + e * a.F + 4 * f4);
+    return make_float4(x.x * w.x, x.y * w.y, x.z * w.z, x.w * w.w);
+  } else {
+    const int64_t c = a.x_map ? a.x_map[col] : col;
+    const int64_t e = a.w_map ? a.w_map[eid] : eid;
+    const int64_t H = a.F / a.head_dim;
+    const float4 x = ld4(a.x + c * a.F + 4 * f4);
+    const float w = a.w[e * H + (4 * f4) / a.head_dim];
+    return make_float4(x.x * w, x.y * w, x.z * w, x.w * w);
+  }
+}
+
+// L lanes per group, NV float4 per lane, U gathers in flight per lane-slot.
+template <int KIND, int RED, int L, int NV>
+__global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32_t* __restrict__ indptr) {
+  constexpr int G = kBlock / L;           // groups per block
+  constexpr int B = L > 16 ? L : 16;      // positions staged per step
+  constexpr int U = NV == 1 ? 8 : (NV == 2 ? 4 : 2);
+  static_assert(B % U == 0, "B must be a multiple of U");
+  __shared__ int32_t s_row[G][B];
+  __shared__ int32_t s_col[G][B];
+  __shared__ int32_t s_eid[needs_eid<KIND>() ? G : 1][needs_eid<KIND>() ? B : 1];
+
+  const int g = threadIdx.x / L;
+  const int lane = threadIdx.x % L;
+  const int64_t chunk = (int64_t)blockIdx.x * G + g;
+  const int64_t K = a.chunk;
+  const int64_t p0 = chunk * K;
+  if (p0 >= a.nnz) return;  // whole group exits together
+  const int64_t p1 = p0 + K < a.nnz ? p0 + K : a.nnz;
+  const int F4 = static_cast<int>(a.F / 4);
+  const float4 I = ident4<RED>();
+
+  int64_t cur = a.rows[p0];
+  bool cont = p0 > 0 && a.rows[p0 - 1] == cur;
+  // leading empty rows: those after the previous chunk's last row (or from 0)
+  if (!cont) {
+    const int64_t first_gap = p0 > 0 ? (int64_t)a.rows[p0 - 1] + 1 : 0;
+    for (int64_t r = first_gap; r < cur; ++r)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int f4 = lane + v * L;
+        if (f4 < F4) st4(a.out + r * a.F + 4 * f4, I);
+      }
+  }
+  float4 acc[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) acc[v] = I;
+
+  for (int64_t base = p0; base < p1; base += B) {
+    // stage B positions through LDS (coalesced, one row/col/eid per lane slot)
+    for (int q = lane; q < B; q += L) {
+      const int64_t p = base + q;
+      const bool ok = p < p1;
+      s_row[g][q] = ok ? a.rows[p] : INT_MAX;
+      s_col[g][q] = ok ? a.indices[p] : 0;
+      if constexpr (needs_eid<KIND>()) s_eid[needs_eid<KIND>() ? g : 0][q] = ok ? a.eids[p] : 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int ub = 0; ub < B; ub += U) {
+      float4 val[U][NV];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int32_t col = s_col[g][ub + u];
+        const int32_t eid = needs_eid<KIND>() ? s_eid[needs_eid<KIND>() ? g : 0][ub + u] : 0;
+        const bool ok = s_row[g][ub + u] != INT_MAX;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          const int f4 = lane + v * L;
+          val[u][v] = (ok && f4 < F4) ? edge_value<KIND>(a, col, eid, f4) : I;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int32_t r = s_row[g][ub + u];
+        if (r == INT_MAX) break;
+        if (r != cur) {
+          // flush the finished row, fill the empty rows in between
+          float* dst = cont ? a.carry + chunk * a.F : a.out + cur * a.F;
+#pragma unroll
+          for (int v = 0; v < NV; ++v) {
+            const int f4 = lane + v * L;
+            if (f4 < F4) st4(dst + 4 * f4, acc[v]);
+            acc[v] = I;
+          }
+          for (int64_t e = cur + 1; e < r; ++e)
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+              const int f4 = lane + v * L;
+              if (f4 < F4) st4(a.out + e * a.F + 4 * f4, I);
+            }
+          cur = r;
+          cont = false;
+        }
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[v] = red4<RED>(acc[v], val[u][v]);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  {
+    float* dst = cont ? a.carry + chunk * a.F : a.out + cur * a.F;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int f4 = lane + v * L;
+      if (f4 < F4) st4(dst + 4 * f4, acc[v]);
+    }
+  }
+  if (p1 == a.nnz) {  // trailing empty rows
+    for (int64_t r = cur + 1; r < a.num_rows; ++r)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int f4 = lane + v * L;
+        if (f4 < F4) st4(a.out + r * a.F + 4 * f4, I);
+      }
+  }
+  (void)indptr;
+}
+
+// Fold the carries of every row cut by chunk boundaries into its head, in
+// chunk order.  One group per chunk; only a row's first continuation chunk
+// does work.
+template <int RED, int L, int NV>
+__global__ void __launch_bounds__(kBlock) k_chunk_fixup(FastArgs a, const int32_t* __restrict__ indptr) {
+  constexpr int G = kBlock / L;
+  const int g = threadIdx.x / L;
+  const int lane = threadIdx.x % L;
+  const int64_t chunk = (int64_t)blockIdx.x * G + g;
+  const int64_t K = a.chunk;
+  const int64_t p0 = chunk * K;
+  if (chunk == 0 || p0 >= a.nnz) return;
+  const int64_t r = a.rows[p0];
+  const int64_t start = indptr[r];
+  if (start >= p0 || start < p0 - K) return;  // not a continuation / not the first one
+  const int64_t last = (indptr[r + 1] - 1) / K;
+  const int F4 = static_cast<int>(a.F / 4);
+  float4 acc[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int f4 = lane + v * L;
+    acc[v] = f4 < F4 ? ld4(a.out + r * a.F + 4 * f4) : ident4<RED>();
+  }
+  int64_t c = chunk;
+  for (; c + 3 <= last; c += 4) {
+    float4 t[4][NV];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int f4 = lane + v * L;
+        t[k][v] = f4 < F4 ? ld4(a.carry + (c + k) * a.F + 4 * f4) : ident4<RED>();
+      }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) acc[v] = red4<RED>(acc[v], t[k][v]);
+  }
+  for (; c <= last; ++c)
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int f4 = lane + v * L;
+      if (f4 < F4) acc[v] = red4<RED>(acc[v], ld4(a.carry + c * a.F + 4 * f4));
+    }
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int f4 = lane + v * L;
+    if (f4 < F4) st4(a.out + r * a.F + 4 * f4, acc[v]);
+  }
+}
+
+struct Cfg {
+  int L, NV;
+};
+Cfg pick(int64_t F) {
+  const int64_t F4 = F / 4;
+  if (F4 <= 4) return {4, 1};
+  if (F4 <= 8) return {8, 1};
+  if (F4 <= 16) return {16, 1};
+  if (F4 <= 32) return {32, 1};
+  if (F4 <= 64) return {64, 1};
+  if (F4 <= 128) return {64, 2};
+  return {64, 4};
+}
+
+template <int KIND, int RED, int L, int NV>
+void run(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
+  constexpr int G = kBlock / L;
+  const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
+  const unsigned blocks = static_cast<unsigned>((chunks + G - 1) / G);
+  hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV>), dim3(blocks), dim3(kBlock), 0, s, a,
+                     indptr);
+  if (chunks > 1)
+    hipLaunchKernelGGL((k_chunk_fixup<RED, L, NV>), dim3(blocks), dim3(kBlock), 0, s, a, indptr);
+}
+
+template <int KIND, int RED>
+void run_cfg(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
+  const Cfg c = pick(a.F);
+  switch (c.L * 10 + c.NV) {
+    case 41: run<KIND, RED, 4, 1>(a, indptr, s); break;
+    case 81: run<KIND, RED, 8, 1>(a, indptr, s); break;
+    case 161: run<KIND, RED, 16, 1>(a, indptr, s); break;
+    case 321: run<KIND, RED, 32, 1>(a, indptr, s); break;
+    case 641: run<KIND, RED, 64, 1>(a, indptr, s); break;
+    case 642: run<KIND, RED, 64, 2>(a, indptr, s); break;
+    default: run<KIND, RED, 64, 4>(a, indptr, s); break;
+  }
+}
+
+}  // namespace
+
+int64_t fast_chunk_edges(int64_t nnz, int64_t F) {
+  // Enough chunks to give every CU several groups; long chunks otherwise so
+  // that fewer rows are cut (each cut row costs one carry write + read).
+  int64_t k = 256;
+  const int64_t groups_wanted = 256 /*CUs*/ * 64;
+  while (k > 32 && nnz / k < groups_wanted) k >>= 1;
+  (void)F;
+  return k;
+}
+
+int64_t fast_workspace_bytes(int64_t nnz, int64_t F) {
+  if (nnz == 0) return 0;
+  const int64_t k = fast_chunk_edges(nnz, F);
+  return ((nnz + k - 1) / k) * F * static_cast<int64_t>(sizeof(float));
+}
+
+bool fast_supported(int kind, int64_t F, int64_t head_dim) {
+  if (F < 16 || F % 4 != 0 || F > 1024) return false;
+  if (kind == FAST_COL_MUL_EDGE_BCAST && (head_dim % 4 != 0 || F % head_dim != 0)) return false;
+  return true;
+}
+
+void launch_fast_reduce(int kind, int red, const FastArgs& a, hipStream_t s) {
+  const int32_t* indptr = a.indptr;
+  switch (kind) {
+    case FAST_COPY_COL:
+      if (red == RED_MAX) run_cfg<FAST_COPY_COL, RED_MAX>(a, indptr, s);
+      else if (red == RED_MIN) run_cfg<FAST_COPY_COL, RED_MIN>(a, indptr, s);
+      else run_cfg<FAST_COPY_COL, RED_SUM>(a, indptr, s);
+      break;
+    case FAST_COPY_EDGE:
+      if (red == RED_MAX) run_cfg<FAST_COPY_EDGE, RED_MAX>(a, indptr, s);
+      else if (red == RED_MIN) run_cfg<FAST_COPY_EDGE, RED_MIN>(a, indptr, s);
+      else run_cfg<FAST_COPY_EDGE, RED_SUM>(a, indptr, s);
+      break;
+    case FAST_COL_MUL_EDGE: run_cfg<FAST_COL_MUL_EDGE, RED_SUM>(a, indptr, s); break;
+    default: run_cfg<FAST_COL_MUL_EDGE_BCAST, RED_SUM>(a, indptr, s); break;
+  }
+}
+
+}  // namespace dglmi

@@ -1,0 +1,136 @@
+"""ctypes binding of libdglmi.so (the C ABI in include/dglmi.h).
+
+Mirrors the reference's FFI conventions (``python/dgl/_ffi/base.py``):
+the library is loaded once with ``RTLD_GLOBAL`` (:31-43, search path
+``DGL_LIBRARY_PATH`` like ``_ffi/libinfo.py:32-33``), and every call goes
+through :func:`check_call`, which raises :class:`DGLError` with the
+library's thread-local last error when a function returns non-zero
+(:50-62).  There is no fallback: if the HIP library is missing, importing
+the kernel layer fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+MAX_NDIM = 8
+
+
+class DGLError(Exception):
+    """Error raised by the engine (python/dgl/_ffi/base.py:24)."""
+
+
+class CSR(ctypes.Structure):
+    _fields_ = [
+        ("num_rows", ctypes.c_int64),
+        ("num_cols", ctypes.c_int64),
+        ("nnz", ctypes.c_int64),
+        ("indptr", ctypes.c_void_p),
+        ("indices", ctypes.c_void_p),
+        ("data", ctypes.c_void_p),
+        ("rows", ctypes.c_void_p),
+    ]
+
+
+class Graph(ctypes.Structure):
+    _fields_ = [
+        ("in_csr", CSR),
+        ("out_csr", CSR),
+        ("num_bits", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("workspace", ctypes.c_void_p),
+        ("workspace_bytes", ctypes.c_int64),
+    ]
+
+
+class Array(ctypes.Structure):
+    _fields_ = [
+        ("data", ctypes.c_void_p),
+        ("ndim", ctypes.c_int32),
+        ("shape", ctypes.c_int64 * (MAX_NDIM + 1)),
+    ]
+
+
+def _lib_path():
+    env = os.environ.get("DGL_LIBRARY_PATH")
+    cands = []
+    if env:
+        cands.append(os.path.join(env, "libdglmi.so"))
+    cands.append(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libdglmi.so"))
+    for c in cands:
+        if os.path.exists(c):
+            return c
+    raise DGLError(
+        "libdglmi.so not found (looked in %s). Build it with `make -C dgl-hack_amd` or "
+        "__graft_entry__.build(); the engine has no CPU fallback." % ", ".join(cands))
+
+
+_LIB = None
+
+_SIGS = {
+    "DGLMIGetLastError": (ctypes.c_char_p, []),
+    "DGLMIVersion": (ctypes.c_char_p, []),
+    "DGLMIKernelInferBinaryFeatureShape": (ctypes.c_int, [
+        ctypes.c_char_p, ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32)]),
+    "DGLMIKernelBinaryOpReduce": (ctypes.c_int, [
+        ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(Graph), ctypes.c_int32, ctypes.c_int32,
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "DGLMIKernelBackwardLhsBinaryOpReduce": (ctypes.c_int, [
+        ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(Graph), ctypes.c_int32, ctypes.c_int32,
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.c_void_p]),
+    "DGLMIKernelBackwardRhsBinaryOpReduce": (ctypes.c_int, [
+        ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(Graph), ctypes.c_int32, ctypes.c_int32,
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.c_void_p]),
+    "DGLMIKernelCopyReduce": (ctypes.c_int, [
+        ctypes.c_char_p, ctypes.POINTER(Graph), ctypes.c_int32, ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "DGLMIKernelBackwardCopyReduce": (ctypes.c_int, [
+        ctypes.c_char_p, ctypes.POINTER(Graph), ctypes.c_int32, ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "DGLMIKernelWorkspaceBytes": (ctypes.c_int64, [ctypes.POINTER(CSR), ctypes.c_int64]),
+    "DGLMICOOToCSR": (ctypes.c_int, [
+        ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "DGLMICSRTranspose": (ctypes.c_int, [
+        ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "DGLMICOOToCSRDeviceWorkspaceBytes": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int64]),
+    "DGLMICOOToCSRDevice": (ctypes.c_int, [
+        ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+        ctypes.c_void_p]),
+    "DGLMICSRExpandRows": (ctypes.c_int, [
+        ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+
+def lib():
+    """The loaded library (loaded on first use)."""
+    global _LIB
+    if _LIB is None:
+        L = ctypes.CDLL(_lib_path(), mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def last_error():
+    return lib().DGLMIGetLastError().decode()
+
+
+def check_call(ret):
+    """Raise DGLError if a C ABI call failed (python/dgl/_ffi/base.py:50-62)."""
+    if ret != 0:
+        raise DGLError(last_error())

@@ -1,0 +1,142 @@
+"""Backend operator layer: autograd Functions over the kernels.
+
+Mirrors the reference's operator contract ``F.binary_reduce`` /
+``F.copy_reduce`` (``python/dgl/backend/backend.py:1189-1225, 1276-1302``)
+and its PyTorch implementation (``backend/pytorch/tensor.py:291-381,
+519-601``):
+
+* the output is allocated by the operator (``new_empty``) and filled by the
+  kernel;
+* ``mean`` is ``sum`` divided by ``clamp(deg, 1)``, where the degree is a
+  second ``copy_reduce('sum')`` over ones (``tensor.py:308-325, 530-539``);
+* gradients of broadcast operands are summed over the broadcast dimensions
+  (``_reduce_grad``, ``tensor.py:572-601``);
+* mappings are ``(forward, backward)`` pairs; node maps are node-id
+  indexed, and in this engine edge maps are edge-id indexed (see
+  include/dglmi.h), so both entries of an edge pair are usually the same.
+"""
+from __future__ import annotations
+
+import torch as th
+
+from . import kernel as K
+
+SRC, DST, EDGE, NONE = 0, 1, 2, 3
+_NOMAP = (None, None)
+
+
+def _degs(reducer_target, graph, n, out_size, in_map, out_map, like):
+    ones = like.new_ones((n,))
+    degs = like.new_empty((out_size,))
+    K.copy_reduce("sum", graph, reducer_target, ones, degs, in_map, out_map)
+    return degs
+
+
+class BinaryReduce(th.autograd.Function):
+    @staticmethod
+    def forward(ctx, reducer, binary_op, graph, lhs, rhs, lhs_data, rhs_data, out_data,
+                out_size, lhs_map, rhs_map, out_map):
+        feat_shape = K.infer_binary_feature_shape(binary_op, lhs_data, rhs_data)
+        K.binary_op_reduce(reducer if reducer != "mean" else "sum", binary_op, graph, lhs, rhs,
+                           lhs_data, rhs_data, out_data, lhs_map[0], rhs_map[0], out_map[0])
+        if reducer == "mean":
+            if lhs != DST:
+                target, n, in_map = lhs, lhs_data.shape[0], lhs_map[0]
+            else:
+                target, n, in_map = rhs, rhs_data.shape[0], rhs_map[0]
+            degs = _degs(target, graph, n, out_data.shape[0], in_map, out_map[0], lhs_data)
+            degs = degs.reshape((out_data.shape[0],) + (1,) * (out_data.dim() - 1)).clamp(min=1)
+            out_data = out_data / degs
+        else:
+            degs = None
+        ctx.backward_cache = (reducer, binary_op, graph, lhs, rhs, lhs_map, rhs_map, out_map,
+                              feat_shape, degs)
+        ctx.save_for_backward(lhs_data, rhs_data, out_data)
+        return out_data
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        (reducer, binary_op, graph, lhs, rhs, lhs_map, rhs_map, out_map, feat_shape,
+         degs) = ctx.backward_cache
+        lhs_data, rhs_data, out_data = ctx.saved_tensors
+        grad_lhs = grad_rhs = None
+        if reducer == "mean":
+            grad_out = grad_out / degs
+        grad_out = grad_out.contiguous()
+        red = reducer if reducer != "mean" else "sum"
+        if ctx.needs_input_grad[5]:
+            grad_lhs = grad_out.new_empty((lhs_data.shape[0],) + tuple(feat_shape))
+            K.backward_lhs_binary_op_reduce(red, binary_op, graph, lhs, rhs, lhs_data, rhs_data,
+                                            out_data, grad_out, grad_lhs, lhs_map[1], rhs_map[1],
+                                            out_map[1])
+            grad_lhs = _reduce_grad(grad_lhs, lhs_data.shape)
+        if ctx.needs_input_grad[6]:
+            grad_rhs = grad_out.new_empty((rhs_data.shape[0],) + tuple(feat_shape))
+            K.backward_rhs_binary_op_reduce(red, binary_op, graph, lhs, rhs, lhs_data, rhs_data,
+                                            out_data, grad_out, grad_rhs, lhs_map[1], rhs_map[1],
+                                            out_map[1])
+            grad_rhs = _reduce_grad(grad_rhs, rhs_data.shape)
+        return None, None, None, None, None, grad_lhs, grad_rhs, None, None, None, None, None
+
+
+def binary_reduce(reducer, binary_op, graph, lhs, rhs, lhs_data, rhs_data, out_size,
+                  lhs_map=_NOMAP, rhs_map=_NOMAP, out_map=_NOMAP):
+    """backend.py:1189-1225 / tensor.py:368-381."""
+    lhs_data = lhs_data.contiguous()
+    rhs_data = rhs_data.contiguous()
+    feat_shape = K.infer_binary_feature_shape(binary_op, lhs_data, rhs_data)
+    out_shape = feat_shape[:-1] if binary_op == "dot" else feat_shape
+    out_data = lhs_data.new_empty((out_size,) + tuple(out_shape))
+    return BinaryReduce.apply(reducer, binary_op, graph, lhs, rhs, lhs_data, rhs_data, out_data,
+                              out_size, lhs_map, rhs_map, out_map)
+
+
+class CopyReduce(th.autograd.Function):
+    @staticmethod
+    def forward(ctx, reducer, graph, target, in_data, out_data, out_size, in_map, out_map):
+        K.copy_reduce(reducer if reducer != "mean" else "sum", graph, target, in_data, out_data,
+                      in_map[0], out_map[0])
+        if reducer == "mean":
+            degs = _degs(target, graph, in_data.shape[0], out_data.shape[0], in_map[0],
+                         out_map[0], in_data)
+            degs = degs.reshape((out_data.shape[0],) + (1,) * (out_data.dim() - 1)).clamp(min=1)
+            out_data = out_data / degs
+        else:
+            degs = None
+        ctx.backward_cache = (reducer, graph, target, in_map, out_map, degs)
+        ctx.save_for_backward(in_data, out_data)
+        return out_data
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        reducer, graph, target, in_map, out_map, degs = ctx.backward_cache
+        in_data, out_data = ctx.saved_tensors
+        grad_in = None
+        if reducer == "mean":
+            grad_out = grad_out / degs
+        grad_out = grad_out.contiguous()
+        if ctx.needs_input_grad[3]:
+            grad_in = grad_out.new_empty(in_data.shape)
+            K.backward_copy_reduce(reducer if reducer != "mean" else "sum", graph, target,
+                                   in_data, out_data, grad_out, grad_in, in_map[1], out_map[1])
+        return None, None, None, grad_in, None, None, None, None
+
+
+def copy_reduce(reducer, graph, target, in_data, out_size, in_map=_NOMAP, out_map=_NOMAP):
+    """backend.py:1276-1302 / tensor.py:566-569."""
+    in_data = in_data.contiguous()
+    out_data = in_data.new_empty((out_size,) + tuple(in_data.shape[1:]))
+    return CopyReduce.apply(reducer, graph, target, in_data, out_data, out_size, in_map, out_map)
+
+
+def _reduce_grad(grad, shape):
+    """tensor.py:572-601: sum the gradient over broadcast dimensions."""
+    grad_shape = grad.shape[1:]
+    in_shape = tuple(shape[1:])
+    if tuple(grad_shape) == in_shape:
+        return grad
+    num_to_squeeze = len(grad_shape) - len(in_shape)
+    in_shape = (1,) * num_to_squeeze + in_shape
+    reduce_idx = tuple(i + 1 for i, (a, b) in enumerate(zip(grad_shape, in_shape)) if a != b)
+    grad = grad.sum(dim=reduce_idx, keepdim=True)
+    return grad.view(shape)

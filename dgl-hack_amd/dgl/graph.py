@@ -1,0 +1,543 @@
+"""DGLGraph: the drop-in graph object for the g-SpMM / g-SDDMM path.
+
+A thin, reference-compatible subset of ``python/dgl/graph.py``: node / edge
+storage with ``ndata`` / ``edata`` (and the ``srcdata`` / ``dstdata``
+aliases of a homogeneous graph), ``local_var``, degree queries, and the
+message-passing entry points whose builtin forms lower to one kernel each:
+
+* ``update_all(msg, reduce)``        -> ``F.copy_reduce`` / ``F.binary_reduce``
+  (``graph.py:3221-3264``, ``runtime/scheduler.py:196-252, 905-917``);
+* ``pull(v, msg, reduce)`` / ``send_and_recv(edges, msg, reduce)`` -> the same
+  kernels on the in-edge subgraph (``scheduler.py:154-194, 254-332``);
+* ``apply_edges(msg)``              -> reducer ``"none"`` (``graph.py:2600``,
+  ``scheduler.py:334-375``).
+
+User-defined functions are accepted by ``apply_edges`` / ``apply_nodes``
+(plain tensor gathers).  A user-defined *reduce* (degree bucketing,
+``runtime/degree_bucketing.py``) is outside this engine's scope and raises
+:class:`DGLError` (see DESIGN.md "Scope").
+"""
+from __future__ import annotations
+
+from collections.abc import MutableMapping
+
+import numpy as np
+import torch as th
+
+from ._ffi import DGLError
+from .function.message import MessageFunction
+from .function.reducer import ReduceFunction
+from .graph_index import GraphIndex
+
+ALL = "__ALL__"
+
+
+def is_all(x):
+    return isinstance(x, str) and x == ALL
+
+
+def _to_index_array(x, name):
+    if isinstance(x, th.Tensor):
+        return x.detach().to("cpu", th.int64).numpy().reshape(-1)
+    return np.asarray(x, dtype=np.int64).reshape(-1)
+
+
+class Frame(MutableMapping):
+    """Columns of per-node or per-edge features (``python/dgl/frame.py``)."""
+
+    def __init__(self, num_rows_fn, data=None):
+        self._num_rows = num_rows_fn
+        self._cols = dict(data) if data else {}
+
+    def __getitem__(self, key):
+        return self._cols[key]
+
+    def __setitem__(self, key, val):
+        if not isinstance(val, th.Tensor):
+            raise DGLError("Feature %s must be a torch tensor" % key)
+        n = self._num_rows()
+        if val.dim() == 0 or val.shape[0] != n:
+            raise DGLError("Expected feature %s with first dimension %d, got shape %s"
+                           % (key, n, tuple(val.shape)))
+        self._cols[key] = val
+
+    def __delitem__(self, key):
+        del self._cols[key]
+
+    def __iter__(self):
+        return iter(self._cols)
+
+    def __len__(self):
+        return len(self._cols)
+
+    def __repr__(self):
+        return repr({k: tuple(v.shape) for k, v in self._cols.items()})
+
+    def clone(self):
+        return Frame(self._num_rows, self._cols)
+
+
+class EdgeBatch(object):
+    """Edges given to a message UDF (``python/dgl/udf.py:EdgeBatch``)."""
+
+    def __init__(self, src, dst, eid, src_data, dst_data, edge_data):
+        self._src, self._dst, self._eid = src, dst, eid
+        self.src = src_data
+        self.dst = dst_data
+        self.data = edge_data
+
+    def edges(self):
+        return self._src, self._dst, self._eid
+
+    def batch_size(self):
+        return int(self._eid.shape[0])
+
+    def __len__(self):
+        return self.batch_size()
+
+
+class NodeBatch(object):
+    """Nodes given to an apply UDF (``python/dgl/udf.py:NodeBatch``)."""
+
+    def __init__(self, nodes, data):
+        self._nodes = nodes
+        self.data = data
+
+    def nodes(self):
+        return self._nodes
+
+    def batch_size(self):
+        return int(self._nodes.shape[0])
+
+    def __len__(self):
+        return self.batch_size()
+
+
+class DGLGraph(object):
+    """Base graph class (``python/dgl/graph.py:DGLGraph``, homogeneous)."""
+
+    def __init__(self, graph_data=None, node_frame=None, edge_frame=None, multigraph=None,
+                 readonly=False):
+        self._graph = GraphIndex(0)
+        self._readonly = False
+        self._node_frame = Frame(self.number_of_nodes)
+        self._edge_frame = Frame(self.number_of_edges)
+        if graph_data is not None:
+            self._init_from(graph_data)
+        if node_frame is not None:
+            for k, v in node_frame.items():
+                self._node_frame[k] = v
+        if edge_frame is not None:
+            for k, v in edge_frame.items():
+                self._edge_frame[k] = v
+        self._readonly = bool(readonly)
+
+    def _init_from(self, data):
+        if isinstance(data, GraphIndex):
+            self._graph = data
+            return
+        if isinstance(data, DGLGraph):
+            src, dst, _ = data._graph.edges()
+            self._graph.add_nodes(data.number_of_nodes())
+            self._graph.add_edges(src, dst)
+            return
+        try:
+            import networkx as nx
+        except ImportError:  # pragma: no cover
+            nx = None
+        if nx is not None and isinstance(data, nx.Graph):
+            self.from_networkx(data)
+            return
+        try:
+            import scipy.sparse as sp
+            if sp.issparse(data):
+                self.from_scipy_sparse_matrix(data)
+                return
+        except ImportError:  # pragma: no cover
+            pass
+        if isinstance(data, (tuple, list)) and len(data) == 2:
+            src = _to_index_array(data[0], "src")
+            dst = _to_index_array(data[1], "dst")
+            n = int(max(src.max(initial=-1), dst.max(initial=-1)) + 1)
+            self._graph.add_nodes(n)
+            self._graph.add_edges(src, dst)
+            return
+        raise DGLError("Unsupported graph data type: %s" % type(data))
+
+    @classmethod
+    def from_device_coo(cls, src, dst, num_nodes):
+        """Read-only graph from device int32 (src, dst) tensors; CSRs built on the GPU."""
+        g = cls()
+        g._graph = GraphIndex.from_device_coo(src, dst, num_nodes)
+        g._readonly = True
+        return g
+
+    # ---- conversion (graph_index.py:1078-1135, :1138-1163) -------------------------
+    def from_networkx(self, nx_graph):
+        import networkx as nx
+        if not nx_graph.is_directed():
+            nx_graph = nx_graph.to_directed()
+        n = nx_graph.number_of_nodes()
+        m = nx_graph.number_of_edges()
+        has_id = m > 0 and "id" in next(iter(nx_graph.edges(data=True)))[-1]
+        if has_id:
+            src = np.zeros(m, np.int64)
+            dst = np.zeros(m, np.int64)
+            for u, v, attr in nx_graph.edges(data=True):
+                src[attr["id"]] = u
+                dst[attr["id"]] = v
+        else:
+            es = list(nx_graph.edges)
+            src = np.array([e[0] for e in es], np.int64)
+            dst = np.array([e[1] for e in es], np.int64)
+        self._graph.add_nodes(n)
+        self._graph.add_edges(src, dst)
+
+    def from_scipy_sparse_matrix(self, spmat):
+        coo = spmat.tocoo()
+        self._graph.add_nodes(coo.shape[0])
+        self._graph.add_edges(coo.row.astype(np.int64), coo.col.astype(np.int64))
+
+    # ---- mutation ---------------------------------------------------------------
+    def _check_mutable(self):
+        if self._readonly:
+            raise DGLError("Mutation is not allowed in read-only graph.")
+
+    def add_nodes(self, num, data=None):
+        self._check_mutable()
+        old = self.number_of_nodes()
+        self._graph.add_nodes(num)
+        self._extend_frame(self._node_frame, old, int(num), data)
+
+    def add_edge(self, u, v, data=None):
+        self.add_edges([u], [v], data)
+
+    def add_edges(self, u, v, data=None):
+        self._check_mutable()
+        old = self.number_of_edges()
+        self._graph.add_edges(_to_index_array(u, "u"), _to_index_array(v, "v"))
+        self._extend_frame(self._edge_frame, old, self.number_of_edges() - old, data)
+
+    @staticmethod
+    def _extend_frame(frame, old, num, data):
+        for k in list(frame._cols.keys()):
+            col = frame._cols[k]
+            if data is not None and k in data:
+                ext = data[k]
+            else:
+                ext = col.new_zeros((num,) + tuple(col.shape[1:]))
+            frame._cols[k] = th.cat([col, ext.to(col.device, col.dtype)], 0)
+        if data is not None:
+            for k, v in data.items():
+                if k not in frame._cols:
+                    if old != 0:
+                        raise DGLError("Cannot add new feature %s to a non-empty frame" % k)
+                    frame._cols[k] = v
+
+    # ---- queries ----------------------------------------------------------------
+    def number_of_nodes(self):
+        return self._graph.number_of_nodes()
+
+    def number_of_src_nodes(self):
+        return self.number_of_nodes()
+
+    def number_of_dst_nodes(self):
+        return self.number_of_nodes()
+
+    def number_of_edges(self):
+        return self._graph.number_of_edges()
+
+    def __len__(self):
+        return self.number_of_nodes()
+
+    @property
+    def is_multigraph(self):
+        return True
+
+    @property
+    def is_readonly(self):
+        return self._readonly
+
+    def nodes(self):
+        return th.arange(self.number_of_nodes(), dtype=th.int64)
+
+    def edges(self, form="uv", order=None):
+        src, dst, eid = self._graph.edges()
+        s, d, e = th.from_numpy(src.copy()), th.from_numpy(dst.copy()), th.from_numpy(eid.copy())
+        if form == "uv":
+            return s, d
+        if form == "eid":
+            return e
+        if form == "all":
+            return s, d, e
+        raise DGLError("Invalid form: %s" % form)
+
+    def all_edges(self, form="uv", order=None):
+        return self.edges(form, order)
+
+    def in_degrees(self, v=ALL):
+        d = th.from_numpy(self._graph.in_degrees())
+        return d if is_all(v) else d[th.as_tensor(_to_index_array(v, "v"))]
+
+    def out_degrees(self, v=ALL):
+        d = th.from_numpy(self._graph.out_degrees())
+        return d if is_all(v) else d[th.as_tensor(_to_index_array(v, "v"))]
+
+    def in_degree(self, v):
+        return int(self.in_degrees([v])[0])
+
+    def out_degree(self, v):
+        return int(self.out_degrees([v])[0])
+
+    def in_edges(self, v, form="uv"):
+        vs = _to_index_array(v, "v")
+        src, dst, eid = self._graph.edges()
+        mask = np.isin(dst, vs)
+        s, d, e = (th.from_numpy(a[mask].copy()) for a in (src, dst, eid))
+        return {"uv": (s, d), "eid": e, "all": (s, d, e)}[form]
+
+    def out_edges(self, u, form="uv"):
+        us = _to_index_array(u, "u")
+        src, dst, eid = self._graph.edges()
+        mask = np.isin(src, us)
+        s, d, e = (th.from_numpy(a[mask].copy()) for a in (src, dst, eid))
+        return {"uv": (s, d), "eid": e, "all": (s, d, e)}[form]
+
+    def adjacency_matrix_scipy(self, transpose=False, fmt="csr"):
+        import scipy.sparse as sp
+        src, dst, _ = self._graph.edges()
+        n = self.number_of_nodes()
+        r, c = (dst, src) if transpose else (src, dst)
+        m = sp.coo_matrix((np.ones(len(src), np.float32), (r, c)), shape=(n, n))
+        return m.asformat(fmt)
+
+    # ---- features ---------------------------------------------------------------
+    @property
+    def ndata(self):
+        return self._node_frame
+
+    @property
+    def edata(self):
+        return self._edge_frame
+
+    @property
+    def srcdata(self):
+        return self._node_frame
+
+    @property
+    def dstdata(self):
+        return self._node_frame
+
+    def local_var(self):
+        """Shallow copy whose feature writes do not leak out (graph.py:local_var)."""
+        g = DGLGraph.__new__(DGLGraph)
+        g._graph = self._graph
+        g._readonly = self._readonly
+        g._node_frame = Frame(g.number_of_nodes, self._node_frame._cols)
+        g._edge_frame = Frame(g.number_of_edges, self._edge_frame._cols)
+        return g
+
+    def local_scope(self):
+        import contextlib
+
+        @contextlib.contextmanager
+        def scope():
+            old_n, old_e = self._node_frame, self._edge_frame
+            self._node_frame = old_n.clone()
+            self._edge_frame = old_e.clone()
+            try:
+                yield
+            finally:
+                self._node_frame, self._edge_frame = old_n, old_e
+        return scope()
+
+    def to(self, device):
+        g = self.local_var()
+        for k, v in list(g._node_frame._cols.items()):
+            g._node_frame._cols[k] = v.to(device)
+        for k, v in list(g._edge_frame._cols.items()):
+            g._edge_frame._cols[k] = v.to(device)
+        return g
+
+    # ---- message passing ----------------------------------------------------------
+    def _device(self, *frames):
+        for fr in frames:
+            for v in fr.values():
+                return v.device
+        return th.device("cuda", th.cuda.current_device()) if th.cuda.is_available() else th.device("cpu")
+
+    def _gidx(self, device):
+        return self._graph.get_immutable_gidx(device)
+
+    @staticmethod
+    def _as_list(f):
+        if f is None:
+            return []
+        return list(f) if isinstance(f, (list, tuple)) else [f]
+
+    def _builtin_reduce(self, gidx, mfuncs, rfuncs, src_frame, edge_frame, out_size,
+                        edge_map=None):
+        fld2mfunc = {fn.out_field: fn for fn in mfuncs}
+        out = {}
+        for rfn in rfuncs:
+            if rfn.msg_field not in fld2mfunc:
+                raise DGLError('Reduce function requires message field "%s", but no message '
+                               'function generates it.' % rfn.msg_field)
+            mfn = fld2mfunc[rfn.msg_field]
+            out[rfn.out_field] = mfn._invoke(gidx, src_frame, src_frame, edge_frame, out_size,
+                                             None, None, edge_map, None, reducer=rfn.name)
+        return out
+
+    def _check_builtin(self, mfuncs, rfuncs):
+        for f in mfuncs:
+            if not isinstance(f, MessageFunction):
+                raise DGLError("update_all/pull/send_and_recv take builtin message functions "
+                               "(dgl.function.*); user-defined message functions are only "
+                               "supported by apply_edges on this engine")
+        for f in rfuncs:
+            if not isinstance(f, ReduceFunction):
+                raise DGLError("user-defined reduce functions (degree bucketing) are not "
+                               "supported by the MI355X engine; use dgl.function reducers")
+
+    def update_all(self, message_func, reduce_func, apply_node_func=None):
+        """Send messages along all edges and reduce them on every node."""
+        mfuncs, rfuncs = self._as_list(message_func), self._as_list(reduce_func)
+        self._check_builtin(mfuncs, rfuncs)
+        if self.number_of_nodes() == 0:
+            return
+        dev = self._device(self._node_frame, self._edge_frame)
+        gidx = self._gidx(dev)
+        res = self._builtin_reduce(gidx, mfuncs, rfuncs, self._node_frame, self._edge_frame,
+                                   self.number_of_nodes())
+        if apply_node_func is not None:
+            nb = NodeBatch(self.nodes().to(dev), dict(self._node_frame, **res))
+            res.update(apply_node_func(nb))
+        for k, v in res.items():
+            self._node_frame[k] = v
+
+    def _subgraph_index(self, src, dst, eid):
+        """Index over all nodes holding only the given edges; CSR data = parent eids."""
+        sub = GraphIndex(self.number_of_nodes())
+        sub.add_edges(src, dst)
+        sub._parent_eid = eid
+        return sub
+
+    def _partial_reduce(self, src, dst, eid, message_func, reduce_func, apply_node_func,
+                        recv_nodes):
+        mfuncs, rfuncs = self._as_list(message_func), self._as_list(reduce_func)
+        self._check_builtin(mfuncs, rfuncs)
+        dev = self._device(self._node_frame, self._edge_frame)
+        sub = _PartialIndex(self.number_of_nodes(), src, dst, eid)
+        gidx = sub.get_immutable_gidx(dev)
+        res = self._builtin_reduce(gidx, mfuncs, rfuncs, self._node_frame, self._edge_frame,
+                                   self.number_of_nodes())
+        v = th.as_tensor(np.unique(recv_nodes), device=dev)
+        if apply_node_func is not None:
+            nb = NodeBatch(v, {k: t[v] for k, t in res.items()})
+            for k, t in apply_node_func(nb).items():
+                res[k] = th.zeros((self.number_of_nodes(),) + tuple(t.shape[1:]), dtype=t.dtype,
+                                  device=dev).index_copy(0, v, t)
+        for k, t in res.items():
+            if k in self._node_frame:
+                base = self._node_frame[k]
+            else:
+                base = th.zeros_like(t)
+            self._node_frame[k] = base.index_copy(0, v, t[v])
+
+    def pull(self, v, message_func, reduce_func, apply_node_func=None):
+        """Pull messages from the in-edges of ``v`` and reduce them on ``v``."""
+        vs = _to_index_array(v, "v")
+        src, dst, eid = self._graph.edges()
+        mask = np.isin(dst, vs)
+        self._partial_reduce(src[mask], dst[mask], eid[mask], message_func, reduce_func,
+                             apply_node_func, vs)
+
+    def send_and_recv(self, edges, message_func, reduce_func, apply_node_func=None):
+        """Send messages along ``edges`` (eids or (u, v)) and reduce on their destinations."""
+        src, dst, eid = self._resolve_edges(edges)
+        self._partial_reduce(src, dst, eid, message_func, reduce_func, apply_node_func, dst)
+
+    def _resolve_edges(self, edges):
+        src, dst, eid = self._graph.edges()
+        if is_all(edges):
+            return src, dst, eid
+        if isinstance(edges, tuple) and len(edges) == 2:
+            u = _to_index_array(edges[0], "u")
+            v = _to_index_array(edges[1], "v")
+            lookup = {}
+            for i in range(len(src)):
+                lookup.setdefault((int(src[i]), int(dst[i])), []).append(i)
+            sel = []
+            for a, b in zip(u, v):
+                if (int(a), int(b)) not in lookup:
+                    raise DGLError("Edge (%d, %d) does not exist" % (a, b))
+                sel.extend(lookup[(int(a), int(b))])
+            sel = np.array(sel, np.int64)
+        else:
+            sel = _to_index_array(edges, "eid")
+        return src[sel], dst[sel], eid[sel]
+
+    def apply_edges(self, func, edges=ALL, inplace=False):
+        """Compute per-edge features with a builtin (reducer 'none') or a UDF."""
+        src, dst, eid = self._resolve_edges(edges)
+        dev = self._device(self._node_frame, self._edge_frame)
+        if isinstance(func, MessageFunction):
+            m = self.number_of_edges()
+            if is_all(edges):
+                gidx = self._gidx(dev)
+                res = func._invoke(gidx, self._node_frame, self._node_frame, self._edge_frame, m,
+                                   reducer="none")
+            else:
+                sub = _PartialIndex(self.number_of_nodes(), src, dst, eid)
+                gidx = sub.get_immutable_gidx(dev)
+                res = func._invoke(gidx, self._node_frame, self._node_frame, self._edge_frame, m,
+                                   reducer="none")
+                sel = th.as_tensor(eid, device=dev)
+                base = self._edge_frame[func.out_field] if func.out_field in self._edge_frame \
+                    else th.zeros_like(res)
+                res = base.index_copy(0, sel, res[sel])
+            self._edge_frame[func.out_field] = res
+            return
+        s = th.as_tensor(src, device=dev)
+        d = th.as_tensor(dst, device=dev)
+        e = th.as_tensor(eid, device=dev)
+        eb = EdgeBatch(s, d, e, {k: v[s] for k, v in self._node_frame.items()},
+                       {k: v[d] for k, v in self._node_frame.items()},
+                       {k: v[e] for k, v in self._edge_frame.items()})
+        out = func(eb)
+        for k, v in out.items():
+            if is_all(edges):
+                self._edge_frame[k] = v
+            else:
+                base = self._edge_frame[k] if k in self._edge_frame else \
+                    v.new_zeros((self.number_of_edges(),) + tuple(v.shape[1:]))
+                self._edge_frame[k] = base.index_copy(0, e, v)
+
+    def apply_nodes(self, func, v=ALL, inplace=False):
+        dev = self._device(self._node_frame)
+        nodes = self.nodes().to(dev) if is_all(v) else th.as_tensor(_to_index_array(v, "v"), device=dev)
+        nb = NodeBatch(nodes, {k: t[nodes] for k, t in self._node_frame.items()})
+        for k, t in func(nb).items():
+            if is_all(v):
+                self._node_frame[k] = t
+            else:
+                base = self._node_frame[k] if k in self._node_frame else \
+                    t.new_zeros((self.number_of_nodes(),) + tuple(t.shape[1:]))
+                self._node_frame[k] = base.index_copy(0, nodes, t)
+
+
+class _PartialIndex(GraphIndex):
+    """In-edge subgraph over all nodes whose CSR ``data`` holds the parent edge ids,
+    so edge features of the parent graph are addressed directly (the reference uses
+    relabel maps for the same purpose, spmv.py:146-180)."""
+
+    def __init__(self, n, src, dst, parent_eid):
+        super().__init__(n)
+        self.add_edges(src, dst)
+        self._parent = np.asarray(parent_eid, np.int64)
+
+    def host_csr(self):
+        if self._host_csr is None:
+            (op, oi, od), (ip, ii, idd) = super().host_csr()
+            self._host_csr = ((op, oi, self._parent[od]), (ip, ii, self._parent[idd]))
+        return self._host_csr

@@ -1,0 +1,282 @@
+"""Graph index: edge storage plus the per-device CSR pair the kernels walk.
+
+Restates the provisioning rules of the reference (``python/dgl/graph_index.py``
+and ``src/graph/{graph,immutable_graph}.cc``):
+
+* a mutable graph stores edges in insertion (edge-id) order;
+* its out-CSR is the adjacency list in edge-id order (``graph.cc:600-660``),
+  i.e. ``COOToCSR(src, dst)`` (a stable counting sort);
+* its in-CSR is ``CSRTranspose(out-CSR)`` (``immutable_graph.cc:407-436``),
+  so every destination row lists (src asc, eid asc);
+* the immutable index is built lazily and cached per device
+  (``graph_index.py:671-686``); any mutation drops the cache.
+
+MI355X specifics: device CSRs are int32 (the reference GPU path is int32
+only, ``kernel/common.h:62-69``) and carry the row id of every position
+(``rows``), which the edge-wise and load-balanced kernels read.  Large
+graphs can be built directly on the GPU (:meth:`GraphIndex.from_device_coo`):
+two stable radix sorts give arrays bit-identical to the host path.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch as th
+
+from . import _ffi
+from ._ffi import DGLError
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class DeviceCSR:
+    """One direction of the adjacency on a device (int32 arrays)."""
+
+    def __init__(self, indptr, indices, data, rows, num_cols):
+        self.indptr = indptr
+        self.indices = indices
+        self.data = data
+        self.rows = rows
+        self.num_rows = int(indptr.shape[0]) - 1
+        self.num_cols = int(num_cols)
+        self.nnz = int(indices.shape[0])
+
+    def cstruct(self):
+        c = _ffi.CSR()
+        c.num_rows = self.num_rows
+        c.num_cols = self.num_cols
+        c.nnz = self.nnz
+        c.indptr = self.indptr.data_ptr()
+        c.indices = self.indices.data_ptr() if self.nnz else None
+        c.data = self.data.data_ptr() if self.nnz else None
+        c.rows = self.rows.data_ptr() if self.nnz else None
+        return c
+
+    def degrees(self):
+        return self.indptr[1:] - self.indptr[:-1]
+
+
+class ImmutableGraphIndex:
+    """The kernels' view of a graph on one device: in-CSR + out-CSR."""
+
+    def __init__(self, in_csr, out_csr, num_src, num_dst, device):
+        self.in_csr = in_csr
+        self.out_csr = out_csr
+        self.num_src = num_src
+        self.num_dst = num_dst
+        self.device = device
+
+    def number_of_edges(self):
+        return self.in_csr.nnz
+
+    def cstruct(self, workspace=None):
+        g = _ffi.Graph()
+        g.in_csr = self.in_csr.cstruct()
+        g.out_csr = self.out_csr.cstruct()
+        g.num_bits = 32
+        g.device = self.device.index if self.device.index is not None else th.cuda.current_device()
+        if workspace is not None:
+            g.workspace = workspace.data_ptr()
+            g.workspace_bytes = workspace.numel() * workspace.element_size()
+        else:
+            g.workspace = None
+            g.workspace_bytes = 0
+        return g
+
+    def workspace_bytes(self, feat_len):
+        L = _ffi.lib()
+        a = L.DGLMIKernelWorkspaceBytes(ctypes.byref(self.in_csr.cstruct()), int(feat_len))
+        b = L.DGLMIKernelWorkspaceBytes(ctypes.byref(self.out_csr.cstruct()), int(feat_len))
+        return max(a, b)
+
+
+def host_coo_to_csr(num_rows, row, col, data=None):
+    """aten::COOToCSR through the C ABI (int64 host arrays)."""
+    row = np.ascontiguousarray(row, dtype=np.int64)
+    col = np.ascontiguousarray(col, dtype=np.int64)
+    data = None if data is None else np.ascontiguousarray(data, dtype=np.int64)
+    nnz = row.shape[0]
+    indptr = np.empty(num_rows + 1, np.int64)
+    indices = np.empty(nnz, np.int64)
+    out = np.empty(nnz, np.int64)
+    _p = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+    rc = _ffi.lib().DGLMICOOToCSR(num_rows, nnz, _p(row), _p(col), _p(data), _p(indptr),
+                                  _p(indices), _p(out))
+    if rc != 0:
+        raise DGLError("COOToCSR: row id out of range")
+    return indptr, indices, out
+
+
+def host_csr_transpose(num_rows, num_cols, indptr, indices, data=None):
+    """aten::CSRTranspose through the C ABI (int64 host arrays)."""
+    indptr = np.ascontiguousarray(indptr, dtype=np.int64)
+    indices = np.ascontiguousarray(indices, dtype=np.int64)
+    data = None if data is None else np.ascontiguousarray(data, dtype=np.int64)
+    nnz = indices.shape[0]
+    bp = np.empty(num_cols + 1, np.int64)
+    bi = np.empty(nnz, np.int64)
+    bx = np.empty(nnz, np.int64)
+    _p = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+    rc = _ffi.lib().DGLMICSRTranspose(num_rows, num_cols, _p(indptr), _p(indices), _p(data),
+                                      _p(bp), _p(bi), _p(bx))
+    if rc != 0:
+        raise DGLError("CSRTranspose: column id out of range")
+    return bp, bi, bx
+
+
+def _stream_ptr(device):
+    return ctypes.c_void_p(th.cuda.current_stream(device).cuda_stream)
+
+
+def device_coo_to_csr(num_rows, row, col, data=None):
+    """COO -> CSR on the GPU (int32 tensors), bit-identical to host_coo_to_csr."""
+    dev = row.device
+    nnz = int(row.shape[0])
+    L = _ffi.lib()
+    indptr = th.empty(num_rows + 1, dtype=th.int32, device=dev)
+    indices = th.empty(nnz, dtype=th.int32, device=dev)
+    out = th.empty(nnz, dtype=th.int32, device=dev)
+    ws = th.empty(int(L.DGLMICOOToCSRDeviceWorkspaceBytes(num_rows, nnz)), dtype=th.uint8, device=dev)
+    rc = L.DGLMICOOToCSRDevice(num_rows, nnz, _ptr(row), _ptr(col), _ptr(data), _ptr(indptr),
+                               _ptr(indices), _ptr(out), _ptr(ws), ws.numel(), _stream_ptr(dev))
+    if rc != 0:
+        raise DGLError("device COOToCSR failed")
+    return indptr, indices, out
+
+
+def device_expand_rows(indptr, nnz):
+    rows = th.empty(nnz, dtype=th.int32, device=indptr.device)
+    if nnz:
+        rc = _ffi.lib().DGLMICSRExpandRows(_ptr(indptr), indptr.shape[0] - 1, nnz, _ptr(rows),
+                                           _stream_ptr(indptr.device))
+        if rc != 0:
+            raise DGLError("CSR row expansion failed")
+    return rows
+
+
+class GraphIndex:
+    """Mutable multigraph index (``python/dgl/graph_index.py:GraphIndex``)."""
+
+    def __init__(self, num_nodes=0):
+        self._n = int(num_nodes)
+        self._src = np.empty(0, np.int64)
+        self._dst = np.empty(0, np.int64)
+        self._cache = {}
+        self._host_csr = None
+        self._device_only = None  # (src, dst) device tensors when built on the GPU
+
+    # ---- construction -----------------------------------------------------
+    @classmethod
+    def from_device_coo(cls, src, dst, num_nodes):
+        """Build directly from device int32 (src, dst) tensors (no host copy)."""
+        g = cls(num_nodes)
+        g._device_only = (src, dst)
+        g._m = int(src.shape[0])
+        return g
+
+    def _invalidate(self):
+        self._cache = {}
+        self._host_csr = None
+
+    def add_nodes(self, num):
+        if self._device_only is not None:
+            raise DGLError("graph built on device is immutable")
+        self._n += int(num)
+        self._invalidate()
+
+    def add_edges(self, u, v):
+        if self._device_only is not None:
+            raise DGLError("graph built on device is immutable")
+        u = np.atleast_1d(np.asarray(u, dtype=np.int64))
+        v = np.atleast_1d(np.asarray(v, dtype=np.int64))
+        if u.shape[0] == 1 and v.shape[0] > 1:
+            u = np.full(v.shape, u[0], np.int64)
+        if v.shape[0] == 1 and u.shape[0] > 1:
+            v = np.full(u.shape, v[0], np.int64)
+        if u.shape != v.shape:
+            raise DGLError("Invalid src/dst lengths: %d vs %d" % (u.shape[0], v.shape[0]))
+        if u.size and (u.min() < 0 or v.min() < 0 or u.max() >= self._n or v.max() >= self._n):
+            raise DGLError("Invalid node id in add_edges (graph has %d nodes)" % self._n)
+        self._src = np.concatenate([self._src, u])
+        self._dst = np.concatenate([self._dst, v])
+        self._invalidate()
+
+    # ---- queries ----------------------------------------------------------
+    def number_of_nodes(self):
+        return self._n
+
+    def number_of_edges(self):
+        if self._device_only is not None:
+            return self._m
+        return int(self._src.shape[0])
+
+    def bits_needed(self):
+        # graph_index.py:941-952
+        return 32 if max(self._n, self.number_of_edges()) < 0x7FFFFFFF else 64
+
+    def edges(self):
+        """(src, dst, eid) in edge-id order (numpy int64)."""
+        if self._device_only is not None:
+            s, d = self._device_only
+            return (s.long().cpu().numpy(), d.long().cpu().numpy(), np.arange(self._m))
+        return self._src, self._dst, np.arange(self._src.shape[0], dtype=np.int64)
+
+    def in_degrees(self):
+        return np.bincount(self.edges()[1], minlength=self._n).astype(np.int64)
+
+    def out_degrees(self):
+        return np.bincount(self.edges()[0], minlength=self._n).astype(np.int64)
+
+    def host_csr(self):
+        """(out-CSR, in-CSR) host arrays, int64, bit-exact with the reference."""
+        if self._host_csr is None:
+            src, dst, _ = self.edges()
+            out_csr = host_coo_to_csr(self._n, src, dst)
+            in_csr = host_csr_transpose(self._n, self._n, *out_csr)
+            self._host_csr = (out_csr, in_csr)
+        return self._host_csr
+
+    def get_immutable_gidx(self, device):
+        """The per-device CSR pair, built once and cached (graph_index.py:671-686)."""
+        device = th.device(device)
+        if device.type != "cuda":
+            raise DGLError("the MI355X engine runs on ROCm devices only; got device %s" % device)
+        if device.index is None:
+            device = th.device("cuda", th.cuda.current_device())
+        key = str(device)
+        if key not in self._cache:
+            if self.bits_needed() != 32:
+                raise DGLError("Unsupported idx bits: 64 (graphs need < 2^31 nodes and edges)")
+            if self._device_only is not None:
+                self._cache[key] = self._build_on_device(device)
+            else:
+                self._cache[key] = self._upload(device)
+        return self._cache[key]
+
+    def _upload(self, device):
+        (op, oi, od), (ip, ii, idd) = self.host_csr()
+        n = self._n
+
+        def mk(indptr, indices, data):
+            rows = np.repeat(np.arange(n, dtype=np.int32), np.diff(indptr).astype(np.int64))
+            t = lambda a: th.from_numpy(np.ascontiguousarray(a, dtype=np.int32)).to(device)
+            return DeviceCSR(t(indptr), t(indices), t(data), t(rows), n)
+
+        return ImmutableGraphIndex(mk(ip, ii, idd), mk(op, oi, od), n, n, device)
+
+    def _build_on_device(self, device):
+        src, dst = self._device_only
+        src = src.to(device=device, dtype=th.int32).contiguous()
+        dst = dst.to(device=device, dtype=th.int32).contiguous()
+        n = self._n
+        # out-CSR: stable sort of the eid-ordered COO by src
+        o_ptr, o_idx, o_dat = device_coo_to_csr(n, src, dst)
+        o_rows = device_expand_rows(o_ptr, self._m)
+        # in-CSR: stable sort of the out-CSR sequence by dst == CSRTranspose(out-CSR)
+        i_ptr, i_idx, i_dat = device_coo_to_csr(n, o_idx, o_rows, o_dat)
+        i_rows = device_expand_rows(i_ptr, self._m)
+        return ImmutableGraphIndex(DeviceCSR(i_ptr, i_idx, i_dat, i_rows, n),
+                                   DeviceCSR(o_ptr, o_idx, o_dat, o_rows, n), n, n, device)

@@ -1,0 +1,172 @@
+"""Kernel wrappers over the C ABI (mirrors ``python/dgl/kernel.py``).
+
+Every function takes the per-device graph index (``ImmutableGraphIndex``),
+torch tensors on that device and optional int32 mapping tensors, and runs on
+torch's current HIP stream.  The output / gradient buffers are caller-owned
+and overwritten completely, exactly like the reference's
+``K.binary_op_reduce`` family (``kernel.py:29-436``).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch as th
+
+from . import _ffi
+from ._ffi import DGLError, check_call
+
+_TARGET = {"src": 0, "dst": 1, "edge": 2, "none": 3}
+
+
+def _arr(t, name):
+    if t is None:
+        return None
+    if not isinstance(t, th.Tensor):
+        raise DGLError("%s must be a torch tensor" % name)
+    if t.device.type != "cuda":
+        raise DGLError("%s is on %s: the MI355X engine runs on ROCm devices only" % (name, t.device))
+    if t.dtype != th.float32:
+        raise DGLError("Unsupported dtype: %s for %s (float32 only, kernel/common.h:49-55)" % (t.dtype, name))
+    if not t.is_contiguous():
+        raise DGLError("%s must be contiguous" % name)
+    if t.dim() > _ffi.MAX_NDIM + 1:
+        raise DGLError("%s has too many dimensions" % name)
+    a = _ffi.Array()
+    a.data = t.data_ptr() if t.numel() else None
+    a.ndim = t.dim() if t.dim() > 0 else 1
+    shape = list(t.shape) if t.dim() > 0 else [1]
+    for i, s in enumerate(shape):
+        a.shape[i] = s
+    a._keep = t
+    return ctypes.byref(a)
+
+
+def _map(m, name):
+    if m is None:
+        return None
+    if not isinstance(m, th.Tensor) or m.dtype != th.int32 or m.device.type != "cuda":
+        raise DGLError("Expected 32 integer array on the graph device for %s" % name)
+    return ctypes.c_void_p(m.contiguous().data_ptr())
+
+
+def _stream(t):
+    return ctypes.c_void_p(th.cuda.current_stream(t.device).cuda_stream)
+
+
+def _check_ctx(graph, tensors):
+    for name, t in tensors:
+        if t is not None and t.device != graph.device:
+            raise DGLError("Expected device context %s. But got %s for %s." % (graph.device, t.device, name))
+
+
+def _workspace(graph, feat_len, device):
+    nbytes = graph.workspace_bytes(feat_len)
+    if nbytes <= 0:
+        return None
+    return th.empty(int(nbytes), dtype=th.uint8, device=device)
+
+
+def _feat_len(t):
+    n = 1
+    for s in t.shape[1:]:
+        n *= s
+    return n
+
+
+def infer_binary_feature_shape(op, lhs, rhs):
+    """kernel.py:8-26 / binary_reduce.cc:281-293 (host-only shape logic)."""
+    def mk(t):
+        a = _ffi.Array()
+        a.data = None
+        shape = list(t.shape)
+        a.ndim = len(shape)
+        for i, s in enumerate(shape):
+            a.shape[i] = s
+        return a
+    la, ra = mk(lhs), mk(rhs)
+    out = (ctypes.c_int64 * (_ffi.MAX_NDIM + 1))()
+    nd = ctypes.c_int32(0)
+    check_call(_ffi.lib().DGLMIKernelInferBinaryFeatureShape(
+        op.encode(), ctypes.byref(la), ctypes.byref(ra), out, ctypes.byref(nd)))
+    return tuple(out[i] for i in range(nd.value))
+
+
+def binary_op_reduce(reducer, op, graph, lhs, rhs, lhs_data, rhs_data, out_data,
+                     lhs_map=None, rhs_map=None, out_map=None):
+    """kernel.py:29-148 -> _CAPI_DGLKernelBinaryOpReduce."""
+    _check_ctx(graph, [("lhs_data", lhs_data), ("rhs_data", rhs_data), ("out_data", out_data)])
+    ws = _workspace(graph, _feat_len(out_data), out_data.device)
+    g = graph.cstruct(ws)
+    check_call(_ffi.lib().DGLMIKernelBinaryOpReduce(
+        reducer.encode(), op.encode(), ctypes.byref(g), _TARGET_CODE(lhs), _TARGET_CODE(rhs),
+        _arr(lhs_data, "lhs_data"), _arr(rhs_data, "rhs_data"), _arr(out_data, "out_data"),
+        _map(lhs_map, "lhs_mapping"), _map(rhs_map, "rhs_mapping"), _map(out_map, "out_mapping"),
+        _stream(out_data)))
+    return out_data
+
+
+def backward_lhs_binary_op_reduce(reducer, op, graph, lhs, rhs, lhs_data, rhs_data, out_data,
+                                  grad_out_data, grad_lhs_data, lhs_map=None, rhs_map=None,
+                                  out_map=None):
+    """kernel.py:151-229 -> _CAPI_DGLKernelBackwardLhsBinaryOpReduce."""
+    _check_ctx(graph, [("lhs_data", lhs_data), ("rhs_data", rhs_data), ("out_data", out_data),
+                       ("grad_out_data", grad_out_data), ("grad_lhs_data", grad_lhs_data)])
+    ws = _workspace(graph, _feat_len(grad_lhs_data), grad_lhs_data.device)
+    g = graph.cstruct(ws)
+    check_call(_ffi.lib().DGLMIKernelBackwardLhsBinaryOpReduce(
+        reducer.encode(), op.encode(), ctypes.byref(g), _TARGET_CODE(lhs), _TARGET_CODE(rhs),
+        _map(lhs_map, "lhs_mapping"), _map(rhs_map, "rhs_mapping"), _map(out_map, "out_mapping"),
+        _arr(lhs_data, "lhs_data"), _arr(rhs_data, "rhs_data"), _arr(out_data, "out_data"),
+        _arr(grad_out_data, "grad_out_data"), _arr(grad_lhs_data, "grad_lhs_data"),
+        _stream(grad_lhs_data)))
+    return grad_lhs_data
+
+
+def backward_rhs_binary_op_reduce(reducer, op, graph, lhs, rhs, lhs_data, rhs_data, out_data,
+                                  grad_out_data, grad_rhs_data, lhs_map=None, rhs_map=None,
+                                  out_map=None):
+    """kernel.py:232-299 -> _CAPI_DGLKernelBackwardRhsBinaryOpReduce."""
+    _check_ctx(graph, [("lhs_data", lhs_data), ("rhs_data", rhs_data), ("out_data", out_data),
+                       ("grad_out_data", grad_out_data), ("grad_rhs_data", grad_rhs_data)])
+    ws = _workspace(graph, _feat_len(grad_rhs_data), grad_rhs_data.device)
+    g = graph.cstruct(ws)
+    check_call(_ffi.lib().DGLMIKernelBackwardRhsBinaryOpReduce(
+        reducer.encode(), op.encode(), ctypes.byref(g), _TARGET_CODE(lhs), _TARGET_CODE(rhs),
+        _map(lhs_map, "lhs_mapping"), _map(rhs_map, "rhs_mapping"), _map(out_map, "out_mapping"),
+        _arr(lhs_data, "lhs_data"), _arr(rhs_data, "rhs_data"), _arr(out_data, "out_data"),
+        _arr(grad_out_data, "grad_out_data"), _arr(grad_rhs_data, "grad_rhs_data"),
+        _stream(grad_rhs_data)))
+    return grad_rhs_data
+
+
+def copy_reduce(reducer, graph, target, in_data, out_data, in_map=None, out_map=None):
+    """kernel.py:302-393 -> _CAPI_DGLKernelCopyReduce."""
+    _check_ctx(graph, [("in_data", in_data), ("out_data", out_data)])
+    ws = _workspace(graph, _feat_len(out_data), out_data.device)
+    g = graph.cstruct(ws)
+    check_call(_ffi.lib().DGLMIKernelCopyReduce(
+        reducer.encode(), ctypes.byref(g), _TARGET_CODE(target), _arr(in_data, "in_data"),
+        _arr(out_data, "out_data"), _map(in_map, "in_mapping"), _map(out_map, "out_mapping"),
+        _stream(out_data)))
+    return out_data
+
+
+def backward_copy_reduce(reducer, graph, target, in_data, out_data, grad_out_data, grad_in_data,
+                         in_map=None, out_map=None):
+    """kernel.py:396-436 -> _CAPI_DGLKernelBackwardCopyReduce."""
+    _check_ctx(graph, [("in_data", in_data), ("out_data", out_data),
+                       ("grad_out_data", grad_out_data), ("grad_in_data", grad_in_data)])
+    ws = _workspace(graph, _feat_len(grad_in_data), grad_in_data.device)
+    g = graph.cstruct(ws)
+    check_call(_ffi.lib().DGLMIKernelBackwardCopyReduce(
+        reducer.encode(), ctypes.byref(g), _TARGET_CODE(target), _arr(in_data, "in_data"),
+        _arr(out_data, "out_data"), _arr(grad_out_data, "grad_out_data"),
+        _arr(grad_in_data, "grad_in_data"), _map(in_map, "in_mapping"),
+        _map(out_map, "out_mapping"), _stream(grad_in_data)))
+    return grad_in_data
+
+
+def _TARGET_CODE(t):
+    if isinstance(t, str):
+        return _TARGET[t]
+    return int(t)

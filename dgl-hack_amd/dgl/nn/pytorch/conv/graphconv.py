@@ -1,0 +1,85 @@
+"""GraphConv (``python/dgl/nn/pytorch/conv/graphconv.py:11-188``).
+
+Same parameters, initialisation and computation order as the reference:
+``norm`` in {'none','both','right'}; the dense projection (a torch GEMM on
+MFMA through hipBLASLt) goes before the aggregation when in_feats >
+out_feats, after it otherwise; the aggregation is one ``copy_u_sum`` on the
+load-balanced HIP kernel.
+"""
+import torch as th
+from torch import nn
+from torch.nn import init
+
+from .... import function as fn
+from ...._ffi import DGLError
+
+
+class GraphConv(nn.Module):
+    def __init__(self, in_feats, out_feats, norm="both", weight=True, bias=True,
+                 activation=None):
+        super(GraphConv, self).__init__()
+        if norm not in ("none", "both", "right"):
+            raise DGLError('Invalid norm value. Must be either "none", "both" or "right".'
+                           ' But got "{}".'.format(norm))
+        self._in_feats = in_feats
+        self._out_feats = out_feats
+        self._norm = norm
+        if weight:
+            self.weight = nn.Parameter(th.Tensor(in_feats, out_feats))
+        else:
+            self.register_parameter("weight", None)
+        if bias:
+            self.bias = nn.Parameter(th.Tensor(out_feats))
+        else:
+            self.register_parameter("bias", None)
+        self.reset_parameters()
+        self._activation = activation
+
+    def reset_parameters(self):
+        if self.weight is not None:
+            init.xavier_uniform_(self.weight)
+        if self.bias is not None:
+            init.zeros_(self.bias)
+
+    def forward(self, graph, feat, weight=None):
+        graph = graph.local_var()
+        if self._norm == "both":
+            degs = graph.out_degrees().to(feat.device).float().clamp(min=1)
+            norm = th.pow(degs, -0.5)
+            norm = th.reshape(norm, norm.shape + (1,) * (feat.dim() - 1))
+            feat = feat * norm
+        if weight is not None:
+            if self.weight is not None:
+                raise DGLError("External weight is provided while at the same time the"
+                               " module has defined its own weight parameter. Please"
+                               " create the module with flag weight=False.")
+        else:
+            weight = self.weight
+        if self._in_feats > self._out_feats:
+            if weight is not None:
+                feat = th.matmul(feat, weight)
+            graph.srcdata["h"] = feat
+            graph.update_all(fn.copy_src(src="h", out="m"), fn.sum(msg="m", out="h"))
+            rst = graph.dstdata["h"]
+        else:
+            graph.srcdata["h"] = feat
+            graph.update_all(fn.copy_src(src="h", out="m"), fn.sum(msg="m", out="h"))
+            rst = graph.dstdata["h"]
+            if weight is not None:
+                rst = th.matmul(rst, weight)
+        if self._norm != "none":
+            degs = graph.in_degrees().to(feat.device).float().clamp(min=1)
+            norm = th.pow(degs, -0.5) if self._norm == "both" else 1.0 / degs
+            norm = th.reshape(norm, norm.shape + (1,) * (feat.dim() - 1))
+            rst = rst * norm
+        if self.bias is not None:
+            rst = rst + self.bias
+        if self._activation is not None:
+            rst = self._activation(rst)
+        return rst
+
+    def extra_repr(self):
+        summary = "in={_in_feats}, out={_out_feats}, normalization={_norm}"
+        if "_activation" in self.__dict__:
+            summary += ", activation={_activation}"
+        return summary.format(**self.__dict__)

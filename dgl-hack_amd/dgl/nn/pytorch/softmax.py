@@ -1,0 +1,62 @@
+"""Edge softmax (``python/dgl/nn/pytorch/softmax.py:15-193``).
+
+Same decomposition as the reference: per destination the max of the incoming
+logits is subtracted before ``exp`` (``copy_e`` max, ``e_sub_v``), the sum of
+the exponentials divides them (``copy_e`` sum, ``e_div_v``), and the
+backward is ``grad_s - out * sum_dst(out * grad_out)``
+(``softmax.py:86-114``).  Each step is one g-SpMM / g-SDDMM kernel call.
+"""
+import torch as th
+
+from ... import backend as F
+from ...function import TargetCode
+from ...graph import ALL, is_all, _PartialIndex
+
+__all__ = ["edge_softmax"]
+
+
+class EdgeSoftmax(th.autograd.Function):
+    @staticmethod
+    def forward(ctx, gidx, score, n_nodes):
+        n_edges = score.shape[0]
+        score = score.contiguous()
+        smax = F.copy_reduce("max", gidx, TargetCode.EDGE, score, n_nodes)
+        out = F.binary_reduce("none", "sub", gidx, TargetCode.EDGE, TargetCode.DST, score, smax,
+                              n_edges)
+        out = th.exp(out)
+        out_sum = F.copy_reduce("sum", gidx, TargetCode.EDGE, out, n_nodes)
+        out = F.binary_reduce("none", "div", gidx, TargetCode.EDGE, TargetCode.DST, out, out_sum,
+                              n_edges)
+        ctx.backward_cache = (n_nodes, n_edges, gidx)
+        ctx.save_for_backward(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        n_nodes, n_edges, gidx = ctx.backward_cache
+        out, = ctx.saved_tensors
+        grad_s = (out * grad_out).contiguous()
+        accum = F.copy_reduce("sum", gidx, TargetCode.EDGE, grad_s, n_nodes)
+        out = F.binary_reduce("none", "mul", gidx, TargetCode.EDGE, TargetCode.DST, out, accum,
+                              n_edges)
+        return None, grad_s - out, None
+
+
+def edge_softmax(graph, logits, eids=ALL):
+    """Softmax over the incoming edges of every node.
+
+    ``logits`` has shape (E, *, 1) (or (E,)); with ``eids`` given, only those
+    edges take part and the result has their rows (``softmax.py:117-193``).
+    """
+    if is_all(eids):
+        gidx = graph._graph.get_immutable_gidx(logits.device)
+        return EdgeSoftmax.apply(gidx, logits, graph.number_of_nodes())
+    import numpy as np
+    eids_np = eids.detach().cpu().numpy().astype(np.int64) if isinstance(eids, th.Tensor) \
+        else np.asarray(eids, np.int64)
+    src, dst, _ = graph._graph.edges()
+    # local edge ids 0..k-1 in the order of `eids`, like edge_subgraph
+    sub = _PartialIndex(graph.number_of_nodes(), src[eids_np], dst[eids_np],
+                        np.arange(len(eids_np), dtype=np.int64))
+    gidx = sub.get_immutable_gidx(logits.device)
+    return EdgeSoftmax.apply(gidx, logits, graph.number_of_nodes())

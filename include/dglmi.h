@@ -1,0 +1,162 @@
+/*
+ * dglmi.h -- C ABI of the MI355X-native g-SpMM / g-SDDMM engine.
+ *
+ * Drop-in boundary for the reference's kernel FFI.  The reference exposes
+ * its hot path as DGL PackedFuncs registered in src/kernel/binary_reduce.cc
+ * and bound by python/dgl/kernel.py through ctypes; every entry point below
+ * names the PackedFunc it replaces.  Arguments are plain pointers and sizes:
+ * graphs are raw CSR arrays, tensors are (pointer, ndim, shape) records of
+ * contiguous row-major fp32 device memory, streams are hipStream_t passed as
+ * void* (NULL = the default stream).
+ *
+ * Conventions shared with the reference:
+ *   - target codes: 0 = src, 1 = dst, 2 = edge, 3 = none
+ *     (binary_reduce_common.h:39-44, function/base.py:13-15);
+ *   - reducer strings "sum" | "max" | "min" | "prod" | "none"; "mean" is
+ *     rejected exactly like the reference C++ (binary_reduce_impl.h:95-98):
+ *     the Python layer divides by the degree (tensor.py:308-325);
+ *   - op strings "add" | "sub" | "mul" | "div" | "dot" | "use_lhs";
+ *   - outputs are OVERWRITTEN completely (identity fill then reduce,
+ *     binary_reduce_impl.h:31-64); gradients likewise (zero fill, :119-160);
+ *   - errors: every function returns 0 on success and -1 on failure, with the
+ *     message available from DGLMIGetLastError() in thread-local storage
+ *     (runtime_base.h:13-32, c_runtime_api.cc:138-148).  Nothing calls exit().
+ *
+ * Deliberate differences (documented in DESIGN.md):
+ *   - device work only (gfx950); fp32 features; int32 indices -- the same
+ *     envelope as the reference GPU path (common.h:49-69);
+ *   - an edge-target mapping is indexed by edge id (the value of csr.data),
+ *     not by CSR position, so one mapping serves every traversal direction;
+ *   - node mappings (src/dst targets) must be injective (they are relabel
+ *     maps in the reference, spmv.py:126-180) because reductions are
+ *     owner-computes (one writer per output row, no atomics).
+ */
+#ifndef DGLMI_H_
+#define DGLMI_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DGLMI_MAX_NDIM 8
+
+enum DGLMITarget {
+  DGLMI_TARGET_SRC = 0,
+  DGLMI_TARGET_DST = 1,
+  DGLMI_TARGET_EDGE = 2,
+  DGLMI_TARGET_NONE = 3
+};
+
+/* One direction of the adjacency (aten::CSRMatrix, include/dgl/array.h). */
+typedef struct {
+  int64_t num_rows;
+  int64_t num_cols;
+  int64_t nnz;
+  const int32_t* indptr;  /* num_rows + 1 */
+  const int32_t* indices; /* nnz, column node ids */
+  const int32_t* data;    /* nnz, edge ids */
+  const int32_t* rows;    /* nnz, row id of every position (COO rows, ascending);
+                             required: the edge-wise kernels and the load-balanced
+                             reduce path read the row of a position from it */
+} DGLMICsr;
+
+/* ImmutableGraph as the kernels see it (csr_interface.h:23-29). */
+typedef struct {
+  DGLMICsr in_csr;        /* rows = destination nodes, cols = source nodes */
+  DGLMICsr out_csr;       /* rows = source nodes, cols = destination nodes */
+  int32_t num_bits;       /* index width; must be 32 */
+  int32_t device;         /* HIP device ordinal the arrays live on */
+  void* workspace;        /* caller-owned scratch for this call (may be NULL) */
+  int64_t workspace_bytes;
+} DGLMIGraph;
+
+/* A contiguous row-major fp32 device array (NDArray / DLTensor subset). */
+typedef struct {
+  float* data;
+  int32_t ndim;
+  int64_t shape[DGLMI_MAX_NDIM + 1];
+} DGLMIArray;
+
+/* Last error message of the calling thread (DGLGetLastError). */
+const char* DGLMIGetLastError(void);
+
+/* Library version string ("0.4-mi355x"). */
+const char* DGLMIVersion(void);
+
+/* _CAPI_DGLKernelInferBinaryFeatureShape (binary_reduce.cc:281-293).
+ * Writes the broadcast feature shape into out_shape (capacity
+ * DGLMI_MAX_NDIM + 1) and its rank into *out_ndim. Host-only. */
+int DGLMIKernelInferBinaryFeatureShape(const char* op, const DGLMIArray* lhs,
+                                       const DGLMIArray* rhs, int64_t* out_shape,
+                                       int32_t* out_ndim);
+
+/* _CAPI_DGLKernelBinaryOpReduce (binary_reduce.cc:357-378). */
+int DGLMIKernelBinaryOpReduce(const char* reducer, const char* op, const DGLMIGraph* graph,
+                              int32_t lhs_target, int32_t rhs_target,
+                              const DGLMIArray* lhs, const DGLMIArray* rhs, DGLMIArray* out,
+                              const int32_t* lhs_mapping, const int32_t* rhs_mapping,
+                              const int32_t* out_mapping, void* stream);
+
+/* _CAPI_DGLKernelBackwardLhsBinaryOpReduce (binary_reduce.cc:502-527). */
+int DGLMIKernelBackwardLhsBinaryOpReduce(
+    const char* reducer, const char* op, const DGLMIGraph* graph, int32_t lhs_target,
+    int32_t rhs_target, const int32_t* lhs_mapping, const int32_t* rhs_mapping,
+    const int32_t* out_mapping, const DGLMIArray* lhs, const DGLMIArray* rhs,
+    const DGLMIArray* out, const DGLMIArray* grad_out, DGLMIArray* grad_lhs, void* stream);
+
+/* _CAPI_DGLKernelBackwardRhsBinaryOpReduce (binary_reduce.cc:600-626). */
+int DGLMIKernelBackwardRhsBinaryOpReduce(
+    const char* reducer, const char* op, const DGLMIGraph* graph, int32_t lhs_target,
+    int32_t rhs_target, const int32_t* lhs_mapping, const int32_t* rhs_mapping,
+    const int32_t* out_mapping, const DGLMIArray* lhs, const DGLMIArray* rhs,
+    const DGLMIArray* out, const DGLMIArray* grad_out, DGLMIArray* grad_rhs, void* stream);
+
+/* _CAPI_DGLKernelCopyReduce (binary_reduce.cc:649-665). */
+int DGLMIKernelCopyReduce(const char* reducer, const DGLMIGraph* graph, int32_t target,
+                          const DGLMIArray* in, DGLMIArray* out, const int32_t* in_mapping,
+                          const int32_t* out_mapping, void* stream);
+
+/* _CAPI_DGLKernelBackwardCopyReduce (binary_reduce.cc:697-716). */
+int DGLMIKernelBackwardCopyReduce(const char* reducer, const DGLMIGraph* graph, int32_t target,
+                                  const DGLMIArray* in, const DGLMIArray* out,
+                                  const DGLMIArray* grad_out, DGLMIArray* grad_in,
+                                  const int32_t* in_mapping, const int32_t* out_mapping,
+                                  void* stream);
+
+/* Bytes of DGLMIGraph.workspace a reduce-to-node call over `csr` with
+ * feature length `feat_len` needs on the load-balanced path (0 if none).
+ * The load-balanced path cuts the CSR positions into fixed-size edge chunks
+ * (no reference counterpart: the reference relies on minigun's per-edge
+ * binary search, binary_reduce_impl.cu:424-466); rows split across chunks
+ * leave per-chunk partials here, combined afterwards in chunk order. */
+int64_t DGLMIKernelWorkspaceBytes(const DGLMICsr* csr, int64_t feat_len);
+
+/* ---- graph ingestion ------------------------------------------------------
+ * aten::COOToCSR (array/cpu/spmat_op_impl_coo.cc:230-283): stable counting
+ * sort by row, data = original position (or data[i] when given).  Host
+ * arrays, int64 (the reference's IdArray width for mutable graphs). */
+int DGLMICOOToCSR(int64_t num_rows, int64_t nnz, const int64_t* row, const int64_t* col,
+                  const int64_t* data, int64_t* indptr, int64_t* indices, int64_t* out_data);
+/* aten::CSRTranspose (array/cpu/spmat_op_impl.cc:323-369). Host, int64. */
+int DGLMICSRTranspose(int64_t num_rows, int64_t num_cols, const int64_t* indptr,
+                      const int64_t* indices, const int64_t* data, int64_t* t_indptr,
+                      int64_t* t_indices, int64_t* t_data);
+/* Device COO -> CSR (int32), bit-identical to DGLMICOOToCSR: a stable
+ * counting sort by row on the GPU.  All pointers are device memory;
+ * `workspace` must hold DGLMICOOToCSRDeviceWorkspaceBytes(num_rows, nnz). */
+int64_t DGLMICOOToCSRDeviceWorkspaceBytes(int64_t num_rows, int64_t nnz);
+int DGLMICOOToCSRDevice(int64_t num_rows, int64_t nnz, const int32_t* row, const int32_t* col,
+                        const int32_t* data, int32_t* indptr, int32_t* indices,
+                        int32_t* out_data, void* workspace, int64_t workspace_bytes,
+                        void* stream);
+/* Row id of every CSR position (CSRToCOO rows, spmat_op_impl.cc:375-387), device. */
+int DGLMICSRExpandRows(const int32_t* indptr, int64_t num_rows, int64_t nnz, int32_t* rows,
+                       void* stream);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif  /* DGLMI_H_ */

@@ -1,0 +1,155 @@
+"""Host-side logic of the product (no GPU): C ABI exports, shape inference,
+host graph ingestion, graph bookkeeping and error behaviour."""
+import ctypes
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+import torch as th
+
+import dgl
+import dgl.function as fn
+from dgl import _ffi
+from dgl.graph_index import GraphIndex, host_coo_to_csr, host_csr_transpose
+from oracle import oracle as O
+from graphs import er_graph, g20, powerlaw
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KAT = json.load(open(os.path.join(ROOT, "tests", "golden", "spmat_kat.json")))
+
+
+def test_library_exports_header_symbols():
+    hdr = open(os.path.join(ROOT, "include", "dglmi.h")).read()
+    declared = set(re.findall(r"\b(DGLMI[A-Za-z0-9]+)\s*\(", hdr))
+    assert declared, "no declarations parsed"
+    lib = ctypes.CDLL(_ffi._lib_path())
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert declared == set(_ffi.EXPORTED)
+    assert _ffi.lib().DGLMIVersion() == b"0.4-mi355x"
+
+
+@pytest.mark.parametrize("op", ["add", "sub", "mul", "div", "dot"])
+def test_infer_shape_matches_oracle(op):
+    rng = np.random.default_rng(0)
+    shapes = [((7, 5, 3, 4), (9, 3, 1)), ((7, 4), (9, 5, 3, 4)), ((7, 5, 1, 4), (9, 5, 3, 4)),
+              ((7, 1), (9, 6)), ((7, 2, 3), (9, 2, 3))]
+    for a, b in shapes:
+        if op == "dot" and a[-1] != b[-1]:
+            continue
+        x, y = th.zeros(a), th.zeros(b)
+        assert dgl.kernel.infer_binary_feature_shape(op, x, y) == \
+            O.infer_binary_feature_shape(op, x.numpy(), y.numpy())
+
+
+def test_infer_shape_error():
+    with pytest.raises(dgl.DGLError, match="Invalid broadcasting"):
+        dgl.kernel.infer_binary_feature_shape("add", th.zeros(3, 5), th.zeros(3, 4))
+
+
+def test_host_ingest_kat():
+    for coo, csr in (("COO1", "CSR1"), ("COO2", "CSR2")):
+        p, i, d = host_coo_to_csr(4, KAT[coo]["row"], KAT[coo]["col"])
+        assert p.tolist() == KAT[csr]["indptr"]
+        assert i.tolist() == KAT[csr]["indices"]
+        assert d.tolist() == KAT[csr]["data"]
+    c = KAT["CSR2"]
+    p, i, d = host_csr_transpose(4, 5, c["indptr"], c["indices"], c["data"])
+    assert p.tolist() == KAT["CSR2_T"]["indptr"]
+    assert i.tolist() == KAT["CSR2_T"]["indices"]
+    assert d.tolist() == KAT["CSR2_T"]["data"]
+
+
+@pytest.mark.parametrize("maker", [g20, er_graph, lambda: powerlaw(5000, 60000, seed=2)])
+def test_graph_csr_matches_oracle(maker):
+    src, dst, n = maker()
+    gi = GraphIndex(n)
+    gi.add_edges(src, dst)
+    (op, oi, od), (ip, ii, idd) = gi.host_csr()
+    ref = O.RefGraph(src, dst, n)
+    for a, b in zip((op, oi, od, ip, ii, idd), ref.out_csr + ref.in_csr):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_ingest_rejects_bad_ids():
+    with pytest.raises(dgl.DGLError):
+        host_coo_to_csr(2, [0, 5], [0, 1])
+
+
+def test_dglgraph_bookkeeping():
+    g = dgl.DGLGraph()
+    g.add_nodes(4)
+    g.add_edges([0, 1, 2], [1, 2, 3])
+    g.add_edge(3, 0)
+    assert g.number_of_nodes() == 4 and g.number_of_edges() == 4
+    assert g.in_degrees().tolist() == [1, 1, 1, 1]
+    s, d = g.edges()
+    assert s.tolist() == [0, 1, 2, 3] and d.tolist() == [1, 2, 3, 0]
+    g.ndata["h"] = th.ones(4, 2)
+    lv = g.local_var()
+    lv.ndata["x"] = th.zeros(4, 1)
+    assert "x" not in g.ndata and "h" in lv.ndata
+    with pytest.raises(dgl.DGLError):
+        g.ndata["bad"] = th.ones(3, 2)
+    g.add_nodes(1)
+    assert g.ndata["h"].shape == (5, 2)
+
+
+def test_networkx_and_scipy_construction():
+    import networkx as nx
+    import scipy.sparse as sp
+    g = dgl.DGLGraph(nx.path_graph(3))
+    assert g.number_of_edges() == 4
+    m = sp.coo_matrix((np.ones(3), ([0, 1, 2], [1, 2, 0])), shape=(3, 3))
+    g2 = dgl.DGLGraph(m)
+    assert g2.edges()[0].tolist() == [0, 1, 2]
+
+
+def test_cpu_tensors_fail_loudly():
+    g = dgl.DGLGraph()
+    g.add_nodes(3)
+    g.add_edges([0, 1], [1, 2])
+    g.ndata["h"] = th.ones(3, 4)
+    with pytest.raises(dgl.DGLError, match="ROCm"):
+        g.update_all(fn.copy_u("h", "m"), fn.sum("m", "s"))
+
+
+def test_udf_reduce_rejected():
+    g = dgl.DGLGraph()
+    g.add_nodes(2)
+    g.add_edges([0], [1])
+    with pytest.raises(dgl.DGLError):
+        g.update_all(fn.copy_u("h", "m"), lambda nodes: {})
+
+
+def test_capi_errors_without_device():
+    """Reducer / op validation happens before any device work (binary_reduce_impl.h:95-98)."""
+    L = _ffi.lib()
+    g = _ffi.Graph()
+    g.num_bits = 32
+    a = _ffi.Array()
+    rc = L.DGLMIKernelCopyReduce(b"mean", ctypes.byref(g), 0, ctypes.byref(a), ctypes.byref(a),
+                                 None, None, None)
+    assert rc == -1 and "reduce mean is not supported" in _ffi.last_error()
+    rc = L.DGLMIKernelBinaryOpReduce(b"sum", b"pow", ctypes.byref(g), 0, 2, ctypes.byref(a),
+                                     ctypes.byref(a), ctypes.byref(a), None, None, None, None)
+    assert rc == -1 and "Unsupported binary op" in _ffi.last_error()
+    g.num_bits = 64
+    rc = L.DGLMIKernelCopyReduce(b"sum", ctypes.byref(g), 0, ctypes.byref(a), ctypes.byref(a),
+                                 None, None, None)
+    assert rc == -1 and "idx bits" in _ffi.last_error()
+
+
+def test_builtin_names():
+    assert fn.copy_src("a", "b").name == "copy_u"
+    assert fn.copy_edge("a", "b").name == "copy_e"
+    assert fn.src_mul_edge("a", "b", "c").name == "u_mul_e"
+    assert fn.e_dot_v("a", "b", "c").name == "e_dot_v"
+    assert fn.mean("m", "h").name == "mean"
+    for lhs in "uve":
+        for rhs in "uve":
+            if lhs != rhs:
+                for op in ["add", "sub", "mul", "div", "dot"]:
+                    assert hasattr(fn, "%s_%s_%s" % (lhs, op, rhs))

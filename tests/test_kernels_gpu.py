@@ -1,0 +1,276 @@
+"""Parity of the HIP kernels with the CPU oracle (needs an MI355X).
+
+Every builtin message x reducer x broadcast x {full, partial} combination of
+tests/compute/test_kernel.py runs through DGLGraph -> dgl.backend -> the C ABI
+-> libdglmi.so and is compared with the oracle (forward and gradients) at the
+reference's tolerance (rtol = atol = 1e-4, 1e-2 for prod; test_kernel.py:292-300).
+max / min forward values are exact (no rounding is involved).
+"""
+import itertools
+
+import numpy as np
+import pytest
+import torch as th
+
+import dgl
+import dgl.function as fn
+from oracle import oracle as O
+from graphs import CODE, binary_case_features, er_graph, g20, powerlaw
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _graph(src, dst, n):
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    return g
+
+
+def _run_binary(g, d, lhs, rhs, op, red, nid=None):
+    feats = {k: th.from_numpy(v).to(DEV).requires_grad_() for k, v in d.items()}
+    g.ndata["u"] = feats["u"]
+    g.ndata["v"] = feats["v"]
+    g.edata["e"] = feats["e"]
+    msg = getattr(fn, "%s_%s_%s" % (lhs, op, rhs))(lhs, rhs, "m")
+    if nid is None:
+        g.update_all(msg, getattr(fn, red)("m", "r1"))
+    else:
+        g.pull(nid, msg, getattr(fn, red)("m", "r1"))
+    r1 = g.ndata.pop("r1")
+    r1.sum().backward()
+    return (r1.detach().cpu().numpy(), feats[lhs].grad.cpu().numpy(),
+            feats[rhs].grad.cpu().numpy())
+
+
+@pytest.mark.parametrize("lhs,rhs", [(a, b) for a, b in itertools.product("uve", "uve") if a != b])
+@pytest.mark.parametrize("op", ["add", "sub", "mul", "div", "dot"])
+def test_all_binary_builtins(lhs, rhs, op):
+    src, dst, n = g20()
+    m = len(src)
+    ref = O.RefGraph(src, dst, n)
+    nid = np.array([0, 1, 4, 5, 7, 12, 14, 15, 18, 19])
+    for red in ["sum", "max", "min", "prod", "mean"]:
+        for bc in ["none", lhs, rhs]:
+            for partial in (False, True):
+                d = binary_case_features(n, m, lhs, rhs, op, bc)
+                g = _graph(src, dst, n)
+                out, gl, gr = _run_binary(g, d, lhs, rhs, op, red, nid if partial else None)
+                go = np.ones((n,) + out.shape[1:], np.float32)
+                if partial:
+                    mask = np.zeros(n, bool)
+                    mask[nid] = True
+                    go[~mask] = 0
+                r_out, r_gl, r_gr = O.binary_reduce(red, op, ref, CODE[lhs], CODE[rhs], d[lhs],
+                                                    d[rhs], n, grad_out=go)
+                tol = 1e-2 if red == "prod" else 1e-4
+                msg = "%s_%s_%s %s bcast=%s partial=%s" % (lhs, op, rhs, red, bc, partial)
+                rows = nid if partial else slice(None)
+                np.testing.assert_allclose(out[rows], r_out[rows], rtol=tol, atol=tol, err_msg=msg)
+                np.testing.assert_allclose(gl, r_gl, rtol=tol, atol=tol, err_msg=msg + " lhs grad")
+                np.testing.assert_allclose(gr, r_gr, rtol=tol, atol=tol, err_msg=msg + " rhs grad")
+
+
+@pytest.mark.parametrize("red", ["sum", "max", "mean"])
+@pytest.mark.parametrize("target", ["u", "e"])
+@pytest.mark.parametrize("partial", [False, True])
+def test_copy_reduce(red, target, partial):
+    """test_kernel.py:77-197: copy_src / copy_edge x {sum, max, mean}."""
+    src, dst, n = er_graph(100, 0.1, seed=1)
+    m = len(src)
+    rs = np.random.RandomState(31)
+    x = rs.uniform(-1, 1, ((n if target == "u" else m), 5, 3, 4)).astype(np.float32)
+    g = _graph(src, dst, n)
+    xt = th.from_numpy(x).to(DEV).requires_grad_()
+    if target == "u":
+        g.ndata["u"] = xt
+        msg = fn.copy_src(src="u", out="m")
+    else:
+        g.edata["e"] = xt
+        msg = fn.copy_edge(edge="e", out="m")
+    nid = np.arange(0, 100, 2)
+    if partial:
+        g.pull(nid, msg, getattr(fn, red)(msg="m", out="r1"))
+    else:
+        g.update_all(msg, getattr(fn, red)(msg="m", out="r1"))
+    r1 = g.ndata["r1"]
+    r1.sum().backward()
+    go = np.ones((n, 5, 3, 4), np.float32)
+    if partial:
+        mask = np.zeros(n, bool)
+        mask[nid] = True
+        go[~mask] = 0
+    ref = O.RefGraph(src, dst, n)
+    r_out, r_g = O.copy_reduce(red, ref, CODE[target], x, n, grad_out=go)
+    rows = nid if partial else slice(None)
+    np.testing.assert_allclose(r1.detach().cpu().numpy()[rows], r_out[rows], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(xt.grad.cpu().numpy(), r_g, rtol=1e-4, atol=1e-4)
+
+
+def test_golden_vectors():
+    """GPU against the committed golden vectors of the oracle."""
+    import os
+    import make_golden
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "kernel_g20.npz"))
+    src, dst, n = z["src"], z["dst"], 20
+    g = _graph(src, dst, n)
+    for lhs, op, rhs, red, bc in make_golden.CASES:
+        name = "%s_%s_%s_%s_%s" % (lhs, op, rhs, red, bc)
+        gidx = g._graph.get_immutable_gidx(DEV)
+        out_rows = len(src) if red == "none" else n
+        t = lambda k: th.from_numpy(z[name + "/" + k]).to(DEV)
+        if op == "use_lhs":
+            x = t("x").requires_grad_()
+            out = dgl.backend.copy_reduce(red, gidx, CODE[lhs], x, out_rows)
+            out.backward(t("grad_out"))
+            pairs = [(out, "out"), (x.grad, "grad_x")]
+        else:
+            l, r = t("lhs").requires_grad_(), t("rhs").requires_grad_()
+            out = dgl.backend.binary_reduce(red, op, gidx, CODE[lhs], CODE[rhs], l, r, out_rows)
+            out.backward(t("grad_out"))
+            pairs = [(out, "out"), (l.grad, "grad_lhs"), (r.grad, "grad_rhs")]
+        for val, k in pairs:
+            np.testing.assert_allclose(val.detach().cpu().numpy(), z[name + "/" + k], rtol=1e-4,
+                                       atol=1e-4, err_msg=name + "/" + k)
+
+
+# --------------------------------------------------------------------------
+# load-balanced path: skewed graphs, hub rows split over many chunks
+# --------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def plaw():
+    src, dst, n = powerlaw(20000, 400000, seed=5)
+    return src, dst, n, _graph(src, dst, n), O.RefGraph(src, dst, n)
+
+
+@pytest.mark.parametrize("F", [16, 20, 64, 128, 256, 512, 1024, 6])
+@pytest.mark.parametrize("red", ["sum", "max", "min"])
+def test_copy_u_powerlaw(plaw, F, red):
+    src, dst, n, g, ref = plaw
+    x = np.random.RandomState(F).uniform(-1, 1, (n, F)).astype(np.float32)
+    gidx = g._graph.get_immutable_gidx(DEV)
+    xt = th.from_numpy(x).to(DEV).requires_grad_()
+    out = dgl.backend.copy_reduce(red, gidx, 0, xt, n)
+    go = np.random.RandomState(1).uniform(-1, 1, (n, F)).astype(np.float32)
+    out.backward(th.from_numpy(go).to(DEV))
+    r_out, r_g = O.copy_reduce(red, ref, O.SRC, x, n, grad_out=go)
+    o = out.detach().cpu().numpy()
+    if red == "sum":
+        np.testing.assert_allclose(o, r_out, rtol=1e-4, atol=1e-4)
+    else:
+        np.testing.assert_array_equal(o, r_out)
+    np.testing.assert_allclose(xt.grad.cpu().numpy(), r_g, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("F", [16, 64, 256])
+def test_copy_e_powerlaw(plaw, F):
+    src, dst, n, g, ref = plaw
+    m = len(src)
+    x = np.random.RandomState(F).uniform(-1, 1, (m, F)).astype(np.float32)
+    gidx = g._graph.get_immutable_gidx(DEV)
+    for red in ("sum", "max"):
+        out = dgl.backend.copy_reduce(red, gidx, 2, th.from_numpy(x).to(DEV), n)
+        r_out = O.copy_reduce(red, ref, O.EDGE, x, n)
+        np.testing.assert_allclose(out.cpu().numpy(), r_out, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("H,D", [(8, 8), (4, 16), (1, 64), (8, 3)])
+def test_u_mul_e_bcast_powerlaw(plaw, H, D):
+    """GAT aggregation: (N, H, D) x (E, H, 1) -> sum, forward and both gradients."""
+    src, dst, n, g, ref = plaw
+    m = len(src)
+    rs = np.random.RandomState(H * D)
+    ft = rs.uniform(-1, 1, (n, H, D)).astype(np.float32)
+    a = rs.uniform(0, 1, (m, H, 1)).astype(np.float32)
+    gidx = g._graph.get_immutable_gidx(DEV)
+    ftt = th.from_numpy(ft).to(DEV).requires_grad_()
+    at = th.from_numpy(a).to(DEV).requires_grad_()
+    out = dgl.backend.binary_reduce("sum", "mul", gidx, 0, 2, ftt, at, n)
+    go = rs.uniform(-1, 1, (n, H, D)).astype(np.float32)
+    out.backward(th.from_numpy(go).to(DEV))
+    r_out, r_gl, r_gr = O.binary_reduce("sum", "mul", ref, 0, 2, ft, a, n, grad_out=go)
+    np.testing.assert_allclose(out.detach().cpu().numpy(), r_out, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(ftt.grad.cpu().numpy(), r_gl, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(at.grad.cpu().numpy(), r_gr, rtol=1e-4, atol=2e-4)
+
+
+def test_u_mul_e_same_shape(plaw):
+    src, dst, n, g, ref = plaw
+    m = len(src)
+    rs = np.random.RandomState(3)
+    x = rs.uniform(-1, 1, (n, 32)).astype(np.float32)
+    w = rs.uniform(-1, 1, (m, 32)).astype(np.float32)
+    gidx = g._graph.get_immutable_gidx(DEV)
+    out = dgl.backend.binary_reduce("sum", "mul", gidx, 0, 2, th.from_numpy(x).to(DEV),
+                                    th.from_numpy(w).to(DEV), n)
+    np.testing.assert_allclose(out.cpu().numpy(), O.binary_reduce("sum", "mul", ref, 0, 2, x, w, n),
+                               rtol=1e-4, atol=1e-4)
+
+
+def test_deterministic(plaw):
+    """Owner-computes + ordered carry fold: bitwise identical across runs."""
+    src, dst, n, g, ref = plaw
+    x = th.randn(n, 64, device=DEV)
+    gidx = g._graph.get_immutable_gidx(DEV)
+    a = dgl.backend.copy_reduce("sum", gidx, 0, x, n)
+    b = dgl.backend.copy_reduce("sum", gidx, 0, x, n)
+    assert th.equal(a, b)
+
+
+def test_single_hub_and_gaps():
+    """All edges into one row (spans every chunk), leading/trailing empty rows."""
+    n, m = 5000, 200000
+    rng = np.random.default_rng(2)
+    src = rng.integers(0, n, m)
+    dst = np.full(m, 2500)
+    dst[:10] = 3  # a small row before the hub
+    g = _graph(src, dst, n)
+    ref = O.RefGraph(src, dst, n)
+    x = rng.uniform(-1, 1, (n, 64)).astype(np.float32)
+    gidx = g._graph.get_immutable_gidx(DEV)
+    for red in ("sum", "max", "min"):
+        out = dgl.backend.copy_reduce(red, gidx, 0, th.from_numpy(x).to(DEV), n).cpu().numpy()
+        r = O.copy_reduce(red, ref, O.SRC, x, n)
+        if red == "sum":
+            np.testing.assert_allclose(out, r, rtol=1e-4, atol=2e-3)
+        else:
+            np.testing.assert_array_equal(out, r)
+
+
+def test_empty_graph_and_isolated():
+    g = dgl.DGLGraph()
+    g.add_nodes(7)
+    g.ndata["h"] = th.ones(7, 16, device=DEV)
+    g.update_all(fn.copy_u("h", "m"), fn.sum("m", "s"))
+    assert th.equal(g.ndata["s"], th.zeros(7, 16, device=DEV))
+    g.update_all(fn.copy_u("h", "m"), fn.max("m", "s"))
+    assert (g.ndata["s"] == -3.4028234663852886e38).all()
+
+
+def test_rejects_cpu_tensors():
+    g = dgl.DGLGraph()
+    g.add_nodes(3)
+    g.add_edges([0, 1], [1, 2])
+    g.ndata["h"] = th.ones(3, 4)
+    with pytest.raises(dgl.DGLError):
+        g.update_all(fn.copy_u("h", "m"), fn.sum("m", "s"))
+
+
+def test_device_ingest_bit_exact():
+    """Device COO->CSR (radix sort) == host counting sort == reference KATs."""
+    from dgl.graph_index import GraphIndex
+    src, dst, n = powerlaw(30000, 500000, seed=9)
+    host = GraphIndex(n)
+    host.add_edges(src, dst)
+    dev = GraphIndex.from_device_coo(th.from_numpy(src).to(DEV, th.int32),
+                                     th.from_numpy(dst).to(DEV, th.int32), n)
+    a = host.get_immutable_gidx(DEV)
+    b = dev.get_immutable_gidx(DEV)
+    for x, y in ((a.in_csr, b.in_csr), (a.out_csr, b.out_csr)):
+        for k in ("indptr", "indices", "data", "rows"):
+            assert th.equal(getattr(x, k), getattr(y, k)), k
+    ref = O.RefGraph(src, dst, n)
+    np.testing.assert_array_equal(b.in_csr.indptr.cpu().numpy(), ref.in_csr[0])
+    np.testing.assert_array_equal(b.in_csr.indices.cpu().numpy(), ref.in_csr[1])
+    np.testing.assert_array_equal(b.in_csr.data.cpu().numpy(), ref.in_csr[2])

@@ -1,0 +1,165 @@
+"""NN-module known answers (tests/pytorch/test_nn.py) on the HIP path."""
+import networkx as nx
+import numpy as np
+import pytest
+import torch as th
+
+import dgl
+import dgl.nn.pytorch as nn
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _AXWb(A, X, W, b):
+    X = th.matmul(X, W)
+    Y = th.matmul(A, X.view(X.shape[0], -1)).view_as(X)
+    return Y + b
+
+
+def _adj(g):
+    s, d = g.edges()
+    n = g.number_of_nodes()
+    A = th.zeros(n, n)
+    A.index_put_((d, s), th.ones(len(s)), accumulate=True)  # row = dst
+    return A.to(DEV)
+
+
+def test_graph_conv_known_answer():
+    """test_nn.py:14-38: GraphConv(norm='none') on path_graph(3) == A X W + b."""
+    g = dgl.DGLGraph(nx.path_graph(3))
+    adj = _adj(g)
+    conv = nn.GraphConv(5, 2, norm="none", bias=True).to(DEV)
+    h0 = th.ones(3, 5, device=DEV)
+    h1 = conv(g, h0)
+    assert len(g.ndata) == 0 and len(g.edata) == 0
+    assert th.allclose(h1, _AXWb(adj, h0, conv.weight, conv.bias), rtol=1e-4, atol=1e-4)
+    h0 = th.ones(3, 5, 5, device=DEV)
+    h1 = conv(g, h0)
+    assert th.allclose(h1, _AXWb(adj, h0, conv.weight, conv.bias), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("norm", ["both", "right", "none"])
+@pytest.mark.parametrize("fin,fout", [(32, 16), (16, 32)])
+def test_graph_conv_dense(norm, fin, fout):
+    """GraphConv vs a dense float64 restatement, forward and parameter grads."""
+    rng = np.random.default_rng(0)
+    n = 300
+    src = rng.integers(0, n, 3000)
+    dst = rng.integers(0, n, 3000)
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    conv = nn.GraphConv(fin, fout, norm=norm).to(DEV)
+    x = th.randn(n, fin, device=DEV)
+    y = conv(g, x)
+    y.sum().backward()
+    A = _adj(g).double()
+    W, b = conv.weight.detach().double().requires_grad_(), conv.bias.detach().double().requires_grad_()
+    xd = x.double()
+    dout = th.from_numpy(g.out_degrees().numpy()).to(DEV).double().clamp(min=1)
+    din = th.from_numpy(g.in_degrees().numpy()).to(DEV).double().clamp(min=1)
+    h = xd * dout.pow(-0.5)[:, None] if norm == "both" else xd
+    r = A @ (h @ W)
+    if norm == "both":
+        r = r * din.pow(-0.5)[:, None]
+    elif norm == "right":
+        r = r / din[:, None]
+    r = r + b
+    r.sum().backward()
+    assert th.allclose(y.double(), r, rtol=1e-4, atol=1e-4)
+    assert th.allclose(conv.weight.grad.double(), W.grad, rtol=1e-3, atol=1e-3)
+
+
+def uniform_attention(g, shape):
+    a = th.ones(shape)
+    target_shape = (g.number_of_edges(),) + (1,) * (len(shape) - 1)
+    return a / g.in_degrees(g.edges()[1]).view(target_shape).float()
+
+
+def test_edge_softmax():
+    """test_nn.py:269-333."""
+    g = dgl.DGLGraph(nx.path_graph(3))
+    a = nn.edge_softmax(g, th.ones(g.number_of_edges(), 1, device=DEV))
+    assert th.allclose(a.cpu(), uniform_attention(g, a.shape))
+    a = nn.edge_softmax(g, th.ones(g.number_of_edges(), 3, 1, device=DEV))
+    assert th.allclose(a.cpu(), uniform_attention(g, a.shape))
+    g = dgl.DGLGraph()
+    g.add_nodes(30)
+    for i in range(30):
+        for j in range(30):
+            g.add_edge(i, j)
+    score = th.randn(900, 1, device=DEV).requires_grad_()
+    grad = th.randn(900, 1, device=DEV)
+    y = th.softmax(score.view(30, 30), dim=0).view(-1, 1)
+    y.backward(grad)
+    grad_score = score.grad.clone()
+    score.grad.zero_()
+    y_dgl = nn.edge_softmax(g, score)
+    assert len(g.ndata) == 0 and len(g.edata) == 0
+    assert th.allclose(y_dgl, y, rtol=1e-4, atol=1e-4)
+    y_dgl.backward(grad)
+    assert th.allclose(score.grad, grad_score, rtol=1e-4, atol=1e-4)
+
+
+def test_partial_edge_softmax():
+    """test_nn.py:334-362: softmax over a subset of edges."""
+    g = dgl.DGLGraph()
+    g.add_nodes(30)
+    for i in range(30):
+        for j in range(30):
+            g.add_edge(i, j)
+    score = th.randn(300, 1, device=DEV).requires_grad_()
+    grad = th.randn(300, 1, device=DEV)
+    eids = np.random.permutation(900)[:300]
+    eids_t = th.from_numpy(eids)
+    s, d = g.edges()
+    s, d = s[eids_t], d[eids_t]
+    # reference: softmax grouped by destination
+    y = th.zeros_like(score)
+    for v in range(30):
+        m = (d == v).nonzero().view(-1).to(DEV)
+        if len(m):
+            y = y.index_put((m,), th.softmax(score[m], dim=0))
+    y.backward(grad)
+    g1 = score.grad.clone()
+    score.grad.zero_()
+    y_dgl = nn.edge_softmax(g, score, eids_t)
+    assert th.allclose(y_dgl, y, rtol=1e-4, atol=1e-4)
+    y_dgl.backward(grad)
+    assert th.allclose(score.grad, g1, rtol=1e-4, atol=1e-4)
+
+
+def test_gat_conv_vs_dense():
+    """GATConv against a dense torch restatement (float64)."""
+    th.manual_seed(0)
+    n, fin, H, D = 200, 24, 4, 8
+    rng = np.random.default_rng(1)
+    src = np.concatenate([rng.integers(0, n, 2000), np.arange(n)])
+    dst = np.concatenate([rng.integers(0, n, 2000), np.arange(n)])
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    gat = nn.GATConv(fin, D, H).to(DEV)
+    x = th.randn(n, fin, device=DEV)
+    out = gat(g, x)
+    assert out.shape == (n, H, D)
+    out.sum().backward()
+    Wd = gat.fc.weight.detach().double().requires_grad_()
+    al = gat.attn_l.detach().double().requires_grad_()
+    ar = gat.attn_r.detach().double().requires_grad_()
+    ft = (x.double() @ Wd.t()).view(n, H, D)
+    el = (ft * al).sum(-1)
+    er = (ft * ar).sum(-1)
+    s = th.from_numpy(src).to(DEV)
+    d = th.from_numpy(dst).to(DEV)
+    e = th.nn.functional.leaky_relu(el[s] + er[d], 0.2)  # (E, H)
+    emax = th.full((n, H), -1e300, dtype=th.float64, device=DEV).index_reduce(0, d, e, "amax")
+    ex = th.exp(e - emax[d])
+    den = th.zeros(n, H, dtype=th.float64, device=DEV).index_add(0, d, ex)
+    a = ex / den[d]
+    rst = th.zeros(n, H, D, dtype=th.float64, device=DEV).index_add(0, d, ft[s] * a[:, :, None])
+    rst.sum().backward()
+    assert th.allclose(out.double(), rst, rtol=1e-4, atol=1e-4)
+    assert th.allclose(gat.fc.weight.grad.double(), Wd.grad, rtol=1e-3, atol=1e-3)
+    assert th.allclose(gat.attn_l.grad.double(), al.grad, rtol=1e-3, atol=1e-3)
