@@ -203,6 +203,24 @@ def main():
     if rel > 1e-3:
         raise SystemExit("copy_u_sum checksum mismatch: %g" % rel)
     del outdeg, expect, got
+    # row-exact spot check: 4096 random rows recomputed with torch gathers (fp64)
+    gen = th.Generator(device=device)
+    gen.manual_seed(7)
+    rows = th.randint(0, n_dst, (4096,), generator=gen, device=device)
+    ip = gidx.in_csr.indptr.long()
+    beg, end = ip[rows], ip[rows + 1]
+    lens = end - beg
+    seg = th.repeat_interleave(th.arange(4096, device=device), lens)
+    pos = th.repeat_interleave(beg - th.cumsum(lens, 0) + lens, lens) + th.arange(int(lens.sum()), device=device)
+    cols = gidx.in_csr.indices.long()[pos]
+    xr = x.double()[cols]
+    exact = th.zeros(4096, FEAT, dtype=th.float64, device=device).index_add_(0, seg, xr)
+    mass = th.zeros(4096, FEAT, dtype=th.float64, device=device).index_add_(0, seg, xr.abs())
+    err = (out[rows].double() - exact).abs()
+    if bool((err > 1e-4 + 1e-6 * mass).any()):
+        raise SystemExit("copy_u_sum row check failed: max err %g" % float(err.max()))
+    log("row spot check (4096 rows, fp64 torch gathers): max abs err %.2e" % float(err.max()))
+    del seg, pos, cols, xr, exact, mass, err
 
     for _ in range(args.warmup):
         step()

@@ -30,6 +30,7 @@
 #include "internal.h"
 
 #include <climits>
+#include <cstdlib>
 
 namespace dglmi {
 namespace {
@@ -287,7 +288,13 @@ void run_cfg(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
 int64_t fast_chunk_edges(int64_t nnz, int64_t F) {
   // Enough chunks to give every CU several groups; long chunks otherwise so
   // that fewer rows are cut (each cut row costs one carry write + read).
-  int64_t k = 256;
+  // DGLMI_CHUNK_EDGES overrides (tuning experiments; power of two >= 16).
+  if (const char* env = std::getenv("DGLMI_CHUNK_EDGES")) {
+    const long v = std::atol(env);
+    if (v >= 16 && (v & (v - 1)) == 0) return v;
+  }
+  // Measured on M1 (F = 16..256): 512 is best or within 1% (scripts/tune_spmm.py).
+  int64_t k = 512;
   const int64_t groups_wanted = 256 /*CUs*/ * 64;
   while (k > 32 && nnz / k < groups_wanted) k >>= 1;
   (void)F;

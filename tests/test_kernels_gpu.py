@@ -135,6 +135,47 @@ def test_golden_vectors():
                                        atol=1e-4, err_msg=name + "/" + k)
 
 
+def _weighted_sums(csr, x, w=None):
+    """fp64 sum_j w_j x[col_j] and its mass sum_j |w_j x[col_j]| per row (scipy)."""
+    import scipy.sparse as sp
+    indptr, indices, eids = csr
+    n = len(indptr) - 1
+    x2 = x.reshape(x.shape[0], -1).astype(np.float64)
+    if w is None:
+        A = sp.csr_matrix((np.ones(len(indices)), indices, indptr), shape=(n, x.shape[0]))
+        return A @ x2, A @ np.abs(x2)
+    # w: per-edge weights (E, H) broadcast over the trailing dim of x (N, H, D)
+    H = w.shape[1]
+    x3 = x.reshape(x.shape[0], H, -1).astype(np.float64)
+    ex = np.zeros((n, H, x3.shape[2]))
+    ms = np.zeros_like(ex)
+    for h in range(H):
+        wh = w[eids, h].astype(np.float64)
+        A = sp.csr_matrix((wh, indices, indptr), shape=(n, x.shape[0]))
+        Aa = sp.csr_matrix((np.abs(wh), indices, indptr), shape=(n, x.shape[0]))
+        ex[:, h] = A @ x3[:, h]
+        ms[:, h] = Aa @ np.abs(x3[:, h])
+    return ex.reshape(n, -1), ms.reshape(n, -1)
+
+
+def assert_sum_close(got, ref32, csr, x, w=None):
+    """fp32 sums over rows with up to 10^4-10^5 terms: the oracle's sequential fp32
+    order and the kernel's chunked order both carry rounding error that grows with
+    the row's mass sum|term|.  Both are checked against an fp64 restatement with a
+    bound of 1e-4 + 1e-6 * mass (fp32 eps = 6e-8; sequential worst case ~ n * eps),
+    and the kernel against the oracle at the reference tolerance 1e-4 on rows whose
+    mass is small (< 100), i.e. everywhere the reference's own tolerance is meaningful."""
+    exact, mass = _weighted_sums(csr, x, w)
+    exact = exact.reshape(got.shape)
+    mass = mass.reshape(got.shape)
+    bound = 1e-4 + 1e-6 * mass
+    # the oracle's single sequential fp32 chain may drift further on 10^5-term rows
+    assert (np.abs(ref32 - exact) <= 1e-4 + 1e-5 * mass).all(), "oracle outside the fp32 bound"
+    assert (np.abs(got - exact) <= bound).all(), float(np.abs(got - exact).max())
+    small = mass < 100
+    np.testing.assert_allclose(got[small], ref32[small], rtol=1e-4, atol=1e-4)
+
+
 # --------------------------------------------------------------------------
 # load-balanced path: skewed graphs, hub rows split over many chunks
 # --------------------------------------------------------------------------
@@ -157,10 +198,12 @@ def test_copy_u_powerlaw(plaw, F, red):
     r_out, r_g = O.copy_reduce(red, ref, O.SRC, x, n, grad_out=go)
     o = out.detach().cpu().numpy()
     if red == "sum":
-        np.testing.assert_allclose(o, r_out, rtol=1e-4, atol=1e-4)
+        assert_sum_close(o, r_out, ref.in_csr, x)
+        assert_sum_close(xt.grad.cpu().numpy(), r_g, ref.out_csr, go)
     else:
         np.testing.assert_array_equal(o, r_out)
-    np.testing.assert_allclose(xt.grad.cpu().numpy(), r_g, rtol=1e-4, atol=1e-4)
+        # gradient goes to every tied (== max) edge: few terms per source row
+        np.testing.assert_allclose(xt.grad.cpu().numpy(), r_g, rtol=1e-4, atol=1e-4)
 
 
 @pytest.mark.parametrize("F", [16, 64, 256])
@@ -172,7 +215,12 @@ def test_copy_e_powerlaw(plaw, F):
     for red in ("sum", "max"):
         out = dgl.backend.copy_reduce(red, gidx, 2, th.from_numpy(x).to(DEV), n)
         r_out = O.copy_reduce(red, ref, O.EDGE, x, n)
-        np.testing.assert_allclose(out.cpu().numpy(), r_out, rtol=1e-4, atol=1e-4)
+        if red == "sum":
+            ip, _, eids = ref.in_csr
+            # edge data gathered by eid: a CSR whose "columns" are the edge ids
+            assert_sum_close(out.cpu().numpy(), r_out, (ip, eids, eids), x)
+        else:
+            np.testing.assert_array_equal(out.cpu().numpy(), r_out)
 
 
 @pytest.mark.parametrize("H,D", [(8, 8), (4, 16), (1, 64), (8, 3)])
@@ -190,7 +238,7 @@ def test_u_mul_e_bcast_powerlaw(plaw, H, D):
     go = rs.uniform(-1, 1, (n, H, D)).astype(np.float32)
     out.backward(th.from_numpy(go).to(DEV))
     r_out, r_gl, r_gr = O.binary_reduce("sum", "mul", ref, 0, 2, ft, a, n, grad_out=go)
-    np.testing.assert_allclose(out.detach().cpu().numpy(), r_out, rtol=1e-4, atol=1e-4)
+    assert_sum_close(out.detach().cpu().numpy(), r_out, ref.in_csr, ft, a.reshape(m, H))
     np.testing.assert_allclose(ftt.grad.cpu().numpy(), r_gl, rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(at.grad.cpu().numpy(), r_gr, rtol=1e-4, atol=2e-4)
 
@@ -203,9 +251,16 @@ def test_u_mul_e_same_shape(plaw):
     w = rs.uniform(-1, 1, (m, 32)).astype(np.float32)
     gidx = g._graph.get_immutable_gidx(DEV)
     out = dgl.backend.binary_reduce("sum", "mul", gidx, 0, 2, th.from_numpy(x).to(DEV),
-                                    th.from_numpy(w).to(DEV), n)
-    np.testing.assert_allclose(out.cpu().numpy(), O.binary_reduce("sum", "mul", ref, 0, 2, x, w, n),
-                               rtol=1e-4, atol=1e-4)
+                                    th.from_numpy(w).to(DEV), n).cpu().numpy()
+    r = O.binary_reduce("sum", "mul", ref, 0, 2, x, w, n)
+    ip, idx, eids = ref.in_csr
+    msg = x[idx].astype(np.float64) * w[eids]
+    exact = np.add.reduceat(np.vstack([msg, np.zeros((1, 32))]), np.minimum(ip[:-1], len(idx)), axis=0)
+    exact[ip[:-1] == ip[1:]] = 0
+    mass = np.add.reduceat(np.vstack([np.abs(msg), np.zeros((1, 32))]), np.minimum(ip[:-1], len(idx)), axis=0)
+    mass[ip[:-1] == ip[1:]] = 0
+    bound = 1e-4 + 1e-6 * mass
+    assert (np.abs(out - exact) <= bound).all() and (np.abs(r - exact) <= bound).all()
 
 
 def test_deterministic(plaw):
@@ -233,7 +288,7 @@ def test_single_hub_and_gaps():
         out = dgl.backend.copy_reduce(red, gidx, 0, th.from_numpy(x).to(DEV), n).cpu().numpy()
         r = O.copy_reduce(red, ref, O.SRC, x, n)
         if red == "sum":
-            np.testing.assert_allclose(out, r, rtol=1e-4, atol=2e-3)
+            assert_sum_close(out, r, ref.in_csr, x)
         else:
             np.testing.assert_array_equal(out, r)
 
