@@ -75,10 +75,10 @@ def rmat_edges(scale, num_edges, seed, device, chunk=25_000_000):
     return th.cat(srcs), th.cat(dsts)
 
 
-def build_workload(world, rank, device):
-    scale = SCALE + int(round(math.log2(world)))
+def build_workload(world, rank, device, edges_per_gpu=EDGES_PER_GPU, scale0=SCALE):
+    scale = scale0 + int(round(math.log2(world)))
     n = 1 << scale
-    m = EDGES_PER_GPU * world
+    m = edges_per_gpu * world
     t0 = time.time()
     src, dst = rmat_edges(scale, m, seed=1234, device=device)
     gp = th.Generator(device=device)
@@ -163,22 +163,33 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    # rehearsal knobs (small graphs, gloo collectives with every rank on one GPU);
+    # the headline run uses the defaults
+    ap.add_argument("--edges-per-gpu", type=int, default=EDGES_PER_GPU)
+    ap.add_argument("--scale", type=int, default=SCALE)
+    ap.add_argument("--dist-backend", default="nccl")
+    ap.add_argument("--same-device", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
     th.cuda.set_device(local)
     device = "cuda:%d" % local
     dist = None
+    cdev = device
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=th.device(device))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=th.device(device))
+        else:
+            dist.init_process_group(args.dist_backend)
+            cdev = "cpu"  # gloo collectives on host tensors
 
     import dgl  # noqa: F401
     from dgl import kernel as K
 
-    n, n_dst, src, dst, x = build_workload(world, rank, device)
+    n, n_dst, src, dst, x = build_workload(world, rank, device, args.edges_per_gpu, args.scale)
     t0 = time.time()
     gidx, (o_ptr, o_idx) = make_local_graph(n, n_dst, src, dst, device)
     m_local = src.shape[0]
@@ -243,13 +254,13 @@ def main():
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     edges_total = m_local
     if dist is not None:
-        t = th.tensor([elapsed], device=device, dtype=th.float64)
+        t = th.tensor([elapsed], device=cdev, dtype=th.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        k = th.tensor([kernel_ms], device=device, dtype=th.float64)
+        k = th.tensor([kernel_ms], device=cdev, dtype=th.float64)
         dist.all_reduce(k, op=dist.ReduceOp.MAX)
         kernel_ms = float(k.item())
-        e = th.tensor([m_local], device=device, dtype=th.float64)
+        e = th.tensor([m_local], device=cdev, dtype=th.float64)
         dist.all_reduce(e)
         edges_total = int(e.item())
 
@@ -276,9 +287,10 @@ def main():
         "data": "synthetic RMAT(0.57,0.19,0.19,0.05) generated on device, ids permuted, "
                 "X~U(-1,1) seed 2",
         "config": {"workload": "M1 copy_u_sum: RMAT scale %d, %d edges, feat %d, int32 in-CSR%s"
-                               % (SCALE + int(round(math.log2(world))), EDGES_PER_GPU * world, FEAT,
-                                  "" if world == 1 else ", %d-way dst-row partition, X replicated" % world),
-                   "nodes": n, "edges": EDGES_PER_GPU * world, "feat": FEAT,
+                               % (args.scale + int(round(math.log2(world))), args.edges_per_gpu * world,
+                                  FEAT, "" if world == 1 else
+                                  ", %d-way dst-row partition, X replicated" % world),
+                   "nodes": n, "edges": args.edges_per_gpu * world, "feat": FEAT,
                    "parallelism": "dst-row partition x%d" % world if world > 1 else "single"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": pmc,

@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -219,3 +221,39 @@ int DGLMICSRExpandRows(const int32_t* indptr, int64_t num_rows, int64_t nnz, int
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Partitioning (no METIS here): Linear Deterministic Greedy, streaming over
+// nodes in id order on the symmetrised adjacency.  Node v goes to the part
+// maximising |N(v) ∩ P| * (1 - |P| / C), C = ceil(n / k) * (1 + slack); ties
+// and neighbourless nodes go to the least-loaded part.  Deterministic.
+// ---------------------------------------------------------------------------
+extern "C" int DGLMIPartitionLDG(int64_t num_nodes, const int64_t* indptr, const int64_t* indices,
+                                 int32_t num_parts, double slack, int64_t* assign) {
+  if (num_nodes < 0 || num_parts < 1 || indptr == nullptr || assign == nullptr) return -1;
+  std::vector<int64_t> size(num_parts, 0);
+  std::vector<int64_t> cnt(num_parts, 0);
+  const double cap = std::ceil(static_cast<double>(num_nodes) / num_parts) * (1.0 + slack);
+  for (int64_t v = 0; v < num_nodes; ++v) assign[v] = -1;
+  for (int64_t v = 0; v < num_nodes; ++v) {
+    std::fill(cnt.begin(), cnt.end(), 0);
+    for (int64_t j = indptr[v]; j < indptr[v + 1]; ++j) {
+      const int64_t u = indices[j];
+      if (u >= 0 && u < num_nodes && assign[u] >= 0) cnt[assign[u]]++;
+    }
+    int best = -1;
+    double best_score = -1.0;
+    for (int p = 0; p < num_parts; ++p) {
+      if (size[p] >= cap) continue;
+      const double score = cnt[p] * (1.0 - size[p] / cap);
+      if (best < 0 || score > best_score || (score == best_score && size[p] < size[best])) {
+        best = p;
+        best_score = score;
+      }
+    }
+    if (best < 0) best = static_cast<int>(std::min_element(size.begin(), size.end()) - size.begin());
+    assign[v] = best;
+    size[best]++;
+  }
+  return 0;
+}

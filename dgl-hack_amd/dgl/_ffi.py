@@ -106,6 +106,9 @@ _SIGS = {
         ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
         ctypes.c_void_p]),
+    "DGLMIPartitionLDG": (ctypes.c_int, [
+        ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_double,
+        ctypes.c_void_p]),
     "DGLMICSRExpandRows": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
 }

@@ -155,6 +155,12 @@ int DGLMICOOToCSRDevice(int64_t num_rows, int64_t nnz, const int32_t* row, const
 int DGLMICSRExpandRows(const int32_t* indptr, int64_t num_rows, int64_t nnz, int32_t* rows,
                        void* stream);
 
+/* ---- partitioning (metis_partition.cc:19-66 replacement; METIS is absent) --
+ * Linear Deterministic Greedy over a symmetrised host CSR (int64): node v goes
+ * to the part maximising |N(v) ∩ P| (1 - |P| / C), C = ceil(n / k)(1 + slack). */
+int DGLMIPartitionLDG(int64_t num_nodes, const int64_t* indptr, const int64_t* indices,
+                      int32_t num_parts, double slack, int64_t* assign);
+
 #ifdef __cplusplus
 }  /* extern "C" */
 #endif

@@ -1,0 +1,85 @@
+"""Partition + halo exchange + gradient all-reduce with gloo, world_size 2 (CPU)."""
+import numpy as np
+import pytest
+import torch as th
+
+from dgl import distributed as D
+from graphs import powerlaw, er_graph
+from dist_util import run_world
+
+
+@pytest.mark.parametrize("method", ["contiguous", "ldg"])
+@pytest.mark.parametrize("k", [2, 3, 4])
+def test_partitions_cover_graph(method, k):
+    src, dst, n = powerlaw(3000, 30000, seed=4)
+    assign = D.partition_assignment(n, src, dst, k, method)
+    assert assign.min() >= 0 and assign.max() < k
+    parts = D.build_partitions(src, dst, n, assign, num_parts=k)
+    seen = np.concatenate([p.parent_eid for p in parts])
+    assert np.array_equal(np.sort(seen), np.arange(len(src)))  # every edge exactly once
+    for p in parts:
+        full = np.concatenate([p.inner, p.halo])
+        np.testing.assert_array_equal(full[p.local_src], src[p.parent_eid])
+        np.testing.assert_array_equal(p.inner[p.local_dst], dst[p.parent_eid])
+        assert (assign[p.inner] == p.part_id).all() and (assign[p.halo] != p.part_id).all()
+        # send plan of q towards p == p's halo rows owned by q, in p's order
+        for q in parts:
+            if q.part_id == p.part_id:
+                continue
+            off = int(q.send_counts[:p.part_id].sum())
+            rows = q.inner[q.send_idx[off:off + q.send_counts[p.part_id]]]
+            np.testing.assert_array_equal(rows, p.halo[p.halo_owner == q.part_id])
+    if method == "ldg":
+        sizes = np.bincount(assign, minlength=k)
+        assert sizes.max() <= np.ceil(n / k) * 1.05 + 1
+
+
+def test_ldg_cuts_fewer_edges_than_random():
+    """A graph with 4 planted communities (ids shuffled): LDG must cut far fewer
+    edges than a random assignment."""
+    rng = np.random.default_rng(0)
+    n, m = 400, 8000
+    block = rng.permutation(np.repeat(np.arange(4), n // 4))
+    members = [np.nonzero(block == b)[0] for b in range(4)]
+    u = rng.integers(0, n, m)
+    intra = rng.random(m) < 0.9
+    v = np.where(intra, np.array([rng.choice(members[block[x]]) for x in u]), rng.integers(0, n, m))
+    a_ldg = D.partition_assignment(n, u, v, 4, "ldg")
+    a_rand = rng.integers(0, 4, n)
+    cut = lambda a: int((a[u] != a[v]).sum())
+    assert cut(a_ldg) < 0.6 * cut(a_rand)
+
+
+def _halo_worker(rank, world, src, dst, n, k):
+    import torch.distributed as dist
+    assign = D.partition_assignment(n, src, dst, k, "ldg")
+    part = D.build_partitions(src, dst, n, assign, num_parts=k)[rank]
+    g = th.Generator().manual_seed(0)
+    xg = th.randn(n, 5, generator=g)
+    wg = th.randn(n, 5, generator=g)
+    x_inner = xg[th.from_numpy(part.inner)].clone().requires_grad_()
+    full = D.halo_exchange(x_inner, part)
+    ids = th.from_numpy(np.concatenate([part.inner, part.halo]))
+    assert th.equal(full.detach(), xg[ids])
+    # loss = sum over every (local use) of w * x ; the gradient of an owned row must
+    # collect the uses on every rank that holds it as halo
+    (full * wg[ids]).sum().backward()
+    uses = th.zeros(n)
+    for p in D.build_partitions(src, dst, n, assign, num_parts=k):
+        uses.index_add_(0, th.from_numpy(np.concatenate([p.inner, p.halo])), th.ones(p.n_inner + p.n_halo))
+    expect = wg[th.from_numpy(part.inner)] * uses[th.from_numpy(part.inner)][:, None]
+    assert th.allclose(x_inner.grad, expect, atol=1e-6)
+    # flattened gradient all-reduce
+    p1 = th.nn.Parameter(th.zeros(3, 2))
+    p2 = th.nn.Parameter(th.zeros(4))
+    p1.grad = th.full((3, 2), float(rank + 1))
+    p2.grad = th.full((4,), float(10 * (rank + 1)))
+    D.allreduce_gradients([p1, p2])
+    assert th.allclose(p1.grad, th.full((3, 2), sum(r + 1 for r in range(world)) / world))
+    assert th.allclose(p2.grad, th.full((4,), sum(10 * (r + 1) for r in range(world)) / world))
+    dist.barrier()
+
+
+def test_halo_exchange_gloo_world2():
+    src, dst, n = powerlaw(500, 4000, seed=1)
+    run_world(_halo_worker, 2, (src, dst, n, 2))
