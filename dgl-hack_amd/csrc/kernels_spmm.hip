@@ -244,6 +244,183 @@ __global__ void __launch_bounds__(kBlock) k_chunk_fixup(FastArgs a, const int32_
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Narrow rows (F < 16 floats: attention logits per head, edge-softmax sums):
+// a group of 4+ lanes would idle most lanes, so ONE lane owns a chunk and the
+// whole (tiny) row, keeping 8 gathers of F floats in flight per lane.
+// ---------------------------------------------------------------------------
+template <int F>
+__device__ __forceinline__ void load_row(const float* __restrict__ p, float (&v)[F]) {
+  if constexpr (F % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < F / 4; ++i) {
+      const float4 t = ld4(p + 4 * i);
+      v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
+    }
+  } else if constexpr (F % 2 == 0) {
+#pragma unroll
+    for (int i = 0; i < F / 2; ++i) {
+      const float2 t = *reinterpret_cast<const float2*>(p + 2 * i);
+      v[2 * i] = t.x; v[2 * i + 1] = t.y;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < F; ++i) v[i] = p[i];
+  }
+}
+
+template <int F>
+__device__ __forceinline__ void store_row(float* __restrict__ p, const float (&v)[F]) {
+  if constexpr (F % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < F / 4; ++i) st4(p + 4 * i, make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]));
+  } else {
+#pragma unroll
+    for (int i = 0; i < F; ++i) p[i] = v[i];
+  }
+}
+
+template <int KIND, int F>
+__device__ __forceinline__ void lane_value(const FastArgs& a, int32_t col, int32_t eid, float (&v)[F]) {
+  if constexpr (KIND == FAST_COPY_COL) {
+    const int64_t c = a.x_map ? a.x_map[col] : col;
+    load_row<F>(a.x + c * F, v);
+  } else if constexpr (KIND == FAST_COPY_EDGE) {
+    const int64_t e = a.x_map ? a.x_map[eid] : eid;
+    load_row<F>(a.x + e * F, v);
+  } else if constexpr (KIND == FAST_COL_MUL_EDGE) {
+    const int64_t c = a.x_map ? a.x_map[col] : col;
+    const int64_t e = a.w_map ? a.w_map[eid] : eid;
+    float w[F];
+    load_row<F>(a.x + c * F, v);
+    load_row<F>(a.w + e * F, w);
+#pragma unroll
+    for (int i = 0; i < F; ++i) v[i] *= w[i];
+  } else {
+    const int64_t c = a.x_map ? a.x_map[col] : col;
+    const int64_t e = a.w_map ? a.w_map[eid] : eid;
+    const int64_t H = F / a.head_dim;
+    load_row<F>(a.x + c * F, v);
+#pragma unroll
+    for (int i = 0; i < F; ++i) v[i] *= a.w[e * H + i / a.head_dim];
+  }
+}
+
+template <int KIND, int RED, int F>
+__global__ void __launch_bounds__(kBlock) k_lane_reduce(FastArgs a) {
+  constexpr int U = 8;
+  const int64_t chunk = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t K = a.chunk;
+  const int64_t p0 = chunk * K;
+  if (p0 >= a.nnz) return;
+  const int64_t p1 = p0 + K < a.nnz ? p0 + K : a.nnz;
+  const float I = red_identity<RED>();
+  float ident[F];
+#pragma unroll
+  for (int i = 0; i < F; ++i) ident[i] = I;
+  int64_t cur = a.rows[p0];
+  bool cont = p0 > 0 && a.rows[p0 - 1] == cur;
+  if (!cont) {
+    const int64_t first_gap = p0 > 0 ? (int64_t)a.rows[p0 - 1] + 1 : 0;
+    for (int64_t r = first_gap; r < cur; ++r) store_row<F>(a.out + r * F, ident);
+  }
+  float acc[F];
+#pragma unroll
+  for (int i = 0; i < F; ++i) acc[i] = I;
+  for (int64_t base = p0; base < p1; base += U) {
+    int32_t r[U], c[U], e[U];
+    if (base + U <= p1) {
+      const int4 r0 = *reinterpret_cast<const int4*>(a.rows + base);
+      const int4 r1 = *reinterpret_cast<const int4*>(a.rows + base + 4);
+      const int4 c0 = *reinterpret_cast<const int4*>(a.indices + base);
+      const int4 c1 = *reinterpret_cast<const int4*>(a.indices + base + 4);
+      r[0] = r0.x; r[1] = r0.y; r[2] = r0.z; r[3] = r0.w; r[4] = r1.x; r[5] = r1.y; r[6] = r1.z; r[7] = r1.w;
+      c[0] = c0.x; c[1] = c0.y; c[2] = c0.z; c[3] = c0.w; c[4] = c1.x; c[5] = c1.y; c[6] = c1.z; c[7] = c1.w;
+      if constexpr (needs_eid<KIND>()) {
+        const int4 e0 = *reinterpret_cast<const int4*>(a.eids + base);
+        const int4 e1 = *reinterpret_cast<const int4*>(a.eids + base + 4);
+        e[0] = e0.x; e[1] = e0.y; e[2] = e0.z; e[3] = e0.w; e[4] = e1.x; e[5] = e1.y; e[6] = e1.z; e[7] = e1.w;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool ok = base + u < p1;
+        r[u] = ok ? a.rows[base + u] : INT_MAX;
+        c[u] = ok ? a.indices[base + u] : 0;
+        if constexpr (needs_eid<KIND>()) e[u] = ok ? a.eids[base + u] : 0;
+      }
+    }
+    float v[U][F];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (r[u] != INT_MAX) lane_value<KIND, F>(a, c[u], needs_eid<KIND>() ? e[u] : 0, v[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (r[u] == INT_MAX) break;
+      if (r[u] != cur) {
+        store_row<F>(cont ? a.carry + chunk * F : a.out + cur * F, acc);
+        for (int64_t g = cur + 1; g < r[u]; ++g) store_row<F>(a.out + g * F, ident);
+#pragma unroll
+        for (int i = 0; i < F; ++i) acc[i] = I;
+        cur = r[u];
+        cont = false;
+      }
+#pragma unroll
+      for (int i = 0; i < F; ++i) acc[i] = red_apply<RED>(acc[i], v[u][i]);
+    }
+  }
+  store_row<F>(cont ? a.carry + chunk * F : a.out + cur * F, acc);
+  if (p1 == a.nnz)
+    for (int64_t g = cur + 1; g < a.num_rows; ++g) store_row<F>(a.out + g * F, ident);
+}
+
+template <int RED, int F>
+__global__ void __launch_bounds__(kBlock) k_lane_fixup(FastArgs a) {
+  const int64_t chunk = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t K = a.chunk;
+  const int64_t p0 = chunk * K;
+  if (chunk == 0 || p0 >= a.nnz) return;
+  const int64_t r = a.rows[p0];
+  const int64_t start = a.indptr[r];
+  if (start >= p0 || start < p0 - K) return;
+  const int64_t last = (a.indptr[r + 1] - 1) / K;
+  float acc[F];
+  load_row<F>(a.out + r * F, acc);
+  for (int64_t c = chunk; c <= last; ++c) {
+    float t[F];
+    load_row<F>(a.carry + c * F, t);
+#pragma unroll
+    for (int i = 0; i < F; ++i) acc[i] = red_apply<RED>(acc[i], t[i]);
+  }
+  store_row<F>(a.out + r * F, acc);
+}
+
+template <int KIND, int RED, int F>
+void run_lane(const FastArgs& a, hipStream_t s) {
+  const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
+  const unsigned blocks = static_cast<unsigned>((chunks + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL((k_lane_reduce<KIND, RED, F>), dim3(blocks), dim3(kBlock), 0, s, a);
+  if (chunks > 1) hipLaunchKernelGGL((k_lane_fixup<RED, F>), dim3(blocks), dim3(kBlock), 0, s, a);
+}
+
+template <int KIND, int RED>
+void run_lane_f(const FastArgs& a, hipStream_t s) {
+  switch (a.F) {
+    case 1: run_lane<KIND, RED, 1>(a, s); break;
+    case 2: run_lane<KIND, RED, 2>(a, s); break;
+    case 3: run_lane<KIND, RED, 3>(a, s); break;
+    case 4: run_lane<KIND, RED, 4>(a, s); break;
+    case 5: run_lane<KIND, RED, 5>(a, s); break;
+    case 6: run_lane<KIND, RED, 6>(a, s); break;
+    case 7: run_lane<KIND, RED, 7>(a, s); break;
+    case 8: run_lane<KIND, RED, 8>(a, s); break;
+    case 12: run_lane<KIND, RED, 12>(a, s); break;
+    default: break;
+  }
+}
+
 struct Cfg {
   int L, NV;
 };
@@ -271,6 +448,10 @@ void run(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
 
 template <int KIND, int RED>
 void run_cfg(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
+  if (a.F < 16) {
+    run_lane_f<KIND, RED>(a, s);
+    return;
+  }
   const Cfg c = pick(a.F);
   switch (c.L * 10 + c.NV) {
     case 41: run<KIND, RED, 4, 1>(a, indptr, s); break;
@@ -294,8 +475,9 @@ int64_t fast_chunk_edges(int64_t nnz, int64_t F) {
     if (v >= 16 && (v & (v - 1)) == 0) return v;
   }
   // Measured on M1 (F = 16..256): 512 is best or within 1% (scripts/tune_spmm.py).
-  int64_t k = 512;
-  const int64_t groups_wanted = 256 /*CUs*/ * 64;
+  // Narrow rows (F < 16) use one lane per chunk: shorter chunks, more lanes.
+  int64_t k = F < 16 ? 128 : 512;
+  const int64_t groups_wanted = F < 16 ? 256 /*CUs*/ * 64 * 16 : 256 * 64;
   while (k > 32 && nnz / k < groups_wanted) k >>= 1;
   (void)F;
   return k;
@@ -308,7 +490,12 @@ int64_t fast_workspace_bytes(int64_t nnz, int64_t F) {
 }
 
 bool fast_supported(int kind, int64_t F, int64_t head_dim) {
-  if (F < 16 || F % 4 != 0 || F > 1024) return false;
+  if (F < 16) {
+    if (F < 1 || (F > 8 && F != 12)) return false;
+    if (kind == FAST_COL_MUL_EDGE_BCAST && (head_dim < 1 || F % head_dim != 0)) return false;
+    return true;
+  }
+  if (F % 4 != 0 || F > 1024) return false;
   if (kind == FAST_COL_MUL_EDGE_BCAST && (head_dim % 4 != 0 || F % head_dim != 0)) return false;
   return true;
 }

@@ -185,7 +185,7 @@ def plaw():
     return src, dst, n, _graph(src, dst, n), O.RefGraph(src, dst, n)
 
 
-@pytest.mark.parametrize("F", [16, 20, 64, 128, 256, 512, 1024, 6])
+@pytest.mark.parametrize("F", [1, 2, 3, 4, 7, 8, 12, 16, 20, 64, 128, 256, 512, 1024, 6, 10])
 @pytest.mark.parametrize("red", ["sum", "max", "min"])
 def test_copy_u_powerlaw(plaw, F, red):
     src, dst, n, g, ref = plaw
@@ -206,7 +206,7 @@ def test_copy_u_powerlaw(plaw, F, red):
         np.testing.assert_allclose(xt.grad.cpu().numpy(), r_g, rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("F", [16, 64, 256])
+@pytest.mark.parametrize("F", [1, 8, 16, 64, 256])
 def test_copy_e_powerlaw(plaw, F):
     src, dst, n, g, ref = plaw
     m = len(src)
@@ -223,7 +223,7 @@ def test_copy_e_powerlaw(plaw, F):
             np.testing.assert_array_equal(out.cpu().numpy(), r_out)
 
 
-@pytest.mark.parametrize("H,D", [(8, 8), (4, 16), (1, 64), (8, 3)])
+@pytest.mark.parametrize("H,D", [(8, 8), (4, 16), (1, 64), (8, 3), (2, 4), (8, 1), (1, 1)])
 def test_u_mul_e_bcast_powerlaw(plaw, H, D):
     """GAT aggregation: (N, H, D) x (E, H, 1) -> sum, forward and both gradients."""
     src, dst, n, g, ref = plaw
