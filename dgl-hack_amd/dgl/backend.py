@@ -64,6 +64,11 @@ class BinaryReduce(th.autograd.Function):
             grad_out = grad_out / degs
         grad_out = grad_out.contiguous()
         red = reducer if reducer != "mean" else "sum"
+        fused = _edge_grad_by_dot(red, binary_op, graph, lhs, rhs, lhs_data, rhs_data, grad_out,
+                                  lhs_map, rhs_map, out_map, ctx.needs_input_grad[5],
+                                  ctx.needs_input_grad[6])
+        if fused is not None:
+            return (None, None, None, None, None) + fused + (None,) * 5
         if ctx.needs_input_grad[5]:
             grad_lhs = grad_out.new_empty((lhs_data.shape[0],) + tuple(feat_shape))
             K.backward_lhs_binary_op_reduce(red, binary_op, graph, lhs, rhs, lhs_data, rhs_data,
@@ -77,6 +82,47 @@ class BinaryReduce(th.autograd.Function):
                                             out_map[1])
             grad_rhs = _reduce_grad(grad_rhs, rhs_data.shape)
         return None, None, None, None, None, grad_lhs, grad_rhs, None, None, None, None, None
+
+
+def _edge_grad_by_dot(red, op, graph, lhs, rhs, lhs_data, rhs_data, grad_out, lhs_map, rhs_map,
+                      out_map, need_l, need_r):
+    """u_mul_e_sum with the edge operand broadcast over the last feature dim
+    (GAT: ft (N, H, D) x a (E, H, 1)).  The reference materialises the edge
+    gradient in the broadcast OUTPUT shape (E, H, D) and sums it afterwards
+    (tensor.py:350-356, 572-601) -- E*H*D floats written and re-read.  The same
+    numbers come from one SDDMM: grad_a[e, h] = sum_d grad_out[dst, h, d] *
+    ft[src, h, d] = u_dot_v(ft, grad_out), so the edge gradient is computed
+    directly in its own shape.  The node gradient is the regular kernel."""
+    if op != "mul" or red != "sum":
+        return None
+    if any(m is not None for pair in (lhs_map, rhs_map, out_map) for m in pair):
+        return None
+    if lhs == SRC and rhs == EDGE:
+        node, edge, node_first = lhs_data, rhs_data, True
+    elif lhs == EDGE and rhs == SRC:
+        node, edge, node_first = rhs_data, lhs_data, False
+    else:
+        return None
+    if node.dim() != edge.dim() or node.dim() < 2 or edge.shape[-1] != 1 or node.shape[-1] == 1 \
+            or tuple(edge.shape[1:-1]) != tuple(node.shape[1:-1]):
+        return None
+    g_edge = grad_out.new_empty((edge.shape[0],) + tuple(node.shape[1:-1]))
+    K.binary_op_reduce("none", "dot", graph, SRC, DST, node, grad_out, g_edge)
+    g_edge = g_edge.view(edge.shape)
+    g_node = None
+    need_node = need_l if node_first else need_r
+    if need_node:
+        g_node = grad_out.new_empty(node.shape)
+        if node_first:
+            K.backward_lhs_binary_op_reduce("sum", "mul", graph, lhs, rhs, lhs_data, rhs_data,
+                                            grad_out, grad_out, g_node)
+        else:
+            K.backward_rhs_binary_op_reduce("sum", "mul", graph, lhs, rhs, lhs_data, rhs_data,
+                                            grad_out, grad_out, g_node)
+    need_edge = need_r if node_first else need_l
+    if not need_edge:
+        g_edge = None
+    return (g_node, g_edge) if node_first else (g_edge, g_node)
 
 
 def binary_reduce(reducer, binary_op, graph, lhs, rhs, lhs_data, rhs_data, out_size,
