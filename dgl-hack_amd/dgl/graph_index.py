@@ -166,6 +166,7 @@ class GraphIndex:
         self._dst = np.empty(0, np.int64)
         self._cache = {}
         self._host_csr = None
+        self._degs = None
         self._device_only = None  # (src, dst) device tensors when built on the GPU
 
     # ---- construction -----------------------------------------------------
@@ -180,6 +181,7 @@ class GraphIndex:
     def _invalidate(self):
         self._cache = {}
         self._host_csr = None
+        self._degs = None
 
     def add_nodes(self, num):
         if self._device_only is not None:
@@ -224,11 +226,24 @@ class GraphIndex:
             return (s.long().cpu().numpy(), d.long().cpu().numpy(), np.arange(self._m))
         return self._src, self._dst, np.arange(self._src.shape[0], dtype=np.int64)
 
+    def _degrees(self):
+        """(in, out) degrees, cached; device-built graphs read them off their CSRs."""
+        if self._degs is None:
+            if self._device_only is not None:
+                g = self.get_immutable_gidx(self._device_only[0].device)
+                self._degs = (g.in_csr.degrees().long().cpu().numpy(),
+                              g.out_csr.degrees().long().cpu().numpy())
+            else:
+                src, dst, _ = self.edges()
+                self._degs = (np.bincount(dst, minlength=self._n).astype(np.int64),
+                              np.bincount(src, minlength=self._n).astype(np.int64))
+        return self._degs
+
     def in_degrees(self):
-        return np.bincount(self.edges()[1], minlength=self._n).astype(np.int64)
+        return self._degrees()[0]
 
     def out_degrees(self):
-        return np.bincount(self.edges()[0], minlength=self._n).astype(np.int64)
+        return self._degrees()[1]
 
     def host_csr(self):
         """(out-CSR, in-CSR) host arrays, int64, bit-exact with the reference."""

@@ -1,0 +1,123 @@
+#!/usr/bin/env python3
+"""Secondary benchmarks for the BASELINE.json configs other than the headline:
+
+  C1  2-layer GraphConv on a Cora-sized graph (2,708 nodes / 13,264 edges incl.
+      self-loops, 1433 -> 16 -> 7): one training step (fwd + bwd + Adam)
+  C2  GraphConv layer on an ogbn-arxiv-sized graph (169,343 / 1,166,243, F = 128)
+  C3  GATConv (8 heads x 8) on a Reddit-sized graph (232,965 / 114,615,892,
+      F_in = 602): forward + backward
+
+Graphs are synthetic Chung-Lu power-law graphs with the configs' (N, E) (the
+datasets need network downloads).  Prints one JSON object per config.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "dgl-hack_amd"))
+
+import numpy as np  # noqa: E402
+import torch as th  # noqa: E402
+
+import dgl  # noqa: E402
+from dgl.nn.pytorch import GraphConv, GATConv  # noqa: E402
+
+
+def chung_lu(n, m, alpha, seed, device, self_loops=False):
+    g = th.Generator(device=device)
+    g.manual_seed(seed)
+    w = th.arange(1, n + 1, device=device, dtype=th.float64).pow(-alpha)
+    w = w[th.randperm(n, generator=g, device=device)]
+    src = th.multinomial(w.float(), m, replacement=True, generator=g).to(th.int32)
+    dst = th.multinomial(w.float(), m, replacement=True, generator=g).to(th.int32)
+    if self_loops:
+        ar = th.arange(n, device=device, dtype=th.int32)
+        src = th.cat([src, ar])
+        dst = th.cat([dst, ar])
+    return dgl.DGLGraph.from_device_coo(src, dst, n)
+
+
+def timeit(fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    th.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    th.cuda.synchronize()
+    return (time.perf_counter() - t) * 1000 / steps
+
+
+def c1(dev, steps, warmup):
+    g = chung_lu(2708, 10556, 0.5, 1, dev, self_loops=True)
+    x = th.randn(2708, 1433, device=dev)
+    y = th.randint(0, 7, (2708,), device=dev)
+    l1, l2 = GraphConv(1433, 16, activation=th.relu).to(dev), GraphConv(16, 7).to(dev)
+    opt = th.optim.Adam(list(l1.parameters()) + list(l2.parameters()), lr=0.01)
+
+    def step():
+        opt.zero_grad()
+        loss = th.nn.functional.cross_entropy(l2(g, l1(g, x)), y)
+        loss.backward()
+        opt.step()
+    ms = timeit(step, steps, warmup)
+    return {"config": "C1 Cora-size 2-layer GCN train step", "nodes": 2708,
+            "edges": g.number_of_edges(), "ms_per_step": ms}
+
+
+def c2(dev, steps, warmup):
+    n, m, f = 169343, 1166243, 128
+    g = chung_lu(n, m, 0.6, 2, dev)
+    x = th.randn(n, f, device=dev, requires_grad=True)
+    conv = GraphConv(f, f).to(dev)
+    gidx = g._graph.get_immutable_gidx(dev)
+    out = th.empty(n, f, device=dev)
+    ms_spmm = timeit(lambda: dgl.kernel.copy_reduce("sum", gidx, 0, x.detach(), out), steps, warmup)
+
+    def layer():
+        conv(g, x).sum().backward()
+    ms = timeit(layer, steps, warmup)
+    alg = 4 * (n + 1) + 4 * m + 4 * f * m + 4 * f * n
+    return {"config": "C2 arxiv-size GraphConv 128->128", "nodes": n, "edges": m,
+            "copy_u_sum_ms": ms_spmm, "copy_u_sum_alg_GBps": alg / ms_spmm / 1e6,
+            "copy_u_sum_Gedges_s": m / ms_spmm / 1e6, "layer_fwd_bwd_ms": ms}
+
+
+def c3(dev, steps, warmup):
+    n, m = 232965, 114615892
+    g = chung_lu(n, m, 0.4, 3, dev)
+    x = th.randn(n, 602, device=dev)
+    gat = GATConv(602, 8, 8).to(dev)
+    gat.train()
+
+    def fwd():
+        with th.no_grad():
+            gat(g, x)
+
+    def fwd_bwd():
+        gat(g, x).sum().backward()
+    ms_f = timeit(fwd, steps, warmup)
+    ms_fb = timeit(fwd_bwd, steps, warmup)
+    return {"config": "C3 Reddit-size GATConv 602 -> 8x8", "nodes": n, "edges": m,
+            "fwd_ms": ms_f, "fwd_bwd_ms": ms_fb, "fwd_Gedges_s": m / ms_f / 1e6,
+            "fwd_bwd_Gedges_s": m / ms_fb / 1e6}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="c1,c2,c3")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    args = ap.parse_args()
+    dev = "cuda:0"
+    for c in args.configs.split(","):
+        res = globals()[c](dev, args.steps, args.warmup)
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
