@@ -477,9 +477,18 @@ class DGLGraph(object):
             sel = _to_index_array(edges, "eid")
         return src[sel], dst[sel], eid[sel]
 
+    def _edge_tensors(self, edges, dev):
+        """(src, dst, eid) device tensors of the selected edges."""
+        if is_all(edges) and self._graph._device_only is not None:
+            s, d = self._graph._device_only
+            s, d = s.to(dev).long(), d.to(dev).long()
+            return s, d, th.arange(s.shape[0], device=dev)
+        src, dst, eid = self._resolve_edges(edges)
+        return (th.as_tensor(src, device=dev), th.as_tensor(dst, device=dev),
+                th.as_tensor(eid, device=dev))
+
     def apply_edges(self, func, edges=ALL, inplace=False):
         """Compute per-edge features with a builtin (reducer 'none') or a UDF."""
-        src, dst, eid = self._resolve_edges(edges)
         dev = self._device(self._node_frame, self._edge_frame)
         if isinstance(func, MessageFunction):
             m = self.number_of_edges()
@@ -488,6 +497,7 @@ class DGLGraph(object):
                 res = func._invoke(gidx, self._node_frame, self._node_frame, self._edge_frame, m,
                                    reducer="none")
             else:
+                src, dst, eid = self._resolve_edges(edges)
                 sub = _PartialIndex(self.number_of_nodes(), src, dst, eid)
                 gidx = sub.get_immutable_gidx(dev)
                 res = func._invoke(gidx, self._node_frame, self._node_frame, self._edge_frame, m,
@@ -498,9 +508,7 @@ class DGLGraph(object):
                 res = base.index_copy(0, sel, res[sel])
             self._edge_frame[func.out_field] = res
             return
-        s = th.as_tensor(src, device=dev)
-        d = th.as_tensor(dst, device=dev)
-        e = th.as_tensor(eid, device=dev)
+        s, d, e = self._edge_tensors(edges, dev)
         eb = EdgeBatch(s, d, e, {k: v[s] for k, v in self._node_frame.items()},
                        {k: v[d] for k, v in self._node_frame.items()},
                        {k: v[e] for k, v in self._edge_frame.items()})
