@@ -493,6 +493,51 @@ void backward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const 
   check_hip(hipGetLastError(), "generic backward launch");
 }
 
+// Shared argument checking of the fused GAT entry points.
+GatArgs gat_args(const DGLMIGraph* g, const DGLMIArray* ft, const DGLMIArray* el,
+                 const DGLMIArray* er, float slope, DGLMIArray* out, DGLMIArray* mx,
+                 DGLMIArray* sm) {
+  check_array(ft, "feat_src");
+  check_array(el, "el");
+  check_array(er, "er");
+  check_array(out, "out");
+  check_array(mx, "max");
+  check_array(sm, "sum");
+  DGLMI_CHECK(ft->ndim == 3, "feat_src must be (N, H, D)");
+  const int64_t H = ft->shape[1], D = ft->shape[2];
+  if (!gat_supported(H, D))
+    throw Error("fused GAT: unsupported heads/head_dim (" + std::to_string(H) + ", " +
+                std::to_string(D) + "); D must be a multiple of 4 with D/4 a power of two");
+  const DGLMICsr& in = g->in_csr;
+  check_csr(in, "in_csr", true);
+  DGLMI_CHECK(in.num_cols == ft->shape[0] || in.nnz == 0, "in_csr columns != feat_src rows");
+  DGLMI_CHECK(el->shape[0] == ft->shape[0] && feat_numel(el) == H, "el must be (N_src, H[, 1])");
+  DGLMI_CHECK(er->shape[0] == in.num_rows && feat_numel(er) == H, "er must be (N_dst, H[, 1])");
+  DGLMI_CHECK(out->shape[0] == in.num_rows && feat_numel(out) == H * D, "out must be (N_dst, H, D)");
+  DGLMI_CHECK(mx->shape[0] == in.num_rows && feat_numel(mx) == H, "max must be (N_dst, H)");
+  DGLMI_CHECK(sm->shape[0] == in.num_rows && feat_numel(sm) == H, "sum must be (N_dst, H)");
+  DGLMI_CHECK(aligned16(ft->data) && aligned16(out->data), "feat_src/out must be 16-byte aligned");
+  GatArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.indptr = in.indptr;
+  a.rows = in.rows;
+  a.indices = in.indices;
+  a.nnz = in.nnz;
+  a.num_rows = in.num_rows;
+  a.H = static_cast<int>(H);
+  a.D = static_cast<int>(D);
+  a.F = H * D;
+  a.slope = slope;
+  a.ft = ft->data;
+  a.el = el->data;
+  a.er = er->data;
+  a.out = out->data;
+  a.m = mx->data;
+  a.l = sm->data;
+  a.chunk = gat_chunk_edges(std::max<int64_t>(in.nnz, 1));
+  return a;
+}
+
 }  // namespace
 
 extern "C" {
@@ -581,6 +626,92 @@ int DGLMIKernelBackwardCopyReduce(const char* reducer, const DGLMIGraph* graph, 
   DeviceGuard guard(graph->device);
   backward(red, OP_USE_LHS, graph, target, DGLMI_TARGET_NONE, in_mapping, nullptr, out_mapping, in,
            nullptr, out, grad_out, grad_in, 0, static_cast<hipStream_t>(stream));
+  API_END();
+}
+
+int DGLMIFusedGatSupported(int64_t heads, int64_t head_dim) {
+  return gat_supported(heads, head_dim) ? 1 : 0;
+}
+
+int DGLMIFusedGatForward(const DGLMIGraph* graph, const DGLMIArray* feat_src, const DGLMIArray* el,
+                         const DGLMIArray* er, float negative_slope, DGLMIArray* out,
+                         DGLMIArray* max_out, DGLMIArray* sum_out, void* stream) {
+  API_BEGIN();
+  check_graph(graph);
+  DeviceGuard guard(graph->device);
+  GatArgs a = gat_args(graph, feat_src, el, er, negative_slope, out, max_out, sum_out);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const DGLMICsr& walk = graph->in_csr;
+  if (a.num_rows * a.F == 0) return 0;
+  if (walk.nnz == 0) {
+    launch_fill(out->data, a.num_rows * a.F, 0.0f, s);
+    launch_fill(max_out->data, a.num_rows * a.H, 0.0f, s);
+    launch_fill(sum_out->data, a.num_rows * a.H, 0.0f, s);
+    return 0;
+  }
+  const int64_t chunks = (walk.nnz + a.chunk - 1) / a.chunk;
+  Scratch carry(graph, chunks * (a.F + 2 * a.H) * static_cast<int64_t>(sizeof(float)), s);
+  a.carry = static_cast<float*>(carry.ptr);
+  launch_gat_forward(a, s);
+  check_hip(hipGetLastError(), "fused GAT forward launch");
+  API_END();
+}
+
+int DGLMIFusedGatBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src, const DGLMIArray* el,
+                          const DGLMIArray* er, float negative_slope, const DGLMIArray* out,
+                          const DGLMIArray* max_in, const DGLMIArray* sum_in,
+                          const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
+                          DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream) {
+  API_BEGIN();
+  check_graph(graph);
+  DeviceGuard guard(graph->device);
+  GatArgs a = gat_args(graph, feat_src, el, er, negative_slope, const_cast<DGLMIArray*>(out),
+                       const_cast<DGLMIArray*>(max_in), const_cast<DGLMIArray*>(sum_in));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  check_array(grad_out, "grad_out");
+  check_array(grad_feat_src, "grad_feat_src");
+  check_array(grad_el, "grad_el");
+  check_array(grad_er, "grad_er");
+  const int64_t n_src = feat_src->shape[0];
+  DGLMI_CHECK(grad_out->shape[0] == a.num_rows && feat_numel(grad_out) == a.F, "grad_out shape");
+  DGLMI_CHECK(grad_feat_src->shape[0] == n_src && feat_numel(grad_feat_src) == a.F, "grad_feat_src shape");
+  DGLMI_CHECK(grad_el->shape[0] == n_src && feat_numel(grad_el) == a.H, "grad_el shape");
+  DGLMI_CHECK(grad_er->shape[0] == a.num_rows && feat_numel(grad_er) == a.H, "grad_er shape");
+  const DGLMICsr& in = graph->in_csr;
+  const DGLMICsr& outc = graph->out_csr;
+  check_csr(outc, "out_csr", true);
+  DGLMI_CHECK(outc.num_rows == n_src, "out_csr rows != feat_src rows");
+  if (in.nnz == 0) {
+    launch_fill(grad_feat_src->data, n_src * a.F, 0.0f, s);
+    launch_fill(grad_el->data, n_src * a.H, 0.0f, s);
+    launch_fill(grad_er->data, a.num_rows * a.H, 0.0f, s);
+    return 0;
+  }
+  a.go = grad_out->data;
+  a.fo = out->data;
+  a.m_in = max_in->data;
+  a.l_in = sum_in->data;
+  a.g_er = grad_er->data;
+  a.g_el = grad_el->data;
+  a.g_ft = grad_feat_src->data;
+  const int64_t chunks = (in.nnz + a.chunk - 1) / a.chunk;
+  const int64_t stats_bytes = a.num_rows * a.H * 16;
+  const int64_t carry_bytes = chunks * (a.F + a.H) * static_cast<int64_t>(sizeof(float));
+  Scratch ws(graph, stats_bytes + carry_bytes + 256, s);
+  a.stats = static_cast<float4*>(ws.ptr);
+  a.carry = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + ((stats_bytes + 255) & ~int64_t(255)));
+  // destination side on the in-CSR
+  launch_gat_backward_dst(a, s);
+  check_hip(hipGetLastError(), "fused GAT backward (dst) launch");
+  // source side on the out-CSR
+  GatArgs b = a;
+  b.indptr = outc.indptr;
+  b.rows = outc.rows;
+  b.indices = outc.indices;
+  b.nnz = outc.nnz;
+  b.num_rows = outc.num_rows;
+  launch_gat_backward_src(b, s);
+  check_hip(hipGetLastError(), "fused GAT backward (src) launch");
   API_END();
 }
 

@@ -131,7 +131,7 @@ int bits_for(int64_t n) {
 
 size_t sort_temp_bytes(int64_t n, int64_t nnz) {
   size_t bytes = 0;
-  hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, static_cast<const int32_t*>(nullptr),
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, static_cast<const int32_t*>(nullptr),
                                      static_cast<int32_t*>(nullptr),
                                      static_cast<const int32_t*>(nullptr),
                                      static_cast<int32_t*>(nullptr), static_cast<int>(nnz), 0,
@@ -209,7 +209,7 @@ int DGLMICSRExpandRows(const int32_t* indptr, int64_t num_rows, int64_t nnz, int
   hipLaunchKernelGGL(k_mark_row_starts, dim3(grid_of(num_rows)), dim3(256), 0, s, indptr, num_rows,
                      rows);
   size_t temp_bytes = 0;
-  hipcub::DeviceScan::InclusiveScan(nullptr, temp_bytes, rows, rows, MaxOp(), static_cast<int>(nnz),
+  (void)hipcub::DeviceScan::InclusiveScan(nullptr, temp_bytes, rows, rows, MaxOp(), static_cast<int>(nnz),
                                     s);
   void* temp = nullptr;
   if (hipMallocAsync(&temp, temp_bytes, s) != hipSuccess) return -1;

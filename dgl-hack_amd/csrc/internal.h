@@ -163,4 +163,37 @@ int64_t fast_workspace_bytes(int64_t nnz, int64_t F);
 bool fast_supported(int kind, int64_t F, int64_t head_dim);
 void launch_fast_reduce(int kind, int red, const FastArgs& a, hipStream_t s);  // needs a.indptr
 
+// Fused GAT (kernels_gat.hip).
+struct GatArgs {
+  const int32_t* indptr;
+  const int32_t* rows;
+  const int32_t* indices;
+  int64_t nnz;
+  int64_t num_rows;
+  int H, D;
+  int64_t F;  // H * D
+  float slope;
+  const float* ft;  // (N_src, H, D)
+  const float* el;  // (N_src, H)
+  const float* er;  // (N_dst, H)
+  float* out;       // (N_dst, H, D)
+  float* m;         // (N_dst, H)
+  float* l;         // (N_dst, H)
+  const float* go;  // grad_out (N_dst, H, D)
+  const float* fo;  // forward out (N_dst, H, D)
+  const float* m_in;
+  const float* l_in;
+  float4* stats;    // (N_dst, H): {er, m, 1/l, delta}
+  float* g_er;
+  float* g_el;
+  float* g_ft;
+  float* carry;
+  int64_t chunk;
+};
+bool gat_supported(int64_t H, int64_t D);
+int64_t gat_chunk_edges(int64_t nnz);
+void launch_gat_forward(const GatArgs& a, hipStream_t s);
+void launch_gat_backward_dst(const GatArgs& a, hipStream_t s);
+void launch_gat_backward_src(const GatArgs& a, hipStream_t s);
+
 }  // namespace dglmi

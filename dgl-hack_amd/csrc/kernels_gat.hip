@@ -1,0 +1,612 @@
+// Fused GAT attention + aggregation for gfx950.
+//
+// The hack's fused GAT (src/kernel/cuda/binary_reduce_impl.cu:46-422 forward,
+// :124-357 + 1248-1308 backward; python FusedGat, tensor.py:383-420) replaces
+//   u_add_v -> leaky_relu -> edge_softmax -> u_mul_e_sum
+// by two kernels that materialise exp[E, H] and sum[N, H] (no max subtraction,
+// and an out-of-bounds row loop at :60), and a backward with atomics.
+//
+// Here, per destination row v and head h, ONE pass over the in-edges computes
+//   s_e = leaky(el[u, h] + er[v, h]),  m = max s_e,  l = sum exp(s_e - m),
+//   out[v, h, :] = sum exp(s_e - m) / l * ft[u, h, :]
+// with an online (running-max) softmax in registers -- no per-edge buffer at
+// all; only m and l (N x H) are kept for the backward pass.  Work is cut into
+// fixed edge chunks like kernels_spmm.hip; a row split across chunks leaves
+// (m, l, acc) partials that the fixup merges with the usual rescaling, in
+// chunk order (deterministic).
+//
+// Backward (attention-backward style, delta = rowsum(grad_out * out)):
+//   a_e    = exp(s_e - m_v) / l_v
+//   g_e    = <grad_out[v, h, :], ft[u, h, :]>
+//   dpre_e = a_e (g_e - delta_v) * (pre_e > 0 ? 1 : slope)
+//   grad_er[v] = sum_in dpre   (in-CSR walk, dst-owner; also writes delta and
+//                               packed per-(v, h) stats {er, m, 1/l, delta})
+//   grad_ft[u] = sum_out a_e grad_out[v],  grad_el[u] = sum_out dpre
+//                              (out-CSR walk, src-owner)
+// Everything owner-computes: no atomics.
+#include "internal.h"
+
+#include <climits>
+#include <cmath>
+
+namespace dglmi {
+
+
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr float kNegInf = -__builtin_huge_valf();
+
+__device__ __forceinline__ float4 ld4g(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4g(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ float leaky(float x, float s) { return x > 0.0f ? x : s * x; }
+__device__ __forceinline__ float dleaky(float x, float s) { return x > 0.0f ? 1.0f : s; }
+__device__ __forceinline__ float dot4(float4 a, float4 b) {
+  return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+}
+// sum over the D4 lanes of one head (D4 = D / 4, a power of two <= L)
+__device__ __forceinline__ float head_sum(float x, int d4) {
+  for (int off = 1; off < d4; off <<= 1) x += __shfl_xor(x, off);
+  return x;
+}
+
+// ---------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------
+template <int L, int NV>
+__global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
+  constexpr int G = kBlock / L;
+  constexpr int B = L > 16 ? L : 16;
+  constexpr int U = NV == 1 ? 8 : 4;
+  __shared__ int32_t s_row[G][B];
+  __shared__ int32_t s_col[G][B];
+  const int g = threadIdx.x / L;
+  const int lane = threadIdx.x % L;
+  const int64_t chunk = (int64_t)blockIdx.x * G + g;
+  const int64_t K = a.chunk;
+  const int64_t p0 = chunk * K;
+  if (p0 >= a.nnz) return;
+  const int64_t p1 = p0 + K < a.nnz ? p0 + K : a.nnz;
+  const int F4 = static_cast<int>(a.F / 4);
+  const int H = a.H, D = a.D;
+  const int64_t CW = a.F + 2 * H;  // carry record: acc[F], m[H], l[H]
+  int hd[NV];
+  bool ok4[NV], lead[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int f4 = lane + v * L;
+    ok4[v] = f4 < F4;
+    hd[v] = ok4[v] ? (4 * f4) / D : 0;
+    lead[v] = ok4[v] && ((4 * f4) % D == 0);
+  }
+  const float4 Z = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto zero_row = [&](int64_t r) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      if (ok4[v]) st4g(a.out + r * a.F + 4 * (lane + v * L), Z);
+      if (lead[v]) {
+        a.m[r * H + hd[v]] = 0.0f;
+        a.l[r * H + hd[v]] = 0.0f;
+      }
+    }
+  };
+  int64_t cur = a.rows[p0];
+  bool cont = p0 > 0 && a.rows[p0 - 1] == cur;
+  if (!cont) {
+    const int64_t first_gap = p0 > 0 ? (int64_t)a.rows[p0 - 1] + 1 : 0;
+    for (int64_t r = first_gap; r < cur; ++r) zero_row(r);
+  }
+  float mx[NV], sm[NV], erv[NV];
+  float4 acc[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    mx[v] = kNegInf;
+    sm[v] = 0.0f;
+    acc[v] = Z;
+    erv[v] = ok4[v] ? a.er[cur * H + hd[v]] : 0.0f;
+  }
+  // write a finished / partial row.  final: normalise; else raw (m, l, acc)
+  auto flush = [&](int64_t r, bool is_cont, bool final) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      if (!ok4[v]) continue;
+      const int f4 = lane + v * L;
+      if (is_cont) {
+        float* c = a.carry + chunk * CW;
+        st4g(c + 4 * f4, acc[v]);
+        if (lead[v]) {
+          c[a.F + hd[v]] = mx[v];
+          c[a.F + H + hd[v]] = sm[v];
+        }
+      } else {
+        float4 o = acc[v];
+        if (final) {
+          const float inv = sm[v] > 0.0f ? 1.0f / sm[v] : 0.0f;
+          o = make_float4(o.x * inv, o.y * inv, o.z * inv, o.w * inv);
+        }
+        st4g(a.out + r * a.F + 4 * f4, o);
+        if (lead[v]) {
+          a.m[r * H + hd[v]] = mx[v];
+          a.l[r * H + hd[v]] = sm[v];
+        }
+      }
+    }
+  };
+  for (int64_t base = p0; base < p1; base += B) {
+    for (int q = lane; q < B; q += L) {
+      const int64_t p = base + q;
+      const bool ok = p < p1;
+      s_row[g][q] = ok ? a.rows[p] : INT_MAX;
+      s_col[g][q] = ok ? a.indices[p] : 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int ub = 0; ub < B; ub += U) {
+      float4 val[U][NV];
+      float elv[U][NV];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t col = s_col[g][ub + u];
+        const bool ok = s_row[g][ub + u] != INT_MAX;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          const int f4 = lane + v * L;
+          val[u][v] = (ok && ok4[v]) ? ld4g(a.ft + col * a.F + 4 * f4) : Z;
+          elv[u][v] = (ok && ok4[v]) ? a.el[col * H + hd[v]] : 0.0f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int32_t r = s_row[g][ub + u];
+        if (r == INT_MAX) break;
+        if (r != cur) {
+          flush(cur, cont, true);
+          for (int64_t e = cur + 1; e < r; ++e) zero_row(e);
+          cur = r;
+          cont = false;
+#pragma unroll
+          for (int v = 0; v < NV; ++v) {
+            mx[v] = kNegInf;
+            sm[v] = 0.0f;
+            acc[v] = Z;
+            erv[v] = ok4[v] ? a.er[cur * H + hd[v]] : 0.0f;
+          }
+        }
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          const float s = leaky(elv[u][v] + erv[v], a.slope);
+          if (s > mx[v]) {
+            const float sc = expf(mx[v] - s);
+            acc[v] = make_float4(acc[v].x * sc, acc[v].y * sc, acc[v].z * sc, acc[v].w * sc);
+            sm[v] *= sc;
+            mx[v] = s;
+          }
+          const float pe = expf(s - mx[v]);
+          const float4 x = val[u][v];
+          acc[v] = make_float4(acc[v].x + pe * x.x, acc[v].y + pe * x.y, acc[v].z + pe * x.z,
+                               acc[v].w + pe * x.w);
+          sm[v] += pe;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  const bool continues = p1 < a.nnz && a.rows[p1] == cur;
+  flush(cur, cont, !continues);
+  if (p1 == a.nnz)
+    for (int64_t r = cur + 1; r < a.num_rows; ++r) zero_row(r);
+}
+
+template <int L, int NV>
+__global__ void __launch_bounds__(kBlock) k_gat_fwd_fixup(GatArgs a) {
+  constexpr int G = kBlock / L;
+  const int g = threadIdx.x / L;
+  const int lane = threadIdx.x % L;
+  const int64_t chunk = (int64_t)blockIdx.x * G + g;
+  const int64_t K = a.chunk;
+  const int64_t p0 = chunk * K;
+  if (chunk == 0 || p0 >= a.nnz) return;
+  const int64_t r = a.rows[p0];
+  const int64_t start = a.indptr[r];
+  if (start >= p0 || start < p0 - K) return;
+  const int64_t last = (a.indptr[r + 1] - 1) / K;
+  const int F4 = static_cast<int>(a.F / 4);
+  const int H = a.H;
+  const int64_t CW = a.F + 2 * H;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int f4 = lane + v * L;
+    if (f4 >= F4) continue;
+    const int h = (4 * f4) / a.D;
+    float4 acc = ld4g(a.out + r * a.F + 4 * f4);
+    float mx = a.m[r * H + h], sm = a.l[r * H + h];
+    for (int64_t c = chunk; c <= last; ++c) {
+      const float* cr = a.carry + c * CW;
+      const float4 ca = ld4g(cr + 4 * f4);
+      const float cm = cr[a.F + h], cl = cr[a.F + H + h];
+      const float mn = fmaxf(mx, cm);
+      const float f1 = expf(mx - mn), f2 = expf(cm - mn);
+      acc = make_float4(acc.x * f1 + ca.x * f2, acc.y * f1 + ca.y * f2, acc.z * f1 + ca.z * f2,
+                        acc.w * f1 + ca.w * f2);
+      sm = sm * f1 + cl * f2;
+      mx = mn;
+    }
+    const float inv = sm > 0.0f ? 1.0f / sm : 0.0f;
+    st4g(a.out + r * a.F + 4 * f4, make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv));
+    if ((4 * f4) % a.D == 0) {
+      a.m[r * H + h] = mx;
+      a.l[r * H + h] = sm;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward, destination side (in-CSR): grad_er, delta, packed stats
+// ---------------------------------------------------------------------------
+template <int L, int NV>
+__global__ void __launch_bounds__(kBlock) k_gat_bwd_dst(GatArgs a) {
+  constexpr int G = kBlock / L;
+  constexpr int B = L > 16 ? L : 16;
+  constexpr int U = NV == 1 ? 8 : 4;
+  __shared__ int32_t s_row[G][B];
+  __shared__ int32_t s_col[G][B];
+  const int g = threadIdx.x / L;
+  const int lane = threadIdx.x % L;
+  const int64_t chunk = (int64_t)blockIdx.x * G + g;
+  const int64_t K = a.chunk;
+  const int64_t p0 = chunk * K;
+  if (p0 >= a.nnz) return;
+  const int64_t p1 = p0 + K < a.nnz ? p0 + K : a.nnz;
+  const int F4 = static_cast<int>(a.F / 4);
+  const int H = a.H, D = a.D, D4 = a.D / 4;
+  int hd[NV];
+  bool ok4[NV], lead[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int f4 = lane + v * L;
+    ok4[v] = f4 < F4;
+    hd[v] = ok4[v] ? (4 * f4) / D : 0;
+    lead[v] = ok4[v] && ((4 * f4) % D == 0);
+  }
+  const float4 Z = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto zero_row = [&](int64_t r) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+      if (lead[v]) {
+        a.g_er[r * H + hd[v]] = 0.0f;
+        a.stats[r * H + hd[v]] = make_float4(a.er[r * H + hd[v]], 0.f, 0.f, 0.f);
+      }
+  };
+  float4 gov[NV];
+  float erv[NV], mv[NV], linv[NV], dlt[NV], acc[NV];
+  // per-row state: grad_out slice, er, m, 1/l, delta = <grad_out, out> per head
+  auto load_row = [&](int64_t r) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int f4 = lane + v * L;
+      gov[v] = ok4[v] ? ld4g(a.go + r * a.F + 4 * f4) : Z;
+      const float4 fo = ok4[v] ? ld4g(a.fo + r * a.F + 4 * f4) : Z;
+      dlt[v] = head_sum(dot4(gov[v], fo), D4);
+      erv[v] = ok4[v] ? a.er[r * H + hd[v]] : 0.0f;
+      mv[v] = ok4[v] ? a.m_in[r * H + hd[v]] : 0.0f;
+      const float lv = ok4[v] ? a.l_in[r * H + hd[v]] : 0.0f;
+      linv[v] = lv > 0.0f ? 1.0f / lv : 0.0f;
+      acc[v] = 0.0f;
+    }
+  };
+  auto flush = [&](int64_t r, bool is_cont) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      if (!lead[v]) continue;
+      if (is_cont) {
+        a.carry[chunk * H + hd[v]] = acc[v];
+      } else {
+        a.g_er[r * H + hd[v]] = acc[v];
+        a.stats[r * H + hd[v]] = make_float4(erv[v], mv[v], linv[v], dlt[v]);
+      }
+    }
+  };
+  int64_t cur = a.rows[p0];
+  bool cont = p0 > 0 && a.rows[p0 - 1] == cur;
+  if (!cont) {
+    const int64_t first_gap = p0 > 0 ? (int64_t)a.rows[p0 - 1] + 1 : 0;
+    for (int64_t r = first_gap; r < cur; ++r) zero_row(r);
+  }
+  load_row(cur);
+  for (int64_t base = p0; base < p1; base += B) {
+    for (int q = lane; q < B; q += L) {
+      const int64_t p = base + q;
+      const bool ok = p < p1;
+      s_row[g][q] = ok ? a.rows[p] : INT_MAX;
+      s_col[g][q] = ok ? a.indices[p] : 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int ub = 0; ub < B; ub += U) {
+      float4 ftv[U][NV];
+      float elv[U][NV];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t col = s_col[g][ub + u];
+        const bool ok = s_row[g][ub + u] != INT_MAX;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          const int f4 = lane + v * L;
+          ftv[u][v] = (ok && ok4[v]) ? ld4g(a.ft + col * a.F + 4 * f4) : Z;
+          elv[u][v] = (ok && ok4[v]) ? a.el[col * H + hd[v]] : 0.0f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int32_t r = s_row[g][ub + u];
+        if (r == INT_MAX) break;
+        if (r != cur) {
+          flush(cur, cont);
+          for (int64_t e = cur + 1; e < r; ++e) zero_row(e);
+          cur = r;
+          cont = false;
+          load_row(cur);
+        }
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          const float pre = elv[u][v] + erv[v];
+          const float att = expf(leaky(pre, a.slope) - mv[v]) * linv[v];
+          const float ge = head_sum(dot4(gov[v], ftv[u][v]), D4);
+          acc[v] += att * (ge - dlt[v]) * dleaky(pre, a.slope);
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  flush(cur, cont);
+  if (p1 == a.nnz)
+    for (int64_t r = cur + 1; r < a.num_rows; ++r) zero_row(r);
+}
+
+// ---------------------------------------------------------------------------
+// backward, source side (out-CSR): grad_ft, grad_el
+// ---------------------------------------------------------------------------
+template <int L, int NV>
+__global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
+  constexpr int G = kBlock / L;
+  constexpr int B = L > 16 ? L : 16;
+  constexpr int U = NV == 1 ? 8 : 4;
+  __shared__ int32_t s_row[G][B];
+  __shared__ int32_t s_col[G][B];
+  const int g = threadIdx.x / L;
+  const int lane = threadIdx.x % L;
+  const int64_t chunk = (int64_t)blockIdx.x * G + g;
+  const int64_t K = a.chunk;
+  const int64_t p0 = chunk * K;
+  if (p0 >= a.nnz) return;
+  const int64_t p1 = p0 + K < a.nnz ? p0 + K : a.nnz;
+  const int F4 = static_cast<int>(a.F / 4);
+  const int H = a.H, D = a.D, D4 = a.D / 4;
+  const int64_t CW = a.F + H;
+  int hd[NV];
+  bool ok4[NV], lead[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int f4 = lane + v * L;
+    ok4[v] = f4 < F4;
+    hd[v] = ok4[v] ? (4 * f4) / D : 0;
+    lead[v] = ok4[v] && ((4 * f4) % D == 0);
+  }
+  const float4 Z = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto zero_row = [&](int64_t r) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      if (ok4[v]) st4g(a.g_ft + r * a.F + 4 * (lane + v * L), Z);
+      if (lead[v]) a.g_el[r * H + hd[v]] = 0.0f;
+    }
+  };
+  float4 ftv[NV], accf[NV];
+  float elv[NV], acce[NV];
+  auto load_row = [&](int64_t r) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int f4 = lane + v * L;
+      ftv[v] = ok4[v] ? ld4g(a.ft + r * a.F + 4 * f4) : Z;
+      elv[v] = ok4[v] ? a.el[r * H + hd[v]] : 0.0f;
+      accf[v] = Z;
+      acce[v] = 0.0f;
+    }
+  };
+  auto flush = [&](int64_t r, bool is_cont) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      if (!ok4[v]) continue;
+      const int f4 = lane + v * L;
+      float* dst = is_cont ? a.carry + chunk * CW : a.g_ft + r * a.F;
+      st4g(dst + 4 * f4, accf[v]);
+      if (lead[v]) {
+        if (is_cont) a.carry[chunk * CW + a.F + hd[v]] = acce[v];
+        else a.g_el[r * H + hd[v]] = acce[v];
+      }
+    }
+  };
+  int64_t cur = a.rows[p0];
+  bool cont = p0 > 0 && a.rows[p0 - 1] == cur;
+  if (!cont) {
+    const int64_t first_gap = p0 > 0 ? (int64_t)a.rows[p0 - 1] + 1 : 0;
+    for (int64_t r = first_gap; r < cur; ++r) zero_row(r);
+  }
+  load_row(cur);
+  for (int64_t base = p0; base < p1; base += B) {
+    for (int q = lane; q < B; q += L) {
+      const int64_t p = base + q;
+      const bool ok = p < p1;
+      s_row[g][q] = ok ? a.rows[p] : INT_MAX;
+      s_col[g][q] = ok ? a.indices[p] : 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int ub = 0; ub < B; ub += U) {
+      float4 gov[U][NV], st[U][NV];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t col = s_col[g][ub + u];
+        const bool ok = s_row[g][ub + u] != INT_MAX;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          const int f4 = lane + v * L;
+          gov[u][v] = (ok && ok4[v]) ? ld4g(a.go + col * a.F + 4 * f4) : Z;
+          st[u][v] = (ok && ok4[v]) ? a.stats[col * H + hd[v]] : Z;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int32_t r = s_row[g][ub + u];
+        if (r == INT_MAX) break;
+        if (r != cur) {
+          flush(cur, cont);
+          for (int64_t e = cur + 1; e < r; ++e) zero_row(e);
+          cur = r;
+          cont = false;
+          load_row(cur);
+        }
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          const float4 sv = st[u][v];  // {er, m, 1/l, delta} of the destination
+          const float pre = elv[v] + sv.x;
+          const float att = expf(leaky(pre, a.slope) - sv.y) * sv.z;
+          const float4 gv = gov[u][v];
+          const float ge = head_sum(dot4(gv, ftv[v]), D4);
+          acce[v] += att * (ge - sv.w) * dleaky(pre, a.slope);
+          accf[v] = make_float4(accf[v].x + att * gv.x, accf[v].y + att * gv.y,
+                                accf[v].z + att * gv.z, accf[v].w + att * gv.w);
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  flush(cur, cont);
+  if (p1 == a.nnz)
+    for (int64_t r = cur + 1; r < a.num_rows; ++r) zero_row(r);
+}
+
+// carries of the backward walks: plain sums (W floats per chunk record, the first
+// `wf` of them are per-float4 slots, the rest per head)
+template <int L, int NV>
+__global__ void __launch_bounds__(kBlock) k_gat_bwd_fixup(GatArgs a, float* vec_out, float* head_out,
+                                                          int with_vec) {
+  constexpr int G = kBlock / L;
+  const int g = threadIdx.x / L;
+  const int lane = threadIdx.x % L;
+  const int64_t chunk = (int64_t)blockIdx.x * G + g;
+  const int64_t K = a.chunk;
+  const int64_t p0 = chunk * K;
+  if (chunk == 0 || p0 >= a.nnz) return;
+  const int64_t r = a.rows[p0];
+  const int64_t start = a.indptr[r];
+  if (start >= p0 || start < p0 - K) return;
+  const int64_t last = (a.indptr[r + 1] - 1) / K;
+  const int F4 = static_cast<int>(a.F / 4);
+  const int H = a.H;
+  const int64_t CW = with_vec ? a.F + H : H;
+  const int64_t hoff = with_vec ? a.F : 0;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int f4 = lane + v * L;
+    if (f4 >= F4) continue;
+    const int h = (4 * f4) / a.D;
+    const bool lead = (4 * f4) % a.D == 0;
+    float4 accf = with_vec ? ld4g(vec_out + r * a.F + 4 * f4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float acce = lead ? head_out[r * H + h] : 0.0f;
+    for (int64_t c = chunk; c <= last; ++c) {
+      const float* cr = a.carry + c * CW;
+      if (with_vec) {
+        const float4 t = ld4g(cr + 4 * f4);
+        accf = make_float4(accf.x + t.x, accf.y + t.y, accf.z + t.z, accf.w + t.w);
+      }
+      if (lead) acce += cr[hoff + h];
+    }
+    if (with_vec) st4g(vec_out + r * a.F + 4 * f4, accf);
+    if (lead) head_out[r * H + h] = acce;
+  }
+}
+
+struct Cfg {
+  int L, NV;
+};
+Cfg pick(int64_t F) {
+  const int64_t F4 = F / 4;
+  if (F4 <= 4) return {4, 1};
+  if (F4 <= 8) return {8, 1};
+  if (F4 <= 16) return {16, 1};
+  if (F4 <= 32) return {32, 1};
+  if (F4 <= 64) return {64, 1};
+  if (F4 <= 128) return {64, 2};
+  return {64, 4};
+}
+
+template <int L, int NV>
+void fwd_cfg(const GatArgs& a, hipStream_t s) {
+  constexpr int G = kBlock / L;
+  const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
+  const unsigned blocks = static_cast<unsigned>((chunks + G - 1) / G);
+  hipLaunchKernelGGL((k_gat_fwd<L, NV>), dim3(blocks), dim3(kBlock), 0, s, a);
+  if (chunks > 1) hipLaunchKernelGGL((k_gat_fwd_fixup<L, NV>), dim3(blocks), dim3(kBlock), 0, s, a);
+}
+
+template <int L, int NV>
+void bwd_dst_cfg(const GatArgs& a, hipStream_t s) {
+  constexpr int G = kBlock / L;
+  const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
+  const unsigned blocks = static_cast<unsigned>((chunks + G - 1) / G);
+  hipLaunchKernelGGL((k_gat_bwd_dst<L, NV>), dim3(blocks), dim3(kBlock), 0, s, a);
+  if (chunks > 1)
+    hipLaunchKernelGGL((k_gat_bwd_fixup<L, NV>), dim3(blocks), dim3(kBlock), 0, s, a,
+                       static_cast<float*>(nullptr), a.g_er, 0);
+}
+
+template <int L, int NV>
+void bwd_src_cfg(const GatArgs& a, hipStream_t s) {
+  constexpr int G = kBlock / L;
+  const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
+  const unsigned blocks = static_cast<unsigned>((chunks + G - 1) / G);
+  hipLaunchKernelGGL((k_gat_bwd_src<L, NV>), dim3(blocks), dim3(kBlock), 0, s, a);
+  if (chunks > 1)
+    hipLaunchKernelGGL((k_gat_bwd_fixup<L, NV>), dim3(blocks), dim3(kBlock), 0, s, a, a.g_ft,
+                       a.g_el, 1);
+}
+
+#define DGLMI_GAT_DISPATCH(FN, a, s)                   \
+  do {                                                 \
+    const Cfg c = pick((a).F);                         \
+    switch (c.L * 10 + c.NV) {                         \
+      case 41: FN<4, 1>(a, s); break;                  \
+      case 81: FN<8, 1>(a, s); break;                  \
+      case 161: FN<16, 1>(a, s); break;                \
+      case 321: FN<32, 1>(a, s); break;                \
+      case 641: FN<64, 1>(a, s); break;                \
+      case 642: FN<64, 2>(a, s); break;                \
+      default: FN<64, 4>(a, s); break;                 \
+    }                                                  \
+  } while (0)
+
+}  // namespace
+
+bool gat_supported(int64_t H, int64_t D) {
+  if (H < 1 || D < 4 || D % 4 != 0) return false;
+  const int64_t d4 = D / 4;
+  if ((d4 & (d4 - 1)) != 0) return false;       // head lanes reduce by xor-shuffle
+  const int64_t F = H * D;
+  if (F > 1024) return false;
+  return d4 <= pick(F).L;
+}
+
+int64_t gat_chunk_edges(int64_t nnz) { return fast_chunk_edges(nnz, 64); }
+
+void launch_gat_forward(const GatArgs& a, hipStream_t s) { DGLMI_GAT_DISPATCH(fwd_cfg, a, s); }
+void launch_gat_backward_dst(const GatArgs& a, hipStream_t s) { DGLMI_GAT_DISPATCH(bwd_dst_cfg, a, s); }
+void launch_gat_backward_src(const GatArgs& a, hipStream_t s) { DGLMI_GAT_DISPATCH(bwd_src_cfg, a, s); }
+
+}  // namespace dglmi

@@ -106,6 +106,16 @@ _SIGS = {
         ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
         ctypes.c_void_p]),
+    "DGLMIFusedGatSupported": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64]),
+    "DGLMIFusedGatForward": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_float, ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_void_p]),
+    "DGLMIFusedGatBackward": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_float, ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_void_p]),
     "DGLMIPartitionLDG": (ctypes.c_int, [
         ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_double,
         ctypes.c_void_p]),

@@ -186,3 +186,40 @@ def _reduce_grad(grad, shape):
     reduce_idx = tuple(i + 1 for i, (a, b) in enumerate(zip(grad_shape, in_shape)) if a != b)
     grad = grad.sum(dim=reduce_idx, keepdim=True)
     return grad.view(shape)
+
+
+class FusedGat(th.autograd.Function):
+    """tensor.py:383-413 (FusedGat), max-stabilised and without per-edge buffers."""
+
+    @staticmethod
+    def forward(ctx, gidx, feat_src, el, er, slope):
+        feat_src, el, er = feat_src.contiguous(), el.contiguous(), er.contiguous()
+        n_dst = er.shape[0]
+        H, D = feat_src.shape[1], feat_src.shape[2]
+        out = feat_src.new_empty((n_dst, H, D))
+        mx = feat_src.new_empty((n_dst, H))
+        sm = feat_src.new_empty((n_dst, H))
+        K.fused_gat_forward(gidx, feat_src, el, er, slope, out, mx, sm)
+        ctx.gidx, ctx.slope = gidx, slope
+        ctx.save_for_backward(feat_src, el, er, out, mx, sm)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        feat_src, el, er, out, mx, sm = ctx.saved_tensors
+        grad_out = grad_out.contiguous()
+        g_ft = th.empty_like(feat_src)
+        g_el = th.empty_like(el)
+        g_er = th.empty_like(er)
+        K.fused_gat_backward(ctx.gidx, feat_src, el, er, ctx.slope, out, mx, sm, grad_out, g_ft,
+                             g_el, g_er)
+        return None, g_ft, g_el, g_er, None
+
+
+def fused_gat(graph, feat_src, el, er, slope):
+    """backend.py:1235 / tensor.py:415-420: softmax attention + aggregation in one kernel.
+
+    ``graph`` is a DGLGraph (or an ImmutableGraphIndex); feat_src (N, H, D), el / er
+    (N, H, 1).  Returns (N, H, D)."""
+    gidx = graph if hasattr(graph, "in_csr") else graph._graph.get_immutable_gidx(feat_src.device)
+    return FusedGat.apply(gidx, feat_src, el, er, float(slope))

@@ -170,3 +170,30 @@ def _TARGET_CODE(t):
     if isinstance(t, str):
         return _TARGET[t]
     return int(t)
+
+
+def fused_gat_supported(heads, head_dim):
+    return bool(_ffi.lib().DGLMIFusedGatSupported(int(heads), int(head_dim)))
+
+
+def fused_gat_forward(graph, feat_src, el, er, slope, out, max_out, sum_out):
+    """_CAPI_DGLFusedGatKernel (binary_reduce.cc:380-396) -> DGLMIFusedGatForward."""
+    _check_ctx(graph, [("feat_src", feat_src), ("el", el), ("er", er), ("out", out)])
+    g = graph.cstruct(None)
+    check_call(_ffi.lib().DGLMIFusedGatForward(
+        ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"),
+        float(slope), _arr(out, "out"), _arr(max_out, "max_out"), _arr(sum_out, "sum_out"),
+        _stream(out)))
+    return out
+
+
+def fused_gat_backward(graph, feat_src, el, er, slope, out, max_in, sum_in, grad_out,
+                       grad_feat_src, grad_el, grad_er):
+    """_CAPI_DGLKernelBackwardFusedGat (binary_reduce.cc:529-549) -> DGLMIFusedGatBackward."""
+    _check_ctx(graph, [("feat_src", feat_src), ("grad_out", grad_out)])
+    g = graph.cstruct(None)
+    check_call(_ffi.lib().DGLMIFusedGatBackward(
+        ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"), float(slope),
+        _arr(out, "out"), _arr(max_in, "max_in"), _arr(sum_in, "sum_in"),
+        _arr(grad_out, "grad_out"), _arr(grad_feat_src, "grad_feat_src"), _arr(grad_el, "grad_el"),
+        _arr(grad_er, "grad_er"), _stream(grad_out)))

@@ -1,0 +1,43 @@
+"""FusedGATConv (``python/dgl/nn/pytorch/conv/fusedGatConv.py:16-166``).
+
+GATConv whose attention softmax and aggregation run as one fused HIP kernel
+(``dgl.backend.fused_gat``, csrc/kernels_gat.hip).  Falls back to the
+unfused GATConv composition when the head size is not supported by the fused
+kernel or attention dropout is active (the fused kernel has no per-edge
+buffer to drop out).  The reference's timing prints are not reproduced.
+"""
+import torch as th
+
+from .... import backend as B
+from .... import kernel as K
+from .gatconv import GATConv
+
+
+class FusedGATConv(GATConv):
+    def __init__(self, in_feats, out_feats, num_heads, feat_drop=0., attn_drop=0.,
+                 negative_slope=0.2, residual=False, activation=None):
+        super(FusedGATConv, self).__init__(in_feats, out_feats, num_heads, feat_drop, attn_drop,
+                                           negative_slope, residual, activation)
+        self.negative_slope = negative_slope
+
+    def forward(self, graph, feat):
+        attn_dropout = self.training and self.attn_drop.p > 0
+        if attn_dropout or not K.fused_gat_supported(self._num_heads, self._out_feats):
+            return super(FusedGATConv, self).forward(graph, feat)
+        if isinstance(feat, tuple):
+            h_src = self.feat_drop(feat[0])
+            h_dst = self.feat_drop(feat[1])
+            feat_src = self.fc_src(h_src).view(-1, self._num_heads, self._out_feats)
+            feat_dst = self.fc_dst(h_dst).view(-1, self._num_heads, self._out_feats)
+        else:
+            h_src = h_dst = self.feat_drop(feat)
+            feat_src = feat_dst = self.fc(h_src).view(-1, self._num_heads, self._out_feats)
+        el = (feat_src * self.attn_l).sum(dim=-1).unsqueeze(-1)
+        er = (feat_dst * self.attn_r).sum(dim=-1).unsqueeze(-1)
+        rst = B.fused_gat(graph, feat_src, el, er, self.negative_slope)
+        if self.res_fc is not None:
+            resval = self.res_fc(h_dst).view(h_dst.shape[0], -1, self._out_feats)
+            rst = rst + resval
+        if self.activation:
+            rst = self.activation(rst)
+        return rst

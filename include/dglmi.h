@@ -155,6 +155,25 @@ int DGLMICOOToCSRDevice(int64_t num_rows, int64_t nnz, const int32_t* row, const
 int DGLMICSRExpandRows(const int32_t* indptr, int64_t num_rows, int64_t nnz, int32_t* rows,
                        void* stream);
 
+/* ---- fused GAT (hack kernels _CAPI_DGLFusedGatKernel / _CAPI_DGLKernelBackwardFusedGat,
+ * binary_reduce.cc:380-396, 529-549) ------------------------------------------
+ * out[v,h,:] = sum_{u->v} softmax_v(leaky(el[u,h] + er[v,h])) * feat_src[u,h,:], with a
+ * max-stabilised online softmax; instead of the reference's per-edge exp[E,H] and
+ * sum[N,H] buffers the forward keeps max_out[N,H] and sum_out[N,H] (= sum exp(s - max)).
+ * feat_src (N_src, H, D) with D a multiple of 4 and D/4 a power of two, H*D <= 1024;
+ * el (N_src, H[, 1]); er (N_dst, H[, 1]); out (N_dst, H, D).  The backward writes all
+ * three gradients (overwriting). */
+int DGLMIFusedGatForward(const DGLMIGraph* graph, const DGLMIArray* feat_src, const DGLMIArray* el,
+                         const DGLMIArray* er, float negative_slope, DGLMIArray* out,
+                         DGLMIArray* max_out, DGLMIArray* sum_out, void* stream);
+int DGLMIFusedGatBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src, const DGLMIArray* el,
+                          const DGLMIArray* er, float negative_slope, const DGLMIArray* out,
+                          const DGLMIArray* max_in, const DGLMIArray* sum_in,
+                          const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
+                          DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream);
+/* 1 if the fused GAT kernels support (heads, head_dim), else 0. */
+int DGLMIFusedGatSupported(int64_t heads, int64_t head_dim);
+
 /* ---- partitioning (metis_partition.cc:19-66 replacement; METIS is absent) --
  * Linear Deterministic Greedy over a symmetrised host CSR (int64): node v goes
  * to the part maximising |N(v) ∩ P| (1 - |P| / C), C = ceil(n / k)(1 + slack). */

@@ -24,7 +24,7 @@ import numpy as np  # noqa: E402
 import torch as th  # noqa: E402
 
 import dgl  # noqa: E402
-from dgl.nn.pytorch import GraphConv, GATConv  # noqa: E402
+from dgl.nn.pytorch import GraphConv, GATConv, FusedGATConv  # noqa: E402
 
 
 def chung_lu(n, m, alpha, seed, device, self_loops=False):
@@ -102,9 +102,21 @@ def c3(dev, steps, warmup):
         gat(g, x).sum().backward()
     ms_f = timeit(fwd, steps, warmup)
     ms_fb = timeit(fwd_bwd, steps, warmup)
+    fgat = FusedGATConv(602, 8, 8).to(dev)
+    fgat.load_state_dict(gat.state_dict())
+
+    def ffwd():
+        with th.no_grad():
+            fgat(g, x)
+
+    def ffwd_bwd():
+        fgat(g, x).sum().backward()
+    ms_ff = timeit(ffwd, steps, warmup)
+    ms_ffb = timeit(ffwd_bwd, steps, warmup)
     return {"config": "C3 Reddit-size GATConv 602 -> 8x8", "nodes": n, "edges": m,
-            "fwd_ms": ms_f, "fwd_bwd_ms": ms_fb, "fwd_Gedges_s": m / ms_f / 1e6,
-            "fwd_bwd_Gedges_s": m / ms_fb / 1e6}
+            "unfused_fwd_ms": ms_f, "unfused_fwd_bwd_ms": ms_fb,
+            "fused_fwd_ms": ms_ff, "fused_fwd_bwd_ms": ms_ffb,
+            "fused_fwd_Gedges_s": m / ms_ff / 1e6, "fused_fwd_bwd_Gedges_s": m / ms_ffb / 1e6}
 
 
 def main():

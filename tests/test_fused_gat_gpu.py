@@ -1,0 +1,118 @@
+"""Fused GAT kernel vs the unfused builtin composition (the hack's own
+examples/pytorch/gat/fused_gat_unit_test.py strategy: 65,536 nodes, every node
+-> hub 0 and hub 1, 8 heads x 8 hidden, slope 0.2) and vs a dense fp64
+restatement on a skewed graph with empty rows."""
+import numpy as np
+import pytest
+import torch as th
+
+import dgl
+import dgl.backend as B
+import dgl.function as fn
+from graphs import powerlaw
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def unfused(g, feat_src, el, er, slope):
+    """fused_gat_unit_test.py:37-52 (exp without max subtraction, as the reference)."""
+    g = g.local_var()
+    g.srcdata.update({"ft": feat_src, "el": el})
+    g.dstdata.update({"er": er})
+    g.apply_edges(fn.u_add_v("el", "er", "e"))
+    e = th.nn.functional.leaky_relu(g.edata.pop("e"), slope)
+    g.edata["out"] = th.exp(e)
+    g.update_all(fn.copy_e("out", "m"), fn.sum("m", "out_sum"))
+    g.apply_edges(fn.e_div_v("out", "out_sum", "out1"))
+    g.edata["a"] = g.edata["out1"]
+    g.update_all(fn.u_mul_e("ft", "a", "m"), fn.sum("m", "ft"))
+    return g.dstdata["ft"]
+
+
+@pytest.mark.parametrize("H,D", [(8, 8), (4, 16), (1, 4), (2, 32), (8, 128)])
+def test_fused_gat_two_hubs(H, D):
+    n = 65536 if H * D <= 64 else 8192
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(list(range(n)), 0)
+    g.add_edges(list(range(n)), 1)
+    th.manual_seed(0)
+    ft = th.rand(n, H, D, device=DEV, requires_grad=True)
+    el = th.rand(n, H, 1, device=DEV, requires_grad=True)
+    er = th.rand(n, H, 1, device=DEV, requires_grad=True)
+    r1 = unfused(g, ft, el, er, 0.2)
+    r2 = B.fused_gat(g, ft, el, er, 0.2)
+    assert th.allclose(r1, r2, rtol=1e-4, atol=1e-5)
+    go = th.rand_like(r1)
+    g1 = th.autograd.grad(r1, (ft, el, er), go)
+    g2 = th.autograd.grad(r2, (ft, el, er), go)
+    for a, b, name in zip(g1, g2, ("ft", "el", "er")):
+        assert th.allclose(a, b, rtol=1e-3, atol=1e-5), name
+
+
+def dense_gat(src, dst, n, ft, el, er, slope):
+    s = th.from_numpy(src).to(DEV)
+    d = th.from_numpy(dst).to(DEV)
+    H = ft.shape[1]
+    e = th.nn.functional.leaky_relu(el[s, :, 0] + er[d, :, 0], slope)
+    emax = th.full((n, H), -1e300, dtype=th.float64, device=DEV).index_reduce(0, d, e, "amax")
+    ex = th.exp(e - emax[d])
+    den = th.zeros(n, H, dtype=th.float64, device=DEV).index_add(0, d, ex)
+    a = ex / den[d]
+    return th.zeros(n, H, ft.shape[2], dtype=th.float64, device=DEV).index_add(0, d, ft[s] * a[:, :, None])
+
+
+@pytest.mark.parametrize("H,D", [(8, 8), (4, 4), (3, 16)])
+def test_fused_gat_powerlaw_vs_dense(H, D):
+    src, dst, n = powerlaw(20000, 300000, seed=11)
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    gen = th.Generator(device=DEV).manual_seed(3)
+    ft = th.randn(n, H, D, device=DEV, generator=gen).requires_grad_()
+    el = (3 * th.randn(n, H, 1, device=DEV, generator=gen)).requires_grad_()  # large logits
+    er = (3 * th.randn(n, H, 1, device=DEV, generator=gen)).requires_grad_()
+    out = B.fused_gat(g, ft, el, er, 0.2)
+    go = th.randn(out.shape, device=DEV, generator=gen)
+    gf = th.autograd.grad(out, (ft, el, er), go)
+    fd, eld, erd = (t.detach().double().requires_grad_() for t in (ft, el, er))
+    ref = dense_gat(src, dst, n, fd, eld, erd, 0.2)
+    gr = th.autograd.grad(ref, (fd, eld, erd), go.double())
+    assert th.allclose(out.double(), ref, rtol=1e-4, atol=1e-4)
+    for a, b, name in zip(gf, gr, ("ft", "el", "er")):
+        err = (a.double() - b).abs().max().item()
+        assert th.allclose(a.double(), b, rtol=1e-3, atol=1e-3), (name, err)
+    # zero in-degree rows are exact zeros
+    zero = th.from_numpy(np.bincount(dst, minlength=n) == 0).to(DEV)
+    assert (out[zero] == 0).all()
+
+
+def test_fused_gatconv_matches_gatconv():
+    from dgl.nn.pytorch import GATConv, FusedGATConv
+    src, dst, n = powerlaw(5000, 60000, seed=2)
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(np.concatenate([src, np.arange(n)]), np.concatenate([dst, np.arange(n)]))
+    th.manual_seed(0)
+    a = GATConv(32, 8, 8).to(DEV)
+    b = FusedGATConv(32, 8, 8).to(DEV)
+    b.load_state_dict(a.state_dict())
+    x = th.randn(n, 32, device=DEV)
+    ya, yb = a(g, x), b(g, x)
+    assert th.allclose(ya, yb, rtol=1e-4, atol=1e-5)
+    ya.pow(2).sum().backward()
+    yb.pow(2).sum().backward()
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert th.allclose(pa.grad, pb.grad, rtol=1e-3, atol=1e-4)
+
+
+def test_fused_gat_deterministic():
+    src, dst, n = powerlaw(20000, 300000, seed=1)
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    ft = th.randn(n, 8, 8, device=DEV)
+    el = th.randn(n, 8, 1, device=DEV)
+    er = th.randn(n, 8, 1, device=DEV)
+    assert th.equal(B.fused_gat(g, ft, el, er, 0.2), B.fused_gat(g, ft, el, er, 0.2))
