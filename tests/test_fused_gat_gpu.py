@@ -47,8 +47,11 @@ def test_fused_gat_two_hubs(H, D):
     go = th.rand_like(r1)
     g1 = th.autograd.grad(r1, (ft, el, er), go)
     g2 = th.autograd.grad(r2, (ft, el, er), go)
-    for a, b, name in zip(g1, g2, ("ft", "el", "er")):
-        assert th.allclose(a, b, rtol=1e-3, atol=1e-5), name
+    # grad_er of a hub is sum_e a_e (g_e - delta) over 65,536 in-edges, which cancels
+    # to exactly 0 here (all logits > 0, so the leaky derivative is 1): both paths
+    # return fp32 noise of ~1e-5 relative to sum |a_e (g_e - delta)| ~ O(1)
+    for a, b, name, atol in zip(g1, g2, ("ft", "el", "er"), (1e-5, 1e-5, 1e-4)):
+        assert th.allclose(a, b, rtol=1e-3, atol=atol), name
 
 
 def dense_gat(src, dst, n, ft, el, er, slope):
