@@ -83,12 +83,33 @@ __device__ __forceinline__ float4 edge_value(const FastArgs& a, int32_t col, int
   }
 }
 
+template <int VAR>
+__device__ __forceinline__ int32_t ld_stream(const int32_t* p) {
+  if constexpr (VAR & 1) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <int VAR>
+__device__ __forceinline__ void st_out(float* p, float4 v) {
+  if constexpr (VAR & 2) {
+    __builtin_nontemporal_store(v.x, p);
+    __builtin_nontemporal_store(v.y, p + 1);
+    __builtin_nontemporal_store(v.z, p + 2);
+    __builtin_nontemporal_store(v.w, p + 3);
+  } else {
+    st4(p, v);
+  }
+}
+
 // L lanes per group, NV float4 per lane, U gathers in flight per lane-slot.
-template <int KIND, int RED, int L, int NV>
+// VAR (tuning variants): bit 0 non-temporal index/row stream loads, bit 1
+// non-temporal output stores, bit 2 twice the gathers in flight.  Default 3:
+// keeping the once-read CSR stream and the once-written output out of L2/MALL
+// leaves more room for re-read source rows (M1: 3.30 -> 3.25 ms; 4 and 7 spill).
+template <int KIND, int RED, int L, int NV, int VAR = 3>
 __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32_t* __restrict__ indptr) {
   constexpr int G = kBlock / L;           // groups per block
-  constexpr int B = L > 16 ? L : 16;      // positions staged per step
-  constexpr int U = NV == 1 ? 8 : (NV == 2 ? 4 : 2);
+  constexpr int B = (L > 16 ? L : 16) * ((VAR & 4) ? 2 : 1);  // positions staged per step
+  constexpr int U = (NV == 1 ? 8 : (NV == 2 ? 4 : 2)) * ((VAR & 4) ? 2 : 1);
   static_assert(B % U == 0, "B must be a multiple of U");
   __shared__ int32_t s_row[G][B];
   __shared__ int32_t s_col[G][B];
@@ -113,7 +134,7 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
         const int f4 = lane + v * L;
-        if (f4 < F4) st4(a.out + r * a.F + 4 * f4, I);
+        if (f4 < F4) st_out<VAR>(a.out + r * a.F + 4 * f4, I);
       }
   }
   float4 acc[NV];
@@ -125,9 +146,9 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
     for (int q = lane; q < B; q += L) {
       const int64_t p = base + q;
       const bool ok = p < p1;
-      s_row[g][q] = ok ? a.rows[p] : INT_MAX;
-      s_col[g][q] = ok ? a.indices[p] : 0;
-      if constexpr (needs_eid<KIND>()) s_eid[needs_eid<KIND>() ? g : 0][q] = ok ? a.eids[p] : 0;
+      s_row[g][q] = ok ? ld_stream<VAR>(a.rows + p) : INT_MAX;
+      s_col[g][q] = ok ? ld_stream<VAR>(a.indices + p) : 0;
+      if constexpr (needs_eid<KIND>()) s_eid[needs_eid<KIND>() ? g : 0][q] = ok ? ld_stream<VAR>(a.eids + p) : 0;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -156,14 +177,14 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
 #pragma unroll
           for (int v = 0; v < NV; ++v) {
             const int f4 = lane + v * L;
-            if (f4 < F4) st4(dst + 4 * f4, acc[v]);
+            if (f4 < F4) st_out<VAR>(dst + 4 * f4, acc[v]);
             acc[v] = I;
           }
           for (int64_t e = cur + 1; e < r; ++e)
 #pragma unroll
             for (int v = 0; v < NV; ++v) {
               const int f4 = lane + v * L;
-              if (f4 < F4) st4(a.out + e * a.F + 4 * f4, I);
+              if (f4 < F4) st_out<VAR>(a.out + e * a.F + 4 * f4, I);
             }
           cur = r;
           cont = false;
@@ -179,7 +200,7 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int f4 = lane + v * L;
-      if (f4 < F4) st4(dst + 4 * f4, acc[v]);
+      if (f4 < F4) st_out<VAR>(dst + 4 * f4, acc[v]);
     }
   }
   if (p1 == a.nnz) {  // trailing empty rows
@@ -187,7 +208,7 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
         const int f4 = lane + v * L;
-        if (f4 < F4) st4(a.out + r * a.F + 4 * f4, I);
+        if (f4 < F4) st_out<VAR>(a.out + r * a.F + 4 * f4, I);
       }
   }
   (void)indptr;
@@ -435,13 +456,30 @@ Cfg pick(int64_t F) {
   return {64, 4};
 }
 
+int spmm_variant() {
+  const char* env = std::getenv("DGLMI_SPMM_VARIANT");
+  return env ? std::atoi(env) : 3;
+}
+
 template <int KIND, int RED, int L, int NV>
 void run(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
   constexpr int G = kBlock / L;
   const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
   const unsigned blocks = static_cast<unsigned>((chunks + G - 1) / G);
-  hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV>), dim3(blocks), dim3(kBlock), 0, s, a,
-                     indptr);
+  if constexpr (KIND == FAST_COPY_COL && RED == RED_SUM && L == 16 && NV == 1) {
+    // tuning variants of the headline kernel (scripts/tune_spmm.py)
+    switch (spmm_variant()) {
+      case 0: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 0>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
+      case 1: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 1>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
+      case 2: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 2>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
+      case 4: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 4>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
+      case 7: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 7>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
+      default: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
+    }
+  } else {
+    hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV>), dim3(blocks), dim3(kBlock), 0, s, a,
+                       indptr);
+  }
   if (chunks > 1)
     hipLaunchKernelGGL((k_chunk_fixup<RED, L, NV>), dim3(blocks), dim3(kBlock), 0, s, a, indptr);
 }

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--chunks", default="64,128,256,512,1024")
     ap.add_argument("--feats", default="64")
+    ap.add_argument("--variants", default="0")
     args = ap.parse_args()
     dev = "cuda:0"
     th.cuda.set_device(0)
@@ -45,10 +46,13 @@ def main():
         return
     xs = {f: (x if f == 64 else th.rand(n, f, device=dev)) for f in feats}
     outs = {f: th.empty(n_dst, f, device=dev) for f in feats}
+    variants = [int(v) for v in args.variants.split(",")]
     for r in range(args.rounds):
         for f in feats:
             for c in chunks:
+              for var in variants:
                 os.environ["DGLMI_CHUNK_EDGES"] = str(c)
+                os.environ["DGLMI_SPMM_VARIANT"] = str(var)
                 K.copy_reduce("sum", gidx, 0, xs[f], outs[f])
                 evs = [(th.cuda.Event(enable_timing=True), th.cuda.Event(enable_timing=True))
                        for _ in range(args.steps)]
@@ -58,8 +62,9 @@ def main():
                     b.record()
                 th.cuda.synchronize()
                 ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
-                res.setdefault("F%d_K%d" % (f, c), []).append(ms)
+                res.setdefault("F%d_K%d_V%d" % (f, c, var), []).append(ms)
     os.environ.pop("DGLMI_CHUNK_EDGES", None)
+    os.environ.pop("DGLMI_SPMM_VARIANT", None)
     summary = {}
     for k, v in res.items():
         f = int(k.split("_")[0][1:])
