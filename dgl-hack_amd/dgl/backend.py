@@ -223,3 +223,39 @@ def fused_gat(graph, feat_src, el, er, slope):
     (N, H, 1).  Returns (N, H, D)."""
     gidx = graph if hasattr(graph, "in_csr") else graph._graph.get_immutable_gidx(feat_src.device)
     return FusedGat.apply(gidx, feat_src, el, er, float(slope))
+
+
+# --------------------------------------------------------------------------- #
+# R-GCN (hack: RgcnFirstLayer / RgcnSecondLayer, tensor.py:440-495;
+# kernels binary_reduce_impl.cu:913-1246)
+# --------------------------------------------------------------------------- #
+def _typed_aggregate(graph, num_rels, y, norm, etypes):
+    """out[v] = sum_{e=(u->v)} norm_e * y[type_e * N + u]: every relation in ONE
+    load-balanced gather over the relation-expanded graph (no per-relation SpMMs,
+    no per-edge weight products)."""
+    gidx = graph._graph.typed_gidx(y.device, num_rels, etypes)
+    n = graph.number_of_nodes()
+    if norm is None:
+        return copy_reduce("sum", gidx, SRC, y, n)
+    return binary_reduce("sum", "mul", gidx, SRC, EDGE, y, norm.reshape(norm.shape[0], 1), n)
+
+
+def rgcn_layer0(graph, weight, norm, etypes=None):
+    """Layer with one-hot (node id) input: ret[v] = sum_e W[type_e, u] * norm_e.
+
+    weight (R, N, F_out).  The hack's backward overwrites instead of accumulating
+    when a (src, type) pair repeats (binary_reduce_impl.cu:1004); here the
+    gradient is the exact one (autograd through the gather)."""
+    R, n, f = weight.shape
+    return _typed_aggregate(graph, R, weight.reshape(R * n, f), norm, etypes)
+
+
+def rgcn_layer1(graph, x, weight, norm, etypes=None):
+    """ret[v] = sum_e (x[u] @ W[type_e]) * norm_e.
+
+    The per-edge (F_in x F_out) products of the hack's kernel (binary_reduce_impl.cu:
+    1050-1117) become R dense GEMMs Y_r = X W_r (MFMA via hipBLASLt) plus one typed
+    gather; the hack also drops the weight gradient (tensor.py:493), autograd keeps it."""
+    R = weight.shape[0]
+    y = th.matmul(x.unsqueeze(0), weight)  # (R, N, F_out)
+    return _typed_aggregate(graph, R, y.reshape(R * x.shape[0], weight.shape[2]), norm, etypes)

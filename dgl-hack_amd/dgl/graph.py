@@ -218,6 +218,14 @@ class DGLGraph(object):
         self._graph.add_edges(_to_index_array(u, "u"), _to_index_array(v, "v"))
         self._extend_frame(self._edge_frame, old, self.number_of_edges() - old, data)
 
+    def add_edges_with_type(self, u, v, etypes, data=None):
+        """Add typed edges (the hack's graph.py:1229); types feed R-GCN kernels."""
+        self._check_mutable()
+        old = self.number_of_edges()
+        self._graph.add_edges_with_type(_to_index_array(u, "u"), _to_index_array(v, "v"),
+                                        _to_index_array(etypes, "etypes"))
+        self._extend_frame(self._edge_frame, old, self.number_of_edges() - old, data)
+
     @staticmethod
     def _extend_frame(frame, old, num, data):
         for k in list(frame._cols.keys()):

@@ -167,6 +167,8 @@ class GraphIndex:
         self._cache = {}
         self._host_csr = None
         self._degs = None
+        self._etype = None        # per-edge relation ids (add_edges_with_type), numpy int64
+        self._typed = {}
         self._device_only = None  # (src, dst) device tensors when built on the GPU
 
     # ---- construction -----------------------------------------------------
@@ -182,12 +184,74 @@ class GraphIndex:
         self._cache = {}
         self._host_csr = None
         self._degs = None
+        self._typed = {}
 
     def add_nodes(self, num):
         if self._device_only is not None:
             raise DGLError("graph built on device is immutable")
         self._n += int(num)
         self._invalidate()
+
+    def add_edges_with_type(self, u, v, etypes):
+        """graph.py:1229 (hack): edges plus their relation ids."""
+        old = self.number_of_edges()
+        self.add_edges(u, v)
+        t = np.atleast_1d(np.asarray(etypes, dtype=np.int64))
+        m = self.number_of_edges() - old
+        if t.shape[0] == 1 and m > 1:
+            t = np.full(m, t[0], np.int64)
+        if t.shape[0] != m:
+            raise DGLError("etypes length %d != number of new edges %d" % (t.shape[0], m))
+        prev = self._etype if self._etype is not None else np.zeros(old, np.int64)
+        self._etype = np.concatenate([prev, t])
+
+    def edge_types(self):
+        if self._etype is None:
+            return None
+        if self._etype.shape[0] != self.number_of_edges():  # untyped edges added later
+            pad = np.zeros(self.number_of_edges() - self._etype.shape[0], np.int64)
+            self._etype = np.concatenate([self._etype, pad])
+        return self._etype
+
+    def typed_gidx(self, device, num_rels, etypes=None):
+        """Relation-expanded graph for R-GCN: source (type_e * N + u) -> v, R*N sources.
+
+        Built on the device (two stable radix sorts) and cached per (device, R, etypes)."""
+        device = th.device(device)
+        if etypes is None:
+            et = self.edge_types()
+            if et is None:
+                raise DGLError("graph has no edge types; pass etypes")
+            key = (str(device), int(num_rels), "graph")
+            etypes = th.from_numpy(et)
+        else:
+            key = (str(device), int(num_rels), etypes.data_ptr(), etypes._version,
+                   int(etypes.shape[0]))
+        if key not in self._typed:
+            n = self._n
+            if num_rels * n >= 0x7FFFFFFF:
+                raise DGLError("num_rels * num_nodes exceeds int32 indexing")
+            if self._device_only is not None:
+                src, dst = (t.to(device=device, dtype=th.int64) for t in self._device_only)
+            else:
+                src = th.from_numpy(self._src).to(device)
+                dst = th.from_numpy(self._dst).to(device)
+            et = etypes.to(device=device, dtype=th.int64).reshape(-1)
+            if et.shape[0] != src.shape[0]:
+                raise DGLError("etypes must have one entry per edge")
+            if et.numel() and (int(et.min()) < 0 or int(et.max()) >= num_rels):
+                raise DGLError("edge type out of range [0, %d)" % num_rels)
+            tsrc = (et * n + src).to(th.int32).contiguous()
+            dst = dst.to(th.int32).contiguous()
+            m = int(tsrc.shape[0])
+            o_ptr, o_idx, o_dat = device_coo_to_csr(num_rels * n, tsrc, dst)
+            o_rows = device_expand_rows(o_ptr, m)
+            i_ptr, i_idx, i_dat = device_coo_to_csr(n, o_idx, o_rows, o_dat)
+            i_rows = device_expand_rows(i_ptr, m)
+            self._typed[key] = ImmutableGraphIndex(DeviceCSR(i_ptr, i_idx, i_dat, i_rows, num_rels * n),
+                                                   DeviceCSR(o_ptr, o_idx, o_dat, o_rows, n),
+                                                   num_rels * n, n, device)
+        return self._typed[key]
 
     def add_edges(self, u, v):
         if self._device_only is not None:

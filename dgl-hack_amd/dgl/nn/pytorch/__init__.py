@@ -1,3 +1,3 @@
 """PyTorch modules (``dgl.nn.pytorch``)."""
-from .conv import GraphConv, GATConv, FusedGATConv  # noqa: F401
+from .conv import GraphConv, GATConv, FusedGATConv, RelGraphConv  # noqa: F401
 from .softmax import edge_softmax  # noqa: F401

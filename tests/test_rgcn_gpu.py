@@ -1,0 +1,109 @@
+"""R-GCN on the typed-gather path vs fp64 restatements of the hack's layer
+kernels (binary_reduce_impl.cu:913-1246) and of RelGraphConv's per-edge bmm
+message function (nn/pytorch/conv/relgraphconv.py:125-150)."""
+import numpy as np
+import pytest
+import torch as th
+
+import dgl
+import dgl.backend as B
+from dgl.nn.pytorch import RelGraphConv
+from graphs import powerlaw
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def typed_graph(n=3000, m=40000, R=4, seed=0):
+    src, dst, n = powerlaw(n, m, seed=seed)
+    et = np.random.default_rng(seed).integers(0, R, len(src))
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges_with_type(src, dst, et)
+    return g, src, dst, et, n
+
+
+def dense_typed(src, dst, et, n, y, norm):
+    """out[v] = sum_e norm_e * y[t_e, u_e]   (y: (R, N, F))"""
+    s, d, t = (th.from_numpy(a).to(DEV) for a in (src, dst, et))
+    msg = y[t, s] * (norm if norm is not None else 1.0)
+    return th.zeros(n, y.shape[2], dtype=y.dtype, device=DEV).index_add(0, d, msg)
+
+
+@pytest.mark.parametrize("F", [16, 7])
+def test_rgcn_layer0(F):
+    g, src, dst, et, n = typed_graph()
+    R = 4
+    W = th.randn(R, n, F, device=DEV, requires_grad=True)
+    norm = th.rand(len(src), 1, device=DEV, requires_grad=True)
+    out = B.rgcn_layer0(g, W, norm)
+    go = th.randn_like(out)
+    gW, gn = th.autograd.grad(out, (W, norm), go)
+    Wd, nd = W.detach().double().requires_grad_(), norm.detach().double().requires_grad_()
+    ref = dense_typed(src, dst, et, n, Wd, nd)
+    rW, rn = th.autograd.grad(ref, (Wd, nd), go.double())
+    assert th.allclose(out.double(), ref, rtol=1e-4, atol=1e-4)
+    assert th.allclose(gW.double(), rW, rtol=1e-4, atol=1e-4)
+    assert th.allclose(gn.double(), rn, rtol=1e-4, atol=1e-4)
+
+
+def test_rgcn_layer1():
+    g, src, dst, et, n = typed_graph(seed=1)
+    R, fin, fout = 4, 24, 16
+    x = th.randn(n, fin, device=DEV, requires_grad=True)
+    W = th.randn(R, fin, fout, device=DEV, requires_grad=True)
+    norm = th.rand(len(src), 1, device=DEV)
+    out = B.rgcn_layer1(g, x, W, norm)
+    go = th.randn_like(out)
+    gx, gW = th.autograd.grad(out, (x, W), go)
+    xd, Wd = x.detach().double().requires_grad_(), W.detach().double().requires_grad_()
+    ref = dense_typed(src, dst, et, n, th.matmul(xd.unsqueeze(0), Wd), norm.double())
+    rx, rW = th.autograd.grad(ref, (xd, Wd), go.double())
+    assert th.allclose(out.double(), ref, rtol=1e-4, atol=1e-3)
+    assert th.allclose(gx.double(), rx, rtol=1e-3, atol=1e-3)
+    assert th.allclose(gW.double(), rW, rtol=1e-3, atol=1e-2)
+
+
+def ref_relgraphconv(conv, src, dst, x, et, norm, n):
+    """relgraphconv.py:125-150 + update_all(sum), in fp64."""
+    s, d, t = (th.from_numpy(a).to(DEV) for a in (src, dst, et))
+    if conv.regularizer == "basis":
+        W = conv._relation_weights().double()
+        if x.dtype == th.int64:
+            msg = W[t, x[s]]
+        else:
+            msg = th.bmm(x.double()[s].unsqueeze(1), W[t]).squeeze(1)
+    else:
+        w = conv.weight.double().index_select(0, t).view(-1, conv.submat_in, conv.submat_out)
+        node = x.double()[s].view(-1, 1, conv.submat_in)
+        msg = th.bmm(node, w).view(-1, conv.out_feat)
+    if norm is not None:
+        msg = msg * norm.double()
+    out = th.zeros(n, conv.out_feat, dtype=th.float64, device=DEV).index_add(0, d, msg)
+    if conv.bias:
+        out = out + conv.h_bias.double()
+    if conv.self_loop:
+        out = out + (conv.loop_weight.double()[x] if x.dtype == th.int64 else x.double() @ conv.loop_weight.double())
+    return out
+
+
+@pytest.mark.parametrize("reg,bases,ids,loop", [("basis", 2, False, False), ("basis", None, True, True),
+                                                ("bdd", 4, False, True)])
+def test_relgraphconv(reg, bases, ids, loop):
+    g, src, dst, et, n = typed_graph(seed=2)
+    R = 4
+    th.manual_seed(0)
+    conv = RelGraphConv(n if ids else 32, 16, R, regularizer=reg, num_bases=bases,
+                        self_loop=loop).to(DEV)
+    x = th.arange(n, device=DEV) if ids else th.randn(n, 32, device=DEV)
+    etypes = th.from_numpy(et).to(DEV)
+    norm = th.rand(len(src), 1, device=DEV)
+    out = conv(g, x, etypes, norm)
+    ref = ref_relgraphconv(conv, src, dst, x, et, norm, n)
+    assert th.allclose(out.double(), ref, rtol=1e-4, atol=1e-3)
+    out.pow(2).sum().backward()
+    grads = [p.grad.clone() for p in conv.parameters()]
+    conv.zero_grad()
+    ref.pow(2).sum().backward()
+    for a, p in zip(grads, conv.parameters()):
+        assert th.allclose(a, p.grad, rtol=1e-3, atol=1e-2)
