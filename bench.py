@@ -207,7 +207,10 @@ def main():
     step()
     th.cuda.synchronize()
     outdeg = th.bincount(gidx.in_csr.indices.long(), minlength=n).double()
-    expect = (outdeg[:, None] * x.double()).sum(0)
+    expect = th.zeros(FEAT, dtype=th.float64, device=device)
+    for lo in range(0, n, 1 << 22):  # chunked: x.double() of a 2^26-row table is 34 GB
+        hi = min(n, lo + (1 << 22))
+        expect += (outdeg[lo:hi, None] * x[lo:hi].double()).sum(0)
     got = out.double().sum(0)
     rel = float(((got - expect).abs().max() / expect.abs().max().clamp(min=1)).item())
     log("checksum-of-checksums rel err %.2e" % rel)

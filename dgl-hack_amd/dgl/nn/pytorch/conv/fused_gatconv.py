@@ -18,11 +18,9 @@ class FusedGATConv(GATConv):
                  negative_slope=0.2, residual=False, activation=None):
         super(FusedGATConv, self).__init__(in_feats, out_feats, num_heads, feat_drop, attn_drop,
                                            negative_slope, residual, activation)
-        self.negative_slope = negative_slope
 
     def forward(self, graph, feat):
-        attn_dropout = self.training and self.attn_drop.p > 0
-        if attn_dropout or not K.fused_gat_supported(self._num_heads, self._out_feats):
+        if not self._fused_ok():
             return super(FusedGATConv, self).forward(graph, feat)
         if isinstance(feat, tuple):
             h_src = self.feat_drop(feat[0])

@@ -3,14 +3,20 @@
 Same parameters, initialisation and math as the reference: projection
 (torch GEMM), el / er attention terms, ``u_add_v`` SDDMM, LeakyReLU,
 max-stabilised ``edge_softmax`` and ``u_mul_e_sum`` with the attention
-broadcast over the head dimension (the load-balanced HIP kernel).  The
-reference's unconditional ``th.cuda.synchronize()`` + timing prints
+broadcast over the head dimension (the load-balanced HIP kernel).  When no
+attention dropout is active and the head size suits the fused kernel, the
+middle of that chain (u_add_v .. u_mul_e_sum) runs as ONE fused HIP kernel
+(``dgl.backend.fused_gat``; same math, max-stabilised in both forms) --
+set ``use_fused = False`` on the module to force the unfused composition.
+The reference's unconditional ``th.cuda.synchronize()`` + timing prints
 (:146-170) are not reproduced.
 """
 import torch as th
 from torch import nn
 
+from .... import backend as B
 from .... import function as fn
+from .... import kernel as K
 from ..softmax import edge_softmax
 
 
@@ -49,6 +55,13 @@ class GATConv(nn.Module):
             self.register_buffer("res_fc", None)
         self.reset_parameters()
         self.activation = activation
+        self.negative_slope = negative_slope
+        self.use_fused = True
+
+    def _fused_ok(self):
+        if not self.use_fused or (self.training and self.attn_drop.p > 0):
+            return False
+        return K.fused_gat_supported(self._num_heads, self._out_feats)
 
     def reset_parameters(self):
         gain = nn.init.calculate_gain("relu")
@@ -74,13 +87,16 @@ class GATConv(nn.Module):
             feat_src = feat_dst = self.fc(h_src).view(-1, self._num_heads, self._out_feats)
         el = (feat_src * self.attn_l).sum(dim=-1).unsqueeze(-1)
         er = (feat_dst * self.attn_r).sum(dim=-1).unsqueeze(-1)
-        graph.srcdata.update({"ft": feat_src, "el": el})
-        graph.dstdata.update({"er": er})
-        graph.apply_edges(fn.u_add_v("el", "er", "e"))
-        e = self.leaky_relu(graph.edata.pop("e"))
-        graph.edata["a"] = self.attn_drop(edge_softmax(graph, e))
-        graph.update_all(fn.u_mul_e("ft", "a", "m"), fn.sum("m", "ft"))
-        rst = graph.dstdata["ft"]
+        if self._fused_ok():
+            rst = B.fused_gat(graph, feat_src, el, er, self.negative_slope)
+        else:
+            graph.srcdata.update({"ft": feat_src, "el": el})
+            graph.dstdata.update({"er": er})
+            graph.apply_edges(fn.u_add_v("el", "er", "e"))
+            e = self.leaky_relu(graph.edata.pop("e"))
+            graph.edata["a"] = self.attn_drop(edge_softmax(graph, e))
+            graph.update_all(fn.u_mul_e("ft", "a", "m"), fn.sum("m", "ft"))
+            rst = graph.dstdata["ft"]
         if self.res_fc is not None:
             resval = self.res_fc(h_dst).view(h_dst.shape[0], -1, self._out_feats)
             rst = rst + resval

@@ -92,6 +92,7 @@ def c3(dev, steps, warmup):
     g = chung_lu(n, m, 0.4, 3, dev)
     x = th.randn(n, 602, device=dev)
     gat = GATConv(602, 8, 8).to(dev)
+    gat.use_fused = False  # the reference's unfused composition
     gat.train()
 
     def fwd():

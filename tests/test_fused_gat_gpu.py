@@ -99,6 +99,7 @@ def test_fused_gatconv_matches_gatconv():
     g.add_edges(np.concatenate([src, np.arange(n)]), np.concatenate([dst, np.arange(n)]))
     th.manual_seed(0)
     a = GATConv(32, 8, 8).to(DEV)
+    a.use_fused = False
     b = FusedGATConv(32, 8, 8).to(DEV)
     b.load_state_dict(a.state_dict())
     x = th.randn(n, 32, device=DEV)

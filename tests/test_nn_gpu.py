@@ -130,7 +130,8 @@ def test_partial_edge_softmax():
     assert th.allclose(score.grad, g1, rtol=1e-4, atol=1e-4)
 
 
-def test_gat_conv_vs_dense():
+@pytest.mark.parametrize("use_fused", [False, True])
+def test_gat_conv_vs_dense(use_fused):
     """GATConv against a dense torch restatement (float64)."""
     th.manual_seed(0)
     n, fin, H, D = 200, 24, 4, 8
@@ -141,6 +142,7 @@ def test_gat_conv_vs_dense():
     g.add_nodes(n)
     g.add_edges(src, dst)
     gat = nn.GATConv(fin, D, H).to(DEV)
+    gat.use_fused = use_fused
     x = th.randn(n, fin, device=DEV)
     out = gat(g, x)
     assert out.shape == (n, H, D)
