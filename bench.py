@@ -103,17 +103,9 @@ def build_workload(world, rank, device, edges_per_gpu=EDGES_PER_GPU, scale0=SCAL
 
 def make_local_graph(n_src, n_dst, src, dst, device):
     """Local in-CSR (rows = owned dst, cols = global src) built on the GPU."""
-    from dgl.graph_index import (DeviceCSR, ImmutableGraphIndex, device_coo_to_csr,
-                                 device_expand_rows)
-    nodes = max(n_src, n_dst)
-    # out-CSR (rows = src) then in-CSR = stable re-sort by dst == CSRTranspose(out-CSR)
-    o_ptr, o_idx, o_dat = device_coo_to_csr(nodes, src, dst)
-    o_rows = device_expand_rows(o_ptr, src.shape[0])
-    i_ptr, i_idx, i_dat = device_coo_to_csr(n_dst, o_idx, o_rows, o_dat)
-    i_rows = device_expand_rows(i_ptr, src.shape[0])
-    in_csr = DeviceCSR(i_ptr, i_idx, i_dat, i_rows, n_src)
-    out_csr = DeviceCSR(o_ptr, o_idx, o_dat, o_rows, n_dst)
-    return ImmutableGraphIndex(in_csr, out_csr, n_src, n_dst, th.device(device)), (o_ptr, o_idx)
+    from dgl.graph_index import device_block_gidx
+    g = device_block_gidx(n_src, n_dst, src, dst)
+    return g, (g.out_csr.indptr, g.out_csr.indices)
 
 
 def cpu_baseline(o_ptr, o_idx, x, n_dst, budget_s=20.0, sample_edges=None):
@@ -157,6 +149,78 @@ def load_pmc_traffic():
         return None
 
 
+def _timed(fn, steps, dist, cdev):
+    """barrier + sync bracketed wall time of `steps` calls, max over ranks (s)."""
+    if dist is not None:
+        dist.barrier()
+    th.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    th.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t
+    if dist is not None:
+        v = th.tensor([el], device=cdev, dtype=th.float64)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        el = float(v.item())
+    return el
+
+
+def measure_exchange(part, x, out_ref, args, dist, cdev, device, edges_total):
+    """copy_u_sum with the source rows NOT replicated: each step first fetches
+    the halo rows with one all-to-all-v (RCCL over xGMI), then aggregates over
+    the local [owned | halo] block.  SURVEY §8(e): the with-exchange line."""
+    from dgl import distributed as D
+    from dgl import kernel as K
+    x_full = th.empty(part.n_inner + part.n_halo, FEAT, device=device)
+    x_full[:part.n_inner] = x[part.lo:part.hi]
+    send_buf = th.empty(int(part.send_counts.sum()), FEAT, device=device)
+    out = th.empty_like(out_ref)
+    g = part.gidx()
+
+    def xstep():
+        D.halo_exchange_into(x_full, part, None, send_buf)
+        K.copy_reduce("sum", g, 0, x_full, out)
+    xstep()
+    th.cuda.synchronize()
+    err = float((out - out_ref).abs().max() / out_ref.abs().max().clamp(min=1e-30))
+    if err > 1e-4:
+        raise SystemExit("with-exchange copy_u_sum differs from the replicated one: %g" % err)
+    steps = max(1, min(args.steps, 5))
+    for _ in range(2):
+        xstep()
+    el = _timed(xstep, steps, dist, cdev)
+    moved = th.tensor([float(part.n_halo) * FEAT * 4], device=cdev, dtype=th.float64)
+    halo_max = th.tensor([float(part.n_halo)], device=cdev, dtype=th.float64)
+    dist.all_reduce(moved)
+    dist.all_reduce(halo_max, op=dist.ReduceOp.MAX)
+    ex_el = _timed(lambda: D.halo_exchange_into(x_full, part, None, send_buf), steps, dist, cdev)
+    return {"value": edges_total * steps / el, "unit": "edges/s", "ms_per_step": el * 1e3 / steps,
+            "exchange_only_ms": ex_el * 1e3 / steps, "steps": steps,
+            "halo_bytes_per_step_all_ranks": float(moved.item()),
+            "max_halo_rows_per_rank": int(halo_max.item()),
+            "exchange": "all_to_all_single (%s) of halo source rows, then local copy_u_sum"
+                        % dist.get_backend(),
+            "rel_err_vs_replicated": err}
+
+
+def measure_update_all(g, x, out_ref, args):
+    """End-to-end DGLGraph.update_all(copy_u, sum) through the Python boundary
+    (frame lookup, output allocation, autograd Function, ctypes call)."""
+    import dgl.function as fn
+    g.ndata["h"] = x
+    g.update_all(fn.copy_u("h", "m"), fn.sum("m", "h2"))  # builds + caches the device CSRs
+    th.cuda.synchronize()
+    if not th.equal(g.ndata["h2"], out_ref):
+        raise SystemExit("update_all result differs from the direct kernel call")
+    steps = max(1, min(args.steps, 10))
+    el = _timed(lambda: g.update_all(fn.copy_u("h", "m"), fn.sum("m", "h2")), steps, None, None)
+    return {"ms_per_call": el * 1e3 / steps, "edges_per_sec": g.number_of_edges() * steps / el,
+            "path": "DGLGraph.update_all(fn.copy_u, fn.sum) incl. output allocation"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -169,6 +233,10 @@ def main():
     ap.add_argument("--scale", type=int, default=SCALE)
     ap.add_argument("--dist-backend", default="nccl")
     ap.add_argument("--same-device", action="store_true")
+    ap.add_argument("--no-exchange", action="store_true",
+                    help="N>1: skip the with-halo-exchange measurement")
+    ap.add_argument("--no-update-all", action="store_true",
+                    help="N=1: skip the end-to-end DGLGraph.update_all measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -193,9 +261,25 @@ def main():
     t0 = time.time()
     gidx, (o_ptr, o_idx) = make_local_graph(n, n_dst, src, dst, device)
     m_local = src.shape[0]
-    del src, dst
     th.cuda.synchronize()
     log("CSRs built on device in %.2fs" % (time.time() - t0))
+    part = None
+    if world > 1 and not args.no_exchange:
+        # the same rows planned as a halo partition (owned X rows + halo rows
+        # fetched by one all-to-all-v per step), for the with-exchange line
+        from dgl import distributed as D
+        t0 = time.time()
+        bounds = [n * p // world for p in range(world + 1)]
+        part = D.build_device_partition(src, dst, bounds, rank)
+        part.release_edges()
+        th.cuda.synchronize()
+        log("halo plan built on device in %.2fs: %d halo rows on rank 0"
+            % (time.time() - t0, part.n_halo))
+    upd = None
+    if world == 1 and not args.no_update_all:
+        import dgl
+        upd = dgl.DGLGraph.from_device_coo(src, dst, n)
+    del src, dst
 
     out = th.empty(n_dst, FEAT, device=device)
 
@@ -269,6 +353,13 @@ def main():
 
     ms_per_step = elapsed * 1000.0 / args.steps
     value = edges_total * args.steps / elapsed
+    exch = None
+    if part is not None:
+        exch = measure_exchange(part, x, out, args, dist, cdev, device, edges_total)
+    upd_res = None
+    if upd is not None:
+        upd_res = measure_update_all(upd, x, out, args)
+        del upd
     # algorithmic bytes per launch (per rank): indptr + indices + one
     # gathered 4F-byte source row per edge + one 4F-byte output row per destination
     alg_bytes = 4 * (n_dst + 1) + 4 * m_local + 4 * FEAT * m_local + 4 * FEAT * n_dst
@@ -305,6 +396,10 @@ def main():
         "hbm_gbps_achieved": achieved,
         "edges_per_sec_per_gpu": value / world,
     }
+    if exch is not None:
+        res["with_exchange"] = exch
+    if upd_res is not None:
+        res["update_all"] = upd_res
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             res["cpu_baseline"] = cpu_baseline(o_ptr, o_idx, x, n_dst)

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -269,6 +270,34 @@ void run_fast(const DGLMIGraph* g, const DGLMICsr& walk, int kind, int red, cons
   check_hip(hipGetLastError(), "fast reduce launch");
 }
 
+// Items of a per-edge kernel.  Edge-id order (the graph's COO) streams the
+// output and any edge operand sequentially and gathers both node rows; in-CSR
+// order keeps the destination row in cache along its run but scatters the
+// output by eid.  Measured on M1 (100M edges, scripts/bench_configs.py sd):
+// edge-id order wins even for wide node-only ops (u_dot_v F = 64: 6.07 vs
+// 7.28 ms; u_add_v H = 8: 3.66 vs 5.25 ms), so it is used whenever the COO is
+// there.  DGLMI_SDDMM_ORDER=coo|csr forces one (tests).
+SddmmArgs sddmm_items(const DGLMIGraph* g, const DGLMICsr& walk) {
+  SddmmArgs e;
+  std::memset(&e, 0, sizeof(e));
+  e.nnz = walk.nnz;
+  bool coo = g->coo_src != nullptr && g->coo_dst != nullptr;
+  if (coo) {
+    const char* env = std::getenv("DGLMI_SDDMM_ORDER");
+    if (env && std::string(env) == "csr") coo = false;
+  }
+  if (coo) {
+    e.rows = g->coo_dst;
+    e.cols = g->coo_src;
+    e.eids = nullptr;
+  } else {
+    e.rows = walk.rows;
+    e.cols = walk.indices;
+    e.eids = walk.data;
+  }
+  return e;
+}
+
 EdgeArgs base_args(const DGLMICsr& walk) {
   EdgeArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -363,7 +392,27 @@ void forward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const D
     }
   }
 
-  // ---- generic path ----
+  if (need_fill) launch_fill(out->data, out_rows * D, identity_of(red), s);
+  if (red == RED_NONE && walk.nnz > 0) DGLMI_CHECK(walk.rows != nullptr, "in_csr.rows required");
+
+  // ---- per-edge outputs (g-SDDMM) ----
+  if (red == RED_NONE && !bc && !lhs_map && !rhs_map && !out_map && walk.nnz > 0 &&
+      sddmm_supported(op == OP_DOT && len == 1 ? OP_MUL : op, false, D, len) &&
+      aligned16(out->data) && aligned16(lhs->data) && (op == OP_USE_LHS || aligned16(rhs->data))) {
+    SddmmArgs e = sddmm_items(g, walk);
+    e.lhs = lhs->data;
+    e.lhs_role = role_of(lhs_t, true);
+    e.rhs = op == OP_USE_LHS ? nullptr : rhs->data;
+    e.rhs_role = op == OP_USE_LHS ? ROLE_NONE : role_of(rhs_t, true);
+    e.out = out->data;
+    e.D = D;
+    e.len = len;
+    launch_sddmm(op == OP_DOT && len == 1 ? OP_MUL : op, false, e, s);
+    check_hip(hipGetLastError(), "sddmm launch");
+    return;
+  }
+
+  // ---- generic path (load-balanced for reductions) ----
   EdgeArgs a = base_args(walk);
   a.lhs = Operand{lhs->data, lhs_map, role_of(lhs_t, true)};
   if (op == OP_USE_LHS) a.rhs = Operand{nullptr, nullptr, ROLE_NONE};
@@ -375,8 +424,18 @@ void forward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const D
   a.len = len;
   a.out_rows = out_rows;
   a.bc = binfo;
-  if (need_fill) launch_fill(out->data, out_rows * D, identity_of(red), s);
-  if (red == RED_NONE && walk.nnz > 0) DGLMI_CHECK(walk.rows != nullptr, "in_csr.rows required");
+  if (red != RED_NONE && walk.rows != nullptr && generic_lb_supported(D)) {
+    if (walk.nnz == 0) {
+      if (!need_fill) launch_fill(out->data, walk.num_rows * D, identity_of(red), s);
+      return;
+    }
+    a.chunk = fast_chunk_edges(walk.nnz, D);
+    Scratch carry(g, fast_workspace_bytes(walk.nnz, D), s);
+    a.carry = static_cast<float*>(carry.ptr);
+    launch_generic_lb(op, red, bc, false, a, s);
+    check_hip(hipGetLastError(), "generic lb forward launch");
+    return;
+  }
   launch_generic_forward(op, red, bc, a, s);
   check_hip(hipGetLastError(), "generic forward launch");
 }
@@ -473,6 +532,30 @@ void backward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const 
     }
   }
 
+  if (need_fill) launch_fill(grad->data, grad_rows * Dg, 0.0f, s);
+
+  // ---- per-edge gradients (g-SDDMM shape) for reducers none / sum ----
+  if (x_t == DGLMI_TARGET_EDGE && (red == RED_NONE || red == RED_SUM) && !bc && !lhs_map &&
+      !rhs_map && !out_map && walk.nnz > 0 && walk.rows != nullptr &&
+      sddmm_supported(op == OP_DOT && len == 1 ? OP_MUL : op, true, D, len) &&
+      aligned16(grad->data) && aligned16(grad_out->data) && aligned16(lhs->data) &&
+      (op == OP_USE_LHS || aligned16(rhs->data))) {
+    SddmmArgs e = sddmm_items(g, walk);
+    e.lhs = lhs->data;
+    e.lhs_role = role_of(lhs_t, true);
+    e.rhs = op == OP_USE_LHS ? nullptr : rhs->data;
+    e.rhs_role = op == OP_USE_LHS ? ROLE_NONE : role_of(rhs_t, true);
+    e.out = grad->data;
+    e.go = grad_out->data;
+    e.go_role = red == RED_NONE ? ROLE_EDGE : ROLE_ROW;
+    e.want = want;
+    e.D = D;
+    e.len = len;
+    launch_sddmm(op == OP_DOT && len == 1 ? OP_MUL : op, true, e, s);
+    check_hip(hipGetLastError(), "sddmm backward launch");
+    return;
+  }
+
   EdgeArgs a = base_args(walk);
   a.lhs = Operand{lhs->data, lhs_map, role_of(lhs_t, walk_in)};
   if (op == OP_USE_LHS) a.rhs = Operand{nullptr, nullptr, ROLE_NONE};
@@ -488,7 +571,19 @@ void backward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const 
   a.fo_role = red == RED_NONE ? ROLE_EDGE : role_of(DGLMI_TARGET_DST, walk_in);
   a.want = want;
   a.bc = binfo;
-  if (need_fill) launch_fill(grad->data, grad_rows * Dg, 0.0f, s);
+  // node-owned gradients: load-balanced over CSR positions
+  if (x_t != DGLMI_TARGET_EDGE && walk.rows != nullptr && generic_lb_supported(Dg)) {
+    if (walk.nnz == 0) {
+      if (!need_fill) launch_fill(grad->data, walk.num_rows * Dg, 0.0f, s);
+      return;
+    }
+    a.chunk = fast_chunk_edges(walk.nnz, Dg);
+    Scratch carry(g, fast_workspace_bytes(walk.nnz, Dg), s);
+    a.carry = static_cast<float*>(carry.ptr);
+    launch_generic_lb(op, red, bc, true, a, s);
+    check_hip(hipGetLastError(), "generic lb backward launch");
+    return;
+  }
   launch_generic_backward(op, red, bc, a, s);
   check_hip(hipGetLastError(), "generic backward launch");
 }

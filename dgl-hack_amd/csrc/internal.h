@@ -60,6 +60,9 @@ struct EdgeArgs {
   int fo_role;             // ROLE_COL/ROLE_ROW (node output) or ROLE_EDGE
   int want;                // 0 = grad wrt lhs, 1 = grad wrt rhs
   Bcast bc;
+  // load-balanced reduce-to-row (launch_generic_lb)
+  float* carry;            // workspace: num_chunks * out-row floats
+  int64_t chunk;           // CSR positions per chunk
 };
 
 // ---- device helpers ---------------------------------------------------------
@@ -132,6 +135,31 @@ void launch_fill_i32(int32_t* out, int64_t n, int32_t value, hipStream_t s);
 void launch_generic_forward(int op, int red, bool bcast, const EdgeArgs& a, hipStream_t s);
 // Generic backward for one operand (a.want), reduce to row nodes or per edge.
 void launch_generic_backward(int op, int red, bool bcast, const EdgeArgs& a, hipStream_t s);
+
+// Load-balanced reduce-to-row for every op / reducer / broadcast (fixed chunks
+// of CSR positions + carry fixup).  Needs a.rows; returns false (nothing
+// launched) when the output row is too wide for it.
+bool generic_lb_supported(int64_t out_row_len);
+void launch_generic_lb(int op, int red, bool bcast, bool bwd, const EdgeArgs& a, hipStream_t s);
+
+// Per-edge outputs (kernels_sddmm.hip).  Roles are relative to the in-CSR:
+// ROLE_ROW = destination node, ROLE_COL = source node, ROLE_EDGE = edge id.
+struct SddmmArgs {
+  const int32_t* rows;  // destination node per item
+  const int32_t* cols;  // source node per item
+  const int32_t* eids;  // edge id per item; NULL: item index == edge id (COO order)
+  int64_t nnz;
+  const float* lhs;
+  const float* rhs;
+  int lhs_role, rhs_role;
+  float* out;           // forward: (E, D); backward: (E, D * len) gradient rows
+  const float* go;      // backward: grad of the forward output
+  int go_role;          // ROLE_EDGE (reducer none) or ROLE_ROW (reducer sum)
+  int want;             // backward: 0 = lhs, 1 = rhs
+  int64_t D, len;       // output features, dot length (1 otherwise)
+};
+bool sddmm_supported(int op, bool bwd, int64_t D, int64_t len);
+void launch_sddmm(int op, bool bwd, const SddmmArgs& a, hipStream_t s);
 
 // Load-balanced reduce-to-row kernels (kernels_spmm.hip).
 enum FastKind : int {

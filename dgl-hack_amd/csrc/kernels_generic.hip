@@ -141,6 +141,127 @@ __global__ void __launch_bounds__(kBlock) k_edge_bwd(EdgeArgs a, int lane_bits) 
   for (int64_t k = lane; k < Dg; k += L) g[k] = bwd_value<OP, RED, BC>(a, row, col, eid, k);
 }
 
+// ---- load-balanced reduce-to-row: fixed chunks of CSR positions -----------
+// The row-per-group kernels above serialise a hub row's in-edges on one
+// group; on power-law graphs (a 10^5-edge hub next to degree-1 rows) that
+// group runs alone for most of the launch.  Here a group of L lanes (features
+// strided over lanes, up to kNV per lane) owns K consecutive CSR positions,
+// folds each row's run in CSR order, writes rows wholly inside the chunk
+// directly, the continuation of a row begun in an earlier chunk to the carry
+// workspace, and fills zero-degree rows with the identity; k_lb_fixup folds the
+// carries into the row head in chunk order (deterministic).
+constexpr int kNV = 4;
+
+template <bool BWD>
+__device__ __forceinline__ int64_t lb_out_row(const EdgeArgs& a, int64_t r) {
+  const int32_t* m = BWD ? (a.want == 0 ? a.lhs.map : a.rhs.map) : a.out_map;
+  return m ? m[r] : r;
+}
+
+template <int OP, int RED, bool BC, bool BWD>
+__global__ void __launch_bounds__(kBlock) k_lb_reduce(EdgeArgs a, int lane_bits) {
+  constexpr int U = 4;
+  const int L = 1 << lane_bits;
+  const int G = kBlock >> lane_bits;
+  const int g = threadIdx.x >> lane_bits;
+  const int lane = threadIdx.x & (L - 1);
+  const int64_t chunk = (int64_t)blockIdx.x * G + g;
+  const int64_t K = a.chunk;
+  const int64_t p0 = chunk * K;
+  if (p0 >= a.nnz) return;
+  const int64_t p1 = p0 + K < a.nnz ? p0 + K : a.nnz;
+  const int64_t Do = BWD ? a.D * a.len : a.D;
+  const int nv = static_cast<int>((Do + L - 1) / L);
+  const float I = BWD ? 0.0f : red_identity<RED>();
+
+  auto fill_row = [&](int64_t r) {
+    float* o = a.out + lb_out_row<BWD>(a, r) * Do;
+#pragma unroll
+    for (int v = 0; v < kNV; ++v) {
+      const int64_t k = lane + v * L;
+      if (v < nv && k < Do) o[k] = I;
+    }
+  };
+  int64_t cur = a.rows[p0];
+  bool cont = p0 > 0 && a.rows[p0 - 1] == cur;
+  if (!cont)
+    for (int64_t r = p0 > 0 ? (int64_t)a.rows[p0 - 1] + 1 : 0; r < cur; ++r) fill_row(r);
+  float acc[kNV];
+#pragma unroll
+  for (int v = 0; v < kNV; ++v) acc[v] = I;
+  auto flush = [&]() {
+    float* o = cont ? a.carry + chunk * Do : a.out + lb_out_row<BWD>(a, cur) * Do;
+#pragma unroll
+    for (int v = 0; v < kNV; ++v) {
+      const int64_t k = lane + v * L;
+      if (v < nv && k < Do) o[k] = acc[v];
+      acc[v] = I;
+    }
+  };
+  for (int64_t base = p0; base < p1; base += U) {
+    int64_t rr[U], cc[U], ee[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t p = base + u < p1 ? base + u : p1 - 1;
+      rr[u] = a.rows[p];
+      cc[u] = a.indices[p];
+      ee[u] = a.eids[p];
+    }
+    float val[U][kNV];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int v = 0; v < kNV; ++v) {
+        const int64_t k = lane + v * L;
+        val[u][v] = 0.0f;
+        if (v < nv && k < Do && base + u < p1) {
+          if constexpr (BWD) val[u][v] = bwd_value<OP, RED, BC>(a, rr[u], cc[u], ee[u], k);
+          else val[u][v] = fwd_value<OP, BC>(a, rr[u], cc[u], ee[u], k);
+        }
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (base + u >= p1) break;
+      if (rr[u] != cur) {
+        flush();
+        for (int64_t r = cur + 1; r < rr[u]; ++r) fill_row(r);
+        cur = rr[u];
+        cont = false;
+      }
+#pragma unroll
+      for (int v = 0; v < kNV; ++v) acc[v] = BWD ? acc[v] + val[u][v] : red_apply<RED>(acc[v], val[u][v]);
+    }
+  }
+  flush();
+  if (p1 == a.nnz)
+    for (int64_t r = cur + 1; r < a.num_rows; ++r) fill_row(r);
+}
+
+template <int RED, bool BWD>
+__global__ void __launch_bounds__(kBlock) k_lb_fixup(EdgeArgs a, int lane_bits) {
+  const int L = 1 << lane_bits;
+  const int G = kBlock >> lane_bits;
+  const int lane = threadIdx.x & (L - 1);
+  const int64_t chunk = (int64_t)blockIdx.x * G + (threadIdx.x >> lane_bits);
+  const int64_t K = a.chunk;
+  const int64_t p0 = chunk * K;
+  if (chunk == 0 || p0 >= a.nnz) return;
+  const int64_t r = a.rows[p0];
+  const int64_t start = a.indptr[r];
+  if (start >= p0 || start < p0 - K) return;  // not the first continuation of row r
+  const int64_t last = (a.indptr[r + 1] - 1) / K;
+  const int64_t Do = BWD ? a.D * a.len : a.D;
+  float* o = a.out + lb_out_row<BWD>(a, r) * Do;
+  for (int64_t k = lane; k < Do; k += L) {
+    float acc = o[k];
+    for (int64_t c = chunk; c <= last; ++c) {
+      const float t = a.carry[c * Do + k];
+      acc = BWD ? acc + t : red_apply<RED>(acc, t);
+    }
+    o[k] = acc;
+  }
+}
+
 __global__ void k_fill(float* __restrict__ out, int64_t n, float v) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = v;
@@ -225,7 +346,35 @@ struct EdgeBwd {
   }
 };
 
+template <int OP, int RED, bool BC>
+struct LbFwd {
+  static void run(const EdgeArgs& a, int lb, unsigned blocks, hipStream_t s) {
+    hipLaunchKernelGGL((k_lb_reduce<OP, RED, BC, false>), dim3(blocks), dim3(kBlock), 0, s, a, lb);
+    hipLaunchKernelGGL((k_lb_fixup<RED, false>), dim3(blocks), dim3(kBlock), 0, s, a, lb);
+  }
+};
+template <int OP, int RED, bool BC>
+struct LbBwd {
+  static void run(const EdgeArgs& a, int lb, unsigned blocks, hipStream_t s) {
+    hipLaunchKernelGGL((k_lb_reduce<OP, RED, BC, true>), dim3(blocks), dim3(kBlock), 0, s, a, lb);
+    hipLaunchKernelGGL((k_lb_fixup<RED, true>), dim3(blocks), dim3(kBlock), 0, s, a, lb);
+  }
+};
+
 }  // namespace
+
+bool generic_lb_supported(int64_t out_row_len) { return out_row_len >= 1 && out_row_len <= 64 * kNV; }
+
+void launch_generic_lb(int op, int red, bool bcast, bool bwd, const EdgeArgs& a, hipStream_t s) {
+  if (a.nnz == 0) return;
+  const int64_t Do = bwd ? a.D * a.len : a.D;
+  const int lb = lane_bits_for(Do);
+  const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
+  const unsigned blocks = grid_for(chunks, lb);
+  if (red == RED_NONE) red = RED_SUM;
+  if (bwd) dispatch3<LbBwd>(op, red, bcast, a, lb, blocks, s);
+  else dispatch3<LbFwd>(op, red, bcast, a, lb, blocks, s);
+}
 
 void launch_fill(float* out, int64_t n, float value, hipStream_t s) {
   if (n <= 0) return;

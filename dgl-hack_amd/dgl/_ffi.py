@@ -40,6 +40,8 @@ class Graph(ctypes.Structure):
         ("device", ctypes.c_int32),
         ("workspace", ctypes.c_void_p),
         ("workspace_bytes", ctypes.c_int64),
+        ("coo_src", ctypes.c_void_p),
+        ("coo_dst", ctypes.c_void_p),
     ]
 
 

@@ -33,7 +33,8 @@ import torch.distributed as dist
 
 from . import _ffi
 from ._ffi import DGLError
-from .graph_index import ImmutableGraphIndex, DeviceCSR, host_coo_to_csr, host_csr_transpose
+from .graph_index import (ImmutableGraphIndex, DeviceCSR, device_block_gidx, host_coo_to_csr,
+                          host_csr_transpose)
 
 
 # --------------------------------------------------------------------------- #
@@ -127,7 +128,7 @@ class Partition:
                 return DeviceCSR(t(indptr), t(indices), t(data), t(rows), cols_n)
 
             self._gidx[key] = ImmutableGraphIndex(mk(in_csr, n_dst, n_src), mk(out_csr, n_src, n_dst),
-                                                  n_src, n_dst, th.device(device))
+                                                  n_src, n_dst, th.device(device), eid_perm=True)
         return self._gidx[key]
 
     def device_plan(self, device):
@@ -183,6 +184,76 @@ def build_partitions(src, dst, num_nodes, assign, parts=None, num_parts=None):
     return out
 
 
+class DevicePartition:
+    """A rank's halo subgraph planned ON THE DEVICE for a contiguous (id-range)
+    node partition -- the path for graphs whose edge lists only ever live in
+    HBM (hundreds of millions of edges per rank).  Same local-id convention as
+    :class:`Partition` (owned rows first, then halo rows grouped by owner, each
+    group ascending by global id), so :func:`halo_exchange` and
+    :class:`DistGraphConv` accept either."""
+
+    def __init__(self, part_id, num_parts, lo, hi, halo, send_idx, send_counts, recv_counts,
+                 local_src, local_dst):
+        self.part_id = part_id
+        self.num_parts = num_parts
+        self.lo, self.hi = lo, hi
+        self.n_inner = hi - lo
+        self.halo = halo                  # device int64 global ids
+        self.n_halo = int(halo.shape[0])
+        self.send_idx = send_idx          # device int64 local inner ids, peer order
+        self.send_counts = send_counts    # numpy int64
+        self.recv_counts = recv_counts    # numpy int64
+        self.local_src = local_src        # device int32, [0, n_inner + n_halo)
+        self.local_dst = local_dst        # device int32, [0, n_inner)
+        self._g = None
+
+    def number_of_edges(self):
+        return int(self.local_src.shape[0])
+
+    def gidx(self, device=None):
+        """Local block CSRs, built on the GPU at first use (the edge list may be
+        dropped afterwards with :meth:`release_edges`)."""
+        if self._g is None:
+            self._g = device_block_gidx(self.n_inner + self.n_halo, self.n_inner,
+                                        self.local_src, self.local_dst)
+        return self._g
+
+    def release_edges(self):
+        self.gidx()
+        self.local_src = self.local_dst = None
+
+    def device_plan(self, device=None):
+        return self.send_idx
+
+
+def build_device_partition(src, dst, bounds, rank, group=None):
+    """Plan rank ``rank``'s halo partition from its in-edges, all on the device.
+
+    ``src``: GLOBAL source ids of the edges whose destination this rank owns;
+    ``dst``: their LOCAL destination ids in ``[0, hi - lo)``; ``bounds``: the
+    ``world + 1`` node-id boundaries (rank p owns ``[bounds[p], bounds[p+1])``).
+    Collective over ``group`` (two all-to-alls: halo counts, then halo ids)."""
+    world = len(bounds) - 1
+    lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+    dev = src.device
+    s = src.long()
+    remote = (s < lo) | (s >= hi)
+    halo = th.unique(s[remote])                      # sorted => grouped by owner
+    edges = th.tensor([int(b) for b in bounds], dtype=th.int64, device=dev)
+    recv = th.diff(th.searchsorted(halo, edges))     # halo rows owned by each peer
+    send = th.empty_like(recv)
+    _a2av(send, recv, [1] * world, [1] * world, group)
+    recv_counts = recv.cpu().numpy().astype(np.int64)
+    send_counts = send.cpu().numpy().astype(np.int64)
+    req = th.empty(int(send_counts.sum()), dtype=th.int64, device=dev)
+    _a2av(req, halo, send_counts.tolist(), recv_counts.tolist(), group)
+    send_idx = req - lo
+    local = th.where(remote, (hi - lo) + th.searchsorted(halo, s), s - lo).to(th.int32)
+    del s, remote
+    return DevicePartition(rank, world, lo, hi, halo, send_idx, send_counts, recv_counts, local,
+                           dst.to(th.int32))
+
+
 # --------------------------------------------------------------------------- #
 # collectives
 # --------------------------------------------------------------------------- #
@@ -223,6 +294,20 @@ class HaloExchange(th.autograd.Function):
 
 def halo_exchange(x_inner, part, group=None):
     return HaloExchange.apply(x_inner, part, group)
+
+
+def halo_exchange_into(x_full, part, group=None, send_buf=None):
+    """In-place forward exchange (inference / benchmarking, no autograd):
+    ``x_full[:n_inner]`` already holds the owned rows; the halo rows land in
+    ``x_full[n_inner:]`` straight from the all-to-all-v (no concatenation copy)."""
+    n = part.n_inner
+    idx = part.device_plan(x_full.device)
+    if send_buf is None:
+        send_buf = x_full.new_empty((idx.shape[0],) + tuple(x_full.shape[1:]))
+    th.index_select(x_full[:n], 0, idx, out=send_buf)
+    _a2av(x_full[n:n + part.n_halo], send_buf, part.recv_counts.tolist(),
+          part.send_counts.tolist(), group)
+    return x_full
 
 
 def allreduce_gradients(params, group=None, average=True):

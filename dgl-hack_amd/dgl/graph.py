@@ -546,6 +546,7 @@ class _PartialIndex(GraphIndex):
     """In-edge subgraph over all nodes whose CSR ``data`` holds the parent edge ids,
     so edge features of the parent graph are addressed directly (the reference uses
     relabel maps for the same purpose, spmv.py:146-180)."""
+    _eid_is_perm = False
 
     def __init__(self, n, src, dst, parent_eid):
         super().__init__(n)

@@ -62,20 +62,43 @@ class DeviceCSR:
 class ImmutableGraphIndex:
     """The kernels' view of a graph on one device: in-CSR + out-CSR."""
 
-    def __init__(self, in_csr, out_csr, num_src, num_dst, device):
+    def __init__(self, in_csr, out_csr, num_src, num_dst, device, eid_perm=False):
         self.in_csr = in_csr
         self.out_csr = out_csr
         self.num_src = num_src
         self.num_dst = num_dst
         self.device = device
+        # in_csr.data is a permutation of [0, nnz) (whole graphs; parent-eid
+        # subgraphs are not), so an edge-id ordered COO exists
+        self.eid_perm = eid_perm
+        self._coo = None
 
     def number_of_edges(self):
         return self.in_csr.nnz
 
-    def cstruct(self, workspace=None):
+    def coo(self):
+        """(src, dst) by edge id, int32 on the device, scattered from the in-CSR
+        once and cached (8 B per edge); None for parent-eid subgraphs."""
+        if not self.eid_perm:
+            return None
+        if self._coo is None:
+            c = self.in_csr
+            src = th.empty(c.nnz, dtype=th.int32, device=c.indices.device)
+            dst = th.empty_like(src)
+            if c.nnz:
+                e = c.data.long()
+                src[e] = c.indices
+                dst[e] = c.rows
+            self._coo = (src, dst)
+        return self._coo
+
+    def cstruct(self, workspace=None, coo=False):
         g = _ffi.Graph()
         g.in_csr = self.in_csr.cstruct()
         g.out_csr = self.out_csr.cstruct()
+        pair = self.coo() if coo else None
+        g.coo_src = pair[0].data_ptr() if pair is not None and self.in_csr.nnz else None
+        g.coo_dst = pair[1].data_ptr() if pair is not None and self.in_csr.nnz else None
         g.num_bits = 32
         g.device = self.device.index if self.device.index is not None else th.cuda.current_device()
         if workspace is not None:
@@ -157,8 +180,29 @@ def device_expand_rows(indptr, nnz):
     return rows
 
 
+def device_block_gidx(num_src, num_dst, src, dst):
+    """In/out CSRs of a (num_src -> num_dst) block from device int32 COO, on the GPU.
+
+    out-CSR = stable sort of the eid-ordered COO by src; in-CSR = stable re-sort
+    of that sequence by dst == CSRTranspose(out-CSR) (``spmat_op_impl.cc:323-369``),
+    so every dst row lists its sources ascending, eids ascending within a source.
+    """
+    dev = src.device
+    m = int(src.shape[0])
+    src = src.to(th.int32).contiguous()
+    dst = dst.to(th.int32).contiguous()
+    o_ptr, o_idx, o_dat = device_coo_to_csr(num_src, src, dst)
+    o_rows = device_expand_rows(o_ptr, m)
+    i_ptr, i_idx, i_dat = device_coo_to_csr(num_dst, o_idx, o_rows, o_dat)
+    i_rows = device_expand_rows(i_ptr, m)
+    return ImmutableGraphIndex(DeviceCSR(i_ptr, i_idx, i_dat, i_rows, num_src),
+                               DeviceCSR(o_ptr, o_idx, o_dat, o_rows, num_dst),
+                               num_src, num_dst, dev, eid_perm=True)
+
+
 class GraphIndex:
     """Mutable multigraph index (``python/dgl/graph_index.py:GraphIndex``)."""
+    _eid_is_perm = True  # CSR data = own edge ids 0..E-1 (subgraph views override)
 
     def __init__(self, num_nodes=0):
         self._n = int(num_nodes)
@@ -242,15 +286,7 @@ class GraphIndex:
             if et.numel() and (int(et.min()) < 0 or int(et.max()) >= num_rels):
                 raise DGLError("edge type out of range [0, %d)" % num_rels)
             tsrc = (et * n + src).to(th.int32).contiguous()
-            dst = dst.to(th.int32).contiguous()
-            m = int(tsrc.shape[0])
-            o_ptr, o_idx, o_dat = device_coo_to_csr(num_rels * n, tsrc, dst)
-            o_rows = device_expand_rows(o_ptr, m)
-            i_ptr, i_idx, i_dat = device_coo_to_csr(n, o_idx, o_rows, o_dat)
-            i_rows = device_expand_rows(i_ptr, m)
-            self._typed[key] = ImmutableGraphIndex(DeviceCSR(i_ptr, i_idx, i_dat, i_rows, num_rels * n),
-                                                   DeviceCSR(o_ptr, o_idx, o_dat, o_rows, n),
-                                                   num_rels * n, n, device)
+            self._typed[key] = device_block_gidx(num_rels * n, n, tsrc, dst)
         return self._typed[key]
 
     def add_edges(self, u, v):
@@ -333,6 +369,7 @@ class GraphIndex:
                 self._cache[key] = self._build_on_device(device)
             else:
                 self._cache[key] = self._upload(device)
+            self._cache[key].eid_perm = self._eid_is_perm
         return self._cache[key]
 
     def _upload(self, device):
@@ -348,14 +385,6 @@ class GraphIndex:
 
     def _build_on_device(self, device):
         src, dst = self._device_only
-        src = src.to(device=device, dtype=th.int32).contiguous()
-        dst = dst.to(device=device, dtype=th.int32).contiguous()
-        n = self._n
-        # out-CSR: stable sort of the eid-ordered COO by src
-        o_ptr, o_idx, o_dat = device_coo_to_csr(n, src, dst)
-        o_rows = device_expand_rows(o_ptr, self._m)
-        # in-CSR: stable sort of the out-CSR sequence by dst == CSRTranspose(out-CSR)
-        i_ptr, i_idx, i_dat = device_coo_to_csr(n, o_idx, o_rows, o_dat)
-        i_rows = device_expand_rows(i_ptr, self._m)
-        return ImmutableGraphIndex(DeviceCSR(i_ptr, i_idx, i_dat, i_rows, n),
-                                   DeviceCSR(o_ptr, o_idx, o_dat, o_rows, n), n, n, device)
+        g = device_block_gidx(self._n, self._n, src.to(device), dst.to(device))
+        g.device = th.device(device)
+        return g

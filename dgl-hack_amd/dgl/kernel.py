@@ -66,6 +66,11 @@ def _workspace(graph, feat_len, device):
     return th.empty(int(nbytes), dtype=th.uint8, device=device)
 
 
+def _cgraph(graph, ws, per_edge):
+    """Graph struct for a call; per-edge outputs also get the edge-id ordered COO."""
+    return graph.cstruct(ws, coo=per_edge)
+
+
 def _feat_len(t):
     n = 1
     for s in t.shape[1:]:
@@ -96,7 +101,7 @@ def binary_op_reduce(reducer, op, graph, lhs, rhs, lhs_data, rhs_data, out_data,
     """kernel.py:29-148 -> _CAPI_DGLKernelBinaryOpReduce."""
     _check_ctx(graph, [("lhs_data", lhs_data), ("rhs_data", rhs_data), ("out_data", out_data)])
     ws = _workspace(graph, _feat_len(out_data), out_data.device)
-    g = graph.cstruct(ws)
+    g = _cgraph(graph, ws, reducer == "none")
     check_call(_ffi.lib().DGLMIKernelBinaryOpReduce(
         reducer.encode(), op.encode(), ctypes.byref(g), _TARGET_CODE(lhs), _TARGET_CODE(rhs),
         _arr(lhs_data, "lhs_data"), _arr(rhs_data, "rhs_data"), _arr(out_data, "out_data"),
@@ -112,7 +117,7 @@ def backward_lhs_binary_op_reduce(reducer, op, graph, lhs, rhs, lhs_data, rhs_da
     _check_ctx(graph, [("lhs_data", lhs_data), ("rhs_data", rhs_data), ("out_data", out_data),
                        ("grad_out_data", grad_out_data), ("grad_lhs_data", grad_lhs_data)])
     ws = _workspace(graph, _feat_len(grad_lhs_data), grad_lhs_data.device)
-    g = graph.cstruct(ws)
+    g = _cgraph(graph, ws, _TARGET_CODE(lhs) == 2)
     check_call(_ffi.lib().DGLMIKernelBackwardLhsBinaryOpReduce(
         reducer.encode(), op.encode(), ctypes.byref(g), _TARGET_CODE(lhs), _TARGET_CODE(rhs),
         _map(lhs_map, "lhs_mapping"), _map(rhs_map, "rhs_mapping"), _map(out_map, "out_mapping"),
@@ -129,7 +134,7 @@ def backward_rhs_binary_op_reduce(reducer, op, graph, lhs, rhs, lhs_data, rhs_da
     _check_ctx(graph, [("lhs_data", lhs_data), ("rhs_data", rhs_data), ("out_data", out_data),
                        ("grad_out_data", grad_out_data), ("grad_rhs_data", grad_rhs_data)])
     ws = _workspace(graph, _feat_len(grad_rhs_data), grad_rhs_data.device)
-    g = graph.cstruct(ws)
+    g = _cgraph(graph, ws, _TARGET_CODE(rhs) == 2)
     check_call(_ffi.lib().DGLMIKernelBackwardRhsBinaryOpReduce(
         reducer.encode(), op.encode(), ctypes.byref(g), _TARGET_CODE(lhs), _TARGET_CODE(rhs),
         _map(lhs_map, "lhs_mapping"), _map(rhs_map, "rhs_mapping"), _map(out_map, "out_mapping"),
@@ -143,7 +148,7 @@ def copy_reduce(reducer, graph, target, in_data, out_data, in_map=None, out_map=
     """kernel.py:302-393 -> _CAPI_DGLKernelCopyReduce."""
     _check_ctx(graph, [("in_data", in_data), ("out_data", out_data)])
     ws = _workspace(graph, _feat_len(out_data), out_data.device)
-    g = graph.cstruct(ws)
+    g = _cgraph(graph, ws, reducer == "none")
     check_call(_ffi.lib().DGLMIKernelCopyReduce(
         reducer.encode(), ctypes.byref(g), _TARGET_CODE(target), _arr(in_data, "in_data"),
         _arr(out_data, "out_data"), _map(in_map, "in_mapping"), _map(out_map, "out_mapping"),
@@ -157,7 +162,7 @@ def backward_copy_reduce(reducer, graph, target, in_data, out_data, grad_out_dat
     _check_ctx(graph, [("in_data", in_data), ("out_data", out_data),
                        ("grad_out_data", grad_out_data), ("grad_in_data", grad_in_data)])
     ws = _workspace(graph, _feat_len(grad_in_data), grad_in_data.device)
-    g = graph.cstruct(ws)
+    g = _cgraph(graph, ws, _TARGET_CODE(target) == 2)
     check_call(_ffi.lib().DGLMIKernelBackwardCopyReduce(
         reducer.encode(), ctypes.byref(g), _TARGET_CODE(target), _arr(in_data, "in_data"),
         _arr(out_data, "out_data"), _arr(grad_out_data, "grad_out_data"),

@@ -70,6 +70,13 @@ typedef struct {
   int32_t device;         /* HIP device ordinal the arrays live on */
   void* workspace;        /* caller-owned scratch for this call (may be NULL) */
   int64_t workspace_bytes;
+  /* Optional edge list in edge-id order (ImmutableGraph's COO, immutable_graph.h):
+   * coo_src[e], coo_dst[e] for e in [0, in_csr.nnz).  Only valid when in_csr.data
+   * is a permutation of [0, nnz) (whole graphs, not parent-eid subgraphs).  When
+   * present, per-edge outputs (reducer "none", edge gradients) are produced in
+   * edge-id order: sequential writes and edge-operand reads.  May be NULL. */
+  const int32_t* coo_src;
+  const int32_t* coo_dst;
 } DGLMIGraph;
 
 /* A contiguous row-major fp32 device array (NDArray / DLTensor subset). */

@@ -6,6 +6,8 @@
   C2  GraphConv layer on an ogbn-arxiv-sized graph (169,343 / 1,166,243, F = 128)
   C3  GATConv (8 heads x 8) on a Reddit-sized graph (232,965 / 114,615,892,
       F_in = 602): forward + backward
+  C5  RelGraphConv (4 relations, basis, 64 -> 64, per-edge norm) on 5,000,000
+      nodes / 80,000,000 typed edges: forward + backward, and the typed gather alone
 
 Graphs are synthetic Chung-Lu power-law graphs with the configs' (N, E) (the
 datasets need network downloads).  Prints one JSON object per config.
@@ -24,7 +26,7 @@ import numpy as np  # noqa: E402
 import torch as th  # noqa: E402
 
 import dgl  # noqa: E402
-from dgl.nn.pytorch import GraphConv, GATConv, FusedGATConv  # noqa: E402
+from dgl.nn.pytorch import GraphConv, GATConv, FusedGATConv, RelGraphConv  # noqa: E402
 
 
 def chung_lu(n, m, alpha, seed, device, self_loops=False):
@@ -120,9 +122,70 @@ def c3(dev, steps, warmup):
             "fused_fwd_Gedges_s": m / ms_ff / 1e6, "fused_fwd_bwd_Gedges_s": m / ms_ffb / 1e6}
 
 
+def c5(dev, steps, warmup):
+    n, m, R, f = 5_000_000, 80_000_000, 4, 64
+    g = chung_lu(n, m, 0.5, 8, dev)
+    gen = th.Generator(device=dev)
+    gen.manual_seed(8)
+    et = th.randint(0, R, (m,), generator=gen, device=dev)
+    src, dst = g._graph._device_only
+    indeg = th.bincount(dst.long(), minlength=n).float().clamp(min=1)
+    norm = (1.0 / indeg)[dst.long()].reshape(m, 1)
+    x = th.randn(n, f, device=dev, requires_grad=True)
+    conv = RelGraphConv(f, f, R, "basis", num_bases=R, self_loop=True).to(dev)
+
+    def fwd_bwd():
+        conv(g, x, et, norm).sum().backward()
+
+    def fwd():
+        with th.no_grad():
+            conv(g, x, et, norm)
+    ms_fb = timeit(fwd_bwd, steps, warmup)
+    ms_f = timeit(fwd, steps, warmup)
+    from dgl import backend as B
+    y = th.randn(R * n, f, device=dev)
+    ms_g = timeit(lambda: B._typed_aggregate(g, R, y, norm, et), steps, warmup)
+    # typed gather (u_mul_e_sum, edge weight broadcast): idx + eid + row + weight per
+    # edge, indptr + output row per node
+    alg = 4 * (n + 1) + m * (4 + 4 + 4 * f + 4) + 4 * f * n
+    return {"config": "C5 R-GCN RelGraphConv 4 rel basis 64->64", "nodes": n, "edges": m,
+            "layer_fwd_ms": ms_f, "layer_fwd_bwd_ms": ms_fb, "typed_gather_ms": ms_g,
+            "typed_gather_alg_GBps": alg / ms_g / 1e6, "typed_gather_Gedges_s": m / ms_g / 1e6}
+
+
+def sd(dev, steps, warmup):
+    """g-SDDMM on the M1 graph (RMAT scale 23, 100M edges): u_dot_v with F = 64
+    (link-prediction scoring) and u_add_v with H = 8 (GAT logits), in both item
+    orders.  Algorithmic bytes per edge (SURVEY §8d): u_dot_v 8 + 8F + 4;
+    u_add_v 8 + 2*4H + 4H."""
+    import bench
+    n, n_dst, src, dst, x = bench.build_workload(1, 0, dev)
+    g = dgl.DGLGraph.from_device_coo(src, dst, n)
+    gidx = g._graph.get_immutable_gidx(dev)
+    m = int(src.shape[0])
+    del src, dst
+    el = th.rand(n, 8, device=dev)
+    er = th.rand(n, 8, device=dev)
+    res = {"config": "SDDMM on M1 (RMAT scale 23, 100M edges)", "nodes": n, "edges": m}
+    cases = [("u_dot_v_F64", "dot", x, x, 8 + 8 * 64 + 4),
+             ("u_add_v_H8", "add", el, er, 8 + 2 * 32 + 32)]
+    for name, op, a, b, per_edge in cases:
+        for order in ("auto", "coo", "csr"):
+            if order != "auto":
+                os.environ["DGLMI_SDDMM_ORDER"] = order
+            try:
+                ms = timeit(lambda: dgl.backend.binary_reduce("none", op, gidx, 0, 1, a, b, m),
+                            steps, warmup)
+            finally:
+                os.environ.pop("DGLMI_SDDMM_ORDER", None)
+            res["%s_%s_ms" % (name, order)] = ms
+            res["%s_%s_alg_GBps" % (name, order)] = per_edge * m / ms / 1e6
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="c1,c2,c3")
+    ap.add_argument("--configs", default="c1,c2,c3,c5")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     args = ap.parse_args()

@@ -83,3 +83,33 @@ def _halo_worker(rank, world, src, dst, n, k):
 def test_halo_exchange_gloo_world2():
     src, dst, n = powerlaw(500, 4000, seed=1)
     run_world(_halo_worker, 2, (src, dst, n, 2))
+
+
+def _device_plan_worker(rank, world, src, dst, n):
+    bounds = [n * p // world for p in range(world + 1)]
+    assign = np.searchsorted(np.asarray(bounds[1:]), np.arange(n), side="right")
+    ref = D.build_partitions(src, dst, n, assign, num_parts=world)[rank]
+    lo, hi = bounds[rank], bounds[rank + 1]
+    sel = (dst >= lo) & (dst < hi)
+    part = D.build_device_partition(th.from_numpy(src[sel]).int(), th.from_numpy(dst[sel] - lo).int(),
+                                    bounds, rank)
+    # same halo set / order, same exchange plan and local numbering as the host planner
+    assert part.n_inner == ref.n_inner and part.n_halo == ref.n_halo
+    assert np.array_equal(part.halo.numpy(), ref.halo)
+    assert np.array_equal(part.send_counts, ref.send_counts)
+    assert np.array_equal(part.recv_counts, ref.recv_counts)
+    assert np.array_equal(part.send_idx.numpy(), ref.send_idx)
+    assert np.array_equal(part.local_src.numpy(), ref.local_src)
+    assert np.array_equal(part.local_dst.numpy(), ref.local_dst)
+    # in-place exchange fills the halo rows with the owners' features
+    xg = th.randn(n, 3, generator=th.Generator().manual_seed(1))
+    full = th.empty(part.n_inner + part.n_halo, 3)
+    full[:part.n_inner] = xg[lo:hi]
+    D.halo_exchange_into(full, part)
+    assert th.equal(full[part.n_inner:], xg[part.halo])
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_device_partition_plan_matches_host(world):
+    src, dst, n = powerlaw(700, 6000, seed=3)
+    run_world(_device_plan_worker, world, (np.asarray(src), np.asarray(dst), n))
