@@ -130,7 +130,16 @@ def cpu_baseline(o_ptr, o_idx, x, n_dst, budget_s=20.0, sample_edges=None):
         if time.time() - t_start > budget_s:
             break
     t = float(np.median(times))
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
     return {"value": e / t, "unit": "edges/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "host_cpus": os.cpu_count(),
             "sample": "reference CPU algorithm (oracle/dgl_ref.c ref_copy_src_sum_i32: out-CSR, "
                       "OpenMP over src rows, omp-atomic scatter, zero fill of all %d dst rows) on "
                       "%d source rows (%d edges) of the M1 graph, F=%d, median of %d pass(es), "
@@ -204,6 +213,24 @@ def measure_exchange(part, x, out_ref, args, dist, cdev, device, edges_total):
             "exchange": "all_to_all_single (%s) of halo source rows, then local copy_u_sum"
                         % dist.get_backend(),
             "rel_err_vs_replicated": err}
+
+
+def stream_copy_peak(device, nbytes=4 << 30, reps=5):
+    """Measured HBM stream rate: device-to-device copy of a 4 GiB buffer,
+    (read + write bytes) / time -- BASELINE.md §3's measured peak beside the spec."""
+    a = th.empty(nbytes // 4, dtype=th.float32, device=device)
+    b = th.empty_like(a)
+    a.fill_(1.0)
+    b.copy_(a)
+    s, e = th.cuda.Event(enable_timing=True), th.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e.record()
+    th.cuda.synchronize()
+    ms = s.elapsed_time(e) / reps
+    del a, b
+    return 2 * nbytes / (ms * 1e-3) / 1e9
 
 
 def measure_update_all(g, x, out_ref, args):
@@ -396,6 +423,13 @@ def main():
         "hbm_gbps_achieved": achieved,
         "edges_per_sec_per_gpu": value / world,
     }
+    try:
+        peak = stream_copy_peak(device)
+        res["roofline"]["measured_stream_copy_GBps"] = peak
+        res["roofline"]["frac_of_measured_stream"] = achieved / peak
+    except RuntimeError as exc:  # out of memory on a crowded device: report, don't fail
+        res["roofline"]["measured_stream_copy_GBps"] = None
+        log("stream copy peak skipped: %r" % exc)
     if exch is not None:
         res["with_exchange"] = exch
     if upd_res is not None:
