@@ -426,7 +426,7 @@ def main():
     try:
         peak = stream_copy_peak(device)
         res["roofline"]["measured_stream_copy_GBps"] = peak
-        res["roofline"]["frac_of_measured_stream"] = achieved / peak
+        res["roofline"]["stream_copy_method"] = "torch copy_ of a 4 GiB fp32 buffer, (read + write) / time"
     except RuntimeError as exc:  # out of memory on a crowded device: report, don't fail
         res["roofline"]["measured_stream_copy_GBps"] = None
         log("stream copy peak skipped: %r" % exc)

@@ -97,6 +97,8 @@ def _edge_grad_by_dot(red, op, graph, lhs, rhs, lhs_data, rhs_data, grad_out, lh
         return None
     if any(m is not None for pair in (lhs_map, rhs_map, out_map) for m in pair):
         return None
+    if not (need_l or need_r):
+        return None
     if lhs == SRC and rhs == EDGE:
         node, edge, node_first = lhs_data, rhs_data, True
     elif lhs == EDGE and rhs == SRC:
@@ -106,9 +108,12 @@ def _edge_grad_by_dot(red, op, graph, lhs, rhs, lhs_data, rhs_data, grad_out, lh
     if node.dim() != edge.dim() or node.dim() < 2 or edge.shape[-1] != 1 or node.shape[-1] == 1 \
             or tuple(edge.shape[1:-1]) != tuple(node.shape[1:-1]):
         return None
-    g_edge = grad_out.new_empty((edge.shape[0],) + tuple(node.shape[1:-1]))
-    K.binary_op_reduce("none", "dot", graph, SRC, DST, node, grad_out, g_edge)
-    g_edge = g_edge.view(edge.shape)
+    need_edge = need_r if node_first else need_l
+    g_edge = None
+    if need_edge:  # (skipped for constant edge weights, e.g. R-GCN norms)
+        g_edge = grad_out.new_empty((edge.shape[0],) + tuple(node.shape[1:-1]))
+        K.binary_op_reduce("none", "dot", graph, SRC, DST, node, grad_out, g_edge)
+        g_edge = g_edge.view(edge.shape)
     g_node = None
     need_node = need_l if node_first else need_r
     if need_node:
@@ -119,9 +124,6 @@ def _edge_grad_by_dot(red, op, graph, lhs, rhs, lhs_data, rhs_data, grad_out, lh
         else:
             K.backward_rhs_binary_op_reduce("sum", "mul", graph, lhs, rhs, lhs_data, rhs_data,
                                             grad_out, grad_out, g_node)
-    need_edge = need_r if node_first else need_l
-    if not need_edge:
-        g_edge = None
     return (g_node, g_edge) if node_first else (g_edge, g_node)
 
 
@@ -188,6 +190,58 @@ def _reduce_grad(grad, shape):
     return grad.view(shape)
 
 
+# --------------------------------------------------------------------------- #
+# dense projections that bracket the aggregations (MFMA GEMMs)
+# --------------------------------------------------------------------------- #
+def weight_grad(x, gy):
+    """dW = X^T dY for a feature projection Y = X W over N nodes (N >> F).
+
+    As one GEMM the whole node dimension is the reduction: a (F_in x F_out)
+    output of a few hundred tiles cannot fill 256 CUs and hipBLASLt runs it at
+    1-2 TB/s (5.6 ms for N = 5 M, 64 -> 256).  Split-K instead: the node rows are
+    cut into S slices, one batched GEMM computes the S partial products on MFMA
+    (S x more tiles) and a sum folds them (1.35 ms; 0.41 -> 0.07 ms at the arxiv
+    shape; scripts/gemm_splitk_probe.py)."""
+    k, n = x.shape[-1], gy.shape[-1]
+    x2 = x.reshape(-1, k).contiguous()
+    g2 = gy.reshape(-1, n).contiguous()
+    m = x2.shape[0]
+    s = 1
+    while s * 2 <= min(128, m // 1024):
+        s *= 2
+    if s < 8:
+        return x2.t() @ g2
+    mm = (m // s) * s
+    out = th.bmm(x2[:mm].view(s, mm // s, k).transpose(1, 2), g2[:mm].view(s, mm // s, n)).sum(0)
+    if mm < m:
+        out.addmm_(x2[mm:].t(), g2[mm:])
+    return out
+
+
+class _Project(th.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return th.matmul(x, w)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            gx = th.matmul(gy, w.t())
+        if ctx.needs_input_grad[1]:
+            gw = weight_grad(x, gy)
+        return gx, gw
+
+
+def project(x, w):
+    """Y = X W (X: (..., F_in), W: (F_in, F_out)) with the split-K weight gradient."""
+    if w.dim() != 2:
+        return th.matmul(x, w)
+    return _Project.apply(x, w)
+
+
 class FusedGat(th.autograd.Function):
     """tensor.py:383-413 (FusedGat), max-stabilised and without per-edge buffers."""
 
@@ -229,11 +283,11 @@ def fused_gat(graph, feat_src, el, er, slope):
 # R-GCN (hack: RgcnFirstLayer / RgcnSecondLayer, tensor.py:440-495;
 # kernels binary_reduce_impl.cu:913-1246)
 # --------------------------------------------------------------------------- #
-def _typed_aggregate(graph, num_rels, y, norm, etypes):
-    """out[v] = sum_{e=(u->v)} norm_e * y[type_e * N + u]: every relation in ONE
-    load-balanced gather over the relation-expanded graph (no per-relation SpMMs,
-    no per-edge weight products)."""
-    gidx = graph._graph.typed_gidx(y.device, num_rels, etypes)
+def _typed_aggregate(graph, num_rels, y, norm, etypes, node_major=False):
+    """out[v] = sum_{e=(u->v)} norm_e * y[type_e * N + u] (or y[u * R + type_e] with
+    ``node_major``): every relation in ONE load-balanced gather over the
+    relation-expanded graph (no per-relation SpMMs, no per-edge weight products)."""
+    gidx = graph._graph.typed_gidx(y.device, num_rels, etypes, node_major)
     n = graph.number_of_nodes()
     if norm is None:
         return copy_reduce("sum", gidx, SRC, y, n)
@@ -254,8 +308,9 @@ def rgcn_layer1(graph, x, weight, norm, etypes=None):
     """ret[v] = sum_e (x[u] @ W[type_e]) * norm_e.
 
     The per-edge (F_in x F_out) products of the hack's kernel (binary_reduce_impl.cu:
-    1050-1117) become R dense GEMMs Y_r = X W_r (MFMA via hipBLASLt) plus one typed
-    gather; the hack also drops the weight gradient (tensor.py:493), autograd keeps it."""
-    R = weight.shape[0]
-    y = th.matmul(x.unsqueeze(0), weight)  # (R, N, F_out)
-    return _typed_aggregate(graph, R, y.reshape(R * x.shape[0], weight.shape[2]), norm, etypes)
+    1050-1117) become ONE dense GEMM Y = X [W_0 | ... | W_{R-1}] (N x R*F_out, MFMA
+    via hipBLASLt) plus one typed gather over rows u * R + type; the hack also drops
+    the weight gradient (tensor.py:493), autograd keeps it."""
+    R, fi, fo = weight.shape
+    y = project(x, weight.permute(1, 0, 2).reshape(fi, R * fo))  # (N, R * F_out)
+    return _typed_aggregate(graph, R, y.view(x.shape[0] * R, fo), norm, etypes, node_major=True)

@@ -355,13 +355,13 @@ class DistGraphConv(th.nn.Module):
             feat = feat * norm.reshape(norm.shape + (1,) * (feat.dim() - 1))
         w = conv.weight
         if conv._in_feats > conv._out_feats:
-            feat = th.matmul(feat, w)
+            feat = B.project(feat, w)
             full = halo_exchange(feat, part, group)
             rst = B.copy_reduce("sum", gidx, 0, full, part.n_inner)
         else:
             full = halo_exchange(feat, part, group)
             rst = B.copy_reduce("sum", gidx, 0, full, part.n_inner)
-            rst = th.matmul(rst, w)
+            rst = B.project(rst, w)
         if conv._norm != "none":
             degs = in_deg_inner.float().clamp(min=1)
             norm = th.pow(degs, -0.5) if conv._norm == "both" else 1.0 / degs

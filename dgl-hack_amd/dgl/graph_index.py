@@ -257,20 +257,23 @@ class GraphIndex:
             self._etype = np.concatenate([self._etype, pad])
         return self._etype
 
-    def typed_gidx(self, device, num_rels, etypes=None):
-        """Relation-expanded graph for R-GCN: source (type_e * N + u) -> v, R*N sources.
+    def typed_gidx(self, device, num_rels, etypes=None, node_major=False):
+        """Relation-expanded graph for R-GCN: source (type_e * N + u) -> v, R*N sources
+        (relation-major rows, as a (R, N, F) weight/feature tensor is laid out), or
+        source (u * R + type_e) with ``node_major`` (the rows of one (N, R*F) GEMM
+        output X @ [W_0 | ... | W_{R-1}]).
 
-        Built on the device (two stable radix sorts) and cached per (device, R, etypes)."""
+        Built on the device (two stable radix sorts) and cached per (device, R, etypes, layout)."""
         device = th.device(device)
         if etypes is None:
             et = self.edge_types()
             if et is None:
                 raise DGLError("graph has no edge types; pass etypes")
-            key = (str(device), int(num_rels), "graph")
+            key = (str(device), int(num_rels), "graph", bool(node_major))
             etypes = th.from_numpy(et)
         else:
             key = (str(device), int(num_rels), etypes.data_ptr(), etypes._version,
-                   int(etypes.shape[0]))
+                   int(etypes.shape[0]), bool(node_major))
         if key not in self._typed:
             n = self._n
             if num_rels * n >= 0x7FFFFFFF:
@@ -285,7 +288,7 @@ class GraphIndex:
                 raise DGLError("etypes must have one entry per edge")
             if et.numel() and (int(et.min()) < 0 or int(et.max()) >= num_rels):
                 raise DGLError("edge type out of range [0, %d)" % num_rels)
-            tsrc = (et * n + src).to(th.int32).contiguous()
+            tsrc = ((src * num_rels + et) if node_major else (et * n + src)).to(th.int32).contiguous()
             self._typed[key] = device_block_gidx(num_rels * n, n, tsrc, dst)
         return self._typed[key]
 

@@ -25,11 +25,11 @@ class FusedGATConv(GATConv):
         if isinstance(feat, tuple):
             h_src = self.feat_drop(feat[0])
             h_dst = self.feat_drop(feat[1])
-            feat_src = self.fc_src(h_src).view(-1, self._num_heads, self._out_feats)
-            feat_dst = self.fc_dst(h_dst).view(-1, self._num_heads, self._out_feats)
+            feat_src = B.project(h_src, self.fc_src.weight.t()).view(-1, self._num_heads, self._out_feats)
+            feat_dst = B.project(h_dst, self.fc_dst.weight.t()).view(-1, self._num_heads, self._out_feats)
         else:
             h_src = h_dst = self.feat_drop(feat)
-            feat_src = feat_dst = self.fc(h_src).view(-1, self._num_heads, self._out_feats)
+            feat_src = feat_dst = B.project(h_src, self.fc.weight.t()).view(-1, self._num_heads, self._out_feats)
         el = (feat_src * self.attn_l).sum(dim=-1).unsqueeze(-1)
         er = (feat_dst * self.attn_r).sum(dim=-1).unsqueeze(-1)
         rst = B.fused_gat(graph, feat_src, el, er, self.negative_slope)

@@ -10,6 +10,7 @@ import torch as th
 from torch import nn
 from torch.nn import init
 
+from .... import backend as B
 from .... import function as fn
 from ...._ffi import DGLError
 
@@ -57,7 +58,7 @@ class GraphConv(nn.Module):
             weight = self.weight
         if self._in_feats > self._out_feats:
             if weight is not None:
-                feat = th.matmul(feat, weight)
+                feat = B.project(feat, weight)
             graph.srcdata["h"] = feat
             graph.update_all(fn.copy_src(src="h", out="m"), fn.sum(msg="m", out="h"))
             rst = graph.dstdata["h"]
@@ -66,7 +67,7 @@ class GraphConv(nn.Module):
             graph.update_all(fn.copy_src(src="h", out="m"), fn.sum(msg="m", out="h"))
             rst = graph.dstdata["h"]
             if weight is not None:
-                rst = th.matmul(rst, weight)
+                rst = B.project(rst, weight)
         if self._norm != "none":
             degs = graph.in_degrees().to(feat.device).float().clamp(min=1)
             norm = th.pow(degs, -0.5) if self._norm == "both" else 1.0 / degs

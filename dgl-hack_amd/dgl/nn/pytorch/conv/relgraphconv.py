@@ -61,27 +61,35 @@ class RelGraphConv(nn.Module):
         return self.weight
 
     def _transform(self, x):
-        """Y[r, u] = x_u W_r for every relation: (R, N, out_feat)."""
+        """Y = x_u W_r for every (node, relation), as rows of the typed gather.
+
+        Returns (y, node_major): one-hot input gives the (R, N, out) slice of the
+        weights (relation-major rows); feature input gives ONE GEMM
+        X [W_0 | ... | W_{R-1}] of shape (N, R * out) (node-major rows) -- not R
+        broadcast GEMMs over an expanded copy of X."""
         if x.dtype == th.int64 and x.dim() == 1:
             if self.regularizer == "bdd":
                 raise TypeError("Block decomposition does not allow integer ID feature.")
-            return self._relation_weights()[:, x, :]          # one-hot input (layer 0)
+            return self._relation_weights()[:, x, :], False   # one-hot input (layer 0)
+        R, fo = self.num_rels, self.out_feat
         if self.regularizer == "basis":
-            return th.matmul(x.unsqueeze(0), self._relation_weights())
-        w = self.weight.view(self.num_rels, self.num_bases, self.submat_in, self.submat_out)
+            w = self._relation_weights().permute(1, 0, 2).reshape(self.in_feat, R * fo)
+            return B.project(x, w), True
+        w = self.weight.view(R, self.num_bases, self.submat_in, self.submat_out)
         xb = x.view(x.shape[0], self.num_bases, self.submat_in)
-        return th.einsum("nbi,rbio->rnbo", xb, w).reshape(self.num_rels, x.shape[0], self.out_feat)
+        return th.einsum("nbi,rbio->nrbo", xb, w), True
 
     def forward(self, g, x, etypes, norm=None):
-        y = self._transform(x).contiguous()
+        y, node_major = self._transform(x)
+        y = y.contiguous()
         n = g.number_of_nodes()
         node_repr = B._typed_aggregate(g, self.num_rels, y.view(self.num_rels * n, self.out_feat),
-                                       norm, etypes)
+                                       norm, etypes, node_major)
         if self.bias:
             node_repr = node_repr + self.h_bias
         if self.self_loop:
             loop = self.loop_weight[x] if (x.dtype == th.int64 and x.dim() == 1) else \
-                th.matmul(x, self.loop_weight)
+                B.project(x, self.loop_weight)
             node_repr = node_repr + loop
         if self.activation:
             node_repr = self.activation(node_repr)

@@ -183,6 +183,31 @@ def sd(dev, steps, warmup):
     return res
 
 
+def gemm(dev, steps, warmup):
+    """The dense feature projections that bracket the aggregations (MFMA via
+    hipBLASLt, fp32 in / fp32 accumulate like the reference): forward X W and the
+    two backward GEMMs, at each config's shape.  Utilisation = achieved TFLOP/s /
+    157.3 TFLOP/s (MI355X dense FP32 matrix peak, MI355X_MICROARCH.md)."""
+    peak = 157.3
+    shapes = {"C1 layer1 2708x1433->16": (2708, 1433, 16),
+              "C2 169343x128->128": (169343, 128, 128),
+              "C3 GAT fc 232965x602->64": (232965, 602, 64),
+              "C5 R-GCN 5Mx64->4x64": (5_000_000, 64, 256)}
+    res = {"config": "bracketing GEMMs (fp32, torch.matmul -> hipBLASLt MFMA)"}
+    for name, (m, k, n) in shapes.items():
+        x = th.randn(m, k, device=dev)
+        w = th.randn(k, n, device=dev)
+        gy = th.randn(m, n, device=dev)
+        fl = 2.0 * m * k * n
+        for tag, fn in (("fwd", lambda: x @ w), ("grad_x", lambda: gy @ w.t()),
+                        ("grad_w", lambda: x.t() @ gy)):
+            ms = timeit(fn, steps, warmup)
+            res["%s %s ms" % (name, tag)] = ms
+            res["%s %s TFLOPs" % (name, tag)] = fl / ms / 1e9
+            res["%s %s mfma_util" % (name, tag)] = fl / ms / 1e9 / peak
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="c1,c2,c3,c5")

@@ -165,3 +165,22 @@ def test_gat_conv_vs_dense(use_fused):
     assert th.allclose(out.double(), rst, rtol=1e-4, atol=1e-4)
     assert th.allclose(gat.fc.weight.grad.double(), Wd.grad, rtol=1e-3, atol=1e-3)
     assert th.allclose(gat.attn_l.grad.double(), al.grad, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("m,k,n", [(5000, 602, 64), (169343, 128, 128), (300001, 64, 32)])
+def test_project_split_k_weight_grad(m, k, n):
+    """dgl.backend.project: Y = X W with the split-K weight gradient (bmm over node
+    slices + sum) equals X^T dY in fp64 to fp32 accuracy; dX = dY W^T."""
+    from dgl import backend as B
+    g = th.Generator(device=DEV).manual_seed(0)
+    x = th.randn(m, k, device=DEV, generator=g).requires_grad_()
+    w = th.randn(k, n, device=DEV, generator=g).requires_grad_()
+    gy = th.randn(m, n, device=DEV, generator=g)
+    y = B.project(x, w)
+    y.backward(gy)
+    ref_w = x.detach().double().t() @ gy.double()
+    ref_x = gy.double() @ w.detach().double().t()
+    scale_w = (x.detach().double().abs().t() @ gy.double().abs())
+    assert th.allclose(y.double(), x.detach().double() @ w.detach().double(), rtol=1e-4, atol=1e-3)
+    assert bool(((w.grad.double() - ref_w).abs() <= 1e-5 * scale_w + 1e-4).all())
+    assert th.allclose(x.grad.double(), ref_x, rtol=1e-4, atol=1e-3)
