@@ -26,6 +26,11 @@ _NOMAP = (None, None)
 
 
 def _degs(reducer_target, graph, n, out_size, in_map, out_map, like):
+    """In-degrees for ``mean`` (tensor.py:308-325 counts them with a copy_reduce of
+    ones each call).  Unmapped calls read the cached CSR degrees instead -- the
+    integers (exact in fp32 below 2^24, where a sum of ones stops counting)."""
+    if in_map is None and out_map is None and out_size == graph.in_csr.num_rows:
+        return graph.in_csr.degrees().to(like.dtype)
     ones = like.new_ones((n,))
     degs = like.new_empty((out_size,))
     K.copy_reduce("sum", graph, reducer_target, ones, degs, in_map, out_map)

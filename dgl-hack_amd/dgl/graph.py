@@ -291,6 +291,12 @@ class DGLGraph(object):
         d = th.from_numpy(self._graph.out_degrees())
         return d if is_all(v) else d[th.as_tensor(_to_index_array(v, "v"))]
 
+    def _device_degrees(self, device, direction):
+        """In- ("in") or out- ("out") degrees of all nodes as a device tensor, from
+        the cached device CSRs (no host round trip; used by GraphConv's norm)."""
+        gidx = self._graph.get_immutable_gidx(device)
+        return (gidx.in_csr if direction == "in" else gidx.out_csr).degrees()
+
     def in_degree(self, v):
         return int(self.in_degrees([v])[0])
 

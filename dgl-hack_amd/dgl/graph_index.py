@@ -56,7 +56,10 @@ class DeviceCSR:
         return c
 
     def degrees(self):
-        return self.indptr[1:] - self.indptr[:-1]
+        """Row degrees on the device (int32), computed once and cached."""
+        if getattr(self, "_deg", None) is None:
+            self._deg = self.indptr[1:] - self.indptr[:-1]
+        return self._deg
 
 
 class ImmutableGraphIndex:

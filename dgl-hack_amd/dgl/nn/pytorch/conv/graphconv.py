@@ -45,7 +45,7 @@ class GraphConv(nn.Module):
     def forward(self, graph, feat, weight=None):
         graph = graph.local_var()
         if self._norm == "both":
-            degs = graph.out_degrees().to(feat.device).float().clamp(min=1)
+            degs = graph._device_degrees(feat.device, "out").float().clamp(min=1)
             norm = th.pow(degs, -0.5)
             norm = th.reshape(norm, norm.shape + (1,) * (feat.dim() - 1))
             feat = feat * norm
@@ -69,7 +69,7 @@ class GraphConv(nn.Module):
             if weight is not None:
                 rst = B.project(rst, weight)
         if self._norm != "none":
-            degs = graph.in_degrees().to(feat.device).float().clamp(min=1)
+            degs = graph._device_degrees(feat.device, "in").float().clamp(min=1)
             norm = th.pow(degs, -0.5) if self._norm == "both" else 1.0 / degs
             norm = th.reshape(norm, norm.shape + (1,) * (feat.dim() - 1))
             rst = rst * norm
