@@ -153,3 +153,31 @@ def test_builtin_names():
             if lhs != rhs:
                 for op in ["add", "sub", "mul", "div", "dot"]:
                     assert hasattr(fn, "%s_%s_%s" % (lhs, op, rhs))
+
+
+def test_ctypes_structs_match_header_layout(tmp_path):
+    """The ctypes mirrors in dgl/_ffi.py have the C layout of include/dglmi.h
+    (sizes and field offsets, compiled with gcc here)."""
+    import ctypes
+    import os
+    import subprocess
+    from dgl import _ffi
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    fields = {"DGLMICsr": (_ffi.CSR, [f[0] for f in _ffi.CSR._fields_]),
+              "DGLMIGraph": (_ffi.Graph, [f[0] for f in _ffi.Graph._fields_]),
+              "DGLMIArray": (_ffi.Array, [f[0] for f in _ffi.Array._fields_])}
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "dglmi.h"', "int main(void) {"]
+    for cname, (_, names) in fields.items():
+        lines.append('printf("%%s %%zu\\n", "%s", sizeof(%s));' % (cname, cname))
+        for f in names:
+            lines.append('printf("%%s.%%s %%zu\\n", "%s", "%s", offsetof(%s, %s));' % (cname, f, cname, f))
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I", os.path.join(root, "include"), str(src), "-o", str(exe)])
+    got = dict(l.rsplit(" ", 1) for l in subprocess.check_output([str(exe)]).decode().split("\n") if l)
+    for cname, (cls, names) in fields.items():
+        assert int(got[cname]) == ctypes.sizeof(cls), cname
+        for f in names:
+            assert int(got["%s.%s" % (cname, f)]) == getattr(cls, f).offset, (cname, f)
