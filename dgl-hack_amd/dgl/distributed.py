@@ -207,8 +207,13 @@ class DevicePartition:
         self.local_dst = local_dst        # device int32, [0, n_inner)
         self._g = None
 
+    @property
+    def inner(self):
+        """Global ids of the owned nodes (as :attr:`Partition.inner`)."""
+        return np.arange(self.lo, self.hi, dtype=np.int64)
+
     def number_of_edges(self):
-        return int(self.local_src.shape[0])
+        return self._g.number_of_edges() if self._g is not None else int(self.local_src.shape[0])
 
     def gidx(self, device=None):
         """Local block CSRs, built on the GPU at first use (the edge list may be
@@ -257,7 +262,15 @@ def build_device_partition(src, dst, bounds, rank, group=None):
 # --------------------------------------------------------------------------- #
 # collectives
 # --------------------------------------------------------------------------- #
+def _single():
+    return not (dist.is_available() and dist.is_initialized())
+
+
 def _a2av(out, inp, out_splits, in_splits, group):
+    if _single():  # one process: nothing leaves the rank
+        if out.numel():
+            out.copy_(inp.reshape(out.shape))
+        return out
     backend = dist.get_backend(group)
     if backend == "gloo" and inp.device.type != "cpu":
         o = out.cpu()
@@ -313,7 +326,7 @@ def halo_exchange_into(x_full, part, group=None, send_buf=None):
 def allreduce_gradients(params, group=None, average=True):
     """One flattened all-reduce for all gradients (RCCL over xGMI)."""
     grads = [p.grad for p in params if p.grad is not None]
-    if not grads:
+    if not grads or _single():
         return
     flat = th.cat([g.reshape(-1) for g in grads])
     if dist.get_backend(group) == "gloo" and flat.device.type != "cpu":

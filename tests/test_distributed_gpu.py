@@ -14,7 +14,7 @@ def _model(fin, hid, fout):
     return GraphConv(fin, hid, activation=th.relu), GraphConv(hid, fout)
 
 
-def _worker(rank, world, src, dst, n, q):
+def _worker(rank, world, src, dst, n, q, planner):
     import dgl
     from dgl import distributed as D
     dev = "cuda:0"
@@ -23,8 +23,15 @@ def _worker(rank, world, src, dst, n, q):
     d1.conv.load_state_dict(c1.state_dict())
     d2.conv.load_state_dict(c2.state_dict())
     d1, d2 = d1.to(dev), d2.to(dev)
-    assign = D.partition_assignment(n, src, dst, world, "ldg")
-    part = D.build_partitions(src, dst, n, assign, num_parts=world)[rank]
+    if planner == "host_ldg":
+        assign = D.partition_assignment(n, src, dst, world, "ldg")
+        part = D.build_partitions(src, dst, n, assign, num_parts=world)[rank]
+    else:  # contiguous id ranges, halo plan built on the device
+        bounds = [n * p // world for p in range(world + 1)]
+        lo, hi = bounds[rank], bounds[rank + 1]
+        sel = (dst >= lo) & (dst < hi)
+        part = D.build_device_partition(th.from_numpy(src[sel]).to(dev).int(),
+                                        th.from_numpy(dst[sel] - lo).to(dev).int(), bounds, rank)
     x = th.from_numpy(np.random.RandomState(0).randn(n, 16).astype(np.float32))
     inner = th.from_numpy(part.inner)
     odeg = th.from_numpy(np.bincount(src, minlength=n))[inner].to(dev)
@@ -57,12 +64,13 @@ def _worker(rank, world, src, dst, n, q):
         q.put("ok")
 
 
-def test_dist_gcn_matches_single_gpu():
+@pytest.mark.parametrize("planner", ["host_ldg", "device_contiguous"])
+def test_dist_gcn_matches_single_gpu(planner):
     import torch.multiprocessing as mp
     from dist_util import run_world
     from graphs import powerlaw
     src, dst, n = powerlaw(3000, 40000, seed=3)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    run_world(_worker, 2, (src, dst, n, q))
+    run_world(_worker, 2, (src, dst, n, q, planner))
     assert q.get(timeout=5) == "ok"
