@@ -115,7 +115,10 @@ def main():
         opt.zero_grad()
         h = l1(part, x, odeg, ideg)
         logits = l2(part, h, odeg, ideg)
-        loss = th.nn.functional.cross_entropy(logits, y, reduction="sum") / n
+        # cross entropy as log_softmax + gather + sum: torch's nll_loss "sum"
+        # reduction is a single-block kernel (13 ms fwd + 10 ms bwd at 10 M rows)
+        logp = th.log_softmax(logits, dim=1)
+        loss = -logp.gather(1, y.view(-1, 1)).sum() / n
         loss.backward()
         D.allreduce_gradients(params, average=False)
         opt.step()
