@@ -186,3 +186,54 @@ def test_coo_order_matches_csr_order_bitwise(sk):
             os.environ.pop("DGLMI_SDDMM_ORDER", None)
     a, b = res
     assert th.equal(a, b)
+
+
+def test_apply_edges_full_and_partial():
+    """DGLGraph.apply_edges with builtins on all edges (edge-id order via the COO)
+    and on a subset (parent-eid subgraph, in-CSR order); untouched rows keep
+    their previous value (graph.py apply_edges semantics)."""
+    import dgl.function as fn
+    src, dst, n = powerlaw(500, 6000, seed=2)
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    rs = np.random.RandomState(4)
+    u = th.from_numpy(rs.uniform(-1, 1, (n, 4, 8)).astype(np.float32)).to(DEV)
+    e = th.from_numpy(rs.uniform(-1, 1, (len(src), 4, 8)).astype(np.float32)).to(DEV)
+    g.ndata["h"] = u
+    g.edata["w"] = e
+    g.apply_edges(fn.u_dot_v("h", "h", "s"))
+    s_ref = (u[th.from_numpy(src)] * u[th.from_numpy(dst)]).sum(-1, keepdim=True)
+    assert th.allclose(g.edata["s"].reshape(s_ref.shape), s_ref, rtol=1e-5, atol=1e-5)
+    g.apply_edges(fn.e_sub_v("w", "h", "d"))
+    d_ref = e - u[th.from_numpy(dst)]
+    assert th.equal(g.edata["d"], d_ref)
+    sub = np.arange(0, len(src), 3)
+    g.edata["d2"] = th.zeros_like(e)
+    g.apply_edges(fn.u_mul_e("h", "w", "d2"), edges=sub)
+    want = th.zeros_like(e)
+    want[th.from_numpy(sub)] = u[th.from_numpy(src[sub])] * e[th.from_numpy(sub)]
+    assert th.equal(g.edata["d2"], want)
+
+
+def test_per_edge_and_generic_on_degenerate_graphs():
+    """No edges / one edge / isolated nodes: identities, no out-of-range access."""
+    for src, dst, n in ((np.zeros(0, np.int64), np.zeros(0, np.int64), 5),
+                        (np.array([3]), np.array([1]), 5)):
+        g = dgl.DGLGraph()
+        g.add_nodes(n)
+        if len(src):
+            g.add_edges(src, dst)
+        gidx = g._graph.get_immutable_gidx(DEV)
+        m = len(src)
+        u = th.rand(n, 8, device=DEV)
+        out = dgl.backend.binary_reduce("none", "add", gidx, 0, 1, u, u, m)
+        assert out.shape == (m, 8)
+        if m:
+            assert th.equal(out[0], u[3] + u[1])
+        for red, ident in (("sum", 0.0), ("max", -3.402823466e38), ("min", 3.402823466e38)):
+            r = dgl.backend.binary_reduce(red, "sub", gidx, 0, 1, u, u, n)
+            rows = [v for v in range(n) if v not in set(dst.tolist())]
+            assert bool((r[rows] == ident).all()), red
+            if m:
+                assert th.equal(r[1], u[3] - u[1])
