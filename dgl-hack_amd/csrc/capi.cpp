@@ -815,4 +815,91 @@ int64_t DGLMIKernelWorkspaceBytes(const DGLMICsr* csr, int64_t feat_len) {
   return fast_workspace_bytes(csr->nnz, feat_len);
 }
 
+int DGLMIEdgeSoftmaxSupported(int64_t values_per_edge) {
+  return softmax_supported(values_per_edge) ? 1 : 0;
+}
+
+int64_t DGLMIEdgeSoftmaxWorkspaceBytes(const DGLMICsr* in_csr, int64_t values_per_edge) {
+  if (in_csr == nullptr || in_csr->nnz <= 0 || values_per_edge <= 0) return 0;
+  const int64_t chunks = (in_csr->nnz + softmax_chunk_edges(in_csr->nnz) - 1) /
+                         softmax_chunk_edges(in_csr->nnz);
+  const int64_t stats = ((2 * in_csr->num_rows * values_per_edge * 4) + 255) & ~int64_t(255);
+  return stats + chunks * 2 * values_per_edge * 4;
+}
+
+namespace {
+// Shared checks of the edge-softmax entry points; returns H.
+int64_t softmax_setup(const DGLMIGraph* g, const DGLMIArray* x, const char* name,
+                      dglmi::SoftmaxArgs& a) {
+  check_graph(g);
+  check_array(x, name);
+  const DGLMICsr& in = g->in_csr;
+  check_csr(in, "in_csr", true);
+  DGLMI_CHECK(x->shape[0] >= in.nnz, std::string(name) + " has fewer rows than edges");
+  const int64_t H = feat_numel(x);
+  DGLMI_CHECK(softmax_supported(H), "edge softmax supports 1, 2, 4, 8 or 16 values per edge");
+  DGLMI_CHECK(aligned16(x->data), std::string(name) + " must be 16-byte aligned");
+  std::memset(&a, 0, sizeof(a));
+  a.indptr = in.indptr;
+  a.rows = in.rows;
+  a.eids = in.data;
+  a.coo_dst = (g->coo_src && g->coo_dst) ? g->coo_dst : nullptr;
+  a.nnz = in.nnz;
+  a.num_rows = in.num_rows;
+  a.H = static_cast<int>(H);
+  a.chunk = softmax_chunk_edges(in.nnz);
+  return H;
+}
+}  // namespace
+
+int DGLMIEdgeSoftmaxForward(const DGLMIGraph* graph, const DGLMIArray* logits, DGLMIArray* out,
+                            void* stream) {
+  API_BEGIN();
+  dglmi::SoftmaxArgs a;
+  const int64_t H = softmax_setup(graph, logits, "logits", a);
+  check_array(out, "out");
+  DGLMI_CHECK(feat_numel(out) == H && out->shape[0] == logits->shape[0], "out shape");
+  DGLMI_CHECK(aligned16(out->data), "out must be 16-byte aligned");
+  DeviceGuard guard(graph->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (a.nnz == 0) return 0;
+  Scratch ws(graph, DGLMIEdgeSoftmaxWorkspaceBytes(&graph->in_csr, H), s);
+  const int64_t stats = ((2 * a.num_rows * H * 4) + 255) & ~int64_t(255);
+  a.stat0 = static_cast<float*>(ws.ptr);
+  a.stat1 = a.stat0 + a.num_rows * H;
+  a.carry = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + stats);
+  a.s = logits->data;
+  a.out = out->data;
+  launch_edge_softmax(a, false, s);
+  check_hip(hipGetLastError(), "edge softmax forward launch");
+  API_END();
+}
+
+int DGLMIEdgeSoftmaxBackward(const DGLMIGraph* graph, const DGLMIArray* out,
+                             const DGLMIArray* grad_out, DGLMIArray* grad_logits, void* stream) {
+  API_BEGIN();
+  dglmi::SoftmaxArgs a;
+  const int64_t H = softmax_setup(graph, out, "out", a);
+  check_array(grad_out, "grad_out");
+  check_array(grad_logits, "grad_logits");
+  DGLMI_CHECK(feat_numel(grad_out) == H && feat_numel(grad_logits) == H &&
+                  grad_out->shape[0] == out->shape[0] && grad_logits->shape[0] == out->shape[0],
+              "grad shapes");
+  DGLMI_CHECK(aligned16(grad_out->data) && aligned16(grad_logits->data),
+              "grads must be 16-byte aligned");
+  DeviceGuard guard(graph->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (a.nnz == 0) return 0;
+  Scratch ws(graph, DGLMIEdgeSoftmaxWorkspaceBytes(&graph->in_csr, H), s);
+  const int64_t stats = ((2 * a.num_rows * H * 4) + 255) & ~int64_t(255);
+  a.stat0 = static_cast<float*>(ws.ptr);
+  a.carry = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + stats);
+  a.s = out->data;
+  a.ga = grad_out->data;
+  a.out = grad_logits->data;
+  launch_edge_softmax(a, true, s);
+  check_hip(hipGetLastError(), "edge softmax backward launch");
+  API_END();
+}
+
 }  // extern "C"

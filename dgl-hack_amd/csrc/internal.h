@@ -161,6 +161,27 @@ struct SddmmArgs {
 bool sddmm_supported(int op, bool bwd, int64_t D, int64_t len);
 void launch_sddmm(int op, bool bwd, const SddmmArgs& a, hipStream_t s);
 
+// Fused edge softmax (kernels_softmax.hip).
+struct SoftmaxArgs {
+  const int32_t* indptr;   // in-CSR
+  const int32_t* rows;
+  const int32_t* eids;
+  const int32_t* coo_dst;  // optional: edge-id order for the per-edge pass
+  int64_t nnz;
+  int64_t num_rows;
+  int H;                   // values per edge
+  const float* s;          // forward: logits; backward: the softmax output
+  const float* ga;         // backward: gradient wrt the output
+  float* stat0;            // forward: row max m; backward: row sum S (num_rows x H)
+  float* stat1;            // forward: row sum of exp l
+  float* out;              // forward: softmax; backward: gradient wrt the logits
+  float* carry;            // num_chunks x 2H
+  int64_t chunk;
+};
+bool softmax_supported(int64_t H);
+int64_t softmax_chunk_edges(int64_t nnz);
+void launch_edge_softmax(const SoftmaxArgs& a, bool backward, hipStream_t s);
+
 // Load-balanced reduce-to-row kernels (kernels_spmm.hip).
 enum FastKind : int {
   FAST_COPY_COL = 0,    // v = X[col]

@@ -118,6 +118,13 @@ _SIGS = {
         ctypes.c_float, ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.c_void_p]),
+    "DGLMIEdgeSoftmaxSupported": (ctypes.c_int, [ctypes.c_int64]),
+    "DGLMIEdgeSoftmaxWorkspaceBytes": (ctypes.c_int64, [ctypes.POINTER(CSR), ctypes.c_int64]),
+    "DGLMIEdgeSoftmaxForward": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.c_void_p]),
+    "DGLMIEdgeSoftmaxBackward": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_void_p]),
     "DGLMIPartitionLDG": (ctypes.c_int, [
         ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_double,
         ctypes.c_void_p]),

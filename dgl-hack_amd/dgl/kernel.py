@@ -202,3 +202,31 @@ def fused_gat_backward(graph, feat_src, el, er, slope, out, max_in, sum_in, grad
         _arr(out, "out"), _arr(max_in, "max_in"), _arr(sum_in, "sum_in"),
         _arr(grad_out, "grad_out"), _arr(grad_feat_src, "grad_feat_src"), _arr(grad_el, "grad_el"),
         _arr(grad_er, "grad_er"), _stream(grad_out)))
+
+
+def edge_softmax_supported(values_per_edge):
+    return bool(_ffi.lib().DGLMIEdgeSoftmaxSupported(int(values_per_edge)))
+
+
+def _softmax_ws(graph, h, device):
+    nbytes = _ffi.lib().DGLMIEdgeSoftmaxWorkspaceBytes(ctypes.byref(graph.in_csr.cstruct()), int(h))
+    return th.empty(int(nbytes), dtype=th.uint8, device=device) if nbytes > 0 else None
+
+
+def edge_softmax_forward(graph, logits, out):
+    """Fused edge softmax (extension of softmax.py:15-84) -> DGLMIEdgeSoftmaxForward."""
+    _check_ctx(graph, [("logits", logits), ("out", out)])
+    g = graph.cstruct(_softmax_ws(graph, _feat_len(logits), logits.device), coo=True)
+    check_call(_ffi.lib().DGLMIEdgeSoftmaxForward(ctypes.byref(g), _arr(logits, "logits"),
+                                                  _arr(out, "out"), _stream(out)))
+    return out
+
+
+def edge_softmax_backward(graph, out, grad_out, grad_logits):
+    """softmax.py:86-114 fused -> DGLMIEdgeSoftmaxBackward."""
+    _check_ctx(graph, [("out", out), ("grad_out", grad_out), ("grad_logits", grad_logits)])
+    g = graph.cstruct(_softmax_ws(graph, _feat_len(out), out.device), coo=True)
+    check_call(_ffi.lib().DGLMIEdgeSoftmaxBackward(ctypes.byref(g), _arr(out, "out"),
+                                                   _arr(grad_out, "grad_out"),
+                                                   _arr(grad_logits, "grad_logits"), _stream(out)))
+    return grad_logits

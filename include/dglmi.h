@@ -181,6 +181,21 @@ int DGLMIFusedGatBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src, c
 /* 1 if the fused GAT kernels support (heads, head_dim), else 0. */
 int DGLMIFusedGatSupported(int64_t heads, int64_t head_dim);
 
+/* Fused edge softmax over the in-edges of every destination node (extension:
+ * the reference composes it from five kernels in Python,
+ * python/dgl/nn/pytorch/softmax.py:15-114; same math, max-stabilised).
+ * logits / out / grads: (E, ...) by edge id with H values per edge
+ * (DGLMIEdgeSoftmaxSupported(H)).  The call needs
+ * DGLMIEdgeSoftmaxWorkspaceBytes(&graph->in_csr, H) bytes of scratch, taken from
+ * graph->workspace when it is large enough (else stream-ordered allocation). */
+int DGLMIEdgeSoftmaxSupported(int64_t values_per_edge);
+int64_t DGLMIEdgeSoftmaxWorkspaceBytes(const DGLMICsr* in_csr, int64_t values_per_edge);
+int DGLMIEdgeSoftmaxForward(const DGLMIGraph* graph, const DGLMIArray* logits, DGLMIArray* out,
+                            void* stream);
+/* grad_logits = out * grad_out - out * sum_{in-edges}(out * grad_out) (softmax.py:86-114). */
+int DGLMIEdgeSoftmaxBackward(const DGLMIGraph* graph, const DGLMIArray* out,
+                             const DGLMIArray* grad_out, DGLMIArray* grad_logits, void* stream);
+
 /* ---- partitioning (metis_partition.cc:19-66 replacement; METIS is absent) --
  * Linear Deterministic Greedy over a symmetrised host CSR (int64): node v goes
  * to the part maximising |N(v) ∩ P| (1 - |P| / C), C = ceil(n / k)(1 + slack). */

@@ -59,16 +59,44 @@ def c1(dev, steps, warmup):
     x = th.randn(2708, 1433, device=dev)
     y = th.randint(0, 7, (2708,), device=dev)
     l1, l2 = GraphConv(1433, 16, activation=th.relu).to(dev), GraphConv(16, 7).to(dev)
-    opt = th.optim.Adam(list(l1.parameters()) + list(l2.parameters()), lr=0.01)
+    params = list(l1.parameters()) + list(l2.parameters())
+    opt = th.optim.Adam(params, lr=0.01, capturable=True)
 
     def step():
-        opt.zero_grad()
+        opt.zero_grad(set_to_none=False)
         loss = th.nn.functional.cross_entropy(l2(g, l1(g, x)), y)
         loss.backward()
         opt.step()
     ms = timeit(step, steps, warmup)
-    return {"config": "C1 Cora-size 2-layer GCN train step", "nodes": 2708,
-            "edges": g.number_of_edges(), "ms_per_step": ms}
+    res = {"config": "C1 Cora-size 2-layer GCN train step", "nodes": 2708,
+           "edges": g.number_of_edges(), "ms_per_step": ms}
+    # the same step captured once into a HIP graph and replayed: the step is
+    # ~40 small launches, so launch overhead, not the kernels, sets its time.
+    # Fresh modules/optimizer (no autograd state from the eager runs), warm-up
+    # on a side stream, then capture (torch.cuda.graphs whole-network recipe).
+    try:
+        m1, m2 = GraphConv(1433, 16, activation=th.relu).to(dev), GraphConv(16, 7).to(dev)
+        ps = list(m1.parameters()) + list(m2.parameters())
+        gopt = th.optim.Adam(ps, lr=0.01, capturable=True)
+
+        def gstep():
+            gopt.zero_grad(set_to_none=False)
+            loss = th.nn.functional.cross_entropy(m2(g, m1(g, x)), y)
+            loss.backward()
+            gopt.step()
+        s = th.cuda.Stream()
+        s.wait_stream(th.cuda.current_stream())
+        with th.cuda.stream(s):
+            for _ in range(3):
+                gstep()
+        th.cuda.current_stream().wait_stream(s)
+        graph = th.cuda.CUDAGraph()
+        with th.cuda.graph(graph):
+            gstep()
+        res["hipgraph_ms_per_step"] = timeit(graph.replay, steps * 10, warmup)
+    except Exception as exc:  # report, keep the eager number
+        res["hipgraph_error"] = repr(exc)[:300]
+    return res
 
 
 def c2(dev, steps, warmup):
