@@ -273,11 +273,16 @@ void run_fast(const DGLMIGraph* g, const DGLMICsr& walk, int kind, int red, cons
 // Items of a per-edge kernel.  Edge-id order (the graph's COO) streams the
 // output and any edge operand sequentially and gathers both node rows; in-CSR
 // order keeps the destination row in cache along its run but scatters the
-// output by eid.  Measured on M1 (100M edges, scripts/bench_configs.py sd):
-// edge-id order wins even for wide node-only ops (u_dot_v F = 64: 6.07 vs
-// 7.28 ms; u_add_v H = 8: 3.66 vs 5.25 ms), so it is used whenever the COO is
-// there.  DGLMI_SDDMM_ORDER=coo|csr forces one (tests).
-SddmmArgs sddmm_items(const DGLMIGraph* g, const DGLMICsr& walk) {
+// output by eid.  Measured (scripts/bench_configs.py sd, scripts/
+// sddmm_order_probe.py): on M1 (average in-degree 12) edge-id order wins even
+// for wide node-only ops (u_dot_v F = 64: 6.07 vs 7.28 ms) and by far for
+// narrow rows (u_add_v H = 8: 3.66 vs 5.25 ms); on the Reddit-size graph
+// (average in-degree 492) in-CSR order wins for wide node-only rows (u_dot_v
+// 8 x 8: 7.38 vs 8.10 ms) while narrow rows still prefer edge-id order (3.64 vs
+// 5.55 ms).  So: in-CSR order only for node-only operands, rows of >= 32
+// floats and average in-degree >= 64.  DGLMI_SDDMM_ORDER=coo|csr forces one.
+SddmmArgs sddmm_items(const DGLMIGraph* g, const DGLMICsr& walk, bool edge_operand,
+                      int64_t row_floats) {
   SddmmArgs e;
   std::memset(&e, 0, sizeof(e));
   e.nnz = walk.nnz;
@@ -285,6 +290,8 @@ SddmmArgs sddmm_items(const DGLMIGraph* g, const DGLMICsr& walk) {
   if (coo) {
     const char* env = std::getenv("DGLMI_SDDMM_ORDER");
     if (env && std::string(env) == "csr") coo = false;
+    else if (!(env && std::string(env) == "coo"))
+      coo = edge_operand || row_floats < 32 || walk.nnz < 64 * std::max<int64_t>(walk.num_rows, 1);
   }
   if (coo) {
     e.rows = g->coo_dst;
@@ -399,7 +406,9 @@ void forward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const D
   if (red == RED_NONE && !bc && !lhs_map && !rhs_map && !out_map && walk.nnz > 0 &&
       sddmm_supported(op == OP_DOT && len == 1 ? OP_MUL : op, false, D, len) &&
       aligned16(out->data) && aligned16(lhs->data) && (op == OP_USE_LHS || aligned16(rhs->data))) {
-    SddmmArgs e = sddmm_items(g, walk);
+    SddmmArgs e = sddmm_items(g, walk, lhs_t == DGLMI_TARGET_EDGE ||
+                                           (op != OP_USE_LHS && rhs_t == DGLMI_TARGET_EDGE),
+                              D * len);
     e.lhs = lhs->data;
     e.lhs_role = role_of(lhs_t, true);
     e.rhs = op == OP_USE_LHS ? nullptr : rhs->data;
@@ -540,7 +549,7 @@ void backward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const 
       sddmm_supported(op == OP_DOT && len == 1 ? OP_MUL : op, true, D, len) &&
       aligned16(grad->data) && aligned16(grad_out->data) && aligned16(lhs->data) &&
       (op == OP_USE_LHS || aligned16(rhs->data))) {
-    SddmmArgs e = sddmm_items(g, walk);
+    SddmmArgs e = sddmm_items(g, walk, true, Dg);  // a gradient row is an edge array
     e.lhs = lhs->data;
     e.lhs_role = role_of(lhs_t, true);
     e.rhs = op == OP_USE_LHS ? nullptr : rhs->data;
