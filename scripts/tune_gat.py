@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""Tuning sweep of the fused GAT kernels on the C3 Reddit-size graph: gathers in
-flight per lane (DGLMI_GAT_U) x chunk size (DGLMI_CHUNK_EDGES), kernel-level
-forward and backward times with HIP events."""
+"""Tuning sweep of the fused GAT kernels on the C3 Reddit-size graph: chunk size
+(DGLMI_CHUNK_EDGES) x gathers in flight per lane (DGLMI_GAT_U, read by a build
+with the U template variants -- removed after the sweep in
+profiles/r01_tune_gat.json showed the shipped U = 8 best; the release build
+ignores it), kernel-level forward and backward times with HIP events."""
 import json
 import os
 import sys
