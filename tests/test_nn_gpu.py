@@ -255,3 +255,47 @@ def test_fused_edge_softmax_masked_logits():
     assert a[0].item() == 0.0
     assert th.allclose(a[[1, 2]], b[[1, 2]], rtol=1e-6)
     assert bool(th.isnan(a[3]).all()) and bool(th.isnan(b[3]).all())
+
+
+@pytest.mark.parametrize("norm", ["none", "both", "right"])
+@pytest.mark.parametrize("weight", [True, False])
+@pytest.mark.parametrize("bias", [True, False])
+def test_graph_conv2_external_weight(norm, weight, bias):
+    """test_nn.py:72-88: module weight or an external one (weight=False), with or
+    without bias, every norm; plus reset_parameters (test_nn.py:66-70)."""
+    g = dgl.DGLGraph(nx.path_graph(3))
+    conv = nn.GraphConv(5, 2, norm=norm, weight=weight, bias=bias).to(DEV)
+    ext_w = th.randn(5, 2, device=DEV)
+    h = th.randn(3, 5, device=DEV)
+    out = conv(g, h) if weight else conv(g, h, weight=ext_w)
+    assert out.shape == (3, 2)
+    w = conv.weight if weight else ext_w
+    ref = nn.GraphConv(5, 2, norm=norm, weight=False, bias=False).to(DEV)(g, h, weight=w)
+    if bias:
+        ref = ref + conv.bias
+    assert th.allclose(out, ref, rtol=1e-5, atol=1e-6)
+    if weight:
+        old = conv.weight.detach().clone()
+        conv.reset_parameters()
+        assert not th.allclose(old, conv.weight)
+
+
+def test_rgcn_reference_shapes():
+    """test_nn.py:363-407 on a readonly scipy-built graph: basis / bdd, with a
+    per-edge norm, and integer id input."""
+    import scipy as sp
+    import scipy.sparse  # noqa: F401
+    g = dgl.DGLGraph(sp.sparse.random(100, 100, density=0.1, random_state=0), readonly=True)
+    R, B, I, O = 5, 2, 10, 8
+    r = th.tensor([i % 5 for i in range(g.number_of_edges())], device=DEV)
+    norm = th.zeros(g.number_of_edges(), 1, device=DEV)
+    for reg in ("basis", "bdd"):
+        conv = nn.RelGraphConv(I, O, R, reg, B).to(DEV)
+        h = th.randn(100, I, device=DEV)
+        assert list(conv(g, h, r).shape) == [100, O]
+        out = conv(g, h, r, norm)
+        assert list(out.shape) == [100, O]
+        assert th.allclose(out, conv.h_bias.expand(100, O))  # zero norm: only the bias
+    conv = nn.RelGraphConv(I, O, R, "basis", B).to(DEV)
+    h = th.randint(0, I, (100,), device=DEV)
+    assert list(conv(g, h, r).shape) == [100, O]
