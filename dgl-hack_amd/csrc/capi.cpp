@@ -243,9 +243,10 @@ struct Scratch {
 // rows own the output; out has `walk.num_rows` rows of F floats.
 void run_fast(const DGLMIGraph* g, const DGLMICsr& walk, int kind, int red, const float* x,
               const int32_t* x_map, const float* w, const int32_t* w_map, float* out, int64_t F,
-              int64_t head_dim, hipStream_t s) {
+              int64_t head_dim, hipStream_t s, const DGLMIEpilogue* epi = nullptr) {
   if (walk.nnz == 0) {
     launch_fill(out, walk.num_rows * F, identity_of(red), s);
+    if (epi) launch_epilogue(out, walk.num_rows, F, epi->row_mul, epi->row_div, epi->bias, s);
     return;
   }
   FastArgs a;
@@ -264,6 +265,11 @@ void run_fast(const DGLMIGraph* g, const DGLMICsr& walk, int kind, int red, cons
   a.F = F;
   a.head_dim = head_dim;
   a.chunk = fast_chunk_edges(walk.nnz, F);
+  if (epi) {
+    a.row_mul = epi->row_mul;
+    a.row_div = epi->row_div;
+    a.bias = epi->bias;
+  }
   Scratch carry(g, fast_workspace_bytes(walk.nnz, F), s);
   a.carry = static_cast<float*>(carry.ptr);
   launch_fast_reduce(kind, red, a, s);
@@ -323,7 +329,10 @@ EdgeArgs base_args(const DGLMICsr& walk) {
 // ---------------------------------------------------------------------------
 void forward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const DGLMIArray* lhs,
              const DGLMIArray* rhs, DGLMIArray* out, const int32_t* lhs_map,
-             const int32_t* rhs_map, const int32_t* out_map, hipStream_t s) {
+             const int32_t* rhs_map, const int32_t* out_map, hipStream_t s,
+             const DGLMIEpilogue* epi = nullptr) {
+  if (epi && !epi->row_mul && !epi->row_div && !epi->bias) epi = nullptr;
+  DGLMI_CHECK(epi == nullptr || red == RED_SUM, "a fused epilogue needs the sum reducer");
   check_graph(g);
   check_array(lhs, "lhs");
   check_array(out, "out");
@@ -394,8 +403,11 @@ void forward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const D
     }
     if (kind >= 0 && fast_supported(kind, D, head_dim) && walk.rows != nullptr) {
       const float* w = (kind == FAST_COL_MUL_EDGE || kind == FAST_COL_MUL_EDGE_BCAST) ? rhs->data : nullptr;
-      run_fast(g, walk, kind, red, lhs->data, lhs_map, w, rhs_map, out->data, D, head_dim, s);
-      return;
+      const bool epi_ok = epi == nullptr || epi->bias == nullptr || aligned16(epi->bias);
+      if (epi_ok) {
+        run_fast(g, walk, kind, red, lhs->data, lhs_map, w, rhs_map, out->data, D, head_dim, s, epi);
+        return;
+      }
     }
   }
 
@@ -436,6 +448,7 @@ void forward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const D
   if (red != RED_NONE && walk.rows != nullptr && generic_lb_supported(D)) {
     if (walk.nnz == 0) {
       if (!need_fill) launch_fill(out->data, walk.num_rows * D, identity_of(red), s);
+      if (epi) launch_epilogue(out->data, out_rows, D, epi->row_mul, epi->row_div, epi->bias, s);
       return;
     }
     a.chunk = fast_chunk_edges(walk.nnz, D);
@@ -443,10 +456,12 @@ void forward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const D
     a.carry = static_cast<float*>(carry.ptr);
     launch_generic_lb(op, red, bc, false, a, s);
     check_hip(hipGetLastError(), "generic lb forward launch");
+    if (epi) launch_epilogue(out->data, out_rows, D, epi->row_mul, epi->row_div, epi->bias, s);
     return;
   }
   launch_generic_forward(op, red, bc, a, s);
   check_hip(hipGetLastError(), "generic forward launch");
+  if (epi) launch_epilogue(out->data, out_rows, D, epi->row_mul, epi->row_div, epi->bias, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -677,6 +692,22 @@ int DGLMIKernelBinaryOpReduce(const char* reducer, const char* op, const DGLMIGr
   API_END();
 }
 
+int DGLMIKernelBinaryOpReduceEx(const char* reducer, const char* op, const DGLMIGraph* graph,
+                                int32_t lhs_target, int32_t rhs_target, const DGLMIArray* lhs,
+                                const DGLMIArray* rhs, DGLMIArray* out,
+                                const int32_t* lhs_mapping, const int32_t* rhs_mapping,
+                                const int32_t* out_mapping, const DGLMIEpilogue* epilogue,
+                                void* stream) {
+  API_BEGIN();
+  const int red = parse_reducer(reducer);
+  const int o = parse_op(op);
+  check_graph(graph);
+  DeviceGuard guard(graph->device);
+  forward(red, o, graph, lhs_target, rhs_target, lhs, rhs, out, lhs_mapping, rhs_mapping,
+          out_mapping, static_cast<hipStream_t>(stream), epilogue);
+  API_END();
+}
+
 int DGLMIKernelBackwardLhsBinaryOpReduce(
     const char* reducer, const char* op, const DGLMIGraph* graph, int32_t lhs_target,
     int32_t rhs_target, const int32_t* lhs_mapping, const int32_t* rhs_mapping,
@@ -716,6 +747,19 @@ int DGLMIKernelCopyReduce(const char* reducer, const DGLMIGraph* graph, int32_t 
   DeviceGuard guard(graph->device);
   forward(red, OP_USE_LHS, graph, target, DGLMI_TARGET_NONE, in, nullptr, out, in_mapping,
           nullptr, out_mapping, static_cast<hipStream_t>(stream));
+  API_END();
+}
+
+int DGLMIKernelCopyReduceEx(const char* reducer, const DGLMIGraph* graph, int32_t target,
+                            const DGLMIArray* in, DGLMIArray* out, const int32_t* in_mapping,
+                            const int32_t* out_mapping, const DGLMIEpilogue* epilogue,
+                            void* stream) {
+  API_BEGIN();
+  const int red = parse_reducer(reducer);
+  check_graph(graph);
+  DeviceGuard guard(graph->device);
+  forward(red, OP_USE_LHS, graph, target, DGLMI_TARGET_NONE, in, nullptr, out, in_mapping,
+          nullptr, out_mapping, static_cast<hipStream_t>(stream), epilogue);
   API_END();
 }
 

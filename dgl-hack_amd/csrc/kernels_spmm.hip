@@ -105,7 +105,29 @@ __device__ __forceinline__ void st_out(float* p, float4 v) {
 // non-temporal output stores, bit 2 twice the gathers in flight.  Default 3:
 // keeping the once-read CSR stream and the once-written output out of L2/MALL
 // leaves more room for re-read source rows (M1: 3.30 -> 3.25 ms; 4 and 7 spill).
-template <int KIND, int RED, int L, int NV, int VAR = 3>
+// EPI: fused epilogue on every finished row, out = acc * row_mul[r] / row_div[r]
+// + bias (GraphConv's norm and bias, the mean reducer's division) -- applied
+// once per row, after the whole row is reduced (split rows: in the fixup).
+template <bool EPI>
+__device__ __forceinline__ float4 epi4(const FastArgs& a, float4 v, int64_t r, int f4) {
+  if constexpr (EPI) {
+    if (a.row_mul) {
+      const float m = a.row_mul[r];
+      v = make_float4(v.x * m, v.y * m, v.z * m, v.w * m);
+    }
+    if (a.row_div) {
+      const float d = a.row_div[r];
+      v = make_float4(v.x / d, v.y / d, v.z / d, v.w / d);
+    }
+    if (a.bias) {
+      const float4 b = ld4(a.bias + 4 * f4);
+      v = make_float4(v.x + b.x, v.y + b.y, v.z + b.z, v.w + b.w);
+    }
+  }
+  return v;
+}
+
+template <int KIND, int RED, int L, int NV, int VAR = 3, bool EPI = false>
 __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32_t* __restrict__ indptr) {
   constexpr int G = kBlock / L;           // groups per block
   constexpr int B = (L > 16 ? L : 16) * ((VAR & 4) ? 2 : 1);  // positions staged per step
@@ -134,7 +156,7 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
         const int f4 = lane + v * L;
-        if (f4 < F4) st_out<VAR>(a.out + r * a.F + 4 * f4, I);
+        if (f4 < F4) st_out<VAR>(a.out + r * a.F + 4 * f4, epi4<EPI>(a, I, r, f4));
       }
   }
   float4 acc[NV];
@@ -177,14 +199,14 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
 #pragma unroll
           for (int v = 0; v < NV; ++v) {
             const int f4 = lane + v * L;
-            if (f4 < F4) st_out<VAR>(dst + 4 * f4, acc[v]);
+            if (f4 < F4) st_out<VAR>(dst + 4 * f4, cont ? acc[v] : epi4<EPI>(a, acc[v], cur, f4));
             acc[v] = I;
           }
           for (int64_t e = cur + 1; e < r; ++e)
 #pragma unroll
             for (int v = 0; v < NV; ++v) {
               const int f4 = lane + v * L;
-              if (f4 < F4) st_out<VAR>(a.out + e * a.F + 4 * f4, I);
+              if (f4 < F4) st_out<VAR>(a.out + e * a.F + 4 * f4, epi4<EPI>(a, I, e, f4));
             }
           cur = r;
           cont = false;
@@ -197,10 +219,12 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
   }
   {
     float* dst = cont ? a.carry + chunk * a.F : a.out + cur * a.F;
+    // a row that goes on in the next chunk stays raw: the fixup finishes it
+    const bool done = !cont && !(EPI && p1 < a.nnz && a.rows[p1] == cur);
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int f4 = lane + v * L;
-      if (f4 < F4) st_out<VAR>(dst + 4 * f4, acc[v]);
+      if (f4 < F4) st_out<VAR>(dst + 4 * f4, done ? epi4<EPI>(a, acc[v], cur, f4) : acc[v]);
     }
   }
   if (p1 == a.nnz) {  // trailing empty rows
@@ -208,7 +232,7 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
         const int f4 = lane + v * L;
-        if (f4 < F4) st_out<VAR>(a.out + r * a.F + 4 * f4, I);
+        if (f4 < F4) st_out<VAR>(a.out + r * a.F + 4 * f4, epi4<EPI>(a, I, r, f4));
       }
   }
   (void)indptr;
@@ -217,7 +241,7 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
 // Fold the carries of every row cut by chunk boundaries into its head, in
 // chunk order.  One group per chunk; only a row's first continuation chunk
 // does work.
-template <int RED, int L, int NV>
+template <int RED, int L, int NV, bool EPI = false>
 __global__ void __launch_bounds__(kBlock) k_chunk_fixup(FastArgs a, const int32_t* __restrict__ indptr) {
   constexpr int G = kBlock / L;
   const int g = threadIdx.x / L;
@@ -261,7 +285,7 @@ __global__ void __launch_bounds__(kBlock) k_chunk_fixup(FastArgs a, const int32_
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int f4 = lane + v * L;
-    if (f4 < F4) st4(a.out + r * a.F + 4 * f4, acc[v]);
+    if (f4 < F4) st4(a.out + r * a.F + 4 * f4, epi4<EPI>(a, acc[v], r, f4));
   }
 }
 
@@ -328,7 +352,23 @@ __device__ __forceinline__ void lane_value(const FastArgs& a, int32_t col, int32
   }
 }
 
-template <int KIND, int RED, int F>
+template <bool EPI, int F>
+__device__ __forceinline__ void epi_row(const FastArgs& a, int64_t r, float (&v)[F]) {
+  if constexpr (EPI) {
+    const float m = a.row_mul ? a.row_mul[r] : 1.0f;
+    const float d = a.row_div ? a.row_div[r] : 1.0f;
+#pragma unroll
+    for (int i = 0; i < F; ++i) {
+      float x = v[i];
+      if (a.row_mul) x = x * m;
+      if (a.row_div) x = x / d;
+      if (a.bias) x = x + a.bias[i];
+      v[i] = x;
+    }
+  }
+}
+
+template <int KIND, int RED, int F, bool EPI = false>
 __global__ void __launch_bounds__(kBlock) k_lane_reduce(FastArgs a) {
   constexpr int U = 8;
   const int64_t chunk = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -340,11 +380,18 @@ __global__ void __launch_bounds__(kBlock) k_lane_reduce(FastArgs a) {
   float ident[F];
 #pragma unroll
   for (int i = 0; i < F; ++i) ident[i] = I;
+  auto put_gap = [&](int64_t r) {
+    float t[F];
+#pragma unroll
+    for (int i = 0; i < F; ++i) t[i] = ident[i];
+    epi_row<EPI, F>(a, r, t);
+    store_row<F>(a.out + r * F, t);
+  };
   int64_t cur = a.rows[p0];
   bool cont = p0 > 0 && a.rows[p0 - 1] == cur;
   if (!cont) {
     const int64_t first_gap = p0 > 0 ? (int64_t)a.rows[p0 - 1] + 1 : 0;
-    for (int64_t r = first_gap; r < cur; ++r) store_row<F>(a.out + r * F, ident);
+    for (int64_t r = first_gap; r < cur; ++r) put_gap(r);
   }
   float acc[F];
 #pragma unroll
@@ -381,8 +428,9 @@ __global__ void __launch_bounds__(kBlock) k_lane_reduce(FastArgs a) {
     for (int u = 0; u < U; ++u) {
       if (r[u] == INT_MAX) break;
       if (r[u] != cur) {
+        if (!cont) epi_row<EPI, F>(a, cur, acc);
         store_row<F>(cont ? a.carry + chunk * F : a.out + cur * F, acc);
-        for (int64_t g = cur + 1; g < r[u]; ++g) store_row<F>(a.out + g * F, ident);
+        for (int64_t g = cur + 1; g < r[u]; ++g) put_gap(g);
 #pragma unroll
         for (int i = 0; i < F; ++i) acc[i] = I;
         cur = r[u];
@@ -392,12 +440,13 @@ __global__ void __launch_bounds__(kBlock) k_lane_reduce(FastArgs a) {
       for (int i = 0; i < F; ++i) acc[i] = red_apply<RED>(acc[i], v[u][i]);
     }
   }
+  if (!cont && !(EPI && p1 < a.nnz && a.rows[p1] == cur)) epi_row<EPI, F>(a, cur, acc);
   store_row<F>(cont ? a.carry + chunk * F : a.out + cur * F, acc);
   if (p1 == a.nnz)
-    for (int64_t g = cur + 1; g < a.num_rows; ++g) store_row<F>(a.out + g * F, ident);
+    for (int64_t g = cur + 1; g < a.num_rows; ++g) put_gap(g);
 }
 
-template <int RED, int F>
+template <int RED, int F, bool EPI = false>
 __global__ void __launch_bounds__(kBlock) k_lane_fixup(FastArgs a) {
   const int64_t chunk = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int64_t K = a.chunk;
@@ -415,13 +464,24 @@ __global__ void __launch_bounds__(kBlock) k_lane_fixup(FastArgs a) {
 #pragma unroll
     for (int i = 0; i < F; ++i) acc[i] = red_apply<RED>(acc[i], t[i]);
   }
+  epi_row<EPI, F>(a, r, acc);
   store_row<F>(a.out + r * F, acc);
 }
+
+bool has_epi(const FastArgs& a) { return a.row_mul || a.row_div || a.bias; }
 
 template <int KIND, int RED, int F>
 void run_lane(const FastArgs& a, hipStream_t s) {
   const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
   const unsigned blocks = static_cast<unsigned>((chunks + kBlock - 1) / kBlock);
+  if constexpr (RED == RED_SUM) {
+    if (has_epi(a)) {
+      hipLaunchKernelGGL((k_lane_reduce<KIND, RED, F, true>), dim3(blocks), dim3(kBlock), 0, s, a);
+      if (chunks > 1)
+        hipLaunchKernelGGL((k_lane_fixup<RED, F, true>), dim3(blocks), dim3(kBlock), 0, s, a);
+      return;
+    }
+  }
   hipLaunchKernelGGL((k_lane_reduce<KIND, RED, F>), dim3(blocks), dim3(kBlock), 0, s, a);
   if (chunks > 1) hipLaunchKernelGGL((k_lane_fixup<RED, F>), dim3(blocks), dim3(kBlock), 0, s, a);
 }
@@ -466,6 +526,16 @@ void run(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
   constexpr int G = kBlock / L;
   const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
   const unsigned blocks = static_cast<unsigned>((chunks + G - 1) / G);
+  if constexpr (RED == RED_SUM) {
+    if (has_epi(a)) {
+      hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 3, true>), dim3(blocks), dim3(kBlock), 0,
+                         s, a, indptr);
+      if (chunks > 1)
+        hipLaunchKernelGGL((k_chunk_fixup<RED, L, NV, true>), dim3(blocks), dim3(kBlock), 0, s, a,
+                           indptr);
+      return;
+    }
+  }
   if constexpr (KIND == FAST_COPY_COL && RED == RED_SUM && L == 16 && NV == 1) {
     // tuning variants of the headline kernel (scripts/tune_spmm.py)
     switch (spmm_variant()) {

@@ -45,6 +45,14 @@ class Graph(ctypes.Structure):
     ]
 
 
+class Epilogue(ctypes.Structure):
+    _fields_ = [
+        ("row_mul", ctypes.c_void_p),
+        ("row_div", ctypes.c_void_p),
+        ("bias", ctypes.c_void_p),
+    ]
+
+
 class Array(ctypes.Structure):
     _fields_ = [
         ("data", ctypes.c_void_p),
@@ -79,6 +87,15 @@ _SIGS = {
         ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(Graph), ctypes.c_int32, ctypes.c_int32,
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "DGLMIKernelBinaryOpReduceEx": (ctypes.c_int, [
+        ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(Graph), ctypes.c_int32, ctypes.c_int32,
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Epilogue),
+        ctypes.c_void_p]),
+    "DGLMIKernelCopyReduceEx": (ctypes.c_int, [
+        ctypes.c_char_p, ctypes.POINTER(Graph), ctypes.c_int32, ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Epilogue),
+        ctypes.c_void_p]),
     "DGLMIKernelBackwardLhsBinaryOpReduce": (ctypes.c_int, [
         ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(Graph), ctypes.c_int32, ctypes.c_int32,
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

@@ -42,18 +42,20 @@ class BinaryReduce(th.autograd.Function):
     def forward(ctx, reducer, binary_op, graph, lhs, rhs, lhs_data, rhs_data, out_data,
                 out_size, lhs_map, rhs_map, out_map):
         feat_shape = K.infer_binary_feature_shape(binary_op, lhs_data, rhs_data)
-        K.binary_op_reduce(reducer if reducer != "mean" else "sum", binary_op, graph, lhs, rhs,
-                           lhs_data, rhs_data, out_data, lhs_map[0], rhs_map[0], out_map[0])
+        degs = None
         if reducer == "mean":
             if lhs != DST:
                 target, n, in_map = lhs, lhs_data.shape[0], lhs_map[0]
             else:
                 target, n, in_map = rhs, rhs_data.shape[0], rhs_map[0]
             degs = _degs(target, graph, n, out_data.shape[0], in_map, out_map[0], lhs_data)
-            degs = degs.reshape((out_data.shape[0],) + (1,) * (out_data.dim() - 1)).clamp(min=1)
-            out_data = out_data / degs
-        else:
-            degs = None
+            degs = degs.clamp(min=1)
+        # mean = the sum divided by the in-degree in the kernel's epilogue (one pass)
+        K.binary_op_reduce(reducer if reducer != "mean" else "sum", binary_op, graph, lhs, rhs,
+                           lhs_data, rhs_data, out_data, lhs_map[0], rhs_map[0], out_map[0],
+                           epilogue=None if degs is None else (None, degs, None))
+        if degs is not None:
+            degs = degs.reshape((out_data.shape[0],) + (1,) * (out_data.dim() - 1))
         ctx.backward_cache = (reducer, binary_op, graph, lhs, rhs, lhs_map, rhs_map, out_map,
                               feat_shape, degs)
         ctx.save_for_backward(lhs_data, rhs_data, out_data)
@@ -147,15 +149,15 @@ def binary_reduce(reducer, binary_op, graph, lhs, rhs, lhs_data, rhs_data, out_s
 class CopyReduce(th.autograd.Function):
     @staticmethod
     def forward(ctx, reducer, graph, target, in_data, out_data, out_size, in_map, out_map):
-        K.copy_reduce(reducer if reducer != "mean" else "sum", graph, target, in_data, out_data,
-                      in_map[0], out_map[0])
+        degs = None
         if reducer == "mean":
             degs = _degs(target, graph, in_data.shape[0], out_data.shape[0], in_map[0],
-                         out_map[0], in_data)
-            degs = degs.reshape((out_data.shape[0],) + (1,) * (out_data.dim() - 1)).clamp(min=1)
-            out_data = out_data / degs
-        else:
-            degs = None
+                         out_map[0], in_data).clamp(min=1)
+        K.copy_reduce(reducer if reducer != "mean" else "sum", graph, target, in_data, out_data,
+                      in_map[0], out_map[0],
+                      epilogue=None if degs is None else (None, degs, None))
+        if degs is not None:
+            degs = degs.reshape((out_data.shape[0],) + (1,) * (out_data.dim() - 1))
         ctx.backward_cache = (reducer, graph, target, in_map, out_map, degs)
         ctx.save_for_backward(in_data, out_data)
         return out_data
@@ -254,26 +256,68 @@ def weight_grad(x, gy):
 
 class _Project(th.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w):
+    def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
-        return th.matmul(x, w)
+        ctx.has_bias = b is not None
+        if b is None:
+            return th.matmul(x, w)
+        # bias in the GEMM epilogue (hipBLASLt addmm), not a separate pass
+        return th.addmm(b, x.reshape(-1, x.shape[-1]), w).view(x.shape[:-1] + (w.shape[1],))
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
-        gx = gw = None
+        gx = gw = gb = None
         if ctx.needs_input_grad[0]:
             gx = th.matmul(gy, w.t())
         if ctx.needs_input_grad[1]:
             gw = weight_grad(x, gy)
-        return gx, gw
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = gy.reshape(-1, gy.shape[-1]).sum(0)
+        return gx, gw, gb
 
 
-def project(x, w):
-    """Y = X W (X: (..., F_in), W: (F_in, F_out)) with the split-K weight gradient."""
+def project(x, w, bias=None):
+    """Y = X W (+ bias) (X: (..., F_in), W: (F_in, F_out)) with the split-K weight
+    gradient; a bias is added inside the GEMM."""
     if w.dim() != 2:
-        return th.matmul(x, w)
-    return _Project.apply(x, w)
+        y = th.matmul(x, w)
+        return y if bias is None else y + bias
+    return _Project.apply(x, w, bias)
+
+
+class _GcnAggregate(th.autograd.Function):
+    """out[v] = (sum_{u->v} X[u]) * row_mul[v] + bias in ONE kernel (copy_u_sum with
+    the fused epilogue): GraphConv's aggregation, norm and bias
+    (graphconv.py:150-170) without two extra passes over the output."""
+
+    @staticmethod
+    def forward(ctx, gidx, x, row_mul, bias, n_dst):
+        out = x.new_empty((n_dst, x.shape[1]))
+        K.copy_reduce("sum", gidx, SRC, x, out, epilogue=(row_mul, None, bias))
+        ctx.gidx = gidx
+        ctx.save_for_backward(x, out, row_mul)
+        ctx.has_bias = bias is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        x, out, row_mul = ctx.saved_tensors
+        gx = gb = None
+        g = grad_out.contiguous()
+        if ctx.needs_input_grad[1]:
+            gs = g * row_mul.view(-1, 1) if row_mul is not None else g
+            gx = th.empty_like(x)
+            K.backward_copy_reduce("sum", ctx.gidx, SRC, x, out, gs.contiguous(), gx)
+        if ctx.has_bias and ctx.needs_input_grad[3]:
+            gb = g.sum(0)
+        return None, gx, None, gb, None
+
+
+def gcn_aggregate(gidx, x, row_mul=None, bias=None, n_dst=None):
+    """Fused GraphConv aggregation (see _GcnAggregate); x is (N_src, F) float32."""
+    n_dst = gidx.in_csr.num_rows if n_dst is None else n_dst
+    return _GcnAggregate.apply(gidx, x.contiguous(), row_mul, bias, n_dst)
 
 
 class FusedGat(th.autograd.Function):

@@ -96,17 +96,45 @@ def infer_binary_feature_shape(op, lhs, rhs):
     return tuple(out[i] for i in range(nd.value))
 
 
+def _epilogue(epilogue, out_data):
+    """(row_mul, row_div, bias) float32 tensors on out's device (None entries allowed)."""
+    if epilogue is None or all(t is None for t in epilogue):
+        return None
+    e = _ffi.Epilogue()
+    keep = []
+    for name, t in zip(("row_mul", "row_div", "bias"), epilogue):
+        if t is None:
+            setattr(e, name, None)
+            continue
+        t = t.contiguous()
+        if t.dtype != th.float32 or t.device != out_data.device:
+            raise DGLError("epilogue %s must be float32 on %s" % (name, out_data.device))
+        want = _feat_len(out_data) if name == "bias" else out_data.shape[0]
+        if t.numel() != want:
+            raise DGLError("epilogue %s has %d values, expected %d" % (name, t.numel(), want))
+        setattr(e, name, t.data_ptr())
+        keep.append(t)
+    e._keep = keep
+    return e
+
+
 def binary_op_reduce(reducer, op, graph, lhs, rhs, lhs_data, rhs_data, out_data,
-                     lhs_map=None, rhs_map=None, out_map=None):
-    """kernel.py:29-148 -> _CAPI_DGLKernelBinaryOpReduce."""
+                     lhs_map=None, rhs_map=None, out_map=None, epilogue=None):
+    """kernel.py:29-148 -> _CAPI_DGLKernelBinaryOpReduce.  ``epilogue`` =
+    (row_mul, row_div, bias) fused into a "sum" reduction (DGLMIKernelBinaryOpReduceEx)."""
     _check_ctx(graph, [("lhs_data", lhs_data), ("rhs_data", rhs_data), ("out_data", out_data)])
     ws = _workspace(graph, _feat_len(out_data), out_data.device)
     g = _cgraph(graph, ws, reducer == "none")
-    check_call(_ffi.lib().DGLMIKernelBinaryOpReduce(
-        reducer.encode(), op.encode(), ctypes.byref(g), _TARGET_CODE(lhs), _TARGET_CODE(rhs),
-        _arr(lhs_data, "lhs_data"), _arr(rhs_data, "rhs_data"), _arr(out_data, "out_data"),
-        _map(lhs_map, "lhs_mapping"), _map(rhs_map, "rhs_mapping"), _map(out_map, "out_mapping"),
-        _stream(out_data)))
+    epi = _epilogue(epilogue, out_data)
+    args = (reducer.encode(), op.encode(), ctypes.byref(g), _TARGET_CODE(lhs), _TARGET_CODE(rhs),
+            _arr(lhs_data, "lhs_data"), _arr(rhs_data, "rhs_data"), _arr(out_data, "out_data"),
+            _map(lhs_map, "lhs_mapping"), _map(rhs_map, "rhs_mapping"),
+            _map(out_map, "out_mapping"))
+    if epi is None:
+        check_call(_ffi.lib().DGLMIKernelBinaryOpReduce(*args, _stream(out_data)))
+    else:
+        check_call(_ffi.lib().DGLMIKernelBinaryOpReduceEx(*args, ctypes.byref(epi),
+                                                          _stream(out_data)))
     return out_data
 
 
@@ -144,15 +172,19 @@ def backward_rhs_binary_op_reduce(reducer, op, graph, lhs, rhs, lhs_data, rhs_da
     return grad_rhs_data
 
 
-def copy_reduce(reducer, graph, target, in_data, out_data, in_map=None, out_map=None):
-    """kernel.py:302-393 -> _CAPI_DGLKernelCopyReduce."""
+def copy_reduce(reducer, graph, target, in_data, out_data, in_map=None, out_map=None,
+                epilogue=None):
+    """kernel.py:302-393 -> _CAPI_DGLKernelCopyReduce (``epilogue``: see binary_op_reduce)."""
     _check_ctx(graph, [("in_data", in_data), ("out_data", out_data)])
     ws = _workspace(graph, _feat_len(out_data), out_data.device)
     g = _cgraph(graph, ws, reducer == "none")
-    check_call(_ffi.lib().DGLMIKernelCopyReduce(
-        reducer.encode(), ctypes.byref(g), _TARGET_CODE(target), _arr(in_data, "in_data"),
-        _arr(out_data, "out_data"), _map(in_map, "in_mapping"), _map(out_map, "out_mapping"),
-        _stream(out_data)))
+    epi = _epilogue(epilogue, out_data)
+    args = (reducer.encode(), ctypes.byref(g), _TARGET_CODE(target), _arr(in_data, "in_data"),
+            _arr(out_data, "out_data"), _map(in_map, "in_mapping"), _map(out_map, "out_mapping"))
+    if epi is None:
+        check_call(_ffi.lib().DGLMIKernelCopyReduce(*args, _stream(out_data)))
+    else:
+        check_call(_ffi.lib().DGLMIKernelCopyReduceEx(*args, ctypes.byref(epi), _stream(out_data)))
     return out_data
 
 

@@ -5,6 +5,14 @@ Same parameters, initialisation and computation order as the reference:
 MFMA through hipBLASLt) goes before the aggregation when in_feats >
 out_feats, after it otherwise; the aggregation is one ``copy_u_sum`` on the
 load-balanced HIP kernel.
+
+On 2-D float32 features the destination-side norm and the bias are fused into
+that aggregation kernel's epilogue (``dgl.backend.gcn_aggregate``): for
+in_feats > out_feats ``out = (A X W) * norm + bias`` in one launch; otherwise
+``(A X) * norm`` in the launch and the bias inside the projection GEMM
+(``project(..., bias)``, hipBLASLt addmm) -- the row scaling commutes with the
+right-multiplication by W.  ``fused = False`` on the module restores the
+reference's separate steps.
 """
 import torch as th
 from torch import nn
@@ -44,11 +52,6 @@ class GraphConv(nn.Module):
 
     def forward(self, graph, feat, weight=None):
         graph = graph.local_var()
-        if self._norm == "both":
-            degs = graph._device_degrees(feat.device, "out").float().clamp(min=1)
-            norm = th.pow(degs, -0.5)
-            norm = th.reshape(norm, norm.shape + (1,) * (feat.dim() - 1))
-            feat = feat * norm
         if weight is not None:
             if self.weight is not None:
                 raise DGLError("External weight is provided while at the same time the"
@@ -56,6 +59,39 @@ class GraphConv(nn.Module):
                                " create the module with flag weight=False.")
         else:
             weight = self.weight
+        if self._norm == "both":
+            degs = graph._device_degrees(feat.device, "out").float().clamp(min=1)
+            norm = th.pow(degs, -0.5)
+            norm = th.reshape(norm, norm.shape + (1,) * (feat.dim() - 1))
+            feat = feat * norm
+        if getattr(self, "fused", True) and feat.dim() == 2 and feat.dtype == th.float32:
+            rst = self._fused_forward(graph, feat, weight)
+        else:
+            rst = self._reference_forward(graph, feat, weight)
+        if self._activation is not None:
+            rst = self._activation(rst)
+        return rst
+
+    def _dst_norm(self, graph, device):
+        if self._norm == "none":
+            return None
+        degs = graph._device_degrees(device, "in").float().clamp(min=1)
+        return th.pow(degs, -0.5) if self._norm == "both" else 1.0 / degs
+
+    def _fused_forward(self, graph, feat, weight):
+        gidx = graph._graph.get_immutable_gidx(feat.device)
+        n_dst = graph.number_of_dst_nodes()
+        norm = self._dst_norm(graph, feat.device)
+        if self._in_feats > self._out_feats:
+            if weight is not None:
+                feat = B.project(feat, weight)
+            return B.gcn_aggregate(gidx, feat, norm, self.bias, n_dst)
+        rst = B.gcn_aggregate(gidx, feat, norm, None, n_dst)
+        if weight is not None:
+            return B.project(rst, weight, self.bias)
+        return rst if self.bias is None else rst + self.bias
+
+    def _reference_forward(self, graph, feat, weight):
         if self._in_feats > self._out_feats:
             if weight is not None:
                 feat = B.project(feat, weight)
@@ -69,14 +105,10 @@ class GraphConv(nn.Module):
             if weight is not None:
                 rst = B.project(rst, weight)
         if self._norm != "none":
-            degs = graph._device_degrees(feat.device, "in").float().clamp(min=1)
-            norm = th.pow(degs, -0.5) if self._norm == "both" else 1.0 / degs
-            norm = th.reshape(norm, norm.shape + (1,) * (feat.dim() - 1))
-            rst = rst * norm
+            norm = self._dst_norm(graph, feat.device)
+            rst = rst * th.reshape(norm, norm.shape + (1,) * (feat.dim() - 1))
         if self.bias is not None:
             rst = rst + self.bias
-        if self._activation is not None:
-            rst = self._activation(rst)
         return rst
 
     def extra_repr(self):

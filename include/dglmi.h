@@ -86,6 +86,18 @@ typedef struct {
   int64_t shape[DGLMI_MAX_NDIM + 1];
 } DGLMIArray;
 
+/* Optional epilogue fused into a "sum" reduction (extension): every output
+ * row r becomes ((out[r] * row_mul[r]) / row_div[r]) + bias, applied once to the
+ * finished row, in that order -- GraphConv's `rst * norm` then `+ bias`
+ * (graphconv.py:158-170) and the mean reducer's `out / degs` (tensor.py:308-325),
+ * without extra passes over the output.  Any pointer may be NULL; row arrays
+ * have one float per output row, bias one per output feature. */
+typedef struct {
+  const float* row_mul;
+  const float* row_div;
+  const float* bias;
+} DGLMIEpilogue;
+
 /* Last error message of the calling thread (DGLGetLastError). */
 const char* DGLMIGetLastError(void);
 
@@ -124,6 +136,19 @@ int DGLMIKernelBackwardRhsBinaryOpReduce(
 int DGLMIKernelCopyReduce(const char* reducer, const DGLMIGraph* graph, int32_t target,
                           const DGLMIArray* in, DGLMIArray* out, const int32_t* in_mapping,
                           const int32_t* out_mapping, void* stream);
+
+/* DGLMIKernelBinaryOpReduce / DGLMIKernelCopyReduce with a fused epilogue
+ * (reducer must be "sum"; epilogue may be NULL). */
+int DGLMIKernelBinaryOpReduceEx(const char* reducer, const char* op, const DGLMIGraph* graph,
+                                int32_t lhs_target, int32_t rhs_target,
+                                const DGLMIArray* lhs, const DGLMIArray* rhs, DGLMIArray* out,
+                                const int32_t* lhs_mapping, const int32_t* rhs_mapping,
+                                const int32_t* out_mapping, const DGLMIEpilogue* epilogue,
+                                void* stream);
+int DGLMIKernelCopyReduceEx(const char* reducer, const DGLMIGraph* graph, int32_t target,
+                            const DGLMIArray* in, DGLMIArray* out, const int32_t* in_mapping,
+                            const int32_t* out_mapping, const DGLMIEpilogue* epilogue,
+                            void* stream);
 
 /* _CAPI_DGLKernelBackwardCopyReduce (binary_reduce.cc:697-716). */
 int DGLMIKernelBackwardCopyReduce(const char* reducer, const DGLMIGraph* graph, int32_t target,
