@@ -367,20 +367,30 @@ class DistGraphConv(th.nn.Module):
             norm = th.pow(out_deg_inner.float().clamp(min=1), -0.5)
             feat = feat * norm.reshape(norm.shape + (1,) * (feat.dim() - 1))
         w = conv.weight
-        if conv._in_feats > conv._out_feats:
-            feat = B.project(feat, w)
-            full = halo_exchange(feat, part, group)
-            rst = B.copy_reduce("sum", gidx, 0, full, part.n_inner)
-        else:
-            full = halo_exchange(feat, part, group)
-            rst = B.copy_reduce("sum", gidx, 0, full, part.n_inner)
-            rst = B.project(rst, w)
+        dnorm = None
         if conv._norm != "none":
             degs = in_deg_inner.float().clamp(min=1)
-            norm = th.pow(degs, -0.5) if conv._norm == "both" else 1.0 / degs
-            rst = rst * norm.reshape(norm.shape + (1,) * (rst.dim() - 1))
-        if conv.bias is not None:
-            rst = rst + conv.bias
+            dnorm = th.pow(degs, -0.5) if conv._norm == "both" else 1.0 / degs
+        if feat.dim() == 2 and feat.dtype == th.float32:
+            # norm and bias fused into the aggregation kernel (GraphConv._fused_forward)
+            if conv._in_feats > conv._out_feats:
+                full = halo_exchange(B.project(feat, w), part, group)
+                rst = B.gcn_aggregate(gidx, full, dnorm, conv.bias, part.n_inner)
+            else:
+                full = halo_exchange(feat, part, group)
+                rst = B.project(B.gcn_aggregate(gidx, full, dnorm, None, part.n_inner), w,
+                                conv.bias)
+        else:
+            if conv._in_feats > conv._out_feats:
+                full = halo_exchange(B.project(feat, w), part, group)
+                rst = B.copy_reduce("sum", gidx, 0, full, part.n_inner)
+            else:
+                full = halo_exchange(feat, part, group)
+                rst = B.project(B.copy_reduce("sum", gidx, 0, full, part.n_inner), w)
+            if dnorm is not None:
+                rst = rst * dnorm.reshape(dnorm.shape + (1,) * (rst.dim() - 1))
+            if conv.bias is not None:
+                rst = rst + conv.bias
         if conv._activation is not None:
             rst = conv._activation(rst)
         return rst
