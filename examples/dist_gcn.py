@@ -160,7 +160,10 @@ def main():
             "config": "C4 full-graph 2-layer GCN, RMAT %d nodes / %d edges, feat %d -> %d -> %d"
                       % (n, m, args.feat, args.hidden, args.classes),
             "n_gpus": world, "epoch_ms": ms, "setup_s": t_setup,
-            "edge_visits_per_s": 4 * edges / (ms * 1e-3),  # 2 layers x (fwd + bwd) SpMM
+            # SpMM passes per epoch: layer 1 forward, layer 2 forward and backward (the
+            # input features need no gradient, so layer 1 has no backward SpMM)
+            "spmm_passes_per_epoch": 3,
+            "edge_visits_per_s": 3 * edges / (ms * 1e-3),
             "halo_rows_total": halo_rows, "max_halo_rows_per_rank": halo_max,
             "halo_bytes_per_layer_fwd": halo_rows * 4 * args.feat,
             "loss": loss_v, "partition": "contiguous id ranges (permuted ids), device halo plan",
