@@ -158,6 +158,15 @@ def load_pmc_traffic():
         return None
 
 
+def _max_over_ranks(v, dist, cdev):
+    """max of a float over all ranks (so every rank takes the same exit path)."""
+    if dist is None:
+        return float(v)
+    t = th.tensor([float(v)], device=cdev, dtype=th.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def _timed(fn, steps, dist, cdev):
     """barrier + sync bracketed wall time of `steps` calls, max over ranks (s)."""
     if dist is not None:
@@ -195,6 +204,7 @@ def measure_exchange(part, x, out_ref, args, dist, cdev, device, edges_total):
     xstep()
     th.cuda.synchronize()
     err = float((out - out_ref).abs().max() / out_ref.abs().max().clamp(min=1e-30))
+    err = _max_over_ranks(err, dist, cdev)
     if err > 1e-4:
         raise SystemExit("with-exchange copy_u_sum differs from the replicated one: %g" % err)
     steps = max(1, min(args.steps, 5))
@@ -324,7 +334,8 @@ def main():
         expect += (outdeg[lo:hi, None] * x[lo:hi].double()).sum(0)
     got = out.double().sum(0)
     rel = float(((got - expect).abs().max() / expect.abs().max().clamp(min=1)).item())
-    log("checksum-of-checksums rel err %.2e" % rel)
+    rel = _max_over_ranks(rel, dist, cdev)
+    log("checksum-of-checksums rel err %.2e (max over ranks)" % rel)
     if rel > 1e-3:
         raise SystemExit("copy_u_sum checksum mismatch: %g" % rel)
     del outdeg, expect, got
@@ -342,7 +353,8 @@ def main():
     exact = th.zeros(4096, FEAT, dtype=th.float64, device=device).index_add_(0, seg, xr)
     mass = th.zeros(4096, FEAT, dtype=th.float64, device=device).index_add_(0, seg, xr.abs())
     err = (out[rows].double() - exact).abs()
-    if bool((err > 1e-4 + 1e-6 * mass).any()):
+    bad = _max_over_ranks(float((err > 1e-4 + 1e-6 * mass).any()), dist, cdev)
+    if bad > 0:
         raise SystemExit("copy_u_sum row check failed: max err %g" % float(err.max()))
     log("row spot check (4096 rows, fp64 torch gathers): max abs err %.2e" % float(err.max()))
     del seg, pos, cols, xr, exact, mass, err
