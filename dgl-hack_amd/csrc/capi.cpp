@@ -246,7 +246,7 @@ void run_fast(const DGLMIGraph* g, const DGLMICsr& walk, int kind, int red, cons
               int64_t head_dim, hipStream_t s, const DGLMIEpilogue* epi = nullptr) {
   if (walk.nnz == 0) {
     launch_fill(out, walk.num_rows * F, identity_of(red), s);
-    if (epi) launch_epilogue(out, walk.num_rows, F, epi->row_mul, epi->row_div, epi->bias, s);
+    if (epi) launch_epilogue(out, walk.num_rows, F, epi->row_mul, epi->row_div, epi->bias, epi->addend, s);
     return;
   }
   FastArgs a;
@@ -269,6 +269,7 @@ void run_fast(const DGLMIGraph* g, const DGLMICsr& walk, int kind, int red, cons
     a.row_mul = epi->row_mul;
     a.row_div = epi->row_div;
     a.bias = epi->bias;
+    a.addend = epi->addend;
   }
   Scratch carry(g, fast_workspace_bytes(walk.nnz, F), s);
   a.carry = static_cast<float*>(carry.ptr);
@@ -331,7 +332,7 @@ void forward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const D
              const DGLMIArray* rhs, DGLMIArray* out, const int32_t* lhs_map,
              const int32_t* rhs_map, const int32_t* out_map, hipStream_t s,
              const DGLMIEpilogue* epi = nullptr) {
-  if (epi && !epi->row_mul && !epi->row_div && !epi->bias) epi = nullptr;
+  if (epi && !epi->row_mul && !epi->row_div && !epi->bias && !epi->addend) epi = nullptr;
   DGLMI_CHECK(epi == nullptr || red == RED_SUM, "a fused epilogue needs the sum reducer");
   check_graph(g);
   check_array(lhs, "lhs");
@@ -403,7 +404,8 @@ void forward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const D
     }
     if (kind >= 0 && fast_supported(kind, D, head_dim) && walk.rows != nullptr) {
       const float* w = (kind == FAST_COL_MUL_EDGE || kind == FAST_COL_MUL_EDGE_BCAST) ? rhs->data : nullptr;
-      const bool epi_ok = epi == nullptr || epi->bias == nullptr || aligned16(epi->bias);
+      const bool epi_ok = epi == nullptr || ((epi->bias == nullptr || aligned16(epi->bias)) &&
+                                             (epi->addend == nullptr || aligned16(epi->addend)));
       if (epi_ok) {
         run_fast(g, walk, kind, red, lhs->data, lhs_map, w, rhs_map, out->data, D, head_dim, s, epi);
         return;
@@ -448,7 +450,7 @@ void forward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const D
   if (red != RED_NONE && walk.rows != nullptr && generic_lb_supported(D)) {
     if (walk.nnz == 0) {
       if (!need_fill) launch_fill(out->data, walk.num_rows * D, identity_of(red), s);
-      if (epi) launch_epilogue(out->data, out_rows, D, epi->row_mul, epi->row_div, epi->bias, s);
+      if (epi) launch_epilogue(out->data, out_rows, D, epi->row_mul, epi->row_div, epi->bias, epi->addend, s);
       return;
     }
     a.chunk = fast_chunk_edges(walk.nnz, D);
@@ -456,12 +458,12 @@ void forward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const D
     a.carry = static_cast<float*>(carry.ptr);
     launch_generic_lb(op, red, bc, false, a, s);
     check_hip(hipGetLastError(), "generic lb forward launch");
-    if (epi) launch_epilogue(out->data, out_rows, D, epi->row_mul, epi->row_div, epi->bias, s);
+    if (epi) launch_epilogue(out->data, out_rows, D, epi->row_mul, epi->row_div, epi->bias, epi->addend, s);
     return;
   }
   launch_generic_forward(op, red, bc, a, s);
   check_hip(hipGetLastError(), "generic forward launch");
-  if (epi) launch_epilogue(out->data, out_rows, D, epi->row_mul, epi->row_div, epi->bias, s);
+  if (epi) launch_epilogue(out->data, out_rows, D, epi->row_mul, epi->row_div, epi->bias, epi->addend, s);
 }
 
 // ---------------------------------------------------------------------------

@@ -130,9 +130,10 @@ __device__ __forceinline__ int64_t resolve(const Operand& o, int64_t row, int64_
 // ---- host-side launchers (defined in the .hip files) ------------------------
 void launch_fill(float* out, int64_t n, float value, hipStream_t s);
 void launch_fill_i32(int32_t* out, int64_t n, int32_t value, hipStream_t s);
-// out[r, :] = out[r, :] * row_mul[r] / row_div[r] + bias (each optional), in place
+// out[r, :] = out[r, :] * row_mul[r] / row_div[r] + bias + addend[r, :] (each optional)
 void launch_epilogue(float* out, int64_t rows, int64_t F, const float* row_mul,
-                     const float* row_div, const float* bias, hipStream_t s);
+                     const float* row_div, const float* bias, const float* addend,
+                     hipStream_t s);
 
 // Generic forward: reduce to row nodes (out_role == ROLE_ROW) or per edge.
 void launch_generic_forward(int op, int red, bool bcast, const EdgeArgs& a, hipStream_t s);
@@ -208,10 +209,11 @@ struct FastArgs {
   int64_t head_dim;     // bcast: features per head (E has F / head_dim values per edge)
   float* carry;         // workspace: num_chunks * F floats
   int64_t chunk;        // edges per chunk
-  // optional fused epilogue (sum only): out = acc * row_mul[r] / row_div[r] + bias
+  // optional fused epilogue (sum only): out = acc * row_mul[r] / row_div[r] + bias + addend[r]
   const float* row_mul;
   const float* row_div;
   const float* bias;
+  const float* addend;
 };
 int64_t fast_chunk_edges(int64_t nnz, int64_t F);
 int64_t fast_workspace_bytes(int64_t nnz, int64_t F);

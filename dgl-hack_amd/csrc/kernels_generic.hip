@@ -268,7 +268,7 @@ __global__ void k_fill(float* __restrict__ out, int64_t n, float v) {
 }
 __global__ void k_epilogue(float* __restrict__ out, int64_t rows, int64_t F,
                            const float* __restrict__ row_mul, const float* __restrict__ row_div,
-                           const float* __restrict__ bias) {
+                           const float* __restrict__ bias, const float* __restrict__ addend) {
   const int64_t n = rows * F;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -277,6 +277,7 @@ __global__ void k_epilogue(float* __restrict__ out, int64_t rows, int64_t F,
     if (row_mul) x = x * row_mul[r];
     if (row_div) x = x / row_div[r];
     if (bias) x = x + bias[i - r * F];
+    if (addend) x = x + addend[i];
     out[i] = x;
   }
 }
@@ -396,12 +397,13 @@ void launch_fill(float* out, int64_t n, float value, hipStream_t s) {
   hipLaunchKernelGGL(k_fill, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, out, n, value);
 }
 void launch_epilogue(float* out, int64_t rows, int64_t F, const float* row_mul,
-                     const float* row_div, const float* bias, hipStream_t s) {
+                     const float* row_div, const float* bias, const float* addend,
+                     hipStream_t s) {
   const int64_t n = rows * F;
-  if (n <= 0 || (!row_mul && !row_div && !bias)) return;
+  if (n <= 0 || (!row_mul && !row_div && !bias && !addend)) return;
   const int64_t blocks = std::min<int64_t>((n + 255) / 256, 8192);
   hipLaunchKernelGGL(k_epilogue, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, out, rows,
-                     F, row_mul, row_div, bias);
+                     F, row_mul, row_div, bias, addend);
 }
 void launch_fill_i32(int32_t* out, int64_t n, int32_t value, hipStream_t s) {
   if (n <= 0) return;

@@ -106,7 +106,8 @@ __device__ __forceinline__ void st_out(float* p, float4 v) {
 // keeping the once-read CSR stream and the once-written output out of L2/MALL
 // leaves more room for re-read source rows (M1: 3.30 -> 3.25 ms; 4 and 7 spill).
 // EPI: fused epilogue on every finished row, out = acc * row_mul[r] / row_div[r]
-// + bias (GraphConv's norm and bias, the mean reducer's division) -- applied
+// + bias + addend[r] (GraphConv's norm and bias, the mean reducer's division,
+// accumulation onto an earlier partial result) -- applied
 // once per row, after the whole row is reduced (split rows: in the fixup).
 template <bool EPI>
 __device__ __forceinline__ float4 epi4(const FastArgs& a, float4 v, int64_t r, int f4) {
@@ -121,6 +122,10 @@ __device__ __forceinline__ float4 epi4(const FastArgs& a, float4 v, int64_t r, i
     }
     if (a.bias) {
       const float4 b = ld4(a.bias + 4 * f4);
+      v = make_float4(v.x + b.x, v.y + b.y, v.z + b.z, v.w + b.w);
+    }
+    if (a.addend) {
+      const float4 b = ld4(a.addend + r * a.F + 4 * f4);
       v = make_float4(v.x + b.x, v.y + b.y, v.z + b.z, v.w + b.w);
     }
   }
@@ -363,6 +368,7 @@ __device__ __forceinline__ void epi_row(const FastArgs& a, int64_t r, float (&v)
       if (a.row_mul) x = x * m;
       if (a.row_div) x = x / d;
       if (a.bias) x = x + a.bias[i];
+      if (a.addend) x = x + a.addend[r * F + i];
       v[i] = x;
     }
   }
@@ -468,7 +474,7 @@ __global__ void __launch_bounds__(kBlock) k_lane_fixup(FastArgs a) {
   store_row<F>(a.out + r * F, acc);
 }
 
-bool has_epi(const FastArgs& a) { return a.row_mul || a.row_div || a.bias; }
+bool has_epi(const FastArgs& a) { return a.row_mul || a.row_div || a.bias || a.addend; }
 
 template <int KIND, int RED, int F>
 void run_lane(const FastArgs& a, hipStream_t s) {

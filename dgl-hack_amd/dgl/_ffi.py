@@ -50,6 +50,7 @@ class Epilogue(ctypes.Structure):
         ("row_mul", ctypes.c_void_p),
         ("row_div", ctypes.c_void_p),
         ("bias", ctypes.c_void_p),
+        ("addend", ctypes.c_void_p),
     ]
 
 

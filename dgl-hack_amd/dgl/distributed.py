@@ -206,6 +206,7 @@ class DevicePartition:
         self.local_src = local_src        # device int32, [0, n_inner + n_halo)
         self.local_dst = local_dst        # device int32, [0, n_inner)
         self._g = None
+        self._split = None
 
     @property
     def inner(self):
@@ -226,6 +227,21 @@ class DevicePartition:
     def release_edges(self):
         self.gidx()
         self.local_src = self.local_dst = None
+
+    def split_gidx(self):
+        """(owned-source block, halo-source block) of the local in-edges -- the two
+        halves of the aggregation that :func:`aggregate_with_halo` runs before and
+        after the halo rows arrive.  Built on the device from the local in-CSR."""
+        if self._split is None:
+            c = self.gidx().in_csr
+            own = c.indices < self.n_inner
+            g_own = device_block_gidx(self.n_inner, self.n_inner, c.indices[own], c.rows[own])
+            g_halo = None
+            if self.n_halo > 0:
+                g_halo = device_block_gidx(self.n_halo, self.n_inner,
+                                           c.indices[~own] - self.n_inner, c.rows[~own])
+            self._split = (g_own, g_halo)
+        return self._split
 
     def device_plan(self, device=None):
         return self.send_idx
@@ -307,6 +323,49 @@ class HaloExchange(th.autograd.Function):
 
 def halo_exchange(x_inner, part, group=None):
     return HaloExchange.apply(x_inner, part, group)
+
+
+def _a2av_async(out, inp, out_splits, in_splits, group):
+    """all_to_all_single enqueued on the collective stream (RCCL), or done now
+    (gloo through host memory, or a single process); returns the Work or None."""
+    if not _single() and dist.get_backend(group) == "nccl":
+        return dist.all_to_all_single(out, inp, out_splits, in_splits, group=group, async_op=True)
+    _a2av(out, inp, out_splits, in_splits, group)
+    return None
+
+
+def aggregate_with_halo(x_inner, part, out=None, group=None, recv=None, send_buf=None, tmp=None):
+    """copy_u_sum over a partition's in-edges with the halo exchange OVERLAPPED
+    (inference / benchmarking, no autograd): the owned rows' gather for the peers
+    and the all-to-all-v go first (RCCL, its own stream), the owned-source half
+    of the aggregation runs meanwhile, and once the halo rows have arrived the
+    halo-source half adds onto it in its epilogue (``addend``) -- no extra pass.
+    Buffers may be passed in to avoid allocations: recv (n_halo, F), send_buf
+    (sum(send_counts), F), tmp and out (n_inner, F)."""
+    from . import kernel as K
+    g_own, g_halo = part.split_gidx()
+    f = x_inner.shape[1:]
+    idx = part.device_plan(x_inner.device)
+    if send_buf is None:
+        send_buf = x_inner.new_empty((idx.shape[0],) + tuple(f))
+    if recv is None:
+        recv = x_inner.new_empty((part.n_halo,) + tuple(f))
+    if tmp is None:
+        tmp = x_inner.new_empty((part.n_inner,) + tuple(f))
+    if out is None:
+        out = x_inner.new_empty((part.n_inner,) + tuple(f))
+    th.index_select(x_inner, 0, idx, out=send_buf)
+    work = _a2av_async(recv, send_buf, part.recv_counts.tolist(), part.send_counts.tolist(), group)
+    if g_halo is None:
+        K.copy_reduce("sum", g_own, 0, x_inner, out)
+        if work is not None:
+            work.wait()
+        return out
+    K.copy_reduce("sum", g_own, 0, x_inner, tmp)
+    if work is not None:
+        work.wait()
+    K.copy_reduce("sum", g_halo, 0, recv, out, epilogue=(None, None, None, tmp))
+    return out
 
 
 def halo_exchange_into(x_full, part, group=None, send_buf=None):

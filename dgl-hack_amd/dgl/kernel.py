@@ -97,21 +97,29 @@ def infer_binary_feature_shape(op, lhs, rhs):
 
 
 def _epilogue(epilogue, out_data):
-    """(row_mul, row_div, bias) float32 tensors on out's device (None entries allowed)."""
+    """(row_mul, row_div, bias[, addend]) float32 tensors on out's device (None allowed)."""
     if epilogue is None or all(t is None for t in epilogue):
         return None
     e = _ffi.Epilogue()
     keep = []
-    for name, t in zip(("row_mul", "row_div", "bias"), epilogue):
+    names = ("row_mul", "row_div", "bias", "addend")
+    for name in names[len(epilogue):]:
+        setattr(e, name, None)
+    for name, t in zip(names, epilogue):
         if t is None:
             setattr(e, name, None)
             continue
         t = t.contiguous()
         if t.dtype != th.float32 or t.device != out_data.device:
             raise DGLError("epilogue %s must be float32 on %s" % (name, out_data.device))
-        want = _feat_len(out_data) if name == "bias" else out_data.shape[0]
+        want = {"bias": _feat_len(out_data), "addend": out_data.numel()}.get(name, out_data.shape[0])
         if t.numel() != want:
             raise DGLError("epilogue %s has %d values, expected %d" % (name, t.numel(), want))
+        if name == "addend":
+            lo, hi = t.data_ptr(), t.data_ptr() + t.numel() * 4
+            olo, ohi = out_data.data_ptr(), out_data.data_ptr() + out_data.numel() * 4
+            if lo < ohi and olo < hi:
+                raise DGLError("epilogue addend must not overlap the output")
         setattr(e, name, t.data_ptr())
         keep.append(t)
     e._keep = keep

@@ -87,15 +87,19 @@ typedef struct {
 } DGLMIArray;
 
 /* Optional epilogue fused into a "sum" reduction (extension): every output
- * row r becomes ((out[r] * row_mul[r]) / row_div[r]) + bias, applied once to the
- * finished row, in that order -- GraphConv's `rst * norm` then `+ bias`
- * (graphconv.py:158-170) and the mean reducer's `out / degs` (tensor.py:308-325),
- * without extra passes over the output.  Any pointer may be NULL; row arrays
- * have one float per output row, bias one per output feature. */
+ * row r becomes (((out[r] * row_mul[r]) / row_div[r]) + bias) + addend[r],
+ * applied once to the finished row, in that order -- GraphConv's `rst * norm`
+ * then `+ bias` (graphconv.py:158-170), the mean reducer's `out / degs`
+ * (tensor.py:308-325), and accumulation onto an earlier partial result (the
+ * halo half of a partitioned aggregation) -- without extra passes over the
+ * output.  Any pointer may be NULL; row_mul / row_div have one float per output
+ * row, bias one per output feature, addend the output's shape (it must not
+ * overlap the output: rows split across work chunks keep partial sums there). */
 typedef struct {
   const float* row_mul;
   const float* row_div;
   const float* bias;
+  const float* addend;
 } DGLMIEpilogue;
 
 /* Last error message of the calling thread (DGLGetLastError). */

@@ -74,3 +74,39 @@ def test_dist_gcn_matches_single_gpu(planner):
     q = ctx.Queue()
     run_world(_worker, 2, (src, dst, n, q, planner))
     assert q.get(timeout=5) == "ok"
+
+
+def _overlap_worker(rank, world, src, dst, n, q):
+    import dgl
+    from dgl import distributed as D
+    dev = "cuda:0"
+    bounds = [n * p // world for p in range(world + 1)]
+    lo, hi = bounds[rank], bounds[rank + 1]
+    sel = (dst >= lo) & (dst < hi)
+    part = D.build_device_partition(th.from_numpy(src[sel]).to(dev).int(),
+                                    th.from_numpy(dst[sel] - lo).to(dev).int(), bounds, rank)
+    x = th.from_numpy(np.random.RandomState(1).randn(n, 16).astype(np.float32)).to(dev)
+    out = D.aggregate_with_halo(x[lo:hi].contiguous(), part)
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    ref = dgl.backend.copy_reduce("sum", g._graph.get_immutable_gidx(dev), 0, x, n)[lo:hi]
+    ok = th.allclose(out, ref, rtol=1e-5, atol=1e-5)
+    import torch.distributed as dist
+    flags = [None] * world
+    dist.all_gather_object(flags, bool(ok))
+    if rank == 0:
+        q.put("ok" if all(flags) else "mismatch")
+
+
+def test_aggregate_with_halo_overlapped():
+    """Owned-source half + halo half (accumulated by the kernel's addend epilogue)
+    == the full aggregation of the owned rows, 2 ranks on one GPU."""
+    import torch.multiprocessing as mp
+    from dist_util import run_world
+    from graphs import powerlaw
+    src, dst, n = powerlaw(3000, 40000, seed=4)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    run_world(_overlap_worker, 2, (src, dst, n, q))
+    assert q.get(timeout=5) == "ok"
