@@ -7,13 +7,20 @@ message-passing entry points whose builtin forms lower to one kernel each:
 
 * ``update_all(msg, reduce)``        -> ``F.copy_reduce`` / ``F.binary_reduce``
   (``graph.py:3221-3264``, ``runtime/scheduler.py:196-252, 905-917``);
-* ``pull(v, msg, reduce)`` / ``send_and_recv(edges, msg, reduce)`` -> the same
-  kernels on the in-edge subgraph (``scheduler.py:154-194, 254-332``);
+* ``pull(v, msg, reduce)`` / ``send_and_recv(edges, msg, reduce)`` / ``push(u, ...)``
+  -> the same kernels on the in-edge subgraph (``scheduler.py:154-194, 254-332,
+  417-449``);
+* ``send(edges, msg)`` + ``recv(v, reduce)`` -> messages materialised per edge
+  (reducer ``"none"``), then ``copy_e`` reduced over the pending edges
+  (``scheduler.py:31-129``);
 * ``apply_edges(msg)``              -> reducer ``"none"`` (``graph.py:2600``,
   ``scheduler.py:334-375``).
 
-User-defined functions are accepted by ``apply_edges`` / ``apply_nodes``
-(plain tensor gathers).  A user-defined *reduce* (degree bucketing,
+Functions registered with ``register_{message,reduce,apply_node,apply_edge}_func``
+are the defaults of every entry point.  User-defined message functions are
+materialised per edge and reduced by a builtin reducer as ``copy_e`` (what the
+reference's scheduler does, ``scheduler.py:919-960``); ``apply_edges`` /
+``apply_nodes`` accept UDFs (plain tensor gathers).  A user-defined *reduce* (degree bucketing,
 ``runtime/degree_bucketing.py``) is outside this engine's scope and raises
 :class:`DGLError` (see DESIGN.md "Scope").
 """
@@ -24,7 +31,9 @@ from collections.abc import MutableMapping
 import numpy as np
 import torch as th
 
+from . import backend as B
 from ._ffi import DGLError
+from .function.base import TargetCode
 from .function.message import MessageFunction
 from .function.reducer import ReduceFunction
 from .graph_index import GraphIndex
@@ -349,6 +358,9 @@ class DGLGraph(object):
         g._readonly = self._readonly
         g._node_frame = Frame(g.number_of_nodes, self._node_frame._cols)
         g._edge_frame = Frame(g.number_of_edges, self._edge_frame._cols)
+        for attr in ("_message_func", "_reduce_func", "_apply_node_func", "_apply_edge_func"):
+            if hasattr(self, attr):
+                setattr(g, attr, getattr(self, attr))
         return g
 
     def local_scope(self):
@@ -390,10 +402,21 @@ class DGLGraph(object):
         return list(f) if isinstance(f, (list, tuple)) else [f]
 
     def _builtin_reduce(self, gidx, mfuncs, rfuncs, src_frame, edge_frame, out_size,
-                        edge_map=None):
-        fld2mfunc = {fn.out_field: fn for fn in mfuncs}
+                        edge_map=None, udf_msgs=None):
+        """One kernel per (message, reducer) pair (scheduler.py:905-917).  With a
+        user-defined message function the messages were materialised first
+        (``udf_msgs``: field -> per-edge tensor indexed by parent edge id) and each
+        reducer runs as ``copy_e`` over them (scheduler.py:919-960)."""
+        fld2mfunc = {fn.out_field: fn for fn in mfuncs if isinstance(fn, MessageFunction)}
         out = {}
         for rfn in rfuncs:
+            if udf_msgs is not None:
+                if rfn.msg_field not in udf_msgs:
+                    raise DGLError('Reduce function requires message field "%s", but the '
+                                   'message function does not generate it.' % rfn.msg_field)
+                out[rfn.out_field] = B.copy_reduce(rfn.name, gidx, TargetCode.EDGE,
+                                                   udf_msgs[rfn.msg_field], out_size)
+                continue
             if rfn.msg_field not in fld2mfunc:
                 raise DGLError('Reduce function requires message field "%s", but no message '
                                'function generates it.' % rfn.msg_field)
@@ -402,27 +425,86 @@ class DGLGraph(object):
                                              None, None, edge_map, None, reducer=rfn.name)
         return out
 
+    @staticmethod
+    def _is_udf(mfuncs):
+        return len(mfuncs) == 1 and not isinstance(mfuncs[0], MessageFunction)
+
     def _check_builtin(self, mfuncs, rfuncs):
-        for f in mfuncs:
-            if not isinstance(f, MessageFunction):
-                raise DGLError("update_all/pull/send_and_recv take builtin message functions "
-                               "(dgl.function.*); user-defined message functions are only "
-                               "supported by apply_edges on this engine")
+        if not mfuncs:
+            raise DGLError("A message function is required (pass one or call "
+                           "register_message_func)")
+        if not rfuncs:
+            raise DGLError("A reduce function is required (pass one or call "
+                           "register_reduce_func)")
+        if not self._is_udf(mfuncs):
+            for f in mfuncs:
+                if not isinstance(f, MessageFunction):
+                    raise DGLError("A list of message functions must hold builtins "
+                                   "(dgl.function.*) only")
         for f in rfuncs:
             if not isinstance(f, ReduceFunction):
                 raise DGLError("user-defined reduce functions (degree bucketing) are not "
                                "supported by the MI355X engine; use dgl.function reducers")
 
-    def update_all(self, message_func, reduce_func, apply_node_func=None):
+    # ---- registered defaults (graph.py:2458-2548) -------------------------------------
+    def register_message_func(self, func):
+        """Default message function of update_all / send / pull / push / send_and_recv."""
+        self._message_func = func
+
+    def register_reduce_func(self, func):
+        """Default reduce function of update_all / recv / pull / push / send_and_recv."""
+        self._reduce_func = func
+
+    def register_apply_node_func(self, func):
+        """Default node update applied after a reduce."""
+        self._apply_node_func = func
+
+    def register_apply_edge_func(self, func):
+        """Default edge function of apply_edges."""
+        self._apply_edge_func = func
+
+    def _default(self, func, attr):
+        if isinstance(func, str) and func == "default":
+            return getattr(self, attr, None)
+        return func
+
+    def _defaults(self, message_func, reduce_func, apply_node_func):
+        return (self._default(message_func, "_message_func"),
+                self._default(reduce_func, "_reduce_func"),
+                self._default(apply_node_func, "_apply_node_func"))
+
+    def _udf_messages(self, func, s, d, e, dev):
+        """Materialise a message UDF on the selected edges as full per-edge tensors
+        indexed by edge id (rows of unselected edges are zero and never read)."""
+        eb = EdgeBatch(s, d, e, {k: v[s] for k, v in self._node_frame.items()},
+                       {k: v[d] for k, v in self._node_frame.items()},
+                       {k: v[e] for k, v in self._edge_frame.items()})
+        m = self.number_of_edges()
+        out = {}
+        for k, v in func(eb).items():
+            if v.shape[0] == m and e.shape[0] == m and bool((e == th.arange(m, device=e.device)).all()):
+                out[k] = v
+            else:
+                out[k] = v.new_zeros((m,) + tuple(v.shape[1:])).index_copy(0, e, v)
+        return out
+
+    def update_all(self, message_func="default", reduce_func="default",
+                   apply_node_func="default"):
         """Send messages along all edges and reduce them on every node."""
+        message_func, reduce_func, apply_node_func = self._defaults(
+            message_func, reduce_func, apply_node_func)
         mfuncs, rfuncs = self._as_list(message_func), self._as_list(reduce_func)
         self._check_builtin(mfuncs, rfuncs)
         if self.number_of_nodes() == 0:
             return
         dev = self._device(self._node_frame, self._edge_frame)
         gidx = self._gidx(dev)
+        udf_msgs = None
+        if self._is_udf(mfuncs):
+            s, d, e = self._edge_tensors(ALL, dev)
+            udf_msgs = self._udf_messages(mfuncs[0], s, d, e, dev)
         res = self._builtin_reduce(gidx, mfuncs, rfuncs, self._node_frame, self._edge_frame,
-                                   self.number_of_nodes())
+                                   self.number_of_nodes(), udf_msgs=udf_msgs)
         if apply_node_func is not None:
             nb = NodeBatch(self.nodes().to(dev), dict(self._node_frame, **res))
             res.update(apply_node_func(nb))
@@ -436,18 +518,14 @@ class DGLGraph(object):
         sub._parent_eid = eid
         return sub
 
-    def _partial_reduce(self, src, dst, eid, message_func, reduce_func, apply_node_func,
-                        recv_nodes):
-        mfuncs, rfuncs = self._as_list(message_func), self._as_list(reduce_func)
-        self._check_builtin(mfuncs, rfuncs)
-        dev = self._device(self._node_frame, self._edge_frame)
-        sub = _PartialIndex(self.number_of_nodes(), src, dst, eid)
-        gidx = sub.get_immutable_gidx(dev)
-        res = self._builtin_reduce(gidx, mfuncs, rfuncs, self._node_frame, self._edge_frame,
-                                   self.number_of_nodes())
+    def _write_partial(self, res, recv_nodes, apply_node_func, dev):
+        """Write reduced rows of ``recv_nodes`` (sorted, unique) into the node frame,
+        after the optional apply function (scheduler.py:_apply_with_accum)."""
         v = th.as_tensor(np.unique(recv_nodes), device=dev)
         if apply_node_func is not None:
-            nb = NodeBatch(v, {k: t[v] for k, t in res.items()})
+            data = {k: t[v] for k, t in self._node_frame.items()}
+            data.update({k: t[v] for k, t in res.items()})
+            nb = NodeBatch(v, data)
             for k, t in apply_node_func(nb).items():
                 res[k] = th.zeros((self.number_of_nodes(),) + tuple(t.shape[1:]), dtype=t.dtype,
                                   device=dev).index_copy(0, v, t)
@@ -458,18 +536,134 @@ class DGLGraph(object):
                 base = th.zeros_like(t)
             self._node_frame[k] = base.index_copy(0, v, t[v])
 
-    def pull(self, v, message_func, reduce_func, apply_node_func=None):
+    def _partial_reduce(self, src, dst, eid, message_func, reduce_func, apply_node_func,
+                        recv_nodes):
+        message_func, reduce_func, apply_node_func = self._defaults(
+            message_func, reduce_func, apply_node_func)
+        mfuncs, rfuncs = self._as_list(message_func), self._as_list(reduce_func)
+        self._check_builtin(mfuncs, rfuncs)
+        dev = self._device(self._node_frame, self._edge_frame)
+        sub = _PartialIndex(self.number_of_nodes(), src, dst, eid)
+        gidx = sub.get_immutable_gidx(dev)
+        udf_msgs = None
+        if self._is_udf(mfuncs):
+            udf_msgs = self._udf_messages(mfuncs[0], th.as_tensor(src, device=dev),
+                                          th.as_tensor(dst, device=dev),
+                                          th.as_tensor(eid, device=dev), dev)
+        res = self._builtin_reduce(gidx, mfuncs, rfuncs, self._node_frame, self._edge_frame,
+                                   self.number_of_nodes(), udf_msgs=udf_msgs)
+        self._write_partial(res, recv_nodes, apply_node_func, dev)
+
+    def pull(self, v, message_func="default", reduce_func="default", apply_node_func="default",
+             inplace=False):
         """Pull messages from the in-edges of ``v`` and reduce them on ``v``."""
         vs = _to_index_array(v, "v")
         src, dst, eid = self._graph.edges()
         mask = np.isin(dst, vs)
+        if not mask.any():  # scheduler.py:472-476: downgrade to apply_nodes
+            apply_node_func = self._default(apply_node_func, "_apply_node_func")
+            if apply_node_func is not None:
+                self.apply_nodes(apply_node_func, vs)
+            return
         self._partial_reduce(src[mask], dst[mask], eid[mask], message_func, reduce_func,
                              apply_node_func, vs)
 
-    def send_and_recv(self, edges, message_func, reduce_func, apply_node_func=None):
+    def send_and_recv(self, edges, message_func="default", reduce_func="default",
+                      apply_node_func="default", inplace=False):
         """Send messages along ``edges`` (eids or (u, v)) and reduce on their destinations."""
         src, dst, eid = self._resolve_edges(edges)
+        if len(eid) == 0:
+            return
         self._partial_reduce(src, dst, eid, message_func, reduce_func, apply_node_func, dst)
+
+    def push(self, u, message_func="default", reduce_func="default", apply_node_func="default",
+             inplace=False):
+        """Send messages along the out-edges of ``u`` and reduce on their destinations
+        (graph.py:3124, scheduler.py:417-449)."""
+        us = _to_index_array(u, "u")
+        src, dst, eid = self._graph.edges()
+        mask = np.isin(src, us)
+        if not mask.any():
+            return
+        self._partial_reduce(src[mask], dst[mask], eid[mask], message_func, reduce_func,
+                             apply_node_func, dst[mask])
+
+    # ---- two-phase send / recv (graph.py:2749-2960, scheduler.py:31-129) ---------------
+    def send(self, edges=ALL, message_func="default"):
+        """Compute messages on ``edges`` and keep them until a ``recv`` consumes them."""
+        message_func = self._default(message_func, "_message_func")
+        mfuncs = self._as_list(message_func)
+        if not mfuncs:
+            raise DGLError("A message function is required (pass one or call "
+                           "register_message_func)")
+        m = self.number_of_edges()
+        if m == 0:
+            return
+        dev = self._device(self._node_frame, self._edge_frame)
+        if self._is_udf(mfuncs):
+            s, d, e = self._edge_tensors(edges, dev)
+            msgs = self._udf_messages(mfuncs[0], s, d, e, dev)
+        else:
+            msgs = {}
+            if is_all(edges):
+                gidx = self._gidx(dev)
+                e = th.arange(m, device=dev)
+            else:
+                src, dst, eid = self._resolve_edges(edges)
+                gidx = _PartialIndex(self.number_of_nodes(), src, dst, eid).get_immutable_gidx(dev)
+                e = th.as_tensor(eid, device=dev)
+            for f in mfuncs:
+                msgs[f.out_field] = f._invoke(gidx, self._node_frame, self._node_frame,
+                                              self._edge_frame, m, reducer="none")
+        if not hasattr(self, "_msg_frame") or self._msg_frame is None:
+            self._msg_frame = {}
+        ind = getattr(self, "_msg_ind", None)
+        if ind is None or ind.shape[0] != m:
+            ind = np.zeros(m, bool)
+        for k, t in msgs.items():
+            old = self._msg_frame.get(k)
+            if old is None or old.shape != t.shape:
+                self._msg_frame[k] = t
+            else:
+                self._msg_frame[k] = old.index_copy(0, e, t[e])
+        ind[e.cpu().numpy()] = True
+        self._msg_ind = ind
+
+    def recv(self, v=ALL, reduce_func="default", apply_node_func="default", inplace=False):
+        """Reduce the pending messages of the in-edges of ``v`` onto ``v``; messages are
+        consumed (scheduler.py:72-129).  Nodes of ``v`` without a pending message get
+        the reducer's value for an empty row."""
+        reduce_func = self._default(reduce_func, "_reduce_func")
+        apply_node_func = self._default(apply_node_func, "_apply_node_func")
+        rfuncs = self._as_list(reduce_func)
+        if not rfuncs:
+            raise DGLError("A reduce function is required (pass one or call "
+                           "register_reduce_func)")
+        for f in rfuncs:
+            if not isinstance(f, ReduceFunction):
+                raise DGLError("user-defined reduce functions (degree bucketing) are not "
+                               "supported by the MI355X engine; use dgl.function reducers")
+        vs = np.arange(self.number_of_nodes()) if is_all(v) else _to_index_array(v, "v")
+        ind = getattr(self, "_msg_ind", None)
+        src, dst, eid = self._graph.edges()
+        mask = np.isin(dst, vs)
+        if ind is not None and ind.shape[0] == len(eid):
+            mask &= ind[eid]
+        else:
+            mask[:] = False
+        if not mask.any():  # scheduler.py:101-107: downgrade to apply_nodes
+            if apply_node_func is not None:
+                self.apply_nodes(apply_node_func, vs)
+            return
+        dev = self._device(self._node_frame, self._edge_frame)
+        gidx = _PartialIndex(self.number_of_nodes(), src[mask], dst[mask],
+                             eid[mask]).get_immutable_gidx(dev)
+        res = self._builtin_reduce(gidx, [], rfuncs, self._node_frame, self._edge_frame,
+                                   self.number_of_nodes(), udf_msgs=self._msg_frame)
+        self._write_partial(res, vs, apply_node_func, dev)
+        ind[eid[mask]] = False
+        if not ind.any():
+            self._msg_frame = {}
 
     def _resolve_edges(self, edges):
         src, dst, eid = self._graph.edges()
@@ -501,8 +695,12 @@ class DGLGraph(object):
         return (th.as_tensor(src, device=dev), th.as_tensor(dst, device=dev),
                 th.as_tensor(eid, device=dev))
 
-    def apply_edges(self, func, edges=ALL, inplace=False):
+    def apply_edges(self, func="default", edges=ALL, inplace=False):
         """Compute per-edge features with a builtin (reducer 'none') or a UDF."""
+        func = self._default(func, "_apply_edge_func")
+        if func is None:
+            raise DGLError("An edge function is required (pass one or call "
+                           "register_apply_edge_func)")
         dev = self._device(self._node_frame, self._edge_frame)
         if isinstance(func, MessageFunction):
             m = self.number_of_edges()

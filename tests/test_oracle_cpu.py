@@ -137,3 +137,22 @@ def test_golden_fixture_regression():
     for name, arrs in make_golden.cases():
         for k, v in arrs.items():
             np.testing.assert_allclose(v, z[name + "/" + k], rtol=1e-6, atol=1e-6, err_msg=name + "/" + k)
+
+
+def test_star_graph_known_answers():
+    """tests/compute/test_function.py:5-67: the reference's star graph (0 -> 1..8 ->
+    9 -> 0), node features 1..10 and its literal edge features; copy_src / copy_edge /
+    src_mul_edge summed into each node give the test's literal vectors."""
+    src = [s for i in range(1, 9) for s in (0, i)] + [9]
+    dst = [d for i in range(1, 9) for d in (i, 9)] + [0]
+    g = O.RefGraph(np.array(src), np.array(dst), 10)
+    h = np.arange(1, 11, dtype=np.float32).reshape(10, 1)
+    eh = np.array([1., 2., 1., 3., 1., 4., 1., 5., 1., 6., 1., 7., 1., 8., 1., 9., 10.],
+                  np.float32).reshape(17, 1)
+    copy_ans = [10., 1., 1., 1., 1., 1., 1., 1., 1., 44.]
+    out = O.copy_reduce("sum", g, O.SRC, h, 10)
+    _eq(out[:, 0], copy_ans)
+    out = O.copy_reduce("sum", g, O.EDGE, eh, 10)
+    _eq(out[:, 0], copy_ans)
+    out = O.binary_reduce("sum", "mul", g, O.SRC, O.EDGE, h, eh, 10)
+    _eq(out[:, 0], [100., 1., 1., 1., 1., 1., 1., 1., 1., 284.])
