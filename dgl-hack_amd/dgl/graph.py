@@ -20,9 +20,11 @@ Functions registered with ``register_{message,reduce,apply_node,apply_edge}_func
 are the defaults of every entry point.  User-defined message functions are
 materialised per edge and reduced by a builtin reducer as ``copy_e`` (what the
 reference's scheduler does, ``scheduler.py:919-960``); ``apply_edges`` /
-``apply_nodes`` accept UDFs (plain tensor gathers).  A user-defined *reduce* (degree bucketing,
-``runtime/degree_bucketing.py``) is outside this engine's scope and raises
-:class:`DGLError` (see DESIGN.md "Scope").
+``apply_nodes`` accept UDFs (plain tensor gathers).  A user-defined *reduce*
+runs the reference's degree bucketing on the device (messages materialised per
+edge, one UDF call per in-degree bucket on a (nodes, degree, ...) mailbox,
+``runtime/degree_bucketing.py``, ``src/scheduler/scheduler.cc``): torch tensor
+ops, off the kernel path, as in the reference.
 """
 from __future__ import annotations
 
@@ -106,11 +108,13 @@ class EdgeBatch(object):
 
 
 class NodeBatch(object):
-    """Nodes given to an apply UDF (``python/dgl/udf.py:NodeBatch``)."""
+    """Nodes given to an apply or reduce UDF (``python/dgl/udf.py:NodeBatch``);
+    ``mailbox`` holds a reduce UDF's messages, (nodes, degree, ...) per field."""
 
-    def __init__(self, nodes, data):
+    def __init__(self, nodes, data, mailbox=None):
         self._nodes = nodes
         self.data = data
+        self.mailbox = mailbox
 
     def nodes(self):
         return self._nodes
@@ -429,22 +433,86 @@ class DGLGraph(object):
     def _is_udf(mfuncs):
         return len(mfuncs) == 1 and not isinstance(mfuncs[0], MessageFunction)
 
+    @staticmethod
+    def _is_udf_reduce(rfuncs):
+        return len(rfuncs) == 1 and not isinstance(rfuncs[0], ReduceFunction)
+
     def _check_builtin(self, mfuncs, rfuncs):
         if not mfuncs:
             raise DGLError("A message function is required (pass one or call "
                            "register_message_func)")
-        if not rfuncs:
-            raise DGLError("A reduce function is required (pass one or call "
-                           "register_reduce_func)")
+        self._check_reduce(rfuncs)
         if not self._is_udf(mfuncs):
             for f in mfuncs:
                 if not isinstance(f, MessageFunction):
                     raise DGLError("A list of message functions must hold builtins "
                                    "(dgl.function.*) only")
-        for f in rfuncs:
-            if not isinstance(f, ReduceFunction):
-                raise DGLError("user-defined reduce functions (degree bucketing) are not "
-                               "supported by the MI355X engine; use dgl.function reducers")
+
+    @staticmethod
+    def _check_reduce(rfuncs):
+        if not rfuncs:
+            raise DGLError("A reduce function is required (pass one or call "
+                           "register_reduce_func)")
+        if len(rfuncs) > 1 or isinstance(rfuncs[0], ReduceFunction):
+            for f in rfuncs:
+                if not isinstance(f, ReduceFunction):
+                    raise DGLError("A list of reduce functions must hold builtins "
+                                   "(dgl.function.*) only")
+        elif not callable(rfuncs[0]):
+            raise DGLError("Invalid reduce function: %r" % (rfuncs[0],))
+
+    def _messages(self, gidx, mfuncs, s, d, e, dev):
+        """Every message of the selected edges as per-edge tensors indexed by (parent)
+        edge id: builtins as one reducer-"none" kernel each, a UDF on an EdgeBatch."""
+        if self._is_udf(mfuncs):
+            return self._udf_messages(mfuncs[0], s, d, e, dev)
+        m = self.number_of_edges()
+        return {f.out_field: f._invoke(gidx, self._node_frame, self._node_frame,
+                                       self._edge_frame, m, reducer="none") for f in mfuncs}
+
+    def _reduce(self, gidx, mfuncs, rfuncs, edges, dev, msgs=None):
+        """Reduce messages on every node of ``gidx`` (the whole graph or an in-edge
+        subgraph).  Builtin reducers: one kernel per (message, reducer) pair, or copy_e
+        over materialised messages.  A reduce UDF: degree bucketing
+        (runtime/degree_bucketing.py:12-80).  ``edges`` returns the selected edges as
+        device (src, dst, eid) tensors in edge-id order."""
+        if self._is_udf_reduce(rfuncs):
+            s, d, e = edges()
+            if msgs is None:
+                msgs = self._messages(gidx, mfuncs, s, d, e, dev)
+            return self._degree_bucket_reduce(rfuncs[0], msgs, d, e, dev)
+        if msgs is None and self._is_udf(mfuncs):
+            s, d, e = edges()
+            msgs = self._udf_messages(mfuncs[0], s, d, e, dev)
+        return self._builtin_reduce(gidx, mfuncs, rfuncs, self._node_frame, self._edge_frame,
+                                    self.number_of_nodes(), udf_msgs=msgs)
+
+    def _degree_bucket_reduce(self, rfunc, msgs, d, e, dev):
+        """runtime/degree_bucketing.py + src/scheduler/scheduler.cc:13-100 on the device:
+        destination nodes grouped by in-degree, one reduce-UDF call per bucket on a
+        (nodes, degree, ...) mailbox whose messages keep their edge-id order, results
+        merged by node id.  Rows of nodes that received nothing stay zero (the zero
+        initializer of the reference's zero-degree bucket)."""
+        n = self.number_of_nodes()
+        d = d.long()
+        order = th.argsort(d, stable=True)
+        ds, es = d[order], e.long()[order]
+        deg = th.bincount(ds, minlength=n)
+        starts = th.cumsum(deg, 0) - deg
+        out = {}
+        for dv in th.unique(deg).tolist():
+            if dv == 0:
+                continue
+            nodes = th.nonzero(deg == dv).squeeze(1)
+            pos = starts[nodes].unsqueeze(1) + th.arange(dv, device=dev)
+            mids = es[pos]
+            mail = {k: t[mids] for k, t in msgs.items()}
+            nb = NodeBatch(nodes, {k: t[nodes] for k, t in self._node_frame.items()}, mail)
+            for k, t in rfunc(nb).items():
+                if k not in out:
+                    out[k] = t.new_zeros((n,) + tuple(t.shape[1:]))
+                out[k] = out[k].index_copy(0, nodes, t)
+        return out
 
     # ---- registered defaults (graph.py:2458-2548) -------------------------------------
     def register_message_func(self, func):
@@ -499,12 +567,7 @@ class DGLGraph(object):
             return
         dev = self._device(self._node_frame, self._edge_frame)
         gidx = self._gidx(dev)
-        udf_msgs = None
-        if self._is_udf(mfuncs):
-            s, d, e = self._edge_tensors(ALL, dev)
-            udf_msgs = self._udf_messages(mfuncs[0], s, d, e, dev)
-        res = self._builtin_reduce(gidx, mfuncs, rfuncs, self._node_frame, self._edge_frame,
-                                   self.number_of_nodes(), udf_msgs=udf_msgs)
+        res = self._reduce(gidx, mfuncs, rfuncs, lambda: self._edge_tensors(ALL, dev), dev)
         if apply_node_func is not None:
             nb = NodeBatch(self.nodes().to(dev), dict(self._node_frame, **res))
             res.update(apply_node_func(nb))
@@ -545,13 +608,9 @@ class DGLGraph(object):
         dev = self._device(self._node_frame, self._edge_frame)
         sub = _PartialIndex(self.number_of_nodes(), src, dst, eid)
         gidx = sub.get_immutable_gidx(dev)
-        udf_msgs = None
-        if self._is_udf(mfuncs):
-            udf_msgs = self._udf_messages(mfuncs[0], th.as_tensor(src, device=dev),
-                                          th.as_tensor(dst, device=dev),
-                                          th.as_tensor(eid, device=dev), dev)
-        res = self._builtin_reduce(gidx, mfuncs, rfuncs, self._node_frame, self._edge_frame,
-                                   self.number_of_nodes(), udf_msgs=udf_msgs)
+        res = self._reduce(gidx, mfuncs, rfuncs,
+                           lambda: (th.as_tensor(src, device=dev), th.as_tensor(dst, device=dev),
+                                    th.as_tensor(eid, device=dev)), dev)
         self._write_partial(res, recv_nodes, apply_node_func, dev)
 
     def pull(self, v, message_func="default", reduce_func="default", apply_node_func="default",
@@ -601,10 +660,9 @@ class DGLGraph(object):
             return
         dev = self._device(self._node_frame, self._edge_frame)
         if self._is_udf(mfuncs):
-            s, d, e = self._edge_tensors(edges, dev)
-            msgs = self._udf_messages(mfuncs[0], s, d, e, dev)
+            s_, d_, e = self._edge_tensors(edges, dev)
+            msgs = self._udf_messages(mfuncs[0], s_, d_, e, dev)
         else:
-            msgs = {}
             if is_all(edges):
                 gidx = self._gidx(dev)
                 e = th.arange(m, device=dev)
@@ -612,9 +670,7 @@ class DGLGraph(object):
                 src, dst, eid = self._resolve_edges(edges)
                 gidx = _PartialIndex(self.number_of_nodes(), src, dst, eid).get_immutable_gidx(dev)
                 e = th.as_tensor(eid, device=dev)
-            for f in mfuncs:
-                msgs[f.out_field] = f._invoke(gidx, self._node_frame, self._node_frame,
-                                              self._edge_frame, m, reducer="none")
+            msgs = self._messages(gidx, mfuncs, None, None, e, dev)
         if not hasattr(self, "_msg_frame") or self._msg_frame is None:
             self._msg_frame = {}
         ind = getattr(self, "_msg_ind", None)
@@ -636,13 +692,7 @@ class DGLGraph(object):
         reduce_func = self._default(reduce_func, "_reduce_func")
         apply_node_func = self._default(apply_node_func, "_apply_node_func")
         rfuncs = self._as_list(reduce_func)
-        if not rfuncs:
-            raise DGLError("A reduce function is required (pass one or call "
-                           "register_reduce_func)")
-        for f in rfuncs:
-            if not isinstance(f, ReduceFunction):
-                raise DGLError("user-defined reduce functions (degree bucketing) are not "
-                               "supported by the MI355X engine; use dgl.function reducers")
+        self._check_reduce(rfuncs)
         vs = np.arange(self.number_of_nodes()) if is_all(v) else _to_index_array(v, "v")
         ind = getattr(self, "_msg_ind", None)
         src, dst, eid = self._graph.edges()
@@ -658,8 +708,11 @@ class DGLGraph(object):
         dev = self._device(self._node_frame, self._edge_frame)
         gidx = _PartialIndex(self.number_of_nodes(), src[mask], dst[mask],
                              eid[mask]).get_immutable_gidx(dev)
-        res = self._builtin_reduce(gidx, [], rfuncs, self._node_frame, self._edge_frame,
-                                   self.number_of_nodes(), udf_msgs=self._msg_frame)
+        res = self._reduce(gidx, [], rfuncs,
+                           lambda: (th.as_tensor(src[mask], device=dev),
+                                    th.as_tensor(dst[mask], device=dev),
+                                    th.as_tensor(eid[mask], device=dev)), dev,
+                           msgs=self._msg_frame)
         self._write_partial(res, vs, apply_node_func, dev)
         ind[eid[mask]] = False
         if not ind.any():

@@ -116,12 +116,17 @@ def test_cpu_tensors_fail_loudly():
         g.update_all(fn.copy_u("h", "m"), fn.sum("m", "s"))
 
 
-def test_udf_reduce_rejected():
+def test_udf_reduce_still_runs_builtin_messages_on_device():
+    """A reduce UDF (degree bucketing) materialises builtin messages with the HIP
+    kernel first: CPU tensors fail loudly there, no CPU fallback."""
     g = dgl.DGLGraph()
     g.add_nodes(2)
     g.add_edges([0], [1])
+    g.ndata["h"] = th.zeros(2, 4)
     with pytest.raises(dgl.DGLError):
-        g.update_all(fn.copy_u("h", "m"), lambda nodes: {})
+        g.update_all(fn.copy_u("h", "m"), lambda nodes: {"o": nodes.mailbox["m"].sum(1)})
+    with pytest.raises(dgl.DGLError):  # a list must hold builtins only
+        g.update_all(fn.copy_u("h", "m"), [fn.sum("m", "o"), lambda nodes: {}])
 
 
 def test_capi_errors_without_device():

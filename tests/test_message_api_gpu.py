@@ -150,6 +150,97 @@ def test_udf_message_matches_builtin_with_grad():
         assert th.allclose(a, b, rtol=1e-4, atol=1e-4)
 
 
+def reducer_both(nodes):
+    """test_function.py:21-22, the reference's own reduce UDF."""
+    return {"out": th.sum(nodes.mailbox["m"], 1)}
+
+
+@pytest.mark.parametrize("msg,expect", [
+    (lambda: fn.copy_src(src="h", out="m"), STAR_COPY),
+    (lambda: fn.copy_edge(edge="h", out="m"), STAR_COPY),
+    (lambda: fn.src_mul_edge(src="h", edge="h", out="m"), STAR_MUL),
+])
+def test_function_known_answers_reduce_udf(msg, expect):
+    """test_function.py:24-67 verbatim in structure: builtin message + the reference's
+    UDF reducer (degree bucketing), update_all() and send() + recv()."""
+    g = star_graph()
+    g.register_message_func(msg())
+    g.register_reduce_func(reducer_both)
+    g.update_all()
+    assert th.equal(g.ndata.pop("out").cpu(), th.tensor(expect))
+    g.send()
+    g.recv()
+    assert th.equal(g.ndata.pop("out").cpu(), th.tensor(expect))
+
+
+def test_recv_docstring_known_answer_reduce_udf():
+    """graph.py:2860-2895 with the docstring's own UDFs."""
+    g = dgl.DGLGraph()
+    g.add_nodes(3)
+    g.ndata["x"] = th.tensor([[1.], [2.], [3.]], device=DEV)
+    g.add_edges([0, 1], [1, 2])
+    g.register_message_func(lambda edges: {"m": edges.src["x"]})
+    g.register_reduce_func(lambda nodes: {"x": nodes.mailbox["m"].sum(1)})
+    g.send(g.edges())
+    g.recv(g.nodes())
+    assert th.equal(g.ndata["x"].cpu(), th.tensor([[0.], [1.], [2.]]))
+    g.recv(g.nodes())
+    assert th.equal(g.ndata["x"].cpu(), th.tensor([[0.], [1.], [2.]]))
+
+
+@pytest.mark.parametrize("red", ["sum", "max", "min", "mean", "prod"])
+def test_degree_bucketing_matches_builtin(red):
+    """A reduce UDF over mailboxes == the builtin reducer (nodes with in-edges; the
+    UDF path leaves zero-in-degree rows at 0), values and gradients."""
+    rng = np.random.default_rng(11)
+    n, m, f = 200, 1500, 8
+    src, dst = rng.integers(0, n, m), (rng.pareto(1.0, m) * 10).astype(np.int64) % n
+    if red in ("max", "min"):
+        # no repeated (u, v) pairs: a tie sends the builtin's gradient to every tied
+        # edge (cpu/functor.h:36-38) but torch.max's to one of them
+        pairs = np.unique(np.stack([src, dst], 1), axis=0)
+        src, dst = pairs[rng.permutation(len(pairs))].T
+    x = th.rand(n, f, device=DEV) + 0.5
+    udf = {"sum": lambda nb: {"o": nb.mailbox["m"].sum(1)},
+           "max": lambda nb: {"o": nb.mailbox["m"].max(1)[0]},
+           "min": lambda nb: {"o": nb.mailbox["m"].min(1)[0]},
+           "mean": lambda nb: {"o": nb.mailbox["m"].mean(1)},
+           "prod": lambda nb: {"o": nb.mailbox["m"].prod(1)}}[red]
+    outs = []
+    for reduce_func in (getattr(fn, red)("m", "o"), udf):
+        g = dgl.DGLGraph()
+        g.add_nodes(n)
+        g.add_edges(src, dst)
+        xs = x.clone().requires_grad_()
+        g.ndata["x"] = xs
+        g.update_all(fn.copy_u("x", "m"), reduce_func)
+        o = g.ndata["o"]
+        o.backward(th.ones_like(o))
+        outs.append((o.detach(), xs.grad))
+    has = th.as_tensor(np.bincount(dst, minlength=n) > 0, device=DEV)
+    tol = 1e-2 if red == "prod" else 1e-4
+    assert th.allclose(outs[0][0][has], outs[1][0][has], rtol=tol, atol=tol)
+    assert th.all(outs[1][0][~has] == 0)
+    assert th.allclose(outs[0][1], outs[1][1], rtol=tol, atol=tol)
+
+
+def test_reduce_udf_pull_and_mailbox_order():
+    """Mailboxes list a node's messages in edge-id order (scheduler.cc:20-24)."""
+    g = dgl.DGLGraph()
+    g.add_nodes(4)
+    g.add_edges([3, 1, 2, 0, 3], [0, 0, 0, 1, 2])
+    g.ndata["x"] = th.tensor([10., 20., 30., 40.], device=DEV).view(4, 1)
+    seen = {}
+
+    def red(nodes):
+        seen[nodes.mailbox["m"].shape[1]] = nodes.mailbox["m"][..., 0].cpu()
+        return {"y": nodes.mailbox["m"][:, 0] * 1000 + nodes.mailbox["m"][:, -1]}
+    g.pull([0, 2, 3], fn.copy_u("x", "m"), red)
+    assert th.equal(seen[3], th.tensor([[40., 20., 30.]]))
+    y = g.ndata["y"].cpu().view(-1)
+    assert y[0] == 40 * 1000 + 30 and y[2] == 40 * 1000 + 40 and y[3] == 0 and y[1] == 0
+
+
 def test_missing_functions_raise():
     g = star_graph()
     with pytest.raises(DGLError):
@@ -159,5 +250,3 @@ def test_missing_functions_raise():
     g.register_message_func(fn.copy_src("h", "m"))
     with pytest.raises(DGLError):
         g.update_all()
-    with pytest.raises(DGLError):  # a UDF reducer is outside the engine
-        g.update_all(reduce_func=lambda nodes: {"out": nodes.mailbox["m"].sum(1)})
