@@ -265,6 +265,15 @@ void run_fast(const DGLMIGraph* g, const DGLMICsr& walk, int kind, int red, cons
   a.F = F;
   a.head_dim = head_dim;
   a.chunk = fast_chunk_edges(walk.nnz, F);
+  // cold-row hints: copy_u sum over a table larger than the Infinity Cache
+  if (kind == FAST_COPY_COL && red == RED_SUM && x_map == nullptr && fast_marked_supported(F)) {
+    const int32_t* marked = &walk == &g->in_csr ? g->in_gather_cols
+                            : (&walk == &g->out_csr ? g->out_gather_cols : nullptr);
+    if (marked != nullptr && walk.num_cols * F * static_cast<int64_t>(sizeof(float)) >= kMarkedMinTableBytes) {
+      a.indices = marked;
+      a.marked = 1;
+    }
+  }
   if (epi) {
     a.row_mul = epi->row_mul;
     a.row_div = epi->row_div;
@@ -862,6 +871,24 @@ int DGLMIFusedGatBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src, c
   b.num_rows = outc.num_rows;
   launch_gat_backward_src(b, s);
   check_hip(hipGetLastError(), "fused GAT backward (src) launch");
+  API_END();
+}
+
+int DGLMIKernelMarkColdColumns(const DGLMIGraph* graph, int32_t direction,
+                               int32_t min_hot_degree, int32_t* out_cols, void* stream) {
+  API_BEGIN();
+  check_graph(graph);
+  DGLMI_CHECK(direction == 0 || direction == 1, "direction must be 0 (in-CSR) or 1 (out-CSR)");
+  const DGLMICsr& c = direction == 0 ? graph->in_csr : graph->out_csr;
+  const DGLMICsr& o = direction == 0 ? graph->out_csr : graph->in_csr;
+  check_csr(c, direction == 0 ? "in_csr" : "out_csr", false);
+  DGLMI_CHECK(o.indptr != nullptr && o.num_rows == c.num_cols,
+              "the opposite CSR must have one row per column node");
+  if (c.nnz > 0) DGLMI_CHECK(out_cols != nullptr, "null out_cols");
+  DeviceGuard guard(graph->device);
+  launch_mark_cold(c.indices, c.nnz, o.indptr, min_hot_degree, out_cols,
+                   static_cast<hipStream_t>(stream));
+  check_hip(hipGetLastError(), "mark cold columns launch");
   API_END();
 }
 

@@ -214,12 +214,22 @@ struct FastArgs {
   const float* row_div;
   const float* bias;
   const float* addend;
+  // copy_u sum: `indices` carries cold-row marks in bit 31 (DGLMIKernelMarkColdColumns);
+  // marked rows are gathered non-temporally
+  int marked;
 };
 int64_t fast_chunk_edges(int64_t nnz, int64_t F);
 int64_t fast_workspace_bytes(int64_t nnz, int64_t F);
 // Returns false if the shape is not supported by the fast path.
 bool fast_supported(int kind, int64_t F, int64_t head_dim);
 void launch_fast_reduce(int kind, int red, const FastArgs& a, hipStream_t s);  // needs a.indptr
+// out_cols[p] = cols[p] | (col_deg(cols[p]) < thresh ? 1 << 31 : 0), col_deg from deg_indptr
+void launch_mark_cold(const int32_t* cols, int64_t nnz, const int32_t* deg_indptr, int32_t thresh,
+                      int32_t* out_cols, hipStream_t s);
+// row widths whose launch config has a marked variant (L >= 16 lanes, one float4 each)
+inline bool fast_marked_supported(int64_t F) { return F > 32 && F <= 256 && F % 4 == 0; }
+// tables smaller than this stay on the plain path (they fit the Infinity Cache)
+constexpr int64_t kMarkedMinTableBytes = int64_t(256) << 20;
 
 // Fused GAT (kernels_gat.hip).
 struct GatArgs {

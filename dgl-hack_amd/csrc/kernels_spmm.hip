@@ -52,6 +52,11 @@ __device__ __forceinline__ float4 ld4(const float* p) {
   return *reinterpret_cast<const float4*>(p);
 }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld4_nt(const float* p) {
+  const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
 
 template <int KIND>
 constexpr bool needs_eid() {
@@ -191,7 +196,17 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
           const int f4 = lane + v * L;
-          val[u][v] = (ok && f4 < F4) ? edge_value<KIND>(a, col, eid, f4) : I;
+          if constexpr ((VAR & 8) != 0 && KIND == FAST_COPY_COL) {
+            // bit 31 of the column marks a cold source row (re-read fewer than
+            // min_hot_degree times): gathered non-temporally so it does not evict
+            // re-read rows from L2 / Infinity Cache (VAR & 16: the reverse, a
+            // tuning control)
+            const bool nt = (col < 0) != ((VAR & 16) != 0);
+            const float* px = a.x + static_cast<int64_t>(col & 0x7fffffff) * a.F + 4 * f4;
+            val[u][v] = (ok && f4 < F4) ? (nt ? ld4_nt(px) : ld4(px)) : I;
+          } else {
+            val[u][v] = (ok && f4 < F4) ? edge_value<KIND>(a, col, eid, f4) : I;
+          }
         }
       }
 #pragma unroll
@@ -532,6 +547,25 @@ void run(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
   constexpr int G = kBlock / L;
   const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
   const unsigned blocks = static_cast<unsigned>((chunks + G - 1) / G);
+  if constexpr (KIND == FAST_COPY_COL && RED == RED_SUM && NV == 1 && L >= 16) {
+    if (a.marked) {  // cold-row hints present (capi.cpp run_fast decides)
+      if (has_epi(a))
+        hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 11, true>), dim3(blocks), dim3(kBlock),
+                           0, s, a, indptr);
+      else
+        hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 11>), dim3(blocks), dim3(kBlock), 0, s,
+                           a, indptr);
+      if (chunks > 1) {
+        if (has_epi(a))
+          hipLaunchKernelGGL((k_chunk_fixup<RED, L, NV, true>), dim3(blocks), dim3(kBlock), 0, s, a,
+                             indptr);
+        else
+          hipLaunchKernelGGL((k_chunk_fixup<RED, L, NV>), dim3(blocks), dim3(kBlock), 0, s, a,
+                             indptr);
+      }
+      return;
+    }
+  }
   if constexpr (RED == RED_SUM) {
     if (has_epi(a)) {
       hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 3, true>), dim3(blocks), dim3(kBlock), 0,
@@ -550,6 +584,7 @@ void run(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
       case 2: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 2>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
       case 4: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 4>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
       case 7: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 7>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
+      case 27: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 27>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
       default: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
     }
   } else {
@@ -578,7 +613,27 @@ void run_cfg(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
   }
 }
 
+__global__ void k_mark_cold(const int32_t* __restrict__ cols, int64_t nnz,
+                            const int32_t* __restrict__ deg_indptr, int32_t thresh,
+                            int32_t* __restrict__ out) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t p = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; p < nnz; p += stride) {
+    const int32_t c = cols[p];
+    const int32_t d = deg_indptr[c + 1] - deg_indptr[c];
+    out[p] = d < thresh ? static_cast<int32_t>(static_cast<uint32_t>(c) | 0x80000000u) : c;
+  }
+}
+
 }  // namespace
+
+void launch_mark_cold(const int32_t* cols, int64_t nnz, const int32_t* deg_indptr, int32_t thresh,
+                      int32_t* out_cols, hipStream_t s) {
+  if (nnz <= 0) return;
+  const int64_t want = (nnz + kBlock - 1) / kBlock;
+  const unsigned blocks = static_cast<unsigned>(want < 65536 ? want : 65536);
+  hipLaunchKernelGGL(k_mark_cold, dim3(blocks), dim3(kBlock), 0, s, cols, nnz, deg_indptr, thresh,
+                     out_cols);
+}
 
 int64_t fast_chunk_edges(int64_t nnz, int64_t F) {
   // Enough chunks to give every CU several groups; long chunks otherwise so

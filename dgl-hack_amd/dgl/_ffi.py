@@ -42,6 +42,8 @@ class Graph(ctypes.Structure):
         ("workspace_bytes", ctypes.c_int64),
         ("coo_src", ctypes.c_void_p),
         ("coo_dst", ctypes.c_void_p),
+        ("in_gather_cols", ctypes.c_void_p),
+        ("out_gather_cols", ctypes.c_void_p),
     ]
 
 
@@ -115,6 +117,8 @@ _SIGS = {
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "DGLMIKernelWorkspaceBytes": (ctypes.c_int64, [ctypes.POINTER(CSR), ctypes.c_int64]),
+    "DGLMIKernelMarkColdColumns": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]),
     "DGLMICOOToCSR": (ctypes.c_int, [
         ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),

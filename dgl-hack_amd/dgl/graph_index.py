@@ -20,6 +20,7 @@ two stable radix sorts give arrays bit-identical to the host path.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch as th
@@ -75,6 +76,7 @@ class ImmutableGraphIndex:
         # subgraphs are not), so an edge-id ordered COO exists
         self.eid_perm = eid_perm
         self._coo = None
+        self._gather_cols = None
 
     def number_of_edges(self):
         return self.in_csr.nnz
@@ -95,6 +97,50 @@ class ImmutableGraphIndex:
             self._coo = (src, dst)
         return self._coo
 
+    # Cold-row hints (DGLMIGraph.{in,out}_gather_cols): built for graphs whose node
+    # tables can outgrow the 256 MiB Infinity Cache (>= 2^20 nodes on a side and
+    # >= 2^22 edges); the library uses them only when the gathered table is
+    # >= 256 MiB.  A row gathered fewer than HOT_DEGREE times per pass is cold.
+    # M1 sweep (scripts/hotcold_probe.py, profiles/r01_hotcold_w{1,8}.json): the
+    # hot set at degree >= 64 gives 3.24 -> 3.11 ms forward, 3.26 -> 3.12 ms
+    # source gradient (world 1) and 3.69 -> 3.52 ms forward (a rank of world 8),
+    # bit-identical; thresholds 16 / 32 / 128 / 256 are no better; every row
+    # non-temporal: 5.5 ms.
+    HOT_DEGREE = 64
+    MIN_HINT_NODES = 1 << 20
+    MIN_HINT_EDGES = 1 << 22
+
+    def gather_cols(self):
+        """(in, out) cold-marked column arrays, built on the device once and cached
+        (4 B per edge and direction); (None, None) for small graphs."""
+        if self._gather_cols is None:
+            self._gather_cols = (None, None)
+            hot = int(os.environ.get("DGLMI_HOT_DEGREE", self.HOT_DEGREE))
+            if hot > 0 and self.in_csr.nnz >= self.MIN_HINT_EDGES and self.in_csr.nnz < 2 ** 31:
+                cols = []
+                g = self._cstruct_base()
+                for direction, csr in ((0, self.in_csr), (1, self.out_csr)):
+                    if csr.num_cols < self.MIN_HINT_NODES:
+                        cols.append(None)
+                        continue
+                    out = th.empty(csr.nnz, dtype=th.int32, device=csr.indices.device)
+                    _ffi.check_call(_ffi.lib().DGLMIKernelMarkColdColumns(
+                        ctypes.byref(g), direction, hot, out.data_ptr(),
+                        th.cuda.current_stream(csr.indices.device).cuda_stream))
+                    cols.append(out)
+                self._gather_cols = tuple(cols)
+        return self._gather_cols
+
+    def _cstruct_base(self):
+        g = _ffi.Graph()
+        g.in_csr = self.in_csr.cstruct()
+        g.out_csr = self.out_csr.cstruct()
+        g.num_bits = 32
+        g.device = self.device.index if self.device.index is not None else th.cuda.current_device()
+        g.workspace = None
+        g.workspace_bytes = 0
+        return g
+
     def cstruct(self, workspace=None, coo=False):
         g = _ffi.Graph()
         g.in_csr = self.in_csr.cstruct()
@@ -102,6 +148,9 @@ class ImmutableGraphIndex:
         pair = self.coo() if coo else None
         g.coo_src = pair[0].data_ptr() if pair is not None and self.in_csr.nnz else None
         g.coo_dst = pair[1].data_ptr() if pair is not None and self.in_csr.nnz else None
+        ic, oc = self.gather_cols()
+        g.in_gather_cols = ic.data_ptr() if ic is not None else None
+        g.out_gather_cols = oc.data_ptr() if oc is not None else None
         g.num_bits = 32
         g.device = self.device.index if self.device.index is not None else th.cuda.current_device()
         if workspace is not None:

@@ -77,6 +77,16 @@ typedef struct {
    * edge-id order: sequential writes and edge-operand reads.  May be NULL. */
   const int32_t* coo_src;
   const int32_t* coo_dst;
+  /* Optional cache-placement hints (extension, no reference counterpart):
+   * in_csr.indices / out_csr.indices with bit 31 set on every column whose
+   * node row is gathered fewer than `min_hot_degree` times per pass over that
+   * CSR (DGLMIKernelMarkColdColumns).  When present and the gathered table
+   * exceeds the 256 MiB Infinity Cache, the copy_u sum kernels load marked rows
+   * non-temporally so that rarely re-read rows do not evict the re-read ones
+   * from L2 / Infinity Cache (M1: 3.24 -> 3.11 ms per copy_u_sum, bit-identical
+   * results).  Either may be NULL. */
+  const int32_t* in_gather_cols;
+  const int32_t* out_gather_cols;
 } DGLMIGraph;
 
 /* A contiguous row-major fp32 device array (NDArray / DLTensor subset). */
@@ -168,6 +178,15 @@ int DGLMIKernelBackwardCopyReduce(const char* reducer, const DGLMIGraph* graph, 
  * binary search, binary_reduce_impl.cu:424-466); rows split across chunks
  * leave per-chunk partials here, combined afterwards in chunk order. */
 int64_t DGLMIKernelWorkspaceBytes(const DGLMICsr* csr, int64_t feat_len);
+
+/* Build DGLMIGraph.{in,out}_gather_cols (extension): out_cols[p] =
+ * csr.indices[p] | (1 << 31) when the column node's row count in the opposite
+ * direction (out-degree of a source for the in-CSR, in-degree of a destination
+ * for the out-CSR) is below min_hot_degree, else csr.indices[p].  `direction`
+ * 0 marks the in-CSR, 1 the out-CSR; out_cols is a device array of csr.nnz
+ * int32.  Stream-ordered. */
+int DGLMIKernelMarkColdColumns(const DGLMIGraph* graph, int32_t direction,
+                               int32_t min_hot_degree, int32_t* out_cols, void* stream);
 
 /* ---- graph ingestion ------------------------------------------------------
  * aten::COOToCSR (array/cpu/spmat_op_impl_coo.cc:230-283): stable counting
