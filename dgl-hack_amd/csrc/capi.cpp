@@ -624,6 +624,23 @@ void backward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const 
 }
 
 // Shared argument checking of the fused GAT entry points.
+// Column blocks usable by the fused GAT kernels: every block non-empty (block 0
+// of the destination-side walk must see every row) and shaped like the graph.
+int gat_blocks(const DGLMIGraph* g) {
+  const int nb = g->num_col_blocks;
+  if (nb <= 1 || g->in_col_blocks == nullptr || g->out_col_blocks == nullptr) return 1;
+  for (int b = 0; b < nb; ++b) {
+    const DGLMICsr& i = g->in_col_blocks[b];
+    const DGLMICsr& o = g->out_col_blocks[b];
+    check_csr(i, "in_col_blocks", true);
+    check_csr(o, "out_col_blocks", true);
+    DGLMI_CHECK(i.num_rows == g->in_csr.num_rows && o.num_rows == g->out_csr.num_rows,
+                "column blocks must keep the graph's rows");
+    if (i.nnz == 0 || o.nnz == 0) return 1;
+  }
+  return nb;
+}
+
 GatArgs gat_args(const DGLMIGraph* g, const DGLMIArray* ft, const DGLMIArray* el,
                  const DGLMIArray* er, float slope, DGLMIArray* out, DGLMIArray* mx,
                  DGLMIArray* sm) {
@@ -808,6 +825,43 @@ int DGLMIFusedGatForward(const DGLMIGraph* graph, const DGLMIArray* feat_src, co
     launch_fill(sum_out->data, a.num_rows * a.H, 0.0f, s);
     return 0;
   }
+  const int nb = gat_blocks(graph);
+  if (nb > 1) {
+    // column-blocked: one raw (unnormalised) launch per source block into its own
+    // partial buffers, then the in-order merge
+    const int64_t N = a.num_rows;
+    const int64_t part_floats = nb * N * (a.F + 2 * a.H);
+    int64_t max_chunks = 0;
+    for (int b = 0; b < nb; ++b) {
+      const int64_t c = graph->in_col_blocks[b].nnz;
+      max_chunks = std::max(max_chunks, (c + gat_chunk_edges(std::max<int64_t>(c, 1)) - 1) /
+                                            gat_chunk_edges(std::max<int64_t>(c, 1)));
+    }
+    const int64_t part_bytes = (part_floats * static_cast<int64_t>(sizeof(float)) + 255) & ~int64_t(255);
+    Scratch ws(graph, part_bytes + max_chunks * (a.F + 2 * a.H) * static_cast<int64_t>(sizeof(float)), s);
+    float* out_part = static_cast<float*>(ws.ptr);
+    float* m_part = out_part + nb * N * a.F;
+    float* l_part = m_part + nb * N * a.H;
+    for (int b = 0; b < nb; ++b) {
+      const DGLMICsr& c = graph->in_col_blocks[b];
+      GatArgs ab = a;
+      ab.indptr = c.indptr;
+      ab.rows = c.rows;
+      ab.indices = c.indices;
+      ab.nnz = c.nnz;
+      ab.chunk = gat_chunk_edges(std::max<int64_t>(c.nnz, 1));
+      ab.out = out_part + b * N * a.F;
+      ab.m = m_part + b * N * a.H;
+      ab.l = l_part + b * N * a.H;
+      ab.raw = 1;
+      ab.carry = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + part_bytes);
+      launch_gat_forward(ab, s);
+    }
+    launch_gat_merge(out_part, m_part, l_part, nb, N, a.H, a.D, out->data, max_out->data,
+                     sum_out->data, s);
+    check_hip(hipGetLastError(), "fused GAT forward (blocked) launch");
+    return 0;
+  }
   const int64_t chunks = (walk.nnz + a.chunk - 1) / a.chunk;
   Scratch carry(graph, chunks * (a.F + 2 * a.H) * static_cast<int64_t>(sizeof(float)), s);
   a.carry = static_cast<float*>(carry.ptr);
@@ -853,12 +907,46 @@ int DGLMIFusedGatBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src, c
   a.g_er = grad_er->data;
   a.g_el = grad_el->data;
   a.g_ft = grad_feat_src->data;
-  const int64_t chunks = (in.nnz + a.chunk - 1) / a.chunk;
+  const int nb = gat_blocks(graph);
+  int64_t chunks = (in.nnz + a.chunk - 1) / a.chunk;
+  for (int b = 0; b < nb && nb > 1; ++b)
+    for (const DGLMICsr* c : {&graph->in_col_blocks[b], &graph->out_col_blocks[b]}) {
+      const int64_t k = gat_chunk_edges(std::max<int64_t>(c->nnz, 1));
+      chunks = std::max(chunks, (c->nnz + k - 1) / k);
+    }
   const int64_t stats_bytes = a.num_rows * a.H * 16;
   const int64_t carry_bytes = chunks * (a.F + a.H) * static_cast<int64_t>(sizeof(float));
   Scratch ws(graph, stats_bytes + carry_bytes + 256, s);
   a.stats = static_cast<float4*>(ws.ptr);
   a.carry = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + ((stats_bytes + 255) & ~int64_t(255)));
+  if (nb > 1) {
+    // column-blocked: block 0 writes every row's stats and the first gradient
+    // terms, later blocks add theirs (block order), first the destination side
+    // over the source blocks, then the source side over the destination blocks
+    auto set_walk = [](GatArgs& g, const DGLMICsr& c) {
+      g.indptr = c.indptr;
+      g.rows = c.rows;
+      g.indices = c.indices;
+      g.nnz = c.nnz;
+      g.num_rows = c.num_rows;
+      g.chunk = gat_chunk_edges(std::max<int64_t>(c.nnz, 1));
+    };
+    for (int b = 0; b < nb; ++b) {
+      GatArgs ab = a;
+      set_walk(ab, graph->in_col_blocks[b]);
+      ab.accumulate = b > 0;
+      ab.skip_stats = b > 0;
+      launch_gat_backward_dst(ab, s);
+    }
+    for (int b = 0; b < nb; ++b) {
+      GatArgs ab = a;
+      set_walk(ab, graph->out_col_blocks[b]);
+      ab.accumulate = b > 0;
+      launch_gat_backward_src(ab, s);
+    }
+    check_hip(hipGetLastError(), "fused GAT backward (blocked) launch");
+    return 0;
+  }
   // destination side on the in-CSR
   launch_gat_backward_dst(a, s);
   check_hip(hipGetLastError(), "fused GAT backward (dst) launch");

@@ -257,11 +257,19 @@ struct GatArgs {
   float* g_ft;
   float* carry;
   int64_t chunk;
+  // column-blocked launches (one launch per block of gathered rows):
+  int raw;          // forward: leave (m, l, acc) unnormalised (merged afterwards)
+  int accumulate;   // backward: add into g_er / g_ft / g_el instead of overwriting
+  int skip_stats;   // backward (dst side): stats already written by an earlier block
 };
 bool gat_supported(int64_t H, int64_t D);
 int64_t gat_chunk_edges(int64_t nnz);
 void launch_gat_forward(const GatArgs& a, hipStream_t s);
 void launch_gat_backward_dst(const GatArgs& a, hipStream_t s);
 void launch_gat_backward_src(const GatArgs& a, hipStream_t s);
+// out[r] = merge over blocks b of the unnormalised partials (out_part[b], m_part[b],
+// l_part[b]), normalised; m / l of the merged softmax (blocks in order)
+void launch_gat_merge(const float* out_part, const float* m_part, const float* l_part, int nb,
+                      int64_t num_rows, int H, int D, float* out, float* m, float* l, hipStream_t s);
 
 }  // namespace dglmi

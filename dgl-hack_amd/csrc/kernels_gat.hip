@@ -121,7 +121,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
         }
       } else {
         float4 o = acc[v];
-        if (final) {
+        if (final && !a.raw) {
           const float inv = sm[v] > 0.0f ? 1.0f / sm[v] : 0.0f;
           o = make_float4(o.x * inv, o.y * inv, o.z * inv, o.w * inv);
         }
@@ -234,7 +234,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_fixup(GatArgs a) {
       sm = sm * f1 + cl * f2;
       mx = mn;
     }
-    const float inv = sm > 0.0f ? 1.0f / sm : 0.0f;
+    const float inv = a.raw ? 1.0f : (sm > 0.0f ? 1.0f / sm : 0.0f);
     st4g(a.out + r * a.F + 4 * f4, make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv));
     if ((4 * f4) % a.D == 0) {
       a.m[r * H + h] = mx;
@@ -272,14 +272,6 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_dst(GatArgs a) {
     lead[v] = ok4[v] && ((4 * f4) % D == 0);
   }
   const float4 Z = make_float4(0.f, 0.f, 0.f, 0.f);
-  auto zero_row = [&](int64_t r) {
-#pragma unroll
-    for (int v = 0; v < NV; ++v)
-      if (lead[v]) {
-        a.g_er[r * H + hd[v]] = 0.0f;
-        a.stats[r * H + hd[v]] = make_float4(a.er[r * H + hd[v]], 0.f, 0.f, 0.f);
-      }
-  };
   float4 gov[NV];
   float erv[NV], mv[NV], linv[NV], dlt[NV], acc[NV];
   // per-row state: grad_out slice, er, m, 1/l, delta = <grad_out, out> per head
@@ -304,9 +296,26 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_dst(GatArgs a) {
       if (is_cont) {
         a.carry[chunk * H + hd[v]] = acc[v];
       } else {
-        a.g_er[r * H + hd[v]] = acc[v];
-        a.stats[r * H + hd[v]] = make_float4(erv[v], mv[v], linv[v], dlt[v]);
+        float* ge = a.g_er + r * H + hd[v];
+        *ge = a.accumulate ? *ge + acc[v] : acc[v];
+        if (!a.skip_stats) a.stats[r * H + hd[v]] = make_float4(erv[v], mv[v], linv[v], dlt[v]);
       }
+    }
+  };
+  // a row without edges (in this launch): no gradient; its stats are the row's own
+  // forward values (m = l = 0 and delta = 0 for a row without any in-edge), so the
+  // source-side walk of a column-blocked backward reads them for every row
+  auto zero_row = [&](int64_t r) {
+    if (!a.skip_stats) {
+      load_row(r);
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+        if (lead[v]) a.stats[r * H + hd[v]] = make_float4(erv[v], mv[v], linv[v], dlt[v]);
+    }
+    if (!a.accumulate) {
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+        if (lead[v]) a.g_er[r * H + hd[v]] = 0.0f;
     }
   };
   int64_t cur = a.rows[p0];
@@ -399,6 +408,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
   }
   const float4 Z = make_float4(0.f, 0.f, 0.f, 0.f);
   auto zero_row = [&](int64_t r) {
+    if (a.accumulate) return;  // nothing to add
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       if (ok4[v]) st4g(a.g_ft + r * a.F + 4 * (lane + v * L), Z);
@@ -423,9 +433,15 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
       if (!ok4[v]) continue;
       const int f4 = lane + v * L;
       float* dst = is_cont ? a.carry + chunk * CW : a.g_ft + r * a.F;
-      st4g(dst + 4 * f4, accf[v]);
+      float4 val = accf[v];
+      if (!is_cont && a.accumulate) {
+        const float4 o = ld4g(dst + 4 * f4);
+        val = make_float4(o.x + val.x, o.y + val.y, o.z + val.z, o.w + val.w);
+      }
+      st4g(dst + 4 * f4, val);
       if (lead[v]) {
         if (is_cont) a.carry[chunk * CW + a.F + hd[v]] = acce[v];
+        else if (a.accumulate) a.g_el[r * H + hd[v]] += acce[v];
         else a.g_el[r * H + hd[v]] = acce[v];
       }
     }
@@ -533,6 +549,46 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_fixup(GatArgs a, float* vec_
   }
 }
 
+// Merge the unnormalised per-block softmax partials of a column-blocked forward
+// (blocks in order; a block that saw no edge of the row has l = 0 and is skipped).
+__global__ void __launch_bounds__(kBlock) k_gat_merge(const float* __restrict__ out_part,
+                                                     const float* __restrict__ m_part,
+                                                     const float* __restrict__ l_part, int nb,
+                                                     int64_t num_rows, int H, int D,
+                                                     float* __restrict__ out, float* __restrict__ m,
+                                                     float* __restrict__ l) {
+  const int64_t F = static_cast<int64_t>(H) * D;
+  const int64_t F4 = F / 4;
+  const int64_t total = num_rows * F4;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int64_t r = i / F4;
+    const int f4 = static_cast<int>(i - r * F4);
+    const int h = (4 * f4) / D;
+    float mx = kNegInf, sm = 0.0f;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int b = 0; b < nb; ++b) {
+      const int64_t hi = (static_cast<int64_t>(b) * num_rows + r) * H + h;
+      const float lb = l_part[hi];
+      if (!(lb > 0.0f)) continue;
+      const float mb = m_part[hi];
+      const float4 ab = ld4g(out_part + (static_cast<int64_t>(b) * num_rows + r) * F + 4 * f4);
+      const float mn = fmaxf(mx, mb);
+      const float f1 = expf(mx - mn), f2 = expf(mb - mn);
+      acc = make_float4(acc.x * f1 + ab.x * f2, acc.y * f1 + ab.y * f2, acc.z * f1 + ab.z * f2,
+                        acc.w * f1 + ab.w * f2);
+      sm = sm * f1 + lb * f2;
+      mx = mn;
+    }
+    const float inv = sm > 0.0f ? 1.0f / sm : 0.0f;
+    st4g(out + r * F + 4 * f4, make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv));
+    if ((4 * f4) % D == 0) {
+      m[r * H + h] = sm > 0.0f ? mx : 0.0f;
+      l[r * H + h] = sm;
+    }
+  }
+}
+
 struct Cfg {
   int L, NV;
 };
@@ -606,6 +662,15 @@ bool gat_supported(int64_t H, int64_t D) {
 int64_t gat_chunk_edges(int64_t nnz) { return fast_chunk_edges(nnz, 64); }
 
 void launch_gat_forward(const GatArgs& a, hipStream_t s) { DGLMI_GAT_DISPATCH(fwd_cfg, a, s); }
+void launch_gat_merge(const float* out_part, const float* m_part, const float* l_part, int nb,
+                      int64_t num_rows, int H, int D, float* out, float* m, float* l, hipStream_t s) {
+  const int64_t total = num_rows * (static_cast<int64_t>(H) * D / 4);
+  if (total <= 0) return;
+  const int64_t want = (total + kBlock - 1) / kBlock;
+  const unsigned blocks = static_cast<unsigned>(want < 65536 ? want : 65536);
+  hipLaunchKernelGGL(k_gat_merge, dim3(blocks), dim3(kBlock), 0, s, out_part, m_part, l_part, nb,
+                     num_rows, H, D, out, m, l);
+}
 void launch_gat_backward_dst(const GatArgs& a, hipStream_t s) { DGLMI_GAT_DISPATCH(bwd_dst_cfg, a, s); }
 void launch_gat_backward_src(const GatArgs& a, hipStream_t s) { DGLMI_GAT_DISPATCH(bwd_src_cfg, a, s); }
 

@@ -44,6 +44,9 @@ class Graph(ctypes.Structure):
         ("coo_dst", ctypes.c_void_p),
         ("in_gather_cols", ctypes.c_void_p),
         ("out_gather_cols", ctypes.c_void_p),
+        ("num_col_blocks", ctypes.c_int32),
+        ("in_col_blocks", ctypes.c_void_p),
+        ("out_col_blocks", ctypes.c_void_p),
     ]
 
 

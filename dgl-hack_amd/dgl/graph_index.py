@@ -77,6 +77,7 @@ class ImmutableGraphIndex:
         self.eid_perm = eid_perm
         self._coo = None
         self._gather_cols = None
+        self._col_blocks = {}
 
     def number_of_edges(self):
         return self.in_csr.nnz
@@ -131,6 +132,38 @@ class ImmutableGraphIndex:
                 self._gather_cols = tuple(cols)
         return self._gather_cols
 
+    @staticmethod
+    def _split_by_column(csr, nb):
+        """``nb`` full-height CSRs holding csr's positions whose column lies in the
+        b-th of nb equal id ranges, positions in their original order (a stable
+        sort by block), built on the device."""
+        dev = csr.indices.device
+        n_rows = csr.num_rows
+        key = (csr.indices.long() * nb) // max(1, csr.num_cols)
+        order = th.argsort(key, stable=True)
+        counts = th.bincount(key, minlength=nb).tolist()
+        rows, cols, data = csr.rows[order], csr.indices[order], csr.data[order]
+        del order, key
+        out, start = [], 0
+        for b in range(nb):
+            end = start + counts[b]
+            r = rows[start:end]
+            indptr = th.zeros(n_rows + 1, dtype=th.int64, device=dev)
+            indptr[1:] = th.cumsum(th.bincount(r.long(), minlength=n_rows), 0)
+            out.append(DeviceCSR(indptr.to(th.int32), cols[start:end], data[start:end], r,
+                                 csr.num_cols))
+            start = end
+        return out
+
+    def col_blocks(self, nb):
+        """(in_blocks, out_blocks): the in-CSR split by source range and the
+        out-CSR by destination range into ``nb`` blocks each (DGLMIGraph
+        .{in,out}_col_blocks), built once per ``nb`` and cached."""
+        if nb not in self._col_blocks:
+            self._col_blocks[nb] = (self._split_by_column(self.in_csr, nb),
+                                    self._split_by_column(self.out_csr, nb))
+        return self._col_blocks[nb]
+
     def _cstruct_base(self):
         g = _ffi.Graph()
         g.in_csr = self.in_csr.cstruct()
@@ -141,8 +174,16 @@ class ImmutableGraphIndex:
         g.workspace_bytes = 0
         return g
 
-    def cstruct(self, workspace=None, coo=False):
+    def cstruct(self, workspace=None, coo=False, col_blocks=0):
         g = _ffi.Graph()
+        if col_blocks > 1:
+            ib, ob = self.col_blocks(col_blocks)
+            arr_i = (_ffi.CSR * col_blocks)(*[c.cstruct() for c in ib])
+            arr_o = (_ffi.CSR * col_blocks)(*[c.cstruct() for c in ob])
+            g._keep = (arr_i, arr_o)  # alive as long as the struct
+            g.num_col_blocks = col_blocks
+            g.in_col_blocks = ctypes.cast(arr_i, ctypes.c_void_p)
+            g.out_col_blocks = ctypes.cast(arr_o, ctypes.c_void_p)
         g.in_csr = self.in_csr.cstruct()
         g.out_csr = self.out_csr.cstruct()
         pair = self.coo() if coo else None

@@ -9,6 +9,7 @@ and overwritten completely, exactly like the reference's
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch as th
 
@@ -221,10 +222,36 @@ def fused_gat_supported(heads, head_dim):
     return bool(_ffi.lib().DGLMIFusedGatSupported(int(heads), int(head_dim)))
 
 
+def gat_col_blocks(graph, feat_src, backward=False):
+    """Column blocks for the fused GAT kernels (DGLMIGraph.num_col_blocks): when the
+    gathered ft + el table fits the Infinity Cache but not L2 (>= 32 MiB) and rows
+    are long (average in-degree >= 64, so merging per-block row partials is cheap),
+    cut the sources into blocks of 6-12 MiB of table each for the forward and twice
+    that for the backward, whose per-block row work (grad_out / out rows loaded,
+    gradient rows read-modified-written) is heavier (a power of two <= 16).
+    C3 (67 MB table; scripts/gat_probe.py, profiles/r01_gat_blocks.json): forward
+    5.65 ms whole / 4.54 (4 blocks) / 4.13 (8) / 4.53 (16); backward 11.98 /
+    10.63 (4) / 11.04 (8) / 12.61 (16).  DGLMI_GAT_BLOCKS overrides (1 = off)."""
+    env = os.environ.get("DGLMI_GAT_BLOCKS")
+    if env is not None:
+        return max(1, int(env))
+    n_src = feat_src.shape[0]
+    h = feat_src.shape[1] if feat_src.dim() == 3 else 1
+    table = n_src * (_feat_len(feat_src) + h) * 4
+    nnz, rows = graph.in_csr.nnz, max(1, graph.in_csr.num_rows)
+    if table < (32 << 20) or nnz < (1 << 22) or nnz < 64 * rows:
+        return 1
+    target = (12 << 20) if backward else (6 << 20)
+    nb = 1
+    while nb < 16 and table / (nb * 2) >= target:
+        nb *= 2
+    return nb
+
+
 def fused_gat_forward(graph, feat_src, el, er, slope, out, max_out, sum_out):
     """_CAPI_DGLFusedGatKernel (binary_reduce.cc:380-396) -> DGLMIFusedGatForward."""
     _check_ctx(graph, [("feat_src", feat_src), ("el", el), ("er", er), ("out", out)])
-    g = graph.cstruct(None)
+    g = graph.cstruct(None, col_blocks=gat_col_blocks(graph, feat_src))
     check_call(_ffi.lib().DGLMIFusedGatForward(
         ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"),
         float(slope), _arr(out, "out"), _arr(max_out, "max_out"), _arr(sum_out, "sum_out"),
@@ -236,7 +263,7 @@ def fused_gat_backward(graph, feat_src, el, er, slope, out, max_in, sum_in, grad
                        grad_feat_src, grad_el, grad_er):
     """_CAPI_DGLKernelBackwardFusedGat (binary_reduce.cc:529-549) -> DGLMIFusedGatBackward."""
     _check_ctx(graph, [("feat_src", feat_src), ("grad_out", grad_out)])
-    g = graph.cstruct(None)
+    g = graph.cstruct(None, col_blocks=gat_col_blocks(graph, feat_src, backward=True))
     check_call(_ffi.lib().DGLMIFusedGatBackward(
         ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"), float(slope),
         _arr(out, "out"), _arr(max_in, "max_in"), _arr(sum_in, "sum_in"),

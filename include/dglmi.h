@@ -87,6 +87,19 @@ typedef struct {
    * results).  Either may be NULL. */
   const int32_t* in_gather_cols;
   const int32_t* out_gather_cols;
+  /* Optional column blocks (extension, no reference counterpart): when
+   * num_col_blocks > 1, in_col_blocks[b] holds the positions of in_csr whose
+   * source lies in the b-th of num_col_blocks equal node-id ranges and
+   * out_col_blocks[b] the positions of out_csr whose destination lies in the
+   * b-th range -- each a full-height CSR (same num_rows / num_cols, rows keep
+   * their positions' original order, `data` = edge ids, `rows` required).  The
+   * fused GAT kernels then run one launch per block, so the rows gathered by a
+   * launch fit the 4 MiB per-XCD L2 better, and merge the per-block softmax
+   * partials (forward) or accumulate the gradients (backward) in block order.
+   * C3 (Reddit-size, 8 blocks): forward 5.54 -> ~4 ms.  NULL / 0 = off. */
+  int32_t num_col_blocks;
+  const DGLMICsr* in_col_blocks;
+  const DGLMICsr* out_col_blocks;
 } DGLMIGraph;
 
 /* A contiguous row-major fp32 device array (NDArray / DLTensor subset). */

@@ -22,7 +22,10 @@ from bench_configs import chung_lu  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--blocks", default=None, help="DGLMI_GAT_BLOCKS (default: automatic)")
     args = ap.parse_args()
+    if args.blocks is not None:
+        os.environ["DGLMI_GAT_BLOCKS"] = args.blocks
     dev = "cuda:0"
     n, m, H, D = 232965, 114615892, 8, 8
     g = chung_lu(n, m, 0.4, 3, dev)
@@ -37,7 +40,7 @@ def main():
     mx, sm = th.empty(n, H, device=dev), th.empty(n, H, device=dev)
     gft, gel, ger = th.empty_like(ft), th.empty_like(el), th.empty_like(er)
     th.cuda.synchronize()
-    res = {}
+    res = {"col_blocks": K.gat_col_blocks(gidx, ft)}
     for name, fn in (("fwd", lambda: K.fused_gat_forward(gidx, ft, el, er, 0.2, out, mx, sm)),
                      ("bwd", lambda: K.fused_gat_backward(gidx, ft, el, er, 0.2, out, mx, sm, go,
                                                           gft, gel, ger))):
