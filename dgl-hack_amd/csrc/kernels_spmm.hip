@@ -63,9 +63,13 @@ constexpr bool needs_eid() {
   return KIND != FAST_COPY_COL;
 }
 
-// Value of one edge for float4 slot f4 of the output row.
+// Value of one edge for float4 slot f4 of the output row.  `hs` (bcast kind):
+// the edge value's index for this slot, (4 * f4) / head_dim, and `wn` the edge
+// values per edge, F / head_dim -- both hoisted out of the edge loop by the
+// caller (64-bit divisions per edge cost 1.7 ms on the C5 typed gather).
 template <int KIND>
-__device__ __forceinline__ float4 edge_value(const FastArgs& a, int32_t col, int32_t eid, int f4) {
+__device__ __forceinline__ float4 edge_value(const FastArgs& a, int32_t col, int32_t eid, int f4,
+                                             int hs = 0, int64_t wn = 1) {
   if constexpr (KIND == FAST_COPY_COL) {
     const int64_t c = a.x_map ? a.x_map[col] : col;
     return ld4(a.x + c * a.F + 4 * f4);
@@ -81,9 +85,8 @@ __device__ __forceinline__ float4 edge_value(const FastArgs& a, int32_t col, int
   } else {
     const int64_t c = a.x_map ? a.x_map[col] : col;
     const int64_t e = a.w_map ? a.w_map[eid] : eid;
-    const int64_t H = a.F / a.head_dim;
     const float4 x = ld4(a.x + c * a.F + 4 * f4);
-    const float w = a.w[e * H + (4 * f4) / a.head_dim];
+    const float w = a.w[e * wn + hs];
     return make_float4(x.x * w, x.y * w, x.z * w, x.w * w);
   }
 }
@@ -156,6 +159,11 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
   const int64_t p1 = p0 + K < a.nnz ? p0 + K : a.nnz;
   const int F4 = static_cast<int>(a.F / 4);
   const float4 I = ident4<RED>();
+  int hsel[NV];  // bcast: edge value index of each float4 slot
+  const int64_t wn = KIND == FAST_COL_MUL_EDGE_BCAST ? a.F / a.head_dim : 1;
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+    hsel[v] = KIND == FAST_COL_MUL_EDGE_BCAST ? static_cast<int>((4 * (lane + v * L)) / a.head_dim) : 0;
 
   int64_t cur = a.rows[p0];
   bool cont = p0 > 0 && a.rows[p0 - 1] == cur;
@@ -205,7 +213,7 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
             const float* px = a.x + static_cast<int64_t>(col & 0x7fffffff) * a.F + 4 * f4;
             val[u][v] = (ok && f4 < F4) ? (nt ? ld4_nt(px) : ld4(px)) : I;
           } else {
-            val[u][v] = (ok && f4 < F4) ? edge_value<KIND>(a, col, eid, f4) : I;
+            val[u][v] = (ok && f4 < F4) ? edge_value<KIND>(a, col, eid, f4, hsel[v], wn) : I;
           }
         }
       }
@@ -346,8 +354,11 @@ __device__ __forceinline__ void store_row(float* __restrict__ p, const float (&v
   }
 }
 
+// `hidx` (bcast kind): edge value index of each of the F floats, i / head_dim, and
+// `wn` = F / head_dim values per edge, computed once per thread by the caller.
 template <int KIND, int F>
-__device__ __forceinline__ void lane_value(const FastArgs& a, int32_t col, int32_t eid, float (&v)[F]) {
+__device__ __forceinline__ void lane_value(const FastArgs& a, int32_t col, int32_t eid, float (&v)[F],
+                                           const int (&hidx)[F], int wn) {
   if constexpr (KIND == FAST_COPY_COL) {
     const int64_t c = a.x_map ? a.x_map[col] : col;
     load_row<F>(a.x + c * F, v);
@@ -365,10 +376,9 @@ __device__ __forceinline__ void lane_value(const FastArgs& a, int32_t col, int32
   } else {
     const int64_t c = a.x_map ? a.x_map[col] : col;
     const int64_t e = a.w_map ? a.w_map[eid] : eid;
-    const int64_t H = F / a.head_dim;
     load_row<F>(a.x + c * F, v);
 #pragma unroll
-    for (int i = 0; i < F; ++i) v[i] *= a.w[e * H + i / a.head_dim];
+    for (int i = 0; i < F; ++i) v[i] *= a.w[e * wn + hidx[i]];
   }
 }
 
@@ -401,6 +411,11 @@ __global__ void __launch_bounds__(kBlock) k_lane_reduce(FastArgs a) {
   float ident[F];
 #pragma unroll
   for (int i = 0; i < F; ++i) ident[i] = I;
+  int hidx[F];
+  const int hd = KIND == FAST_COL_MUL_EDGE_BCAST ? static_cast<int>(a.head_dim) : 1;
+#pragma unroll
+  for (int i = 0; i < F; ++i) hidx[i] = i / hd;
+  const int wn = F / hd;
   auto put_gap = [&](int64_t r) {
     float t[F];
 #pragma unroll
@@ -443,7 +458,7 @@ __global__ void __launch_bounds__(kBlock) k_lane_reduce(FastArgs a) {
     float v[U][F];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (r[u] != INT_MAX) lane_value<KIND, F>(a, c[u], needs_eid<KIND>() ? e[u] : 0, v[u]);
+      if (r[u] != INT_MAX) lane_value<KIND, F>(a, c[u], needs_eid<KIND>() ? e[u] : 0, v[u], hidx, wn);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {

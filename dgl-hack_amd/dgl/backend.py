@@ -369,7 +369,12 @@ def _typed_aggregate(graph, num_rels, y, norm, etypes, node_major=False):
     n = graph.number_of_nodes()
     if norm is None:
         return copy_reduce("sum", gidx, SRC, y, n)
-    return binary_reduce("sum", "mul", gidx, SRC, EDGE, y, norm.reshape(norm.shape[0], 1), n)
+    w = norm.reshape(norm.shape[0], 1)
+    if not w.requires_grad and w.is_cuda and gidx.eid_perm:
+        # constant norm: streamed in in-CSR position order (cached permuted copy)
+        pv, w_pos = gidx.position_operand(w)
+        return binary_reduce("sum", "mul", pv, SRC, EDGE, y, w_pos, n)
+    return binary_reduce("sum", "mul", gidx, SRC, EDGE, y, w, n)
 
 
 def rgcn_layer0(graph, weight, norm, etypes=None):

@@ -29,14 +29,29 @@ def big():
     return n, src, dst, x
 
 
-def _graph(n, src, dst, hot):
+def _graph(n, src, dst, hot, max_cold=1.0):
+    """The graph with hints at threshold `hot` (0 = none); the cold-share rule is
+    relaxed so the marked path is exercised whatever the fixture's share."""
     os.environ["DGLMI_HOT_DEGREE"] = str(hot)
+    g = device_block_gidx(n, n, src, dst)
+    g.MAX_COLD_SHARE = max_cold
     try:
-        g = device_block_gidx(n, n, src, dst)
         g.gather_cols()
     finally:
         os.environ.pop("DGLMI_HOT_DEGREE", None)
     return g
+
+
+def test_mostly_cold_graph_gets_no_hints():
+    """Uniform sources (every row gathered ~6 times): no hot set to protect, so
+    the default rule (cold share <= 0.5) leaves the hints off."""
+    n, m = 1 << 20, 6_000_000
+    gen = th.Generator(device=DEV)
+    gen.manual_seed(3)
+    src = th.randint(0, n, (m,), device=DEV, generator=gen, dtype=th.int32)
+    dst = th.randint(0, n, (m,), device=DEV, generator=gen, dtype=th.int32)
+    g = device_block_gidx(n, n, src, dst)
+    assert g.gather_cols() == (None, None)
 
 
 def test_hints_built_and_marked(big):
@@ -78,7 +93,9 @@ def test_hinted_forward_backward_bit_identical(big):
     assert bool(((out.double() - ref).abs() <= 1e-4 + 1e-6 * mass).all())
 
 
-def test_dglgraph_update_all_uses_hints(big):
+def test_dglgraph_update_all_uses_hints(big, monkeypatch):
+    from dgl.graph_index import ImmutableGraphIndex
+    monkeypatch.setattr(ImmutableGraphIndex, "MAX_COLD_SHARE", 1.0)
     n, src, dst, x = big
     g = dgl.DGLGraph.from_device_coo(src, dst, n)
     g.ndata["h"] = x

@@ -107,3 +107,32 @@ def test_relgraphconv(reg, bases, ids, loop):
     ref.pow(2).sum().backward()
     for a, p in zip(grads, conv.parameters()):
         assert th.allclose(a, p.grad, rtol=1e-3, atol=1e-2)
+
+
+def test_constant_norm_position_cache_follows_the_tensor():
+    """A constant norm is streamed from a cached copy in in-CSR position order
+    (ImmutableGraphIndex.position_operand); an in-place update or another tensor
+    must not reuse a stale copy, and a norm that needs a gradient takes the
+    edge-id path."""
+    g, src, dst, et, n = typed_graph(seed=4)
+    R, fin, fout = 4, 8, 8
+    x = th.randn(n, fin, device=DEV)
+    W = th.randn(R, fin, fout, device=DEV)
+    norm = th.rand(len(src), 1, device=DEV)
+    a = B.rgcn_layer1(g, x, W, norm)
+    norm.mul_(2.0)
+    b = B.rgcn_layer1(g, x, W, norm)
+    assert th.allclose(b, 2 * a, rtol=1e-5, atol=1e-5)
+    c = B.rgcn_layer1(g, x, W, norm / 2)
+    assert th.allclose(c, a, rtol=1e-5, atol=1e-5)
+    # a temporary norm per call (freed in between, so the allocator may hand the
+    # next one the same address) must never hit a stale cached copy
+    outs = [B.rgcn_layer1(g, x, W, th.full((len(src), 1), float(k), device=DEV))
+            for k in (1, 2, 3)]
+    assert th.allclose(outs[1], 2 * outs[0], rtol=1e-5, atol=1e-5)
+    assert th.allclose(outs[2], 3 * outs[0], rtol=1e-4, atol=1e-4)  # x3 rounds
+    ng = norm.clone().requires_grad_()
+    d = B.rgcn_layer1(g, x, W, ng)
+    assert th.equal(d, b)
+    (gn,) = th.autograd.grad(d.sum(), (ng,))
+    assert gn.shape == ng.shape
