@@ -137,6 +137,24 @@ class Partition:
             self._dev[key] = th.from_numpy(self.send_idx).to(device)
         return self._dev[key]
 
+    def local_graph(self, device):
+        """The local block as a DGLGraph over ``n_inner + n_halo`` nodes (owned
+        rows first; only they have in-edges), local edge k = global edge
+        ``parent_eid[k]`` -- what a whole-graph module (GATConv, RelGraphConv)
+        runs on once the halo rows are present."""
+        key = ("g", str(device))
+        if key not in self._dev:
+            from .graph import DGLGraph
+            t = lambda a: th.from_numpy(np.ascontiguousarray(a, np.int32)).to(device)
+            self._dev[key] = DGLGraph.from_device_coo(t(self.local_src), t(self.local_dst),
+                                                      self.n_inner + self.n_halo)
+        return self._dev[key]
+
+    def local_edge_data(self, edge_data):
+        """Rows of a global per-edge tensor for the local edges (in local order)."""
+        idx = th.from_numpy(self.parent_eid).to(edge_data.device)
+        return edge_data.index_select(0, idx)
+
 
 def build_partitions(src, dst, num_nodes, assign, parts=None, num_parts=None):
     """Halo subgraphs of every (or the listed) partition, from the global edge list."""
@@ -227,6 +245,22 @@ class DevicePartition:
     def release_edges(self):
         self.gidx()
         self.local_src = self.local_dst = None
+
+    def local_graph(self, device=None):
+        """The local block as a DGLGraph over ``n_inner + n_halo`` nodes (see
+        :meth:`Partition.local_graph`); local edge k is the k-th in-edge passed to
+        :func:`build_device_partition`."""
+        if getattr(self, "_lg", None) is None:
+            from .graph import DGLGraph
+            if self.local_src is None:
+                raise DGLError("local_graph() needs the edge list (call it before release_edges)")
+            self._lg = DGLGraph.from_device_coo(self.local_src, self.local_dst,
+                                                self.n_inner + self.n_halo)
+        return self._lg
+
+    def local_edge_data(self, edge_data):
+        """Per-edge data of the local edges: already in local order (the caller's)."""
+        return edge_data
 
     def split_gidx(self):
         """(owned-source block, halo-source block) of the local in-edges -- the two
@@ -452,4 +486,92 @@ class DistGraphConv(th.nn.Module):
                 rst = rst + conv.bias
         if conv._activation is not None:
             rst = conv._activation(rst)
+        return rst
+
+
+# --------------------------------------------------------------------------- #
+# partitioned GATConv / RelGraphConv: the whole-graph module on the local block
+# --------------------------------------------------------------------------- #
+class DistGATConv(th.nn.Module):
+    """GATConv on a halo partition (``gatconv.py:103-171``).  The projection and
+    the attention terms el / er are computed for the OWNED rows only; ft and el
+    of the halo sources arrive with one all-to-all-v (packed as one (H*D + H)
+    row per node), er stays local (destinations are owned), and the fused GAT
+    kernel runs on the local block.  Backward: the reverse all-to-all-v returns
+    the halo rows' gradients to their owners (:class:`HaloExchange`); weight
+    gradients need :func:`allreduce_gradients`."""
+
+    def __init__(self, in_feats, out_feats, num_heads, negative_slope=0.2, residual=False,
+                 activation=None):
+        super().__init__()
+        from .nn.pytorch import GATConv
+        self.conv = GATConv(in_feats, out_feats, num_heads, negative_slope=negative_slope,
+                            residual=residual, activation=activation)
+
+    def forward(self, part, feat, group=None):
+        """feat: (n_inner, in_feats) rows of the owned nodes -> (n_inner, H, D)."""
+        from . import backend as B
+        c = self.conv
+        H, D = c._num_heads, c._out_feats
+        ft = B.project(feat, c.fc.weight.t()).view(-1, H, D)
+        el = (ft * c.attn_l).sum(dim=-1)
+        er = (ft * c.attn_r).sum(dim=-1).unsqueeze(-1)
+        full = halo_exchange(th.cat([ft.reshape(-1, H * D), el], 1), part, group)
+        ft_full = full[:, :H * D].reshape(-1, H, D)
+        el_full = full[:, H * D:].reshape(-1, H, 1)
+        gidx = part.gidx(feat.device)
+        if c._fused_ok():
+            rst = B.fused_gat(gidx, ft_full.contiguous(), el_full.contiguous(), er,
+                              c.negative_slope)
+        else:
+            g = part.local_graph(feat.device).local_var()
+            n = g.number_of_nodes()
+            pad = lambda t: th.cat([t, t.new_zeros((n - t.shape[0],) + tuple(t.shape[1:]))])
+            g.srcdata.update({"ft": ft_full, "el": el_full})
+            g.dstdata.update({"er": pad(er)})
+            from . import function as fn
+            from .nn.pytorch import edge_softmax
+            g.apply_edges(fn.u_add_v("el", "er", "e"))
+            e = c.leaky_relu(g.edata.pop("e"))
+            g.edata["a"] = c.attn_drop(edge_softmax(g, e))
+            g.update_all(fn.u_mul_e("ft", "a", "m"), fn.sum("m", "ft"))
+            rst = g.dstdata["ft"][:part.n_inner]
+        if c.res_fc is not None:
+            rst = rst + c.res_fc(feat).view(feat.shape[0], -1, D)
+        if c.activation:
+            rst = c.activation(rst)
+        return rst
+
+
+class DistRelGraphConv(th.nn.Module):
+    """RelGraphConv on a halo partition (``relgraphconv.py``).  The input rows of
+    the halo sources arrive with one all-to-all-v (the narrower of x and the
+    relation transforms is exchanged: x, then the (N, R * out) GEMM over owned +
+    halo rows), and the typed gather runs on the local block; the self-loop and
+    bias use the owned rows.  ``etypes`` / ``norm`` are per LOCAL edge
+    (:meth:`Partition.local_edge_data` slices global ones)."""
+
+    def __init__(self, in_feat, out_feat, num_rels, regularizer="basis", num_bases=None,
+                 bias=True, activation=None, self_loop=False):
+        super().__init__()
+        from .nn.pytorch import RelGraphConv
+        self.conv = RelGraphConv(in_feat, out_feat, num_rels, regularizer, num_bases, bias=bias,
+                                 activation=activation, self_loop=self_loop)
+
+    def forward(self, part, feat, etypes, norm=None, group=None):
+        from . import backend as B
+        c = self.conv
+        g = part.local_graph(feat.device)
+        x_full = halo_exchange(feat, part, group)
+        y, node_major = c._transform(x_full)
+        n = g.number_of_nodes()
+        rst = B._typed_aggregate(g, c.num_rels, y.contiguous().view(c.num_rels * n, c.out_feat),
+                                 norm, etypes, node_major)[:part.n_inner]
+        if c.bias:
+            rst = rst + c.h_bias
+        if c.self_loop:
+            ids = feat.dtype == th.int64 and feat.dim() == 1
+            rst = rst + (c.loop_weight[feat] if ids else B.project(feat, c.loop_weight))
+        if c.activation:
+            rst = c.activation(rst)
         return rst
