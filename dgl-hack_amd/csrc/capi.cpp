@@ -221,6 +221,24 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 
 // Scratch for the load-balanced path: the caller's workspace, or a
 // stream-ordered allocation released on the same stream.
+// Keep stream-ordered scratch in the device's default pool between calls: with
+// the default release threshold (0) every synchronisation hands the pool's
+// memory back and the next call maps it again (hundreds of MB for the blocked
+// GAT partials).  The engine's own allocations are the only users of the pool
+// (torch has its caching allocator), so the pool's size stays at the largest
+// scratch a call needed.
+void keep_pool_memory() {
+  static bool done[64] = {false};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || done[dev]) return;
+  hipMemPool_t pool;
+  if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+    uint64_t thr = UINT64_MAX;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+  }
+  done[dev] = true;
+}
+
 struct Scratch {
   void* ptr = nullptr;
   bool owned = false;
@@ -230,6 +248,7 @@ struct Scratch {
     if (g->workspace != nullptr && g->workspace_bytes >= bytes) {
       ptr = g->workspace;
     } else {
+      keep_pool_memory();
       check_hip(hipMallocAsync(&ptr, static_cast<size_t>(bytes), stream), "hipMallocAsync");
       owned = true;
     }
@@ -243,7 +262,68 @@ struct Scratch {
 // rows own the output; out has `walk.num_rows` rows of F floats.
 void run_fast(const DGLMIGraph* g, const DGLMICsr& walk, int kind, int red, const float* x,
               const int32_t* x_map, const float* w, const int32_t* w_map, float* out, int64_t F,
-              int64_t head_dim, hipStream_t s, const DGLMIEpilogue* epi = nullptr) {
+              int64_t head_dim, hipStream_t s, const DGLMIEpilogue* epi = nullptr);
+
+// Column blocks (DGLMIGraph.num_col_blocks) on the load-balanced sum: one pass
+// per non-empty block, so a pass gathers from a slice of the table that fits the
+// 4 MiB per-XCD L2; the partial sums chain through the epilogue's addend
+// (ping-pong between `out` and a scratch buffer, the last pass lands in `out`).
+// Every pass applies row_mul / row_div to its own sum (sum_b acc_b * m / d ==
+// (sum_b acc_b) * m / d up to rounding); the caller's addend enters with the
+// first pass, the bias with the last.  Block order is fixed: deterministic.
+void run_fast_blocked(const DGLMIGraph* g, const DGLMICsr* blocks, const DGLMICsr& walk, int kind,
+                      const float* x, const float* w, const int32_t* w_map, float* out, int64_t F,
+                      int64_t head_dim, hipStream_t s, const DGLMIEpilogue* epi) {
+  std::vector<int> nz;
+  for (int b = 0; b < g->num_col_blocks; ++b) {
+    DGLMI_CHECK(blocks[b].num_rows == walk.num_rows && blocks[b].indptr != nullptr,
+                "column blocks must keep the graph's rows");
+    if (blocks[b].nnz > 0) nz.push_back(b);
+  }
+  DGLMIGraph plain = *g;  // no blocks / hints for the per-block passes
+  plain.num_col_blocks = 0;
+  plain.in_col_blocks = plain.out_col_blocks = nullptr;
+  plain.in_gather_cols = plain.out_gather_cols = nullptr;
+  if (nz.size() <= 1) {
+    run_fast(&plain, nz.empty() ? walk : blocks[nz[0]], kind, RED_SUM, x, nullptr, w, w_map, out, F,
+             head_dim, s, epi);
+    return;
+  }
+  DGLMIGraph no_ws;  // the ping-pong buffer must not alias the carry workspace
+  std::memset(&no_ws, 0, sizeof(no_ws));
+  Scratch tmp(&no_ws, walk.num_rows * F * static_cast<int64_t>(sizeof(float)), s);
+  float* bufs[2] = {out, static_cast<float*>(tmp.ptr)};
+  const int k = static_cast<int>(nz.size());
+  const float* prev = epi ? epi->addend : nullptr;
+  for (int i = 0; i < k; ++i) {
+    float* dst = bufs[(k - 1 - i) % 2];
+    DGLMIEpilogue e;
+    e.row_mul = epi ? epi->row_mul : nullptr;
+    e.row_div = epi ? epi->row_div : nullptr;
+    e.bias = (epi && i == k - 1) ? epi->bias : nullptr;
+    e.addend = prev;
+    const bool any = e.row_mul || e.row_div || e.bias || e.addend;
+    run_fast(&plain, blocks[nz[i]], kind, RED_SUM, x, nullptr, w, w_map, dst, F, head_dim, s,
+             any ? &e : nullptr);
+    prev = dst;
+  }
+}
+
+void run_fast(const DGLMIGraph* g, const DGLMICsr& walk, int kind, int red, const float* x,
+              const int32_t* x_map, const float* w, const int32_t* w_map, float* out, int64_t F,
+              int64_t head_dim, hipStream_t s, const DGLMIEpilogue* epi) {
+  // copy_u only: with an edge operand (u_mul_e) its per-edge gather by edge id
+  // dominates and extra passes cost more than the smaller table saves (Reddit-size,
+  // F = 64: copy_u_sum 3.88 -> 2.96 ms over 8 blocks, u_mul_e_sum 5.94 -> 7.23 ms)
+  if (g->num_col_blocks > 1 && red == RED_SUM && x_map == nullptr && walk.nnz > 0 &&
+      kind == FAST_COPY_COL) {
+    const DGLMICsr* blocks = &walk == &g->in_csr ? g->in_col_blocks
+                             : (&walk == &g->out_csr ? g->out_col_blocks : nullptr);
+    if (blocks != nullptr) {
+      run_fast_blocked(g, blocks, walk, kind, x, w, w_map, out, F, head_dim, s, epi);
+      return;
+    }
+  }
   if (walk.nnz == 0) {
     launch_fill(out, walk.num_rows * F, identity_of(red), s);
     if (epi) launch_epilogue(out, walk.num_rows, F, epi->row_mul, epi->row_div, epi->bias, epi->addend, s);

@@ -67,9 +67,33 @@ def _workspace(graph, feat_len, device):
     return th.empty(int(nbytes), dtype=th.uint8, device=device)
 
 
-def _cgraph(graph, ws, per_edge):
-    """Graph struct for a call; per-edge outputs also get the edge-id ordered COO."""
-    return graph.cstruct(ws, coo=per_edge)
+def spmm_col_blocks(graph, feat_len):
+    """Column blocks for the load-balanced sums (DGLMIGraph.num_col_blocks): when
+    the gathered node table fits the Infinity Cache but not L2 (32-256 MiB) and
+    rows are long (average in-degree >= 64, so chaining per-block partial sums is
+    cheap), one pass per block of ~8 MiB of table (a power of two <= 32).
+    Reddit-size graph (114.6 M edges; scripts/spmm_block_probe.py,
+    profiles/r01_spmm_blocks.json), chained passes included: copy_u_sum F = 64
+    3.88 -> 2.96 ms (8 blocks), F = 128 7.99 -> 4.70 ms (16 blocks).  The library
+    applies them to copy_u sums only.  DGLMI_SPMM_BLOCKS overrides (1 = off)."""
+    env = os.environ.get("DGLMI_SPMM_BLOCKS")
+    if env is not None:
+        return max(1, int(env))
+    ic = graph.in_csr
+    table = ic.num_cols * feat_len * 4
+    if not ((32 << 20) <= table < (256 << 20)) or ic.nnz < (1 << 22) or ic.nnz < 64 * max(1, ic.num_rows):
+        return 1
+    nb = 1
+    while nb < 32 and table / nb > (8 << 20):
+        nb *= 2
+    return nb
+
+
+def _cgraph(graph, ws, per_edge, feat_len=0):
+    """Graph struct for a call; per-edge outputs also get the edge-id ordered COO;
+    reductions over a large-degree graph get its column blocks."""
+    nb = spmm_col_blocks(graph, feat_len) if feat_len and not per_edge else 1
+    return graph.cstruct(ws, coo=per_edge, col_blocks=nb)
 
 
 def _feat_len(t):
@@ -133,7 +157,7 @@ def binary_op_reduce(reducer, op, graph, lhs, rhs, lhs_data, rhs_data, out_data,
     (row_mul, row_div, bias) fused into a "sum" reduction (DGLMIKernelBinaryOpReduceEx)."""
     _check_ctx(graph, [("lhs_data", lhs_data), ("rhs_data", rhs_data), ("out_data", out_data)])
     ws = _workspace(graph, _feat_len(out_data), out_data.device)
-    g = _cgraph(graph, ws, reducer == "none")
+    g = _cgraph(graph, ws, reducer == "none", _feat_len(out_data))
     epi = _epilogue(epilogue, out_data)
     args = (reducer.encode(), op.encode(), ctypes.byref(g), _TARGET_CODE(lhs), _TARGET_CODE(rhs),
             _arr(lhs_data, "lhs_data"), _arr(rhs_data, "rhs_data"), _arr(out_data, "out_data"),
@@ -154,7 +178,7 @@ def backward_lhs_binary_op_reduce(reducer, op, graph, lhs, rhs, lhs_data, rhs_da
     _check_ctx(graph, [("lhs_data", lhs_data), ("rhs_data", rhs_data), ("out_data", out_data),
                        ("grad_out_data", grad_out_data), ("grad_lhs_data", grad_lhs_data)])
     ws = _workspace(graph, _feat_len(grad_lhs_data), grad_lhs_data.device)
-    g = _cgraph(graph, ws, _TARGET_CODE(lhs) == 2)
+    g = _cgraph(graph, ws, _TARGET_CODE(lhs) == 2, _feat_len(grad_lhs_data))
     check_call(_ffi.lib().DGLMIKernelBackwardLhsBinaryOpReduce(
         reducer.encode(), op.encode(), ctypes.byref(g), _TARGET_CODE(lhs), _TARGET_CODE(rhs),
         _map(lhs_map, "lhs_mapping"), _map(rhs_map, "rhs_mapping"), _map(out_map, "out_mapping"),
@@ -171,7 +195,7 @@ def backward_rhs_binary_op_reduce(reducer, op, graph, lhs, rhs, lhs_data, rhs_da
     _check_ctx(graph, [("lhs_data", lhs_data), ("rhs_data", rhs_data), ("out_data", out_data),
                        ("grad_out_data", grad_out_data), ("grad_rhs_data", grad_rhs_data)])
     ws = _workspace(graph, _feat_len(grad_rhs_data), grad_rhs_data.device)
-    g = _cgraph(graph, ws, _TARGET_CODE(rhs) == 2)
+    g = _cgraph(graph, ws, _TARGET_CODE(rhs) == 2, _feat_len(grad_rhs_data))
     check_call(_ffi.lib().DGLMIKernelBackwardRhsBinaryOpReduce(
         reducer.encode(), op.encode(), ctypes.byref(g), _TARGET_CODE(lhs), _TARGET_CODE(rhs),
         _map(lhs_map, "lhs_mapping"), _map(rhs_map, "rhs_mapping"), _map(out_map, "out_mapping"),
@@ -186,7 +210,7 @@ def copy_reduce(reducer, graph, target, in_data, out_data, in_map=None, out_map=
     """kernel.py:302-393 -> _CAPI_DGLKernelCopyReduce (``epilogue``: see binary_op_reduce)."""
     _check_ctx(graph, [("in_data", in_data), ("out_data", out_data)])
     ws = _workspace(graph, _feat_len(out_data), out_data.device)
-    g = _cgraph(graph, ws, reducer == "none")
+    g = _cgraph(graph, ws, reducer == "none", _feat_len(out_data))
     epi = _epilogue(epilogue, out_data)
     args = (reducer.encode(), ctypes.byref(g), _TARGET_CODE(target), _arr(in_data, "in_data"),
             _arr(out_data, "out_data"), _map(in_map, "in_mapping"), _map(out_map, "out_mapping"))
@@ -203,7 +227,7 @@ def backward_copy_reduce(reducer, graph, target, in_data, out_data, grad_out_dat
     _check_ctx(graph, [("in_data", in_data), ("out_data", out_data),
                        ("grad_out_data", grad_out_data), ("grad_in_data", grad_in_data)])
     ws = _workspace(graph, _feat_len(grad_in_data), grad_in_data.device)
-    g = _cgraph(graph, ws, _TARGET_CODE(target) == 2)
+    g = _cgraph(graph, ws, _TARGET_CODE(target) == 2, _feat_len(grad_in_data))
     check_call(_ffi.lib().DGLMIKernelBackwardCopyReduce(
         reducer.encode(), ctypes.byref(g), _TARGET_CODE(target), _arr(in_data, "in_data"),
         _arr(out_data, "out_data"), _arr(grad_out_data, "grad_out_data"),
