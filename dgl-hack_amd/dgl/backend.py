@@ -267,6 +267,10 @@ class _Project(th.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
+        # a loss like out.sum() hands back an expanded (stride-0) gradient; torch's
+        # column sum over such a view took 0.5 ms for 169 343 x 128 (C2 trace)
+        # against ~30 us for one dense copy + a dense sum
+        gy = gy.contiguous()
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
             gx = th.matmul(gy, w.t())

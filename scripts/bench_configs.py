@@ -112,9 +112,30 @@ def c2(dev, steps, warmup):
         conv(g, x).sum().backward()
     ms = timeit(layer, steps, warmup)
     alg = 4 * (n + 1) + 4 * m + 4 * f * m + 4 * f * n
-    return {"config": "C2 arxiv-size GraphConv 128->128", "nodes": n, "edges": m,
-            "copy_u_sum_ms": ms_spmm, "copy_u_sum_alg_GBps": alg / ms_spmm / 1e6,
-            "copy_u_sum_Gedges_s": m / ms_spmm / 1e6, "layer_fwd_bwd_ms": ms}
+    res = {"config": "C2 arxiv-size GraphConv 128->128", "nodes": n, "edges": m,
+           "copy_u_sum_ms": ms_spmm, "copy_u_sum_alg_GBps": alg / ms_spmm / 1e6,
+           "copy_u_sum_Gedges_s": m / ms_spmm / 1e6, "layer_fwd_bwd_ms": ms}
+    # the same layer step captured into a HIP graph: ~20 launches of 5-100 us each,
+    # so the eager number carries the launch + Python overhead
+    try:
+        conv2 = GraphConv(f, f).to(dev)
+        xg = th.randn(n, f, device=dev, requires_grad=True)
+
+        def gstep():
+            conv2(g, xg).sum().backward()
+        st = th.cuda.Stream()
+        st.wait_stream(th.cuda.current_stream())
+        with th.cuda.stream(st):
+            for _ in range(3):
+                gstep()
+        th.cuda.current_stream().wait_stream(st)
+        graph = th.cuda.CUDAGraph()
+        with th.cuda.graph(graph):
+            gstep()
+        res["layer_fwd_bwd_hipgraph_ms"] = timeit(graph.replay, steps * 5, warmup)
+    except Exception as exc:  # report, keep the eager number
+        res["hipgraph_error"] = repr(exc)[:300]
+    return res
 
 
 def c3(dev, steps, warmup):
