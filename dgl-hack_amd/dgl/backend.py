@@ -365,20 +365,61 @@ def fused_gat(graph, feat_src, el, er, slope):
 # R-GCN (hack: RgcnFirstLayer / RgcnSecondLayer, tensor.py:440-495;
 # kernels binary_reduce_impl.cu:913-1246)
 # --------------------------------------------------------------------------- #
-def _typed_aggregate(graph, num_rels, y, norm, etypes, node_major=False):
+class _TypedAggregate(th.autograd.Function):
+    """out[v] = sum_e w_e * y[src_e] (+ bias + addend) on the relation-expanded
+    graph with a CONSTANT per-edge weight w: the forward walks the in-CSR with w
+    in in-CSR position order, the gradient of y walks the out-CSR with w in
+    out-CSR position order (both streamed, both cached), and RelGraphConv's bias
+    and self-loop term ride in the kernel epilogue instead of two extra passes
+    over the output."""
+
+    @staticmethod
+    def forward(ctx, gidx, y, w, bias, addend, n):
+        vin, w_in = gidx.position_operand(w, "in")
+        out = y.new_empty((n, y.shape[1]))
+        epi = None if bias is None and addend is None else (None, None, bias, addend)
+        K.binary_op_reduce("sum", "mul", vin, SRC, EDGE, y, w_in, out, epilogue=epi)
+        ctx.gidx, ctx.w = gidx, w
+        ctx.has_bias, ctx.has_addend = bias is not None, addend is not None
+        ctx.save_for_backward(y, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        y, out = ctx.saved_tensors
+        g = grad_out.contiguous()
+        gy = gb = ga = None
+        if ctx.needs_input_grad[1]:
+            vout, w_out = ctx.gidx.position_operand(ctx.w, "out")
+            gy = th.empty_like(y)
+            K.backward_lhs_binary_op_reduce("sum", "mul", vout, SRC, EDGE, y, w_out, out, g, gy)
+        if ctx.has_bias and ctx.needs_input_grad[3]:
+            gb = g.sum(0)
+        if ctx.has_addend and ctx.needs_input_grad[4]:
+            ga = g
+        return None, gy, None, gb, ga, None
+
+
+def _typed_aggregate(graph, num_rels, y, norm, etypes, node_major=False, bias=None,
+                     addend=None):
     """out[v] = sum_{e=(u->v)} norm_e * y[type_e * N + u] (or y[u * R + type_e] with
     ``node_major``): every relation in ONE load-balanced gather over the
     relation-expanded graph (no per-relation SpMMs, no per-edge weight products)."""
     gidx = graph._graph.typed_gidx(y.device, num_rels, etypes, node_major)
     n = graph.number_of_nodes()
-    if norm is None:
-        return copy_reduce("sum", gidx, SRC, y, n)
-    w = norm.reshape(norm.shape[0], 1)
-    if not w.requires_grad and w.is_cuda and gidx.eid_perm:
-        # constant norm: streamed in in-CSR position order (cached permuted copy)
-        pv, w_pos = gidx.position_operand(w)
-        return binary_reduce("sum", "mul", pv, SRC, EDGE, y, w_pos, n)
-    return binary_reduce("sum", "mul", gidx, SRC, EDGE, y, w, n)
+    if norm is not None:
+        w = norm.reshape(norm.shape[0], 1)
+        if not w.requires_grad and w.is_cuda and gidx.eid_perm and y.dim() == 2:
+            # constant norm: streamed in walk order, bias / addend in the epilogue
+            return _TypedAggregate.apply(gidx, y, w, bias, addend, n)
+        out = binary_reduce("sum", "mul", gidx, SRC, EDGE, y, w, n)
+    else:
+        out = copy_reduce("sum", gidx, SRC, y, n)
+    if bias is not None:
+        out = out + bias
+    if addend is not None:
+        out = out + addend
+    return out
 
 
 def rgcn_layer0(graph, weight, norm, etypes=None):

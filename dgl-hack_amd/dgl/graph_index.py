@@ -160,30 +160,39 @@ class ImmutableGraphIndex:
             start = end
         return out
 
-    def position_operand(self, w):
-        """(view, w_pos): a view of this graph whose edge ids are the in-CSR
-        positions, and the per-edge operand ``w`` permuted into that order, so a
-        reduction over the in-CSR streams it instead of gathering it by edge id
-        (C5 typed gather 6.57 -> 5.60 ms, bit-identical; scripts/typed_probe.py).
-        For constant operands (R-GCN's norm): the permuted copy is cached for the
-        last (tensor, version) seen."""
+    def position_operand(self, w, direction="in"):
+        """(view, w_pos): a view of this graph whose edge ids are the positions of
+        its in-CSR (``direction="in"``, for reductions to destinations) or of its
+        out-CSR (``"out"``, for source-side gradients), and the per-edge operand
+        ``w`` permuted into that order, so the walk streams it instead of
+        gathering it by edge id (C5 typed gather 6.57 -> 5.60 ms, bit-identical;
+        scripts/typed_probe.py).  For constant operands (R-GCN's norm): the
+        permuted copy is cached per direction for the last (tensor, version)
+        seen."""
         ic, oc = self.in_csr, self.out_csr
-        if getattr(self, "_pos_view", None) is None:
+        if getattr(self, "_pos_views", None) is None:
+            self._pos_views, self._pos_operands = {}, {}
+        if direction not in self._pos_views:
             dev = ic.indices.device
             pos = th.arange(ic.nnz, device=dev, dtype=th.int32)
+            walk, other = (ic, oc) if direction == "in" else (oc, ic)
             inv = th.empty_like(pos)
-            inv[ic.data.long()] = pos
-            self._pos_view = ImmutableGraphIndex(
-                DeviceCSR(ic.indptr, ic.indices, pos, ic.rows, ic.num_cols),
-                DeviceCSR(oc.indptr, oc.indices, inv[oc.data.long()], oc.rows, oc.num_cols),
+            inv[walk.data.long()] = pos
+            wv = DeviceCSR(walk.indptr, walk.indices, pos, walk.rows, walk.num_cols)
+            ov = DeviceCSR(other.indptr, other.indices, inv[other.data.long()], other.rows,
+                           other.num_cols)
+            self._pos_views[direction] = ImmutableGraphIndex(
+                wv if direction == "in" else ov, ov if direction == "in" else wv,
                 self.num_src, self.num_dst, self.device, eid_perm=True)
-            self._pos_operand = None
+        walk = ic if direction == "in" else oc
         # the cache holds `w` itself: while it is alive no other tensor can take its
         # address, so (address, version counter, layout) identifies its contents
         key = (w.data_ptr(), w._version, tuple(w.shape), tuple(w.stride()), w.dtype)
-        if self._pos_operand is None or self._pos_operand[0] != key:
-            self._pos_operand = (key, w, w[ic.data.long()].contiguous())
-        return self._pos_view, self._pos_operand[2]
+        cached = self._pos_operands.get(direction)
+        if cached is None or cached[0] != key:
+            cached = (key, w, w[walk.data.long()].contiguous())
+            self._pos_operands[direction] = cached
+        return self._pos_views[direction], cached[2]
 
     def col_blocks(self, nb):
         """(in_blocks, out_blocks): the in-CSR split by source range and the

@@ -83,14 +83,16 @@ class RelGraphConv(nn.Module):
         y, node_major = self._transform(x)
         y = y.contiguous()
         n = g.number_of_nodes()
-        node_repr = B._typed_aggregate(g, self.num_rels, y.view(self.num_rels * n, self.out_feat),
-                                       norm, etypes, node_major)
-        if self.bias:
-            node_repr = node_repr + self.h_bias
+        loop = None
         if self.self_loop:
             loop = self.loop_weight[x] if (x.dtype == th.int64 and x.dim() == 1) else \
                 B.project(x, self.loop_weight)
-            node_repr = node_repr + loop
+        # bias and self-loop term fused into the aggregation's epilogue when the norm
+        # is constant (node_repr = agg + h_bias + loop, as relgraphconv.py:150-160)
+        node_repr = B._typed_aggregate(g, self.num_rels, y.view(self.num_rels * n, self.out_feat),
+                                       norm, etypes, node_major,
+                                       bias=self.h_bias if self.bias else None,
+                                       addend=loop.contiguous() if loop is not None else None)
         if self.activation:
             node_repr = self.activation(node_repr)
         return self.dropout(node_repr)
