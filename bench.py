@@ -464,6 +464,15 @@ def main():
     except RuntimeError as exc:  # out of memory on a crowded device: report, don't fail
         res["roofline"]["measured_stream_copy_GBps"] = None
         log("stream copy peak skipped: %r" % exc)
+    if pmc:
+        # bytes the PMC counters saw leave L2 for the fabric (Infinity Cache + HBM)
+        # per launch, moved in the measured kernel time
+        fab = pmc / (kernel_ms * 1e-3) / 1e9
+        res["roofline"]["traffic_GBps"] = fab
+        res["roofline"]["traffic_frac_of_peak"] = fab / HBM_PEAK_GBPS
+        res["roofline"]["traffic_note"] = ("2 x FETCH_SIZE + WRITE_SIZE of the M1 launch pair "
+                                           "(profiles/pmc_traffic.json, gfx950 wide-read "
+                                           "correction); includes Infinity-Cache hits")
     if exch is not None:
         res["with_exchange"] = exch
     if upd_res is not None:
