@@ -521,8 +521,7 @@ class DistGATConv(th.nn.Module):
         el_full = full[:, H * D:].reshape(-1, H, 1)
         gidx = part.gidx(feat.device)
         if c._fused_ok():
-            rst = B.fused_gat(gidx, ft_full.contiguous(), el_full.contiguous(), er,
-                              c.negative_slope)
+            rst = c._fused(gidx, ft_full.contiguous(), el_full.contiguous(), er)
         else:
             g = part.local_graph(feat.device).local_var()
             n = g.number_of_nodes()

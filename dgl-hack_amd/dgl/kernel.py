@@ -246,6 +246,22 @@ def fused_gat_supported(heads, head_dim):
     return bool(_ffi.lib().DGLMIFusedGatSupported(int(heads), int(head_dim)))
 
 
+def fused_gat_head_dim(heads, head_dim):
+    """Head width the fused GAT kernel runs at: ``head_dim`` itself, or the
+    smallest supported width above it (zero-padded columns aggregate to zero and
+    are sliced off -- e.g. a 41-class output layer runs at 64 instead of falling
+    back to the generic kernels); None if no width up to 1024 / heads works."""
+    d = int(head_dim)
+    if fused_gat_supported(heads, d):
+        return d
+    c = 4
+    while heads * c <= 1024:
+        if c >= d and fused_gat_supported(heads, c):
+            return c
+        c += 4
+    return None
+
+
 def gat_col_blocks(graph, feat_src, backward=False):
     """Column blocks for the fused GAT kernels (DGLMIGraph.num_col_blocks): when the
     gathered ft + el table fits the Infinity Cache but not L2 (>= 32 MiB) and rows

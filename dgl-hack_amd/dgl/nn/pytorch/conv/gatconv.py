@@ -61,7 +61,21 @@ class GATConv(nn.Module):
     def _fused_ok(self):
         if not self.use_fused or (self.training and self.attn_drop.p > 0):
             return False
-        return K.fused_gat_supported(self._num_heads, self._out_feats)
+        return self._fused_dim() is not None
+
+    def _fused_dim(self):
+        """Head width for the fused kernel (the output width itself, or padded to
+        the next supported one; see dgl.kernel.fused_gat_head_dim)."""
+        if not hasattr(self, "_fdim"):
+            self._fdim = K.fused_gat_head_dim(self._num_heads, self._out_feats)
+        return self._fdim
+
+    def _fused(self, graph, feat_src, el, er):
+        d = self._fused_dim()
+        if d == self._out_feats:
+            return B.fused_gat(graph, feat_src, el, er, self.negative_slope)
+        ft = th.nn.functional.pad(feat_src, (0, d - self._out_feats))
+        return B.fused_gat(graph, ft, el, er, self.negative_slope)[..., :self._out_feats]
 
     def reset_parameters(self):
         gain = nn.init.calculate_gain("relu")
@@ -88,7 +102,7 @@ class GATConv(nn.Module):
         el = (feat_src * self.attn_l).sum(dim=-1).unsqueeze(-1)
         er = (feat_dst * self.attn_r).sum(dim=-1).unsqueeze(-1)
         if self._fused_ok():
-            rst = B.fused_gat(graph, feat_src, el, er, self.negative_slope)
+            rst = self._fused(graph, feat_src, el, er)
         else:
             graph.srcdata.update({"ft": feat_src, "el": el})
             graph.dstdata.update({"er": er})

@@ -180,3 +180,29 @@ def test_fused_gat_auto_blocks_match_unblocked(monkeypatch):
         res.append((out,) + grads)
     for a, b in zip(*res):
         assert th.allclose(a, b, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("heads,out", [(1, 41), (3, 5), (2, 100)])
+def test_gatconv_padded_head_width_matches_unfused(heads, out):
+    """Head widths the fused kernel cannot take directly (41 classes, 5, 100) run
+    it zero-padded to the next supported width; values and gradients equal the
+    unfused composition."""
+    from dgl.nn.pytorch import GATConv
+    src, dst, n = powerlaw(4000, 50000, seed=6)
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(np.concatenate([src, np.arange(n)]), np.concatenate([dst, np.arange(n)]))
+    th.manual_seed(0)
+    a = GATConv(24, out, heads).to(DEV)
+    a.use_fused = False
+    b = GATConv(24, out, heads).to(DEV)
+    b.load_state_dict(a.state_dict())
+    assert b._fused_ok() and b._fused_dim() > out
+    x = th.randn(n, 24, device=DEV)
+    ya, yb = a(g, x), b(g, x)
+    assert yb.shape == (n, heads, out)
+    assert th.allclose(ya, yb, rtol=1e-4, atol=1e-5)
+    ya.pow(2).sum().backward()
+    yb.pow(2).sum().backward()
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert th.allclose(pa.grad, pb.grad, rtol=1e-3, atol=1e-4)
