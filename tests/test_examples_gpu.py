@@ -27,3 +27,12 @@ def test_gcn_example_learns():
 def test_gat_example_learns(unfused):
     r = _run("gat_train.py", "--epochs", "60", *(["--unfused"] if unfused else []))
     assert r["test_acc"] > 0.6, r
+
+
+@pytest.mark.parametrize("model", ["gat", "rgcn"])
+def test_dist_train_example_runs(model):
+    """examples/dist_train.py (configs C3 / C5, partition-parallel modules) at 2 %
+    of the config size, one process: trains and reports a finite loss."""
+    r = _run("dist_train.py", "--model", model, "--scale", "0.02", "--epochs", "2",
+             "--warmup", "1")
+    assert r["n_gpus"] == 1 and r["epoch_ms"] > 0 and 0 < r["loss"] < 10, r
