@@ -291,37 +291,49 @@ def project(x, w, bias=None):
 
 
 class _GcnAggregate(th.autograd.Function):
-    """out[v] = (sum_{u->v} X[u]) * row_mul[v] + bias in ONE kernel (copy_u_sum with
-    the fused epilogue): GraphConv's aggregation, norm and bias
-    (graphconv.py:150-170) without two extra passes over the output."""
+    """out[v] = (sum_{u->v} X[u]) * row_mul[v] / row_div[v] + bias + addend[v] in ONE
+    kernel (copy_u_sum with the fused epilogue): GraphConv's aggregation, norm and
+    bias (graphconv.py:150-170), the mean reducer's division (tensor.py:308-325) and
+    the residual terms of SAGE / GIN / APPNP / Cheb without extra passes over the
+    output.  row_mul / row_div are constants (no gradient); addend gets grad_out."""
 
     @staticmethod
-    def forward(ctx, gidx, x, row_mul, bias, n_dst):
+    def forward(ctx, gidx, x, row_mul, bias, n_dst, row_div, addend):
         out = x.new_empty((n_dst, x.shape[1]))
-        K.copy_reduce("sum", gidx, SRC, x, out, epilogue=(row_mul, None, bias))
+        K.copy_reduce("sum", gidx, SRC, x, out, epilogue=(row_mul, row_div, bias, addend))
         ctx.gidx = gidx
-        ctx.save_for_backward(x, out, row_mul)
+        ctx.save_for_backward(x, out, row_mul, row_div)
         ctx.has_bias = bias is not None
+        ctx.has_addend = addend is not None
         return out
 
     @staticmethod
     def backward(ctx, grad_out):
-        x, out, row_mul = ctx.saved_tensors
-        gx = gb = None
+        x, out, row_mul, row_div = ctx.saved_tensors
+        gx = gb = ga = None
         g = grad_out.contiguous()
         if ctx.needs_input_grad[1]:
-            gs = g * row_mul.view(-1, 1) if row_mul is not None else g
+            gs = g
+            if row_mul is not None:
+                gs = gs * row_mul.view(-1, 1)
+            if row_div is not None:
+                gs = gs / row_div.view(-1, 1)
             gx = th.empty_like(x)
             K.backward_copy_reduce("sum", ctx.gidx, SRC, x, out, gs.contiguous(), gx)
         if ctx.has_bias and ctx.needs_input_grad[3]:
             gb = g.sum(0)
-        return None, gx, None, gb, None
+        if ctx.has_addend and ctx.needs_input_grad[6]:
+            ga = g
+        return None, gx, None, gb, None, None, ga
 
 
-def gcn_aggregate(gidx, x, row_mul=None, bias=None, n_dst=None):
-    """Fused GraphConv aggregation (see _GcnAggregate); x is (N_src, F) float32."""
+def gcn_aggregate(gidx, x, row_mul=None, bias=None, n_dst=None, row_div=None, addend=None):
+    """Fused copy_u_sum + epilogue (see _GcnAggregate); x is (N_src, F) float32,
+    row_mul / row_div (N_dst,), bias (F,), addend (N_dst, F)."""
     n_dst = gidx.in_csr.num_rows if n_dst is None else n_dst
-    return _GcnAggregate.apply(gidx, x.contiguous(), row_mul, bias, n_dst)
+    if addend is not None:
+        addend = addend.contiguous()
+    return _GcnAggregate.apply(gidx, x.contiguous(), row_mul, bias, n_dst, row_div, addend)
 
 
 class FusedGat(th.autograd.Function):

@@ -272,6 +272,9 @@ class DGLGraph(object):
         return self.number_of_nodes()
 
     @property
+    def is_homograph(self):
+        return True
+
     def is_multigraph(self):
         return True
 

@@ -272,6 +272,32 @@ class DGLHeteroGraph:
     def __getitem__(self, key):
         return _RelationGraph(self, self.to_canonical_etype(key))
 
+    # ---- single-relation graphs (dgl.graph / dgl.bipartite) used like a DGLGraph by
+    # the nn modules: everything goes to the one relation's view
+    @property
+    def _graph(self):
+        return self._rels[self.to_canonical_etype(None)]
+
+    @property
+    def srcdata(self):
+        return self[None].srcdata
+
+    @property
+    def dstdata(self):
+        return self[None].dstdata
+
+    def number_of_src_nodes(self):
+        return self._graph.n_src
+
+    def number_of_dst_nodes(self):
+        return self._graph.n_dst
+
+    def _device_degrees(self, device, direction):
+        return self[None]._device_degrees(device, direction)
+
+    def is_homograph(self):
+        return len(self._ntypes) == 1 and len(self._cetypes) == 1
+
     def local_var(self):
         g = DGLHeteroGraph.__new__(DGLHeteroGraph)
         g.__dict__.update(self.__dict__)
@@ -479,7 +505,12 @@ def heterograph(data_dict, num_nodes_dict=None):
 
 
 def graph(data, ntype="_N", etype="_E", num_nodes=None):
-    """``dgl.graph``: one node type, one edge type."""
+    """``dgl.graph``: one node type, one edge type.  ``data`` is (u, v), a list of
+    pairs, or a square scipy sparse matrix (rows = source)."""
+    if hasattr(data, "tocoo"):
+        m = data.tocoo()
+        num_nodes = m.shape[0] if num_nodes is None else num_nodes
+        data = (m.row, m.col)
     return heterograph({(ntype, etype, ntype): data},
                        None if num_nodes is None else {ntype: num_nodes})
 

@@ -1,4 +1,6 @@
 """PyTorch modules (``dgl.nn.pytorch``)."""
-from .conv import GraphConv, GATConv, FusedGATConv, RelGraphConv  # noqa: F401
+from .conv import (GraphConv, GATConv, FusedGATConv, RelGraphConv, SAGEConv,  # noqa: F401
+                   GINConv, SGConv, APPNPConv, TAGConv, ChebConv, AGNNConv, EdgeConv,
+                   GMMConv, NNConv, GatedGraphConv, CFConv)
 from .softmax import edge_softmax  # noqa: F401
 from .hetero import HeteroGraphConv  # noqa: F401

@@ -1,0 +1,66 @@
+"""Host-side checks for the conv-module zoo (no GPU): the Laplacian eigenvalue
+known answer (``python/dgl/transform.py:418-423`` docstring), module
+construction / parameter shapes / aggregator validation as the reference
+modules, and that a CPU tensor is refused (the engine has no CPU path)."""
+import pytest
+import scipy as sp
+import scipy.sparse  # noqa: F401
+import torch as th
+
+import dgl
+import dgl.nn.pytorch as nn
+
+
+def test_laplacian_lambda_max_known_answer():
+    g = dgl.DGLGraph()
+    g.add_nodes(5)
+    g.add_edges([0, 1, 2, 3, 4, 0, 1, 2, 3, 4], [1, 2, 3, 4, 0, 4, 0, 1, 2, 3])
+    lam = dgl.laplacian_lambda_max(g)
+    assert len(lam) == 1 and abs(lam[0] - 1.809016994374948) < 1e-9
+
+
+def test_graph_from_scipy():
+    m = sp.sparse.random(50, 50, density=0.1, random_state=0)
+    g = dgl.graph(m)
+    assert g.number_of_nodes() == 50 and g.number_of_edges() == m.nnz and g.is_homograph()
+    assert g.number_of_src_nodes() == g.number_of_dst_nodes() == 50
+
+
+@pytest.mark.parametrize("ctor,params", [
+    (lambda: nn.SAGEConv(5, 10, "mean"), {"fc_self.weight": (10, 5), "fc_neigh.weight": (10, 5)}),
+    (lambda: nn.SAGEConv(5, 10, "gcn"), {"fc_neigh.weight": (10, 5)}),
+    (lambda: nn.SAGEConv(5, 10, "pool"), {"fc_pool.weight": (5, 5)}),
+    (lambda: nn.SGConv(5, 10, 3), {"fc.weight": (10, 5)}),
+    (lambda: nn.TAGConv(5, 2, k=2), {"lin.weight": (2, 15)}),
+    (lambda: nn.ChebConv(5, 2, 3), {"fc.2.weight": (2, 5), "bias": (2,)}),
+    (lambda: nn.EdgeConv(5, 2), {"theta.weight": (2, 5), "phi.weight": (2, 5)}),
+    (lambda: nn.GMMConv(5, 10, 3, 4), {"mu": (4, 3), "inv_sigma": (4, 3), "fc.weight": (40, 5)}),
+    (lambda: nn.GatedGraphConv(5, 10, 5, 3), {"linears.2.weight": (10, 10),
+                                              "gru.weight_ih": (30, 10)}),
+    (lambda: nn.CFConv(2, 3, 2, 3), {"project_node.weight": (2, 2)}),
+    (lambda: nn.AGNNConv(1), {"beta": (1,)}),
+])
+def test_module_parameters(ctor, params):
+    named = dict(ctor().named_parameters())
+    for k, shp in params.items():
+        assert tuple(named[k].shape) == shp
+
+
+def test_bad_aggregators():
+    for ctor in (lambda: nn.SAGEConv(5, 10, "median"), lambda: nn.GINConv(None, "prod"),
+                 lambda: nn.GMMConv(5, 10, 3, 4, "min"),
+                 lambda: nn.NNConv(5, 10, None, "min")):
+        with pytest.raises(KeyError):
+            ctor()
+
+
+def test_cpu_tensors_refused():
+    g = dgl.DGLGraph()
+    g.add_nodes(4)
+    g.add_edges([0, 1, 2], [1, 2, 3])
+    for m, args in ((nn.SAGEConv(3, 2, "mean"), (th.randn(4, 3),)),
+                    (nn.GINConv(None, "sum"), (th.randn(4, 3),)),
+                    (nn.SGConv(3, 2), (th.randn(4, 3),)),
+                    (nn.EdgeConv(3, 2), (th.randn(4, 3),))):
+        with pytest.raises(Exception):
+            m(g, *args)
