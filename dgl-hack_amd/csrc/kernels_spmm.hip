@@ -18,7 +18,8 @@
 //    while ordinary rows cost one pass: every group does the same work.
 //  * A group of L lanes (L * 4 * NV >= F floats) owns a chunk; the chunk's
 //    (row, col, eid) triples are staged through LDS B at a time with coalesced
-//    loads, then each lane gathers float4 slices of U source rows at once
+//    loads, then each lane gathers VW-float slices (float4 / float2 / float,
+//    the widest dividing F) of U source rows at once
 //    (U * 16 B in flight per lane, whole 256-B rows per group at F = 64).
 //  * Rows are folded in registers and written once (owner computes, no
 //    atomics).  A row cut by a chunk boundary writes its head partial to out
@@ -27,301 +28,11 @@
 //    deterministic and independent of scheduling.
 //  * Zero-in-degree rows get the reducer identity from the group that sees
 //    the gap in the row sequence (no separate fill pass over `out`).
-#include "internal.h"
-
-#include <climits>
-#include <cstdlib>
+#include "spmm_chunk.h"
 
 namespace dglmi {
 namespace {
 
-constexpr int kBlock = 256;
-
-template <int RED>
-__device__ __forceinline__ float4 red4(float4 a, float4 b) {
-  return make_float4(red_apply<RED>(a.x, b.x), red_apply<RED>(a.y, b.y),
-                     red_apply<RED>(a.z, b.z), red_apply<RED>(a.w, b.w));
-}
-template <int RED>
-__device__ __forceinline__ float4 ident4() {
-  const float v = red_identity<RED>();
-  return make_float4(v, v, v, v);
-}
-
-__device__ __forceinline__ float4 ld4(const float* p) {
-  return *reinterpret_cast<const float4*>(p);
-}
-__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float4 ld4_nt(const float* p) {
-  const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
-  return make_float4(v.x, v.y, v.z, v.w);
-}
-
-template <int KIND>
-constexpr bool needs_eid() {
-  return KIND != FAST_COPY_COL;
-}
-
-// Value of one edge for float4 slot f4 of the output row.  `hs` (bcast kind):
-// the edge value's index for this slot, (4 * f4) / head_dim, and `wn` the edge
-// values per edge, F / head_dim -- both hoisted out of the edge loop by the
-// caller (64-bit divisions per edge cost 1.7 ms on the C5 typed gather).
-template <int KIND>
-__device__ __forceinline__ float4 edge_value(const FastArgs& a, int32_t col, int32_t eid, int f4,
-                                             int hs = 0, int64_t wn = 1) {
-  if constexpr (KIND == FAST_COPY_COL) {
-    const int64_t c = a.x_map ? a.x_map[col] : col;
-    return ld4(a.x + c * a.F + 4 * f4);
-  } else if constexpr (KIND == FAST_COPY_EDGE) {
-    const int64_t e = a.x_map ? a.x_map[eid] : eid;
-    return ld4(a.x + e * a.F + 4 * f4);
-  } else if constexpr (KIND == FAST_COL_MUL_EDGE) {
-    const int64_t c = a.x_map ? a.x_map[col] : col;
-    const int64_t e = a.w_map ? a.w_map[eid] : eid;
-    const float4 x = ld4(a.x + c * a.F + 4 * f4);
-    const float4 w = ld4(a.w + e * a.F + 4 * f4);
-    return make_float4(x.x * w.x, x.y * w.y, x.z * w.z, x.w * w.w);
-  } else {
-    const int64_t c = a.x_map ? a.x_map[col] : col;
-    const int64_t e = a.w_map ? a.w_map[eid] : eid;
-    const float4 x = ld4(a.x + c * a.F + 4 * f4);
-    const float w = a.w[e * wn + hs];
-    return make_float4(x.x * w, x.y * w, x.z * w, x.w * w);
-  }
-}
-
-template <int VAR>
-__device__ __forceinline__ int32_t ld_stream(const int32_t* p) {
-  if constexpr (VAR & 1) return __builtin_nontemporal_load(p);
-  else return *p;
-}
-template <int VAR>
-__device__ __forceinline__ void st_out(float* p, float4 v) {
-  if constexpr (VAR & 2) {
-    __builtin_nontemporal_store(v.x, p);
-    __builtin_nontemporal_store(v.y, p + 1);
-    __builtin_nontemporal_store(v.z, p + 2);
-    __builtin_nontemporal_store(v.w, p + 3);
-  } else {
-    st4(p, v);
-  }
-}
-
-// L lanes per group, NV float4 per lane, U gathers in flight per lane-slot.
-// VAR (tuning variants): bit 0 non-temporal index/row stream loads, bit 1
-// non-temporal output stores, bit 2 twice the gathers in flight.  Default 3:
-// keeping the once-read CSR stream and the once-written output out of L2/MALL
-// leaves more room for re-read source rows (M1: 3.30 -> 3.25 ms; 4 and 7 spill).
-// EPI: fused epilogue on every finished row, out = acc * row_mul[r] / row_div[r]
-// + bias + addend[r] (GraphConv's norm and bias, the mean reducer's division,
-// accumulation onto an earlier partial result) -- applied
-// once per row, after the whole row is reduced (split rows: in the fixup).
-template <bool EPI>
-__device__ __forceinline__ float4 epi4(const FastArgs& a, float4 v, int64_t r, int f4) {
-  if constexpr (EPI) {
-    if (a.row_mul) {
-      const float m = a.row_mul[r];
-      v = make_float4(v.x * m, v.y * m, v.z * m, v.w * m);
-    }
-    if (a.row_div) {
-      const float d = a.row_div[r];
-      v = make_float4(v.x / d, v.y / d, v.z / d, v.w / d);
-    }
-    if (a.bias) {
-      const float4 b = ld4(a.bias + 4 * f4);
-      v = make_float4(v.x + b.x, v.y + b.y, v.z + b.z, v.w + b.w);
-    }
-    if (a.addend) {
-      const float4 b = ld4(a.addend + r * a.F + 4 * f4);
-      v = make_float4(v.x + b.x, v.y + b.y, v.z + b.z, v.w + b.w);
-    }
-  }
-  return v;
-}
-
-template <int KIND, int RED, int L, int NV, int VAR = 3, bool EPI = false>
-__global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32_t* __restrict__ indptr) {
-  constexpr int G = kBlock / L;           // groups per block
-  constexpr int B = (L > 16 ? L : 16) * ((VAR & 4) ? 2 : 1);  // positions staged per step
-  constexpr int U = (NV == 1 ? 8 : (NV == 2 ? 4 : 2)) * ((VAR & 4) ? 2 : 1);
-  static_assert(B % U == 0, "B must be a multiple of U");
-  __shared__ int32_t s_row[G][B];
-  __shared__ int32_t s_col[G][B];
-  __shared__ int32_t s_eid[needs_eid<KIND>() ? G : 1][needs_eid<KIND>() ? B : 1];
-
-  const int g = threadIdx.x / L;
-  const int lane = threadIdx.x % L;
-  const int64_t chunk = (int64_t)blockIdx.x * G + g;
-  const int64_t K = a.chunk;
-  const int64_t p0 = chunk * K;
-  if (p0 >= a.nnz) return;  // whole group exits together
-  const int64_t p1 = p0 + K < a.nnz ? p0 + K : a.nnz;
-  const int F4 = static_cast<int>(a.F / 4);
-  const float4 I = ident4<RED>();
-  int hsel[NV];  // bcast: edge value index of each float4 slot
-  const int64_t wn = KIND == FAST_COL_MUL_EDGE_BCAST ? a.F / a.head_dim : 1;
-#pragma unroll
-  for (int v = 0; v < NV; ++v)
-    hsel[v] = KIND == FAST_COL_MUL_EDGE_BCAST ? static_cast<int>((4 * (lane + v * L)) / a.head_dim) : 0;
-
-  int64_t cur = a.rows[p0];
-  bool cont = p0 > 0 && a.rows[p0 - 1] == cur;
-  // leading empty rows: those after the previous chunk's last row (or from 0)
-  if (!cont) {
-    const int64_t first_gap = p0 > 0 ? (int64_t)a.rows[p0 - 1] + 1 : 0;
-    for (int64_t r = first_gap; r < cur; ++r)
-#pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        const int f4 = lane + v * L;
-        if (f4 < F4) st_out<VAR>(a.out + r * a.F + 4 * f4, epi4<EPI>(a, I, r, f4));
-      }
-  }
-  float4 acc[NV];
-#pragma unroll
-  for (int v = 0; v < NV; ++v) acc[v] = I;
-
-  for (int64_t base = p0; base < p1; base += B) {
-    // stage B positions through LDS (coalesced, one row/col/eid per lane slot)
-    for (int q = lane; q < B; q += L) {
-      const int64_t p = base + q;
-      const bool ok = p < p1;
-      s_row[g][q] = ok ? ld_stream<VAR>(a.rows + p) : INT_MAX;
-      s_col[g][q] = ok ? ld_stream<VAR>(a.indices + p) : 0;
-      if constexpr (needs_eid<KIND>()) s_eid[needs_eid<KIND>() ? g : 0][q] = ok ? ld_stream<VAR>(a.eids + p) : 0;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int ub = 0; ub < B; ub += U) {
-      float4 val[U][NV];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int32_t col = s_col[g][ub + u];
-        const int32_t eid = needs_eid<KIND>() ? s_eid[needs_eid<KIND>() ? g : 0][ub + u] : 0;
-        const bool ok = s_row[g][ub + u] != INT_MAX;
-#pragma unroll
-        for (int v = 0; v < NV; ++v) {
-          const int f4 = lane + v * L;
-          if constexpr ((VAR & 8) != 0 && KIND == FAST_COPY_COL) {
-            // bit 31 of the column marks a cold source row (re-read fewer than
-            // min_hot_degree times): gathered non-temporally so it does not evict
-            // re-read rows from L2 / Infinity Cache (VAR & 16: the reverse, a
-            // tuning control)
-            const bool nt = (col < 0) != ((VAR & 16) != 0);
-            const float* px = a.x + static_cast<int64_t>(col & 0x7fffffff) * a.F + 4 * f4;
-            val[u][v] = (ok && f4 < F4) ? (nt ? ld4_nt(px) : ld4(px)) : I;
-          } else {
-            val[u][v] = (ok && f4 < F4) ? edge_value<KIND>(a, col, eid, f4, hsel[v], wn) : I;
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int32_t r = s_row[g][ub + u];
-        if (r == INT_MAX) break;
-        if (r != cur) {
-          // flush the finished row, fill the empty rows in between
-          float* dst = cont ? a.carry + chunk * a.F : a.out + cur * a.F;
-#pragma unroll
-          for (int v = 0; v < NV; ++v) {
-            const int f4 = lane + v * L;
-            if (f4 < F4) st_out<VAR>(dst + 4 * f4, cont ? acc[v] : epi4<EPI>(a, acc[v], cur, f4));
-            acc[v] = I;
-          }
-          for (int64_t e = cur + 1; e < r; ++e)
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-              const int f4 = lane + v * L;
-              if (f4 < F4) st_out<VAR>(a.out + e * a.F + 4 * f4, epi4<EPI>(a, I, e, f4));
-            }
-          cur = r;
-          cont = false;
-        }
-#pragma unroll
-        for (int v = 0; v < NV; ++v) acc[v] = red4<RED>(acc[v], val[u][v]);
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-  {
-    float* dst = cont ? a.carry + chunk * a.F : a.out + cur * a.F;
-    // a row that goes on in the next chunk stays raw: the fixup finishes it
-    const bool done = !cont && !(EPI && p1 < a.nnz && a.rows[p1] == cur);
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int f4 = lane + v * L;
-      if (f4 < F4) st_out<VAR>(dst + 4 * f4, done ? epi4<EPI>(a, acc[v], cur, f4) : acc[v]);
-    }
-  }
-  if (p1 == a.nnz) {  // trailing empty rows
-    for (int64_t r = cur + 1; r < a.num_rows; ++r)
-#pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        const int f4 = lane + v * L;
-        if (f4 < F4) st_out<VAR>(a.out + r * a.F + 4 * f4, epi4<EPI>(a, I, r, f4));
-      }
-  }
-  (void)indptr;
-}
-
-// Fold the carries of every row cut by chunk boundaries into its head, in
-// chunk order.  One group per chunk; only a row's first continuation chunk
-// does work.
-template <int RED, int L, int NV, bool EPI = false>
-__global__ void __launch_bounds__(kBlock) k_chunk_fixup(FastArgs a, const int32_t* __restrict__ indptr) {
-  constexpr int G = kBlock / L;
-  const int g = threadIdx.x / L;
-  const int lane = threadIdx.x % L;
-  const int64_t chunk = (int64_t)blockIdx.x * G + g;
-  const int64_t K = a.chunk;
-  const int64_t p0 = chunk * K;
-  if (chunk == 0 || p0 >= a.nnz) return;
-  const int64_t r = a.rows[p0];
-  const int64_t start = indptr[r];
-  if (start >= p0 || start < p0 - K) return;  // not a continuation / not the first one
-  const int64_t last = (indptr[r + 1] - 1) / K;
-  const int F4 = static_cast<int>(a.F / 4);
-  float4 acc[NV];
-#pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    const int f4 = lane + v * L;
-    acc[v] = f4 < F4 ? ld4(a.out + r * a.F + 4 * f4) : ident4<RED>();
-  }
-  int64_t c = chunk;
-  for (; c + 3 <= last; c += 4) {
-    float4 t[4][NV];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        const int f4 = lane + v * L;
-        t[k][v] = f4 < F4 ? ld4(a.carry + (c + k) * a.F + 4 * f4) : ident4<RED>();
-      }
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int v = 0; v < NV; ++v) acc[v] = red4<RED>(acc[v], t[k][v]);
-  }
-  for (; c <= last; ++c)
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int f4 = lane + v * L;
-      if (f4 < F4) acc[v] = red4<RED>(acc[v], ld4(a.carry + c * a.F + 4 * f4));
-    }
-#pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    const int f4 = lane + v * L;
-    if (f4 < F4) st4(a.out + r * a.F + 4 * f4, epi4<EPI>(a, acc[v], r, f4));
-  }
-}
-
-
-// ---------------------------------------------------------------------------
-// Narrow rows (F < 16 floats: attention logits per head, edge-softmax sums):
-// a group of 4+ lanes would idle most lanes, so ONE lane owns a chunk and the
-// whole (tiny) row, keeping 8 gathers of F floats in flight per lane.
 // ---------------------------------------------------------------------------
 template <int F>
 __device__ __forceinline__ void load_row(const float* __restrict__ p, float (&v)[F]) {
@@ -504,7 +215,6 @@ __global__ void __launch_bounds__(kBlock) k_lane_fixup(FastArgs a) {
   store_row<F>(a.out + r * F, acc);
 }
 
-bool has_epi(const FastArgs& a) { return a.row_mul || a.row_div || a.bias || a.addend; }
 
 template <int KIND, int RED, int F>
 void run_lane(const FastArgs& a, hipStream_t s) {
@@ -538,93 +248,17 @@ void run_lane_f(const FastArgs& a, hipStream_t s) {
   }
 }
 
-struct Cfg {
-  int L, NV;
-};
-Cfg pick(int64_t F) {
-  const int64_t F4 = F / 4;
-  if (F4 <= 4) return {4, 1};
-  if (F4 <= 8) return {8, 1};
-  if (F4 <= 16) return {16, 1};
-  if (F4 <= 32) return {32, 1};
-  if (F4 <= 64) return {64, 1};
-  if (F4 <= 128) return {64, 2};
-  return {64, 4};
-}
-
-int spmm_variant() {
-  const char* env = std::getenv("DGLMI_SPMM_VARIANT");
-  return env ? std::atoi(env) : 3;
-}
-
-template <int KIND, int RED, int L, int NV>
-void run(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
-  constexpr int G = kBlock / L;
-  const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
-  const unsigned blocks = static_cast<unsigned>((chunks + G - 1) / G);
-  if constexpr (KIND == FAST_COPY_COL && RED == RED_SUM && NV == 1 && L >= 16) {
-    if (a.marked) {  // cold-row hints present (capi.cpp run_fast decides)
-      if (has_epi(a))
-        hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 11, true>), dim3(blocks), dim3(kBlock),
-                           0, s, a, indptr);
-      else
-        hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 11>), dim3(blocks), dim3(kBlock), 0, s,
-                           a, indptr);
-      if (chunks > 1) {
-        if (has_epi(a))
-          hipLaunchKernelGGL((k_chunk_fixup<RED, L, NV, true>), dim3(blocks), dim3(kBlock), 0, s, a,
-                             indptr);
-        else
-          hipLaunchKernelGGL((k_chunk_fixup<RED, L, NV>), dim3(blocks), dim3(kBlock), 0, s, a,
-                             indptr);
-      }
-      return;
-    }
-  }
-  if constexpr (RED == RED_SUM) {
-    if (has_epi(a)) {
-      hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 3, true>), dim3(blocks), dim3(kBlock), 0,
-                         s, a, indptr);
-      if (chunks > 1)
-        hipLaunchKernelGGL((k_chunk_fixup<RED, L, NV, true>), dim3(blocks), dim3(kBlock), 0, s, a,
-                           indptr);
-      return;
-    }
-  }
-  if constexpr (KIND == FAST_COPY_COL && RED == RED_SUM && L == 16 && NV == 1) {
-    // tuning variants of the headline kernel (scripts/tune_spmm.py)
-    switch (spmm_variant()) {
-      case 0: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 0>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
-      case 1: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 1>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
-      case 2: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 2>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
-      case 4: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 4>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
-      case 7: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 7>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
-      case 27: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 27>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
-      default: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
-    }
-  } else {
-    hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV>), dim3(blocks), dim3(kBlock), 0, s, a,
-                       indptr);
-  }
-  if (chunks > 1)
-    hipLaunchKernelGGL((k_chunk_fixup<RED, L, NV>), dim3(blocks), dim3(kBlock), 0, s, a, indptr);
-}
 
 template <int KIND, int RED>
 void run_cfg(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
-  if (a.F < 16) {
+  if (a.F < 16 && lane_kernel_width(a.F)) {
     run_lane_f<KIND, RED>(a, s);
     return;
   }
-  const Cfg c = pick(a.F);
-  switch (c.L * 10 + c.NV) {
-    case 41: run<KIND, RED, 4, 1>(a, indptr, s); break;
-    case 81: run<KIND, RED, 8, 1>(a, indptr, s); break;
-    case 161: run<KIND, RED, 16, 1>(a, indptr, s); break;
-    case 321: run<KIND, RED, 32, 1>(a, indptr, s); break;
-    case 641: run<KIND, RED, 64, 1>(a, indptr, s); break;
-    case 642: run<KIND, RED, 64, 2>(a, indptr, s); break;
-    default: run<KIND, RED, 64, 4>(a, indptr, s); break;
+  switch (fast_vw(a.F, KIND, a.head_dim)) {
+    case 4: run_vw<KIND, RED, 4>(a, indptr, s); break;
+    case 2: launch_fast_chunk_vw2(KIND, RED, a, s); break;
+    default: launch_fast_chunk_vw1(KIND, RED, a, s); break;
   }
 }
 
@@ -674,14 +308,12 @@ int64_t fast_workspace_bytes(int64_t nnz, int64_t F) {
 }
 
 bool fast_supported(int kind, int64_t F, int64_t head_dim) {
-  if (F < 16) {
-    if (F < 1 || (F > 8 && F != 12)) return false;
-    if (kind == FAST_COL_MUL_EDGE_BCAST && (head_dim < 1 || F % head_dim != 0)) return false;
-    return true;
-  }
-  if (F % 4 != 0 || F > 1024) return false;
-  if (kind == FAST_COL_MUL_EDGE_BCAST && (head_dim % 4 != 0 || F % head_dim != 0)) return false;
-  return true;
+  if (F < 1) return false;
+  if (kind == FAST_COL_MUL_EDGE_BCAST && (head_dim < 1 || F % head_dim != 0)) return false;
+  if (F < 16 && lane_kernel_width(F)) return true;
+  // 64 lanes x up to 8 float4 or 16 float2 / float slots per lane
+  const int vw = fast_vw(F, kind, head_dim);
+  return F <= (vw == 1 ? 1024 : 2048);
 }
 
 void launch_fast_reduce(int kind, int red, const FastArgs& a, hipStream_t s) {

@@ -6,6 +6,9 @@
   C2  GraphConv layer on an ogbn-arxiv-sized graph (169,343 / 1,166,243, F = 128)
   C3  GATConv (8 heads x 8) on a Reddit-sized graph (232,965 / 114,615,892,
       F_in = 602): forward + backward
+  zoo the other conv modules (SAGE, GIN, SG, APPNP, TAG, Cheb, EdgeConv,
+      GatedGraph) on the arxiv-size graph and SAGE-mean on the Reddit-size graph:
+      forward + backward of the epilogue-fused form vs the reference-order form
   C5  RelGraphConv (4 relations, basis, 64 -> 64, per-edge norm) on 5,000,000
       nodes / 80,000,000 typed edges: forward + backward, and the typed gather alone
 
@@ -287,6 +290,52 @@ def gemm(dev, steps, warmup):
             res["%s %s ms" % (name, tag)] = ms
             res["%s %s TFLOPs" % (name, tag)] = fl / ms / 1e9
             res["%s %s mfma_util" % (name, tag)] = fl / ms / 1e9 / peak
+    return res
+
+
+def zoo(dev, steps, warmup):
+    import dgl.nn.pytorch as nn
+    res = {"config": "conv module zoo, fwd+bwd ms: fused / reference order"}
+    n, m, f = 169343, 1166243, 128
+    g = chung_lu(n, m, 0.6, 2, dev)
+    etypes = th.randint(0, 4, (m,), device=dev)
+    mods = {
+        "SAGE_mean_128_128": (nn.SAGEConv(f, f, "mean"), ()),
+        "SAGE_gcn_128_128": (nn.SAGEConv(f, f, "gcn"), ()),
+        "GIN_sum_128": (nn.GINConv(th.nn.Linear(f, f), "sum"), ()),
+        "GIN_mean_128": (nn.GINConv(th.nn.Linear(f, f), "mean"), ()),
+        "SGConv_k2_128_64": (nn.SGConv(f, 64, k=2), ()),
+        "APPNP_k10_128": (nn.APPNPConv(10, 0.1), ()),
+        "TAGConv_k2_128_64": (nn.TAGConv(f, 64, k=2), ()),
+        "ChebConv_k3_128_64": (nn.ChebConv(f, 64, 3), ([2.0],)),
+        "EdgeConv_128_64": (nn.EdgeConv(f, 64), ()),
+        "GatedGraph_4types_128_1step": (nn.GatedGraphConv(f, f, 1, 4), (etypes,)),
+    }
+    x = th.randn(n, f, device=dev, requires_grad=True)
+    for name, (mod, extra) in mods.items():
+        mod = mod.to(dev)
+        for fused in (True, False):
+            mod.fused = fused
+
+            def step():
+                mod(g, x, *extra).sum().backward()
+            res["%s_%s" % (name, "fused" if fused else "ref")] = timeit(step, steps, warmup)
+        res[name + "_speedup"] = res[name + "_ref"] / res[name + "_fused"]
+    del g, x
+    th.cuda.empty_cache()
+    n, m = 232965, 114615892
+    g = chung_lu(n, m, 0.6, 3, dev)
+    x = th.randn(n, 602, device=dev, requires_grad=True)
+    mod = nn.SAGEConv(602, 64, "mean").to(dev)
+    for fused in (True, False):
+        mod.fused = fused
+
+        def step():
+            mod(g, x).sum().backward()
+        res["Reddit_SAGE_mean_602_64_%s" % ("fused" if fused else "ref")] = \
+            timeit(step, max(2, steps // 2), 1)
+    res["Reddit_SAGE_mean_602_64_speedup"] = (res["Reddit_SAGE_mean_602_64_ref"]
+                                              / res["Reddit_SAGE_mean_602_64_fused"])
     return res
 
 
