@@ -262,7 +262,8 @@ struct Scratch {
 // rows own the output; out has `walk.num_rows` rows of F floats.
 void run_fast(const DGLMIGraph* g, const DGLMICsr& walk, int kind, int red, const float* x,
               const int32_t* x_map, const float* w, const int32_t* w_map, float* out, int64_t F,
-              int64_t head_dim, hipStream_t s, const DGLMIEpilogue* epi = nullptr);
+              int64_t head_dim, hipStream_t s, const DGLMIEpilogue* epi = nullptr,
+              const float* xr = nullptr);
 
 // Column blocks (DGLMIGraph.num_col_blocks) on the load-balanced sum: one pass
 // per non-empty block, so a pass gathers from a slice of the table that fits the
@@ -311,7 +312,7 @@ void run_fast_blocked(const DGLMIGraph* g, const DGLMICsr* blocks, const DGLMICs
 
 void run_fast(const DGLMIGraph* g, const DGLMICsr& walk, int kind, int red, const float* x,
               const int32_t* x_map, const float* w, const int32_t* w_map, float* out, int64_t F,
-              int64_t head_dim, hipStream_t s, const DGLMIEpilogue* epi) {
+              int64_t head_dim, hipStream_t s, const DGLMIEpilogue* epi, const float* xr) {
   // copy_u only: with an edge operand (u_mul_e) its per-edge gather by edge id
   // dominates and extra passes cost more than the smaller table saves (Reddit-size,
   // F = 64: copy_u_sum 3.88 -> 2.96 ms over 8 blocks, u_mul_e_sum 5.94 -> 7.23 ms)
@@ -345,6 +346,7 @@ void run_fast(const DGLMIGraph* g, const DGLMICsr& walk, int kind, int red, cons
   a.F = F;
   a.head_dim = head_dim;
   a.chunk = fast_chunk_edges(walk.nnz, F);
+  a.xr = xr;
   // cold-row hints: copy_u sum over a table larger than the Infinity Cache
   if (kind == FAST_COPY_COL && red == RED_SUM && x_map == nullptr && fast_marked_supported(F)) {
     const int32_t* marked = &walk == &g->in_csr ? g->in_gather_cols
@@ -645,6 +647,19 @@ void backward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const 
       run_fast(g, walk, kind, RED_SUM, grad_out->data, nullptr, w, w_map, grad->data, D, head_dim, s);
       return;
     }
+  }
+
+  // copy_u max / min: grad_u[src] = sum over out-edges of grad_out[dst] where
+  // x[src] == out[dst] (every tied edge, the reference's BackwardCall for max /
+  // min) -- a reduce-to-row over the out-CSR with a tie-mask edge value, so the
+  // load-balanced kernels own each source row (no atomics)
+  if ((red == RED_MAX || red == RED_MIN) && op == OP_USE_LHS && x_t == DGLMI_TARGET_SRC &&
+      !need_fill && out_map == nullptr && lhs_map == nullptr && walk.rows != nullptr &&
+      aligned16(grad->data) && aligned16(grad_out->data) && aligned16(out->data) &&
+      aligned16(lhs->data) && fast_supported(FAST_COL_TIE, D, 1)) {
+    run_fast(g, walk, FAST_COL_TIE, RED_SUM, grad_out->data, nullptr, out->data, nullptr, grad->data,
+             D, 1, s, nullptr, lhs->data);
+    return;
   }
 
   if (need_fill) launch_fill(grad->data, grad_rows * Dg, 0.0f, s);

@@ -192,6 +192,7 @@ enum FastKind : int {
   FAST_COPY_EDGE = 1,   // v = E[eid]
   FAST_COL_MUL_EDGE = 2,        // v = X[col] * E[eid]            (same feature shape)
   FAST_COL_MUL_EDGE_BCAST = 3,  // v = X[col, h, :] * E[eid, h]   (E broadcast over the last dim)
+  FAST_COL_TIE = 4,     // v = XR[row] == W[col] ? X[col] : 0  (max / min gradient, tie mask)
 };
 struct FastArgs {
   const int32_t* indptr;
@@ -217,6 +218,7 @@ struct FastArgs {
   // copy_u sum: `indices` carries cold-row marks in bit 31 (DGLMIKernelMarkColdColumns);
   // marked rows are gathered non-temporally
   int marked;
+  const float* xr;      // FAST_COL_TIE: the reduce's input, one row per walk row
 };
 int64_t fast_chunk_edges(int64_t nnz, int64_t F);
 int64_t fast_workspace_bytes(int64_t nnz, int64_t F);

@@ -69,8 +69,15 @@ __device__ __forceinline__ void store_row(float* __restrict__ p, const float (&v
 // `wn` = F / head_dim values per edge, computed once per thread by the caller.
 template <int KIND, int F>
 __device__ __forceinline__ void lane_value(const FastArgs& a, int32_t col, int32_t eid, float (&v)[F],
-                                           const int (&hidx)[F], int wn) {
-  if constexpr (KIND == FAST_COPY_COL) {
+                                           const int (&hidx)[F], int wn, int32_t row) {
+  if constexpr (KIND == FAST_COL_TIE) {
+    float o[F], xr[F];
+    load_row<F>(a.x + static_cast<int64_t>(col) * F, v);
+    load_row<F>(a.w + static_cast<int64_t>(col) * F, o);
+    load_row<F>(a.xr + static_cast<int64_t>(row) * F, xr);
+#pragma unroll
+    for (int i = 0; i < F; ++i) v[i] = xr[i] == o[i] ? v[i] : 0.0f;
+  } else if constexpr (KIND == FAST_COPY_COL) {
     const int64_t c = a.x_map ? a.x_map[col] : col;
     load_row<F>(a.x + c * F, v);
   } else if constexpr (KIND == FAST_COPY_EDGE) {
@@ -169,7 +176,7 @@ __global__ void __launch_bounds__(kBlock) k_lane_reduce(FastArgs a) {
     float v[U][F];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (r[u] != INT_MAX) lane_value<KIND, F>(a, c[u], needs_eid<KIND>() ? e[u] : 0, v[u], hidx, wn);
+      if (r[u] != INT_MAX) lane_value<KIND, F>(a, c[u], needs_eid<KIND>() ? e[u] : 0, v[u], hidx, wn, r[u]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -330,6 +337,7 @@ void launch_fast_reduce(int kind, int red, const FastArgs& a, hipStream_t s) {
       else run_cfg<FAST_COPY_EDGE, RED_SUM>(a, indptr, s);
       break;
     case FAST_COL_MUL_EDGE: run_cfg<FAST_COL_MUL_EDGE, RED_SUM>(a, indptr, s); break;
+    case FAST_COL_TIE: run_cfg<FAST_COL_TIE, RED_SUM>(a, indptr, s); break;
     default: run_cfg<FAST_COL_MUL_EDGE_BCAST, RED_SUM>(a, indptr, s); break;
   }
 }

@@ -18,6 +18,7 @@ void launch_fast_chunk_vw2(int kind, int red, const FastArgs& a, hipStream_t s) 
       else run_vw<FAST_COPY_EDGE, RED_SUM, 2>(a, indptr, s);
       break;
     case FAST_COL_MUL_EDGE: run_vw<FAST_COL_MUL_EDGE, RED_SUM, 2>(a, indptr, s); break;
+    case FAST_COL_TIE: run_vw<FAST_COL_TIE, RED_SUM, 2>(a, indptr, s); break;
     default: run_vw<FAST_COL_MUL_EDGE_BCAST, RED_SUM, 2>(a, indptr, s); break;
   }
 }

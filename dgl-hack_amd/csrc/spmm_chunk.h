@@ -89,10 +89,18 @@ __device__ __forceinline__ float vadd(float a, float b) { return a + b; }
 __device__ __forceinline__ float4 vmul(float4 a, float4 b) { return make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w); }
 __device__ __forceinline__ float2 vmul(float2 a, float2 b) { return make_float2(a.x * b.x, a.y * b.y); }
 __device__ __forceinline__ float vmul(float a, float b) { return a * b; }
+// where(a == b, g, 0) per component: the max / min gradient's tie mask
+__device__ __forceinline__ float vtie(float a, float b, float g) { return a == b ? g : 0.0f; }
+__device__ __forceinline__ float2 vtie(float2 a, float2 b, float2 g) {
+  return make_float2(vtie(a.x, b.x, g.x), vtie(a.y, b.y, g.y));
+}
+__device__ __forceinline__ float4 vtie(float4 a, float4 b, float4 g) {
+  return make_float4(vtie(a.x, b.x, g.x), vtie(a.y, b.y, g.y), vtie(a.z, b.z, g.z), vtie(a.w, b.w, g.w));
+}
 
 template <int KIND>
 constexpr bool needs_eid() {
-  return KIND != FAST_COPY_COL;
+  return KIND != FAST_COPY_COL && KIND != FAST_COL_TIE;
 }
 
 // Value of one edge for VW-float slot fv of the output row.  `hs` (bcast kind):
@@ -101,8 +109,15 @@ constexpr bool needs_eid() {
 // caller (64-bit divisions per edge cost 1.7 ms on the C5 typed gather).
 template <int KIND, int VW>
 __device__ __forceinline__ typename VecT<VW>::T edge_value(const FastArgs& a, int32_t col, int32_t eid,
-                                                          int fv, int hs = 0, int64_t wn = 1) {
-  if constexpr (KIND == FAST_COPY_COL) {
+                                                          int fv, int hs = 0, int64_t wn = 1,
+                                                          int32_t row = 0) {
+  if constexpr (KIND == FAST_COL_TIE) {
+    // grad_x[row] += grad_out[col] where x[row] == out[col] (the reference's
+    // BackwardCall for max / min: every tied edge gets the gradient)
+    const int64_t o = static_cast<int64_t>(col) * a.F + VW * fv;
+    return vtie(vld<VW>(a.xr + static_cast<int64_t>(row) * a.F + VW * fv), vld<VW>(a.w + o),
+                vld<VW>(a.x + o));
+  } else if constexpr (KIND == FAST_COPY_COL) {
     const int64_t c = a.x_map ? a.x_map[col] : col;
     return vld<VW>(a.x + c * a.F + VW * fv);
   } else if constexpr (KIND == FAST_COPY_EDGE) {
@@ -225,7 +240,7 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
             const float* px = a.x + static_cast<int64_t>(col & 0x7fffffff) * a.F + VW * f4;
             val[u][v] = (ok && f4 < F4) ? (nt ? vld_nt<VW>(px) : vld<VW>(px)) : I;
           } else {
-            val[u][v] = (ok && f4 < F4) ? edge_value<KIND, VW>(a, col, eid, f4, hsel[v], wn) : I;
+            val[u][v] = (ok && f4 < F4) ? edge_value<KIND, VW>(a, col, eid, f4, hsel[v], wn, s_row[g][ub + u]) : I;
           }
         }
       }
