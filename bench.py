@@ -416,7 +416,12 @@ def main():
     value = edges_total * args.steps / elapsed
     exch = None
     if part is not None:
-        exch = measure_exchange(part, x, out, args, dist, cdev, device, edges_total)
+        try:
+            exch = measure_exchange(part, x, out, args, dist, cdev, device, edges_total)
+        except SystemExit as exc:
+            # its parity checks agree across ranks (max over ranks) before exiting, so
+            # every rank lands here together; the replicated headline still reports
+            exch = {"error": str(exc)}
     upd_res = None
     if upd is not None:
         upd_res = measure_update_all(upd, x, out, args)
