@@ -333,13 +333,27 @@ class DGLGraph(object):
         s, d, e = (th.from_numpy(a[mask].copy()) for a in (src, dst, eid))
         return {"uv": (s, d), "eid": e, "all": (s, d, e)}[form]
 
-    def adjacency_matrix_scipy(self, transpose=False, fmt="csr"):
+    def adjacency_matrix_scipy(self, transpose=False, fmt="csr", return_edge_ids=None):
+        """(graph.py:3567-3599) A row is a destination and a column a source by
+        default (DGL 0.4); ``transpose=True`` puts sources on the rows.  Entries
+        count parallel edges (``return_edge_ids`` is accepted and ignored: the
+        values are ones)."""
         import scipy.sparse as sp
         src, dst, _ = self._graph.edges()
         n = self.number_of_nodes()
-        r, c = (dst, src) if transpose else (src, dst)
+        r, c = (src, dst) if transpose else (dst, src)
         m = sp.coo_matrix((np.ones(len(src), np.float32), (r, c)), shape=(n, n))
         return m.asformat(fmt)
+
+    def adjacency_matrix(self, transpose=False, ctx=None):
+        """(graph.py:3601-3640) torch sparse COO adjacency, destination rows by
+        default; ``ctx`` a torch device."""
+        src, dst, _ = self._graph.edges()
+        n = self.number_of_nodes()
+        s, d = th.from_numpy(np.asarray(src)), th.from_numpy(np.asarray(dst))
+        idx = th.stack([s, d] if transpose else [d, s])
+        m = th.sparse_coo_tensor(idx, th.ones(len(src)), (n, n))
+        return m if ctx is None else m.to(ctx)
 
     # ---- features ---------------------------------------------------------------
     @property

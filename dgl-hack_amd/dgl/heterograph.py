@@ -298,6 +298,16 @@ class DGLHeteroGraph:
     def is_homograph(self):
         return len(self._ntypes) == 1 and len(self._cetypes) == 1
 
+    def adjacency_matrix(self, transpose=False, ctx=None, etype=None):
+        """(heterograph.py:2134-2180) torch sparse COO adjacency of one relation:
+        (num_dst, num_src) with destination rows by default."""
+        r = self._rels[self.to_canonical_etype(etype)]
+        s, d = th.from_numpy(r.src), th.from_numpy(r.dst)
+        idx = th.stack([s, d] if transpose else [d, s])
+        shape = (r.n_src, r.n_dst) if transpose else (r.n_dst, r.n_src)
+        m = th.sparse_coo_tensor(idx, th.ones(len(r.src)), shape)
+        return m if ctx is None else m.to(ctx)
+
     def local_var(self):
         g = DGLHeteroGraph.__new__(DGLHeteroGraph)
         g.__dict__.update(self.__dict__)

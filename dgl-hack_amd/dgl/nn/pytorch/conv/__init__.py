@@ -15,3 +15,4 @@ from .gmmconv import GMMConv  # noqa: F401
 from .nnconv import NNConv  # noqa: F401
 from .gatedgraphconv import GatedGraphConv  # noqa: F401
 from .cfconv import CFConv  # noqa: F401
+from .dense import DenseGraphConv, DenseSAGEConv, DenseChebConv  # noqa: F401

@@ -64,3 +64,26 @@ def test_cpu_tensors_refused():
                     (nn.EdgeConv(3, 2), (th.randn(4, 3),))):
         with pytest.raises(Exception):
             m(g, *args)
+
+
+def test_adjacency_orientation():
+    """DGL 0.4: a row of adjacency_matrix() is a destination (graph.py:3567-3599)."""
+    g = dgl.DGLGraph()
+    g.add_nodes(3)
+    g.add_edges([0, 0], [1, 2])
+    a = g.adjacency_matrix().to_dense()
+    assert a[1, 0] == 1 and a[2, 0] == 1 and a[0, 1] == 0
+    assert (g.adjacency_matrix(transpose=True).to_dense() == a.t()).all()
+    assert (g.adjacency_matrix_scipy().toarray() == a.numpy()).all()
+    b = dgl.bipartite(([0, 1], [2, 0]), num_nodes=(2, 3))
+    ab = b.adjacency_matrix().to_dense()
+    assert ab.shape == (3, 2) and ab[2, 0] == 1 and ab[0, 1] == 1
+
+
+def test_dense_modules_on_host():
+    """The dense modules are plain torch (GEMMs): they run anywhere."""
+    adj = (th.rand(30, 30) < 0.2).float()
+    x = th.randn(30, 4)
+    assert nn.DenseGraphConv(4, 3)(adj, x).shape == (30, 3)
+    assert nn.DenseSAGEConv(4, 3)(adj, x).shape == (30, 3)
+    assert nn.DenseChebConv(4, 3, 3)(adj, x).shape == (30, 3)

@@ -495,3 +495,67 @@ def test_builtins_only_reach_hip():
     sage = nn.SAGEConv(4, 2, "mean")
     with pytest.raises(Exception):
         sage(g, th.randn(20, 4))
+
+
+# ----------------------------------------------------------------- dense forms
+def _random_graph100():
+    return dgl.DGLGraph(sp.sparse.random(100, 100, density=0.1, random_state=11), readonly=True)
+
+
+def _random_bipartite():
+    return dgl.bipartite(sp.sparse.random(100, 200, density=0.1, random_state=12))
+
+
+@pytest.mark.parametrize("norm_type", ["both", "right", "none"])
+@pytest.mark.parametrize("kind", ["graph", "bipartite"])
+def test_dense_graph_conv(norm_type, kind):
+    """test_nn.py:595-610: DenseGraphConv on adjacency_matrix().to_dense() ==
+    GraphConv on the graph (same weights)."""
+    g = _random_graph100() if kind == "graph" else _random_bipartite()
+    adj = g.adjacency_matrix(ctx=DEV).to_dense()
+    conv = nn.GraphConv(5, 2, norm=norm_type, bias=True).to(DEV)
+    dense = nn.DenseGraphConv(5, 2, norm=norm_type, bias=True).to(DEV)
+    dense.weight.data = conv.weight.data
+    dense.bias.data = conv.bias.data
+    feat = th.randn(g.number_of_src_nodes(), 5, device=DEV)
+    assert th.allclose(conv(g, feat), dense(adj, feat), **TOL)
+
+
+@pytest.mark.parametrize("kind", ["graph", "bipartite"])
+def test_dense_sage_conv(kind):
+    """test_nn.py:612-632: DenseSAGEConv == SAGEConv 'gcn'."""
+    g = _random_graph100() if kind == "graph" else _random_bipartite()
+    adj = g.adjacency_matrix(ctx=DEV).to_dense()
+    sage = nn.SAGEConv(5, 2, "gcn").to(DEV)
+    dense = nn.DenseSAGEConv(5, 2).to(DEV)
+    dense.fc.weight.data = sage.fc_neigh.weight.data
+    dense.fc.bias.data = sage.fc_neigh.bias.data
+    if kind == "bipartite":
+        feat = (th.randn(100, 5, device=DEV), th.randn(200, 5, device=DEV))
+    else:
+        feat = th.randn(100, 5, device=DEV)
+    assert th.allclose(sage(g, feat), dense(adj, feat), **TOL)
+
+
+@pytest.mark.parametrize("k", [1, 2, 3])
+def test_dense_cheb_conv(k):
+    """test_nn.py:649-665: DenseChebConv == ChebConv at lambda_max = 2; and the
+    default lambda (eigvals) against dgl.laplacian_lambda_max."""
+    g = _random_graph100()
+    adj = g.adjacency_matrix(ctx=DEV).to_dense()
+    cheb = nn.ChebConv(5, 2, k).to(DEV)
+    dense = nn.DenseChebConv(5, 2, k).to(DEV)
+    for i in range(len(cheb.fc)):
+        dense.W.data[i] = cheb.fc[i].weight.data.t()
+    dense.bias.data = cheb.bias.data
+    feat = th.randn(100, 5, device=DEV)
+    assert th.allclose(cheb(g, feat, [2.0]), dense(adj, feat, 2.0), **TOL)
+    # a symmetric graph: the dense eigen-solver and the host Lanczos agree
+    gs = _rand_graph(n=60, m=300, seed=13)
+    s, d = _edges(gs)
+    sym = dgl.DGLGraph()
+    sym.add_nodes(60)
+    sym.add_edges(th.cat([s, d]).numpy(), th.cat([d, s]).numpy())
+    adj = sym.adjacency_matrix(ctx=DEV).to_dense()
+    lam = dgl.laplacian_lambda_max(sym)[0]
+    assert th.allclose(cheb(sym, feat[:60]), dense(adj, feat[:60]), rtol=1e-3, atol=1e-3), lam
