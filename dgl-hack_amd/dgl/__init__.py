@@ -15,7 +15,9 @@ from .graph import DGLGraph, ALL  # noqa: F401
 from .graph_index import GraphIndex  # noqa: F401
 from .heterograph import (DGLHeteroGraph, heterograph, graph, bipartite,  # noqa: F401
                           hetero_from_relations)
-from .transform import laplacian_lambda_max  # noqa: F401
+from .transform import (laplacian_lambda_max, add_self_loop, remove_self_loop,  # noqa: F401
+                        reverse, to_bidirected)
+from . import transform  # noqa: F401
 from . import nn  # noqa: F401
 
 __version__ = "0.4"

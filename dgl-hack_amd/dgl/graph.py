@@ -275,6 +275,11 @@ class DGLGraph(object):
     def is_homograph(self):
         return True
 
+    def reverse(self, share_ndata=False, share_edata=False):
+        """``graph.py`` DGLGraph.reverse -> ``dgl.transform.reverse``."""
+        from .transform import reverse
+        return reverse(self, share_ndata, share_edata)
+
     def is_multigraph(self):
         return True
 

@@ -87,3 +87,37 @@ def test_dense_modules_on_host():
     assert nn.DenseGraphConv(4, 3)(adj, x).shape == (30, 3)
     assert nn.DenseSAGEConv(4, 3)(adj, x).shape == (30, 3)
     assert nn.DenseChebConv(4, 3, 3)(adj, x).shape == (30, 3)
+
+
+def test_transform_known_answers():
+    """Docstring known answers of transform.py: add_self_loop (:497-503),
+    to_bidirected (:371-378), reverse (:270-290), remove_self_loop."""
+    g = dgl.DGLGraph()
+    g.add_nodes(5)
+    g.add_edges([0, 1, 2], [1, 1, 2])
+    s, d = dgl.transform.add_self_loop(g).edges()
+    assert s.tolist() == [0, 0, 1, 2, 3, 4] and d.tolist() == [1, 0, 1, 2, 3, 4]
+    s, d = dgl.remove_self_loop(g).edges()
+    assert s.tolist() == [0] and d.tolist() == [1]
+    g = dgl.DGLGraph()
+    g.add_nodes(2)
+    g.add_edges([0, 0], [0, 1])
+    s, d = dgl.to_bidirected(g).edges()
+    assert s.tolist() == [0, 1, 0] and d.tolist() == [0, 0, 1]
+    s, d = dgl.to_bidirected(g, readonly=False).edges()
+    assert sorted(zip(s.tolist(), d.tolist())) == [(0, 0), (0, 1), (1, 0)]
+    g = dgl.DGLGraph()
+    g.add_nodes(3)
+    g.add_edges([0, 1, 2], [1, 2, 0])
+    g.ndata["h"] = th.tensor([[0.], [1.], [2.]])
+    rg = g.reverse(share_ndata=True)
+    s, d = rg.edges()
+    assert s.tolist() == [1, 2, 0] and d.tolist() == [0, 1, 2]
+    assert th.equal(rg.ndata["h"], g.ndata["h"])
+    # multigraph: max of the two directions' multiplicities
+    g = dgl.DGLGraph()
+    g.add_nodes(3)
+    g.add_edges([0, 0, 1, 2], [1, 1, 0, 2])
+    s, d = dgl.to_bidirected(g).edges()
+    pairs = sorted(zip(s.tolist(), d.tolist()))
+    assert pairs == [(0, 1), (0, 1), (1, 0), (1, 0), (2, 2)]
