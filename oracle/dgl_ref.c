@@ -102,6 +102,13 @@ static float red_zero(int red) {
     default: return 0.0f;
   }
 }
+/* std::max(a, b) = (a < b) ? b : a and std::min(a, b) = (b < a) ? b : a, exactly
+ * as <algorithm> defines them (cpu/functor.h:33,44 call them as
+ * std::max(*addr, val)): a NaN `val` never replaces the accumulator, a NaN
+ * accumulator is kept. */
+static inline float std_max(float a, float b) { return (a < b) ? b : a; }
+static inline float std_min(float a, float b) { return (b < a) ? b : a; }
+
 /* cpu/functor.h:19-71 */
 static inline void red_call(int red, float* addr, float val, int par) {
   switch (red) {
@@ -116,17 +123,17 @@ static inline void red_call(int red, float* addr, float val, int par) {
     case R_MAX:
       if (par) {
 #pragma omp critical
-        *addr = *addr > val ? *addr : val;
+        *addr = std_max(*addr, val);
       } else {
-        *addr = *addr > val ? *addr : val;
+        *addr = std_max(*addr, val);
       }
       break;
     case R_MIN:
       if (par) {
 #pragma omp critical
-        *addr = *addr < val ? *addr : val;
+        *addr = std_min(*addr, val);
       } else {
-        *addr = *addr < val ? *addr : val;
+        *addr = std_min(*addr, val);
       }
       break;
     case R_PROD:

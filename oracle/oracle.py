@@ -277,3 +277,16 @@ def copy_src_sum_i32(n_src, indptr, indices, x, n_dst, nthreads):
 
 def max_threads():
     return lib().ref_max_threads()
+
+
+def edge_softmax(g, score):
+    """python/dgl/nn/pytorch/softmax.py:33-78 restated on the kernels above:
+    copy_e max -> e_sub_v -> exp -> copy_e sum -> e_div_v (no fusion)."""
+    score = _f32(score)
+    smax = copy_reduce("max", g, EDGE, score, g.n)
+    out = binary_op_reduce_raw("none", "sub", g, EDGE, DST, score, smax, g.m)
+    with np.errstate(invalid="ignore", over="ignore"):
+        out = np.exp(out).astype(np.float32)
+    out_sum = copy_reduce("sum", g, EDGE, out, g.n)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        return binary_op_reduce_raw("none", "div", g, EDGE, DST, out, out_sum, g.m)

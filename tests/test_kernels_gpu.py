@@ -376,3 +376,58 @@ def test_fused_epilogue(plaw, F):
         K.copy_reduce("max", gidx, 0, x, out, epilogue=(mul, None, None))
     with pytest.raises(dgl.DGLError):
         K.copy_reduce("sum", gidx, 0, x, out, epilogue=(None, None, None, out))
+
+
+_SPECIAL = None
+
+
+def _special():
+    global _SPECIAL
+    if _SPECIAL is None:
+        import json
+        import os
+        p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "special_values.json")
+        _SPECIAL = json.load(open(p))
+    return _SPECIAL
+
+
+@pytest.mark.parametrize("red", ["sum", "max", "min"])
+def test_special_values_known_answers(red):
+    """NaN / +-inf messages and zero-in-degree rows through update_all: the
+    kernels keep std::max / std::min semantics (a NaN message never replaces the
+    accumulator, functor.h:33,44), the identity fill and the tie-mask gradient.
+    Known answers (tests/golden/make_special.py) and the oracle, bit for bit."""
+    d = _special()
+    g = _graph(np.array(d["src"]), np.array(d["dst"]), d["n"])
+    x = th.tensor(d["x"], dtype=th.float32, device=DEV, requires_grad=True)
+    g.ndata["x"] = x
+    g.update_all(fn.copy_u("x", "m"), getattr(fn, red)("m", "o"))
+    o = g.ndata["o"]
+    o.backward(th.ones_like(o))
+    want_o = np.array(d["cases"][red]["out"], np.float32)
+    want_g = np.array(d["cases"][red]["grad_x"], np.float32)
+    np.testing.assert_array_equal(o.detach().cpu().numpy(), want_o)
+    np.testing.assert_array_equal(x.grad.cpu().numpy(), want_g)
+    xr = np.array(d["x"], np.float32)
+    r_o, r_g = O.copy_reduce(red, O.RefGraph(np.array(d["src"]), np.array(d["dst"]), d["n"]),
+                             O.SRC, xr, d["n"], grad_out=np.ones_like(xr))
+    np.testing.assert_array_equal(o.detach().cpu().numpy(), r_o)
+    np.testing.assert_array_equal(x.grad.cpu().numpy(), r_g)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_special_values_edge_softmax(fused, monkeypatch):
+    """All-masked (-inf), NaN and +inf logits: the fused kernel pair and the
+    decomposition both give the reference decomposition's values (NaN rows
+    included, softmax.py:33-78)."""
+    from dgl.nn.pytorch import softmax as S
+    monkeypatch.setattr(S, "FUSED", fused)
+    d = _special()
+    sm = d["softmax"]
+    g = _graph(np.array(sm["src"]), np.array(sm["dst"]), d["n"])
+    s = th.tensor(sm["score"], dtype=th.float32, device=DEV).reshape(-1, 1)
+    got = S.edge_softmax(g, s).reshape(-1).cpu().numpy()
+    np.testing.assert_allclose(got, np.array(sm["out"], np.float32), rtol=1e-6, equal_nan=True)
+    ref = O.edge_softmax(O.RefGraph(np.array(sm["src"]), np.array(sm["dst"]), d["n"]),
+                         np.array(sm["score"], np.float32).reshape(-1, 1)).reshape(-1)
+    np.testing.assert_allclose(got, ref, rtol=1e-6, equal_nan=True)

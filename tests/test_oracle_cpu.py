@@ -156,3 +156,31 @@ def test_star_graph_known_answers():
     _eq(out[:, 0], copy_ans)
     out = O.binary_reduce("sum", "mul", g, O.SRC, O.EDGE, h, eh, 10)
     _eq(out[:, 0], [100., 1., 1., 1., 1., 1., 1., 1., 1., 284.])
+
+
+SPECIAL = json.load(open(os.path.join(HERE, "golden", "special_values.json")))
+
+
+@pytest.mark.parametrize("red", ["sum", "max", "min"])
+def test_special_values_known_answers(red):
+    """NaN / +-inf / zero-in-degree rows: the oracle follows std::max / std::min
+    exactly (functor.h:33,44 -- a NaN message never replaces the accumulator)
+    and the identity fill; known answers from tests/golden/make_special.py."""
+    d = SPECIAL
+    x = np.array(d["x"], np.float32)
+    ref = O.RefGraph(np.array(d["src"]), np.array(d["dst"]), d["n"])
+    for nthreads in (1, 4):
+        out, gx = O.copy_reduce(red, ref, O.SRC, x, d["n"], grad_out=np.ones_like(x),
+                                nthreads=nthreads)
+        np.testing.assert_array_equal(out, np.array(d["cases"][red]["out"], np.float32))
+        np.testing.assert_array_equal(gx, np.array(d["cases"][red]["grad_x"], np.float32))
+
+
+def test_special_values_edge_softmax():
+    """Masked (all -inf), NaN and +inf logits through the reference's edge_softmax
+    decomposition (softmax.py:33-78): NaN rows where the reference makes NaN."""
+    sm = SPECIAL["softmax"]
+    ref = O.RefGraph(np.array(sm["src"]), np.array(sm["dst"]), SPECIAL["n"])
+    s = np.array(sm["score"], np.float32).reshape(-1, 1)
+    got = O.edge_softmax(ref, s).reshape(-1)
+    np.testing.assert_allclose(got, np.array(sm["out"], np.float32), rtol=1e-6, equal_nan=True)
