@@ -26,6 +26,7 @@ the same graph, rank 0 at N = 1 only.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import math
 import os
@@ -108,11 +109,40 @@ def make_local_graph(n_src, n_dst, src, dst, device):
     return g, (g.out_csr.indptr, g.out_csr.indices)
 
 
-def cpu_baseline(o_ptr, o_idx, x, n_dst, budget_s=20.0, sample_edges=None):
-    """Reference CPU algorithm on the M1 graph (or its leading source rows when
-    `sample_edges` is given), passes repeated until `budget_s` is spent (>= 1 pass)."""
+def _physical_cores():
+    """Physical cores of the host (distinct (package, core id) pairs)."""
+    seen, phys, core = set(), None, None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                phys = line.split(":", 1)[1].strip()
+            elif line.startswith("core id"):
+                core = line.split(":", 1)[1].strip()
+            elif not line.strip() and core is not None:
+                seen.add((phys, core))
+                phys = core = None
+    except OSError:
+        return None
+    return len(seen) or None
+
+
+def cpu_baseline(o_ptr, o_idx, x, n_dst, sample_edges=40_000_000, warmup=3, reps=10):
+    """The reference's CPU algorithm (out-CSR traversal, OpenMP over source rows,
+    `omp atomic` scatter, zero fill of every destination row) on the leading
+    source rows of the M1 out-CSR holding `sample_edges` edges (a bounded sample:
+    ~1-2 s per pass on the box's 16-CPU lease), median of `reps` passes after
+    `warmup` passes."""
     from oracle import oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or O.max_threads()
+    affinity = len(os.sched_getaffinity(0))
+    phys = _physical_cores()
+    env_threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    # the lease's CPU share: OMP_NUM_THREADS as the harness sets it (16 per GPU on
+    # the MI355X boxes), else every CPU this process may run on, never more than
+    # the physical cores
+    threads = env_threads or affinity
+    if phys:
+        threads = min(threads, phys)
+    threads = max(1, min(threads, O.max_threads() if not env_threads else threads))
     ptr = o_ptr.cpu().numpy()
     rows = ptr.shape[0] - 1
     if sample_edges is not None:
@@ -121,14 +151,13 @@ def cpu_baseline(o_ptr, o_idx, x, n_dst, budget_s=20.0, sample_edges=None):
     idx = o_idx[:e].cpu().numpy().astype(np.int32)
     xs = np.ascontiguousarray(x[:rows].cpu().numpy())  # features of the sampled source rows
     ptr_s = ptr[:rows + 1].astype(np.int32)
+    for _ in range(warmup):
+        O.copy_src_sum_i32(rows, ptr_s, idx, xs, n_dst, threads)
     times = []
-    t_start = time.time()
-    for it in range(5):
+    for _ in range(reps):
         t0 = time.time()
         O.copy_src_sum_i32(rows, ptr_s, idx, xs, n_dst, threads)
         times.append(time.time() - t0)
-        if time.time() - t_start > budget_s:
-            break
     t = float(np.median(times))
     model = None
     try:
@@ -139,23 +168,129 @@ def cpu_baseline(o_ptr, o_idx, x, n_dst, budget_s=20.0, sample_edges=None):
     except OSError:
         pass
     return {"value": e / t, "unit": "edges/s", "cores": threads, "kind": "port",
-            "cpu_model": model, "host_cpus": os.cpu_count(),
+            "cpu_model": model, "host_cpus": os.cpu_count(), "affinity_cpus": affinity,
+            "physical_cores": phys, "omp_num_threads_env": env_threads or None,
             "sample": "reference CPU algorithm (oracle/dgl_ref.c ref_copy_src_sum_i32: out-CSR, "
                       "OpenMP over src rows, omp-atomic scatter, zero fill of all %d dst rows) on "
-                      "%d source rows (%d edges) of the M1 graph, F=%d, median of %d pass(es), "
-                      "%d OpenMP threads" % (n_dst, rows, e, FEAT, len(times), threads),
+                      "the first %d source rows (%d edges) of the M1 out-CSR, F=%d, median of %d "
+                      "passes after %d warm-up passes, %d OpenMP threads (the lease's CPU share: "
+                      "OMP_NUM_THREADS as set by the harness, capped by affinity and physical cores)"
+                      % (n_dst, rows, e, FEAT, reps, warmup, threads),
             "seconds_per_pass": t}
 
 
-def load_pmc_traffic():
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if present."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(path):
+PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE",), ("TCC_HIT_sum", "TCC_MISS_sum"))
+
+
+def _rocprof():
+    import shutil
+    return shutil.which("rocprofv3") or ("/opt/rocm/bin/rocprofv3"
+                                         if os.path.exists("/opt/rocm/bin/rocprofv3") else None)
+
+
+def pmc_child():
+    """Body of one rocprofv3 --pmc pass (``bench.py --pmc-child``): the M1 launch
+    pair 3 times, then 3 launches over a calibration graph whose bytes are known
+    exactly (a random permutation: every source row gathered once, no reuse)."""
+    import dgl  # noqa: F401
+    from dgl import kernel as K
+    from dgl.graph_index import device_block_gidx
+    device = "cuda:0"
+    th.cuda.set_device(0)
+    n, n_dst, src, dst, x = build_workload(1, 0, device)
+    g, _ = make_local_graph(n, n_dst, src, dst, device)
+    del src, dst
+    out = th.empty(n_dst, FEAT, device=device)
+    for _ in range(3):
+        K.copy_reduce("sum", g, 0, x, out)
+    th.cuda.synchronize()
+    del g
+    gp = th.Generator(device=device)
+    gp.manual_seed(11)
+    csrc = th.randperm(n, generator=gp, device=device).to(th.int32)
+    cdst = th.arange(n, dtype=th.int32, device=device)
+    gc = device_block_gidx(n, n, csrc, cdst)
+    for _ in range(3):
+        K.copy_reduce("sum", gc, 0, x, out)
+    th.cuda.synchronize()
+
+
+def pmc_traffic_live(timeout_s=150):
+    """Fabric bytes of the M1 copy_u_sum launch pair, measured now by rocprofv3 PMC
+    passes over ``bench.py --pmc-child`` (one counter group per pass, as
+    MI355X_MICROARCH.md §rocprofv3 prescribes), run BEFORE this process touches
+    the GPU.  gfx950 FETCH_SIZE under-reports wide reads (MI355X_MICROARCH.md
+    §HBM), so its scale is calibrated in the same pass on a permutation gather
+    whose read bytes are known exactly (4F per source row + 8 per edge);
+    WRITE_SIZE is exact for 16-B stores.  Returns a dict or None."""
+    import csv
+    import glob
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+    prof = _rocprof()
+    if prof is None:
         return None
+    tmp = tempfile.mkdtemp(prefix="dglmi_pmc_")
+    vals = {}
     try:
-        return json.load(open(path)).get("bytes_per_launch")
-    except Exception:
+        for i, counters in enumerate(PMC_PASSES):
+            d = os.path.join(tmp, "p%d" % i)
+            cmd = [prof, "--pmc", *counters, "-d", d, "-o", "run", "--output-format", "csv", "--",
+                   sys.executable, os.path.abspath(__file__), "--pmc-child"]
+            p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                                 start_new_session=True, cwd=ROOT)
+            try:
+                _, err = p.communicate(timeout=timeout_s)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+                log("pmc pass %s timed out" % (counters,))
+                return None
+            if p.returncode != 0:
+                log("pmc pass %s failed rc=%d: %s" % (counters, p.returncode,
+                                                      err.decode(errors="replace")[-500:]))
+                return None
+            files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+            if not files:
+                return None
+            for r in csv.DictReader(open(files[0])):
+                name = r["Kernel_Name"]
+                if "k_chunk_reduce" not in name and "k_chunk_fixup" not in name:
+                    continue
+                key = (int(r["Grid_Size"]), "reduce" if "k_chunk_reduce" in name else "fixup",
+                       r["Counter_Name"])
+                vals.setdefault(key, []).append(float(r["Counter_Value"]))
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    grids = sorted({k[0] for k in vals if k[1] == "reduce"})
+    if len(grids) < 2:
         return None
+    m1_grid, cal_grid = grids[-1], grids[0]
+
+    def per_launch(grid, counter):  # mean per dispatch, reduce + fixup
+        return sum(float(np.mean(v)) for k, v in vals.items() if k[0] == grid and k[2] == counter)
+
+    n = 1 << SCALE
+    cal_known_read = 4 * FEAT * n + 8 * n  # every X row once + rows/indices stream
+    fetch_cal = per_launch(cal_grid, "FETCH_SIZE") * 1024
+    fetch = per_launch(m1_grid, "FETCH_SIZE") * 1024
+    write = per_launch(m1_grid, "WRITE_SIZE") * 1024
+    if fetch_cal <= 0 or fetch <= 0:
+        return None
+    scale = cal_known_read / fetch_cal
+    hit = per_launch(m1_grid, "TCC_HIT_sum")
+    miss = per_launch(m1_grid, "TCC_MISS_sum")
+    return {"bytes_per_launch": scale * fetch + write, "read_bytes": scale * fetch,
+            "write_bytes": write, "fetch_size_bytes_raw": fetch, "fetch_scale": scale,
+            "fetch_scale_from": "permutation gather, %d known read bytes, FETCH_SIZE %d"
+                                % (cal_known_read, fetch_cal),
+            "l2_hit_rate": hit / (hit + miss) if hit + miss > 0 else None,
+            "passes": [list(c) for c in PMC_PASSES],
+            "method": "rocprofv3 --pmc per pass over `bench.py --pmc-child` (M1 launch pair x3), "
+                      "read = FETCH_SIZE x calibrated scale, + WRITE_SIZE; Infinity-Cache hits "
+                      "included (they leave L2)"}
 
 
 def _max_over_ranks(v, dist, cdev):
@@ -248,20 +383,29 @@ def measure_exchange(part, x, out_ref, args, dist, cdev, device, edges_total):
 
 
 def stream_copy_peak(device, nbytes=4 << 30, reps=5):
-    """Measured HBM stream rate: device-to-device copy of a 4 GiB buffer,
-    (read + write bytes) / time -- BASELINE.md §3's measured peak beside the spec."""
+    """Measured HBM stream rate: the library's float4 device copy
+    (DGLMIStreamCopy) of a 4 GiB buffer, (read + write bytes) / time on the
+    launch stream -- the access pattern MI355X_MICROARCH.md quotes 6.29 TB/s on."""
+    from dgl import _ffi
     a = th.empty(nbytes // 4, dtype=th.float32, device=device)
     b = th.empty_like(a)
     a.fill_(1.0)
-    b.copy_(a)
+    stream = th.cuda.current_stream()
+    call = lambda: _ffi.check_call(_ffi.lib().DGLMIStreamCopy(
+        ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(b.data_ptr()), ctypes.c_int64(a.numel()),
+        ctypes.c_void_p(stream.cuda_stream)))
+    call()
     s, e = th.cuda.Event(enable_timing=True), th.cuda.Event(enable_timing=True)
-    s.record()
+    s.record(stream)
     for _ in range(reps):
-        b.copy_(a)
-    e.record()
+        call()
+    e.record(stream)
     th.cuda.synchronize()
+    ok = bool(th.equal(a[:1 << 20], b[:1 << 20]))
     ms = s.elapsed_time(e) / reps
     del a, b
+    if not ok:
+        raise RuntimeError("stream copy check failed")
     return 2 * nbytes / (ms * 1e-3) / 1e9
 
 
@@ -296,10 +440,27 @@ def main():
                     help="N>1: skip the with-halo-exchange measurement")
     ap.add_argument("--no-update-all", action="store_true",
                     help="N=1: skip the end-to-end DGLGraph.update_all measurement")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="N=1: skip the rocprofv3 PMC passes (roofline traffic)")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.pmc_child:
+        pmc_child()
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    m1 = world == 1 and args.edges_per_gpu == EDGES_PER_GPU and args.scale == SCALE
+    pmc = None
+    under_profiler = any(k.startswith("ROCPROF") for k in os.environ)
+    if m1 and not args.no_pmc and not under_profiler:
+        # counters first, in child processes, before this process touches the GPU
+        t0 = time.time()
+        try:
+            pmc = pmc_traffic_live()
+        except Exception as exc:  # the counters must never take the GPU line down
+            log("pmc passes failed: %r" % exc)
+        log("pmc passes: %s (%.1fs)" % ("ok" if pmc else "unavailable", time.time() - t0))
     local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
     th.cuda.set_device(local)
     device = "cuda:%d" % local
@@ -426,14 +587,40 @@ def main():
     if upd is not None:
         upd_res = measure_update_all(upd, x, out, args)
         del upd
-    # algorithmic bytes per launch (per rank): indptr + indices + one
-    # gathered 4F-byte source row per edge + one 4F-byte output row per destination
+    # Bytes models per launch (per rank), DESIGN.md §6:
+    #  * algorithmic: indptr + indices + one gathered 4F-byte source row
+    #    per edge + one 4F-byte output row per destination -- counts the re-reads
+    #    that L2 serves, so its rate exceeds HBM peak on skewed graphs;
+    #  * compulsory: every source row once (the bytes no cache can avoid);
+    #  * traffic: what the PMC counters saw leave L2 for the fabric (Infinity
+    #    Cache + HBM), measured by this run's own rocprofv3 passes -- the bytes the
+    #    kernel is actually bound by.  roofline.achieved = traffic / kernel time.
     alg_bytes = 4 * (n_dst + 1) + 4 * m_local + 4 * FEAT * m_local + 4 * FEAT * n_dst
-    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     compulsory = 4 * (n_dst + 1) + 4 * m_local + 4 * FEAT * n + 4 * FEAT * n_dst
-    # the committed PMC summary was measured on the default M1 launch only
-    m1 = world == 1 and args.edges_per_gpu == EDGES_PER_GPU and args.scale == SCALE
-    pmc = load_pmc_traffic() if m1 else None
+    alg_gbps = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    comp_gbps = compulsory / (kernel_ms * 1e-3) / 1e9
+    if pmc is None and m1:
+        # no live counters (profiler unavailable, or this run is itself under
+        # rocprofv3): the committed passes of the same launch at this head
+        try:
+            pmc = dict(json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json"))))
+            pmc["source"] = "profiles/pmc_traffic.json (committed rocprofv3 passes, same launch)"
+        except (OSError, ValueError):
+            pmc = None
+    traffic = pmc["bytes_per_launch"] if pmc else None
+    achieved = traffic / (kernel_ms * 1e-3) / 1e9 if traffic else None
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBPS if achieved else None, "traffic": traffic,
+            "kernel": "k_chunk_reduce + k_chunk_fixup (one copy_u_sum launch pair)",
+            "kernel_ms": kernel_ms,
+            "achieved_from": "fabric bytes per launch (rocprofv3 PMC, this run) / HIP-event "
+                             "kernel time" if traffic else "no counters this run",
+            "alg_bytes_per_launch": alg_bytes, "alg_GBps": alg_gbps,
+            "alg_note": "SURVEY §8d model: counts L2-served re-reads of hub rows, above peak",
+            "compulsory_bytes_per_launch": compulsory, "compulsory_GBps": comp_gbps,
+            "compulsory_frac": comp_gbps / HBM_PEAK_GBPS}
+    if pmc:
+        roof["pmc"] = pmc
     res = {
         "metric": "edges/sec + achieved HBM GB/s, GCN copy_u_sum on 100M-edge graph, 1/2/4/8 MI355X",
         "value": value,
@@ -454,30 +641,18 @@ def main():
                                   ", %d-way dst-row partition, X replicated" % world),
                    "nodes": n, "edges": args.edges_per_gpu * world, "feat": FEAT,
                    "parallelism": "dst-row partition x%d" % world if world > 1 else "single"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": pmc,
-                     "kernel": "k_chunk_reduce + k_chunk_fixup (one copy_u_sum launch pair)",
-                     "kernel_ms": kernel_ms, "alg_bytes_per_launch": alg_bytes,
-                     "compulsory_bytes_per_launch": compulsory},
+        "roofline": roof,
         "hbm_gbps_achieved": achieved,
         "edges_per_sec_per_gpu": value / world,
     }
     try:
         peak = stream_copy_peak(device)
         res["roofline"]["measured_stream_copy_GBps"] = peak
-        res["roofline"]["stream_copy_method"] = "torch copy_ of a 4 GiB fp32 buffer, (read + write) / time"
+        res["roofline"]["stream_copy_method"] = ("DGLMIStreamCopy: float4 device copy of a 4 GiB "
+                                                 "fp32 buffer, (read + write) / time")
     except RuntimeError as exc:  # out of memory on a crowded device: report, don't fail
         res["roofline"]["measured_stream_copy_GBps"] = None
         log("stream copy peak skipped: %r" % exc)
-    if pmc:
-        # bytes the PMC counters saw leave L2 for the fabric (Infinity Cache + HBM)
-        # per launch, moved in the measured kernel time
-        fab = pmc / (kernel_ms * 1e-3) / 1e9
-        res["roofline"]["traffic_GBps"] = fab
-        res["roofline"]["traffic_frac_of_peak"] = fab / HBM_PEAK_GBPS
-        res["roofline"]["traffic_note"] = ("2 x FETCH_SIZE + WRITE_SIZE of the M1 launch pair "
-                                           "(profiles/pmc_traffic.json, gfx950 wide-read "
-                                           "correction); includes Infinity-Cache hits")
     if exch is not None:
         res["with_exchange"] = exch
     if upd_res is not None:

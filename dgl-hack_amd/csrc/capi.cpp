@@ -354,6 +354,7 @@ void run_fast(const DGLMIGraph* g, const DGLMICsr& walk, int kind, int red, cons
     if (marked != nullptr && walk.num_cols * F * static_cast<int64_t>(sizeof(float)) >= kMarkedMinTableBytes) {
       a.indices = marked;
       a.marked = 1;
+      a.num_cols = walk.num_cols;
     }
   }
   if (epi) {

@@ -219,6 +219,7 @@ struct FastArgs {
   // marked rows are gathered non-temporally
   int marked;
   const float* xr;      // FAST_COL_TIE: the reduce's input, one row per walk row
+  int64_t num_cols;     // rows of the gathered table (policy-probe bound check)
 };
 int64_t fast_chunk_edges(int64_t nnz, int64_t F);
 int64_t fast_workspace_bytes(int64_t nnz, int64_t F);

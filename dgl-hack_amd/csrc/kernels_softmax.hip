@@ -115,7 +115,9 @@ __global__ void __launch_bounds__(kBlock) k_sm_rows(SoftmaxArgs a) {
         if constexpr (MODE == SM_STATS) {
           const float x = s[u][h];
           if (x > m[h]) {
-            l[h] = l[h] * expf(m[h] - x) + 1.0f;
+            // the new maximum's own term exp(x - x): 1, or NaN for x = +inf as in
+            // the reference's exp(score - max) (softmax.py:70-72)
+            l[h] = l[h] * expf(m[h] - x) + (x == INFINITY ? __builtin_nanf("") : 1.0f);
             m[h] = x;
           } else if (x != -INFINITY) {  // a masked logit adds exp(-inf) = 0
             l[h] += expf(x - m[h]);

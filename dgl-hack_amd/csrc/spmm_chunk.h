@@ -98,6 +98,19 @@ __device__ __forceinline__ float4 vtie(float4 a, float4 b, float4 g) {
   return make_float4(vtie(a.x, b.x, g.x), vtie(a.y, b.y, g.y), vtie(a.z, b.z, g.z), vtie(a.w, b.w, g.w));
 }
 
+// VAR bit 15: gathers by raw buffer loads, cold (bit-31-marked) rows with aux
+// policy (VAR >> 5) & 31, the others with (VAR >> 10) & 31 (aux: 1 = sc0,
+// 2 = nt, 16 = sc1) -- the cache-policy probe's variants.
+constexpr int kVarBuf = 1 << 15;
+constexpr int var_pol(int hot_aux, int cold_aux) { return 11 | kVarBuf | (cold_aux << 5) | (hot_aux << 10); }
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <int AUX>
+__device__ __forceinline__ float4 buf_ld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(off), 0, AUX);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                     __uint_as_float(v.w));
+}
+
 template <int KIND>
 constexpr bool needs_eid() {
   return KIND != FAST_COPY_COL && KIND != FAST_COL_TIE;
@@ -186,6 +199,8 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
   using V = typename VecT<VW>::T;
   const int F4 = static_cast<int>(a.F / VW);
   const V I = vident<VW, RED>();
+  [[maybe_unused]] const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x), 0, -1, 0x00020000);
   int hsel[NV];  // bcast: edge value index of each slot
   const int64_t wn = KIND == FAST_COL_MUL_EDGE_BCAST ? a.F / a.head_dim : 1;
 #pragma unroll
@@ -231,7 +246,18 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
           const int f4 = lane + v * L;
-          if constexpr ((VAR & 8) != 0 && KIND == FAST_COPY_COL) {
+          if constexpr ((VAR & kVarBuf) != 0 && KIND == FAST_COPY_COL && VW == 4) {
+            // cache-policy probe (scripts/policy_probe.py): marked / unmarked rows
+            // gathered by buffer loads with the aux policies encoded in VAR
+            // (table < 4 GiB: 32-bit byte offsets, checked by the launcher)
+            const bool cold = col < 0;
+            const uint32_t off = (static_cast<uint32_t>(col & 0x7fffffff) * static_cast<uint32_t>(a.F) +
+                                  static_cast<uint32_t>(VW * f4)) * 4u;
+            if (ok && f4 < F4)
+              val[u][v] = cold ? buf_ld4<(VAR >> 5) & 31>(rsrc, off) : buf_ld4<(VAR >> 10) & 31>(rsrc, off);
+            else
+              val[u][v] = I;
+          } else if constexpr ((VAR & 8) != 0 && KIND == FAST_COPY_COL) {
             // bit 31 of the column marks a cold source row (re-read fewer than
             // min_hot_degree times): gathered non-temporally so it does not evict
             // re-read rows from L2 / Infinity Cache (VAR & 16: the reverse, a
@@ -370,6 +396,11 @@ inline Cfg pick(int64_t slots, int vw) {
   return {64, 16};
 }
 
+inline int spmm_policy() {
+  const char* env = std::getenv("DGLMI_SPMM_POLICY");
+  return env ? std::atoi(env) : 0;
+}
+
 inline int spmm_variant() {
   const char* env = std::getenv("DGLMI_SPMM_VARIANT");
   return env ? std::atoi(env) : 3;
@@ -382,6 +413,24 @@ void run(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
   const unsigned blocks = static_cast<unsigned>((chunks + G - 1) / G);
   if constexpr (KIND == FAST_COPY_COL && RED == RED_SUM && NV == 1 && L >= 16 && VW == 4) {
     if (a.marked) {  // cold-row hints present (capi.cpp run_fast decides)
+      const int pol = spmm_policy();
+      if (pol > 0 && !has_epi(a) && a.num_cols * a.F * 4 <= (int64_t)UINT32_MAX) {
+        switch (pol) {
+#define DGLMI_POL(K_, H_, C_)                                                                    \
+  case K_:                                                                                     \
+    hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, var_pol(H_, C_)>), dim3(blocks),      \
+                       dim3(kBlock), 0, s, a, indptr);                                         \
+    break;
+          DGLMI_POL(1, 0, 2) DGLMI_POL(2, 0, 16) DGLMI_POL(3, 0, 17) DGLMI_POL(4, 0, 18)
+          DGLMI_POL(5, 0, 3) DGLMI_POL(6, 1, 2) DGLMI_POL(7, 16, 2) DGLMI_POL(8, 0, 0)
+          DGLMI_POL(9, 2, 2)
+#undef DGLMI_POL
+          default: break;
+        }
+        if (chunks > 1)
+          hipLaunchKernelGGL((k_chunk_fixup<RED, L, NV>), dim3(blocks), dim3(kBlock), 0, s, a, indptr);
+        return;
+      }
       if (has_epi(a))
         hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 11, true>), dim3(blocks), dim3(kBlock),
                            0, s, a, indptr);

@@ -263,6 +263,12 @@ int DGLMIEdgeSoftmaxBackward(const DGLMIGraph* graph, const DGLMIArray* out,
 int DGLMIPartitionLDG(int64_t num_nodes, const int64_t* indptr, const int64_t* indices,
                       int32_t num_parts, double slack, int64_t* assign);
 
+/* ---- measurement utility (bench.py; no reference counterpart) -------------
+ * dst[i] = src[i] for num_floats fp32 values (a multiple of 4, both 16-B aligned)
+ * by a float4 streaming copy: the access pattern MI355X_MICROARCH.md quotes the
+ * achievable HBM rate on, reported beside the 8 TB/s spec. */
+int DGLMIStreamCopy(const float* src, float* dst, int64_t num_floats, void* stream);
+
 #ifdef __cplusplus
 }  /* extern "C" */
 #endif
