@@ -155,6 +155,8 @@ _SIGS = {
         ctypes.c_void_p]),
     "DGLMICSRExpandRows": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "DGLMIStreamCopy": (ctypes.c_int, [
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
 }
 
 EXPORTED = tuple(_SIGS)
