@@ -102,6 +102,148 @@ def build_workload(world, rank, device, edges_per_gpu=EDGES_PER_GPU, scale0=SCAL
     return n, hi - lo, src.contiguous(), dst.contiguous(), x
 
 
+C4_NODES = 10_000_000
+C4_EDGES = 200_000_000
+
+
+def c4_workload(device, nodes=C4_NODES, edges=C4_EDGES, return_perm=False):
+    """Config C4: RMAT scale 24 with ids >= N rejected, N = 10 M,
+    E = 200 M, ids permuted (seed 3), X ~ U(-1, 1) of shape (N, 64) (seed 4)."""
+    scale = max(1, int(math.ceil(math.log2(nodes))))
+    srcs, dsts, have, seed = [], [], 0, 3
+    while have < edges:
+        want = int((edges - have) * 1.3) + 1024
+        s, d = rmat_edges(scale, want, seed=seed * 1000 + len(srcs), device=device)
+        ok = (s < nodes) & (d < nodes)
+        s, d = s[ok], d[ok]
+        take = min(edges - have, int(s.shape[0]))
+        srcs.append(s[:take])
+        dsts.append(d[:take])
+        have += take
+    src, dst = th.cat(srcs), th.cat(dsts)
+    gp = th.Generator(device=device)
+    gp.manual_seed(seed)
+    perm = th.randperm(nodes, generator=gp, device=device).to(th.int32)
+    src, dst = perm[src.long()], perm[dst.long()]
+    if return_perm:  # analysis only (scripts/halo_probe.py): the generator's id map
+        return src.contiguous(), dst.contiguous(), perm
+    del perm
+    gx = th.Generator(device=device)
+    gx.manual_seed(4)
+    x = th.rand(nodes, FEAT, generator=gx, device=device) * 2 - 1
+    return src.contiguous(), dst.contiguous(), x
+
+
+def measure_c4(world, rank, dist, cdev, device, args):
+    """C4 at fixed size (strong scaling): the 10 M-node / 200 M-edge RMAT graph
+    split over the ranks by the device label-propagation partitioner
+    (``dgl.distributed.partition_labelprop``, standing in for the reference's
+    METIS k-way); a step = the halo all-to-all-v of the remote source rows
+    (RCCL over xGMI) overlapped with the owned-source half of the aggregation,
+    then the halo half (``dgl.distributed.aggregate_with_halo``).  At N = 1 the
+    step is one copy_u_sum over the whole graph.  `value` = 200 M edges / step."""
+    from dgl import distributed as D
+    from dgl import kernel as K
+    from dgl.graph_index import device_block_gidx
+    t0 = time.time()
+    src, dst, x = c4_workload(device)
+    gidx = device_block_gidx(C4_NODES, C4_NODES, src, dst)
+    out_full = th.empty(C4_NODES, FEAT, device=device)
+    K.copy_reduce("sum", gidx, 0, x, out_full)
+    th.cuda.synchronize()
+    res = {"workload": "C4: RMAT scale 24 (ids >= 10M rejected), %d nodes, %d edges, feat %d"
+                       % (C4_NODES, C4_EDGES, FEAT), "scaling": "strong", "n_gpus": world,
+           "setup_s": None}
+    steps = max(1, args.steps)
+    if world == 1:
+        out = th.empty_like(out_full)
+        step = lambda: K.copy_reduce("sum", gidx, 0, x, out)
+        for _ in range(args.warmup):
+            step()
+        el = _timed(step, steps, None, None)
+        if not th.equal(out, out_full):
+            raise SystemExit("C4 copy_u_sum not deterministic")
+        res.update({"value": C4_EDGES * steps / el, "unit": "edges/s",
+                    "ms_per_step": el * 1e3 / steps, "partitioner": None,
+                    "setup_s": time.time() - t0})
+        return res
+    t1 = time.time()
+    assign, info = D.partition_labelprop(gidx, world, rounds=args.c4_rounds)
+    th.cuda.synchronize()
+    lp_s = time.time() - t1
+    # every rank computed the same labels (deterministic kernels); make sure of it
+    h = (assign.long() * th.arange(1, C4_NODES + 1, device=device) % 1000003).sum()
+    hs = th.tensor([float(h.item())], device=cdev, dtype=th.float64)
+    hmax, hmin = hs.clone(), hs.clone()
+    dist.all_reduce(hmax, op=dist.ReduceOp.MAX)
+    dist.all_reduce(hmin, op=dist.ReduceOp.MIN)
+    if float(hmax.item()) != float(hmin.item()):
+        raise SystemExit("ranks disagree on the partition")
+    stats_lp = D.partition_stats(src, dst, assign, world)
+    contig = D.contiguous_parts_device((gidx.in_csr.degrees() + 1).to(th.int32), world)
+    stats_ct = D.partition_stats(src, dst, contig, world)
+    del contig
+    part = D.build_partition_from_assignment(src, dst, assign, rank, None, world,
+                                             exchange="hybrid", tau=args.c4_tau)
+    pull = D.build_partition_from_assignment(src, dst, assign, rank, None, world)
+    pull.release_edges()
+    pull.split_gidx()
+    del gidx, src, dst
+    x_inner = x[part.inner_global].contiguous()
+    ref = out_full[part.inner_global]
+    del out_full, x
+    th.cuda.synchronize()
+    f = FEAT
+    bufs = D.hybrid_buffers(x_inner, part)
+    out = th.empty(part.n_inner, f, device=device)
+    step = lambda: D.aggregate_hybrid(x_inner, part, out, None, bufs)
+    send_p = th.empty(int(pull.send_counts.sum()), f, device=device)
+    recv_p = th.empty(pull.n_halo, f, device=device)
+    tmp_p = th.empty(pull.n_inner, f, device=device)
+    out_p = th.empty(pull.n_inner, f, device=device)
+    pstep = lambda: D.aggregate_with_halo(x_inner, pull, out_p, None, recv_p, send_p, tmp_p)
+    step()
+    pstep()
+    th.cuda.synchronize()
+    scale = ref.abs().max().clamp(min=1e-30)
+    err = _max_over_ranks(float((out - ref).abs().max() / scale), dist, cdev)
+    perr = _max_over_ranks(float((out_p - ref).abs().max() / scale), dist, cdev)
+    if max(err, perr) > 1e-4:
+        raise SystemExit("C4 partitioned copy_u_sum differs from the single-GPU one: "
+                         "hybrid %g, pull %g" % (err, perr))
+    for _ in range(args.warmup):
+        step()
+        pstep()
+    el = _timed(step, steps, dist, cdev)
+    pel = _timed(pstep, steps, dist, cdev)
+    rc, sc = pull.recv_counts.tolist(), pull.send_counts.tolist()
+    ex = _timed(lambda: D._a2av(recv_p, th.index_select(x_inner, 0, pull.send_idx, out=send_p),
+                                rc, sc, None), steps, dist, cdev)
+    moved = th.tensor([float(part.rows_moved()), float(pull.n_halo)], device=cdev,
+                      dtype=th.float64)
+    dist.all_reduce(moved)
+    res.update({"value": C4_EDGES * steps / el, "unit": "edges/s", "ms_per_step": el * 1e3 / steps,
+                "exchange": "hybrid: pulled rows + pushed partial sums (tau %d), two "
+                            "all-to-all-v (%s) overlapped with the owned-source SpMM"
+                            % (args.c4_tau, dist.get_backend()),
+                "rows_moved_per_step": int(moved[0].item()),
+                "bytes_moved_per_step": int(moved[0].item()) * 4 * f,
+                "pull_only": {"ms_per_step": pel * 1e3 / steps,
+                              "edges_per_s": C4_EDGES * steps / pel,
+                              "rows_moved_per_step": int(moved[1].item()),
+                              "exchange_only_ms": ex * 1e3 / steps},
+                "partitioner": "device label propagation, %d rounds, edge-balanced, slack 0.05 "
+                               "(%.2fs)" % (args.c4_rounds, lp_s),
+                "rel_err_vs_single_gpu": max(err, perr),
+                "halo_rows_pull": stats_lp["halo_rows"], "edges_per_part": stats_lp["edges"],
+                "cut_fraction": stats_lp["cut_edges"] / C4_EDGES,
+                "contiguous_partition": {"halo_rows_pull": stats_ct["halo_rows"],
+                                         "edges_per_part": stats_ct["edges"],
+                                         "cut_fraction": stats_ct["cut_edges"] / C4_EDGES},
+                "setup_s": time.time() - t0})
+    return res
+
+
 def make_local_graph(n_src, n_dst, src, dst, device):
     """Local in-CSR (rows = owned dst, cols = global src) built on the GPU."""
     from dgl.graph_index import device_block_gidx
@@ -442,6 +584,13 @@ def main():
                     help="N=1: skip the end-to-end DGLGraph.update_all measurement")
     ap.add_argument("--no-pmc", action="store_true",
                     help="N=1: skip the rocprofv3 PMC passes (roofline traffic)")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="skip the fixed-size C4 (10M / 200M, partitioned, with exchange) line")
+    ap.add_argument("--c4-rounds", type=int, default=24,
+                    help="label-propagation rounds of the C4 partition")
+    ap.add_argument("--c4-tau", type=int, default=8,
+                    help="C4 hybrid exchange: push a partial sum when a part holds >= tau "
+                         "sources of a destination")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.pmc_child:
@@ -662,6 +811,16 @@ def main():
             res["cpu_baseline"] = cpu_baseline(o_ptr, o_idx, x, n_dst)
         except Exception as exc:  # the baseline must never take the GPU line down
             res["cpu_baseline"] = {"value": None, "error": repr(exc)}
+    if not args.no_c4:
+        del gidx, o_ptr, o_idx, x, out
+        if part is not None:
+            del part
+        th.cuda.empty_cache()
+        try:
+            res["c4"] = measure_c4(world, rank, dist, cdev, device, args)
+        except SystemExit as exc:  # parity checks agree across ranks before exiting
+            res["c4"] = {"error": str(exc)}
+        log("C4: %s" % json.dumps(res["c4"]))
     if rank == 0:
         print(json.dumps(res), flush=True)
     if dist is not None:

@@ -783,6 +783,10 @@ GatArgs gat_args(const DGLMIGraph* g, const DGLMIArray* ft, const DGLMIArray* el
 
 }  // namespace
 
+namespace dglmi {
+void set_last_error(const char* msg) { g_last_error = msg ? msg : ""; }
+}  // namespace dglmi
+
 extern "C" {
 
 const char* DGLMIGetLastError(void) { return g_last_error.c_str(); }

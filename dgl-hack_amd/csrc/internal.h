@@ -127,6 +127,10 @@ __device__ __forceinline__ int64_t resolve(const Operand& o, int64_t row, int64_
   return id;
 }
 
+// Set the calling thread's DGLMIGetLastError() message (capi.cpp), for the C
+// entry points defined outside capi.cpp.
+void set_last_error(const char* msg);
+
 // ---- host-side launchers (defined in the .hip files) ------------------------
 void launch_fill(float* out, int64_t n, float value, hipStream_t s);
 void launch_fill_i32(int32_t* out, int64_t n, int32_t value, hipStream_t s);

@@ -155,6 +155,9 @@ _SIGS = {
         ctypes.c_void_p]),
     "DGLMICSRExpandRows": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "DGLMIPartitionLabelProp": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_void_p,
+        ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "DGLMIStreamCopy": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
 }

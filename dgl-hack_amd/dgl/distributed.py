@@ -76,130 +76,119 @@ def partition_assignment(num_nodes, src, dst, num_parts, method="contiguous"):
         return partition_contiguous(num_nodes, dst, num_parts)
     if method == "ldg":
         return partition_ldg(num_nodes, src, dst, num_parts)
+    if method == "labelprop":
+        dev = th.device("cuda", th.cuda.current_device())
+        s = th.as_tensor(np.asarray(src), dtype=th.int32, device=dev)
+        d = th.as_tensor(np.asarray(dst), dtype=th.int32, device=dev)
+        assign, _ = partition_labelprop(device_block_gidx(num_nodes, num_nodes, s, d), num_parts)
+        return assign.cpu().numpy().astype(np.int64)
     raise DGLError("unknown partition method %s" % method)
 
 
-# --------------------------------------------------------------------------- #
-# halo partitions
-# --------------------------------------------------------------------------- #
-class Partition:
-    """One rank's halo subgraph (``graph_op.cc:403-509`` with num_hops = 1).
-
-    Local source ids: ``[0, n_inner)`` are the owned nodes (``inner``, global ids
-    ascending), ``[n_inner, n_inner + n_halo)`` the halo nodes grouped by owner.
-    Local destination ids: ``[0, n_inner)``.  ``parent_eid`` maps local edges to
-    global edge ids (local edges keep global edge-id order).
-    """
-
-    def __init__(self, part_id, num_parts, inner, halo, halo_owner, local_src, local_dst,
-                 parent_eid, send_idx, send_counts, recv_counts):
-        self.part_id = part_id
-        self.num_parts = num_parts
-        self.inner = inner
-        self.halo = halo
-        self.halo_owner = halo_owner
-        self.n_inner = len(inner)
-        self.n_halo = len(halo)
-        self.local_src = local_src
-        self.local_dst = local_dst
-        self.parent_eid = parent_eid
-        self.send_idx = send_idx          # local inner ids, concatenated in peer order
-        self.send_counts = send_counts    # rows sent to each peer
-        self.recv_counts = recv_counts    # halo rows received from each peer
-        self._gidx = {}
-        self._dev = {}
-
-    def number_of_edges(self):
-        return int(self.local_src.shape[0])
-
-    def gidx(self, device):
-        """In/out CSRs of the local block (rows: n_inner dst, cols: n_inner + n_halo src)."""
-        key = str(device)
-        if key not in self._gidx:
-            n_src = self.n_inner + self.n_halo
-            n_dst = self.n_inner
-            out_csr = host_coo_to_csr(n_src, self.local_src, self.local_dst)
-            in_csr = host_csr_transpose(n_src, n_dst, *out_csr)
-
-            def mk(csr, rows_n, cols_n):
-                indptr, indices, data = csr
-                rows = np.repeat(np.arange(rows_n, dtype=np.int32), np.diff(indptr))
-                t = lambda a: th.from_numpy(np.ascontiguousarray(a, np.int32)).to(device)
-                return DeviceCSR(t(indptr), t(indices), t(data), t(rows), cols_n)
-
-            self._gidx[key] = ImmutableGraphIndex(mk(in_csr, n_dst, n_src), mk(out_csr, n_src, n_dst),
-                                                  n_src, n_dst, th.device(device), eid_perm=True)
-        return self._gidx[key]
-
-    def device_plan(self, device):
-        key = str(device)
-        if key not in self._dev:
-            self._dev[key] = th.from_numpy(self.send_idx).to(device)
-        return self._dev[key]
-
-    def local_graph(self, device):
-        """The local block as a DGLGraph over ``n_inner + n_halo`` nodes (owned
-        rows first; only they have in-edges), local edge k = global edge
-        ``parent_eid[k]`` -- what a whole-graph module (GATConv, RelGraphConv)
-        runs on once the halo rows are present."""
-        key = ("g", str(device))
-        if key not in self._dev:
-            from .graph import DGLGraph
-            t = lambda a: th.from_numpy(np.ascontiguousarray(a, np.int32)).to(device)
-            self._dev[key] = DGLGraph.from_device_coo(t(self.local_src), t(self.local_dst),
-                                                      self.n_inner + self.n_halo)
-        return self._dev[key]
-
-    def local_edge_data(self, edge_data):
-        """Rows of a global per-edge tensor for the local edges (in local order)."""
-        idx = th.from_numpy(self.parent_eid).to(edge_data.device)
-        return edge_data.index_select(0, idx)
+def contiguous_parts_device(weight, num_parts):
+    """Contiguous node-id blocks of equal total weight, on the device (int32)."""
+    c = th.cumsum(weight.double(), 0)
+    cuts = th.arange(1, num_parts, device=weight.device, dtype=th.float64) * (c[-1] / num_parts)
+    bounds = th.searchsorted(c, cuts)
+    return th.bucketize(th.arange(weight.shape[0], device=weight.device), bounds,
+                        right=True).to(th.int32)
 
 
-def build_partitions(src, dst, num_nodes, assign, parts=None, num_parts=None):
-    """Halo subgraphs of every (or the listed) partition, from the global edge list."""
-    src = np.asarray(src, np.int64)
-    dst = np.asarray(dst, np.int64)
-    assign = np.asarray(assign, np.int64)
-    k = num_parts if num_parts is not None else (int(assign.max()) + 1 if assign.size else 1)
-    eid = np.arange(src.shape[0], dtype=np.int64)
-    owner_dst = assign[dst]
-    inner = [np.nonzero(assign == p)[0] for p in range(k)]
-    local_of = np.empty(num_nodes, np.int64)
-    for p in range(k):
-        local_of[inner[p]] = np.arange(len(inner[p]))
-    halos = []
-    for p in range(k):
-        sel = owner_dst == p
-        s = src[sel]
-        remote = np.unique(s[assign[s] != p])
-        order = np.lexsort((remote, assign[remote]))
-        halos.append(remote[order])
-    out = []
-    for p in (range(k) if parts is None else parts):
-        sel = owner_dst == p
-        s, d, e = src[sel], dst[sel], eid[sel]
-        halo = halos[p]
-        loc = np.empty(num_nodes, np.int64)  # global -> local source id for this partition
-        loc[inner[p]] = np.arange(len(inner[p]))
-        loc[halo] = len(inner[p]) + np.arange(len(halo))
-        local_src = loc[s]
-        local_dst = local_of[d]
-        halo_owner = assign[halo]
-        recv_counts = np.bincount(halo_owner, minlength=k).astype(np.int64)
-        send_parts = []
-        send_counts = np.zeros(k, np.int64)
-        for q in range(k):
-            if q == p:
-                send_parts.append(np.empty(0, np.int64))
-                continue
-            need = halos[q][assign[halos[q]] == p]  # my nodes that q needs, in q's halo order
-            send_parts.append(local_of[need])
-            send_counts[q] = len(need)
-        send_idx = np.concatenate(send_parts) if send_parts else np.empty(0, np.int64)
-        out.append(Partition(p, k, inner[p], halo, halo_owner, local_src, local_dst, e, send_idx,
-                             send_counts, recv_counts))
-    return out
+def partition_labelprop(gidx, num_parts, rounds=24, slack=0.05, balance="edges", seed=0,
+                        init=None):
+    """Balanced label propagation ON THE DEVICE (``DGLMIPartitionLabelProp``).
+
+    Stands in for METIS k-way (``metis_partition.cc:19-66``), which the reference
+    runs on the symmetrised graph (``transform.py:617-618``): the symmetrised
+    adjacency here is the union of ``gidx``'s in- and out-CSR, so a
+    hundred-million-edge graph is partitioned where it lives, in a few hundred
+    milliseconds.  ``balance``: "edges" keeps every part's in-edges + nodes under
+    (1 + slack) x average (the aggregation's cost), "nodes" its node count (METIS's
+    default constraint).  ``init``: initial device int32 parts (default:
+    contiguous id blocks of equal weight).  Deterministic for a given seed.
+
+    Returns (assign int32 device tensor, {"loads", "cut_edges", "rounds"})."""
+    n = int(gidx.num_src)
+    if gidx.num_src != gidx.num_dst:
+        raise DGLError("partition_labelprop needs a square graph")
+    dev = gidx.in_csr.indptr.device
+    if balance == "edges":
+        weight = (gidx.in_csr.degrees() + 1).to(th.int32)
+    elif balance == "nodes":
+        weight = None
+    else:
+        raise DGLError("balance must be 'edges' or 'nodes'")
+    if init is None:
+        assign = contiguous_parts_device(weight if weight is not None else
+                                         th.ones(n, device=dev, dtype=th.int32), num_parts)
+    else:
+        assign = init.to(device=dev, dtype=th.int32).clone()
+    loads = np.zeros(num_parts, np.int64)
+    cut = np.zeros(1, np.int64)
+    g = gidx._cstruct_base()
+    _ffi.check_call(_ffi.lib().DGLMIPartitionLabelProp(
+        ctypes.byref(g), int(num_parts), int(rounds), ctypes.c_double(slack),
+        weight.data_ptr() if weight is not None else None, ctypes.c_uint64(seed),
+        assign.data_ptr(), loads.ctypes.data_as(ctypes.c_void_p),
+        cut.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(th.cuda.current_stream(dev).cuda_stream)))
+    return assign, {"loads": loads.tolist(), "cut_edges": int(cut[0]), "rounds": rounds}
+
+
+def partition_stats(src, dst, assign, num_parts):
+    """Per-part cost of a node assignment, on the device: owned nodes, local
+    in-edges (the aggregation's work), halo rows (distinct remote sources = rows
+    received per layer) and cut edges."""
+    a = assign.long()
+    n = a.shape[0]
+    pd = a[dst.long()]
+    ps = a[src.long()]
+    remote = ps != pd
+    keys = th.unique(pd[remote] * n + src.long()[remote])
+    halo = th.bincount(keys // n, minlength=num_parts)
+    return {"nodes": th.bincount(a, minlength=num_parts).tolist(),
+            "edges": th.bincount(pd, minlength=num_parts).tolist(),
+            "halo_rows": halo.tolist(), "cut_edges": int(remote.sum())}
+
+
+def relabel_by_parts(assign, num_parts):
+    """Node ids renumbered so that every part is a contiguous id range (parts in
+    order, ascending old id inside a part).  Returns (new2old int64, old2new
+    int64, bounds list of num_parts + 1)."""
+    new2old = th.sort(assign.long(), stable=True).indices
+    old2new = th.empty_like(new2old)
+    old2new[new2old] = th.arange(new2old.shape[0], device=new2old.device)
+    counts = th.bincount(assign.long(), minlength=num_parts).cpu().numpy()
+    bounds = [0] + np.cumsum(counts).tolist()
+    return new2old, old2new, bounds
+
+
+def build_partition_from_assignment(src, dst, assign, rank, group=None, num_parts=None,
+                                    exchange="pull", tau=8):
+    """Rank ``rank``'s halo partition for ANY node assignment (label propagation,
+    LDG, METIS output ...), planned on the device: the nodes are renumbered part
+    by part (:func:`relabel_by_parts`), so the partition is an id range of the
+    renumbered graph.  ``exchange="pull"`` plans the halo subgraph
+    (:func:`build_device_partition`), ``"hybrid"`` the pull / push-partial
+    exchange (:func:`build_hybrid_partition`, copy_u sums).  ``src`` / ``dst``:
+    the GLOBAL edge list (device).  The returned partition's ``inner_global``
+    holds the original ids of its owned rows (in local order) -- ``x[part.
+    inner_global]`` are its feature rows.  Collective over ``group``."""
+    k = num_parts if num_parts is not None else int(assign.max()) + 1
+    new2old, old2new, bounds = relabel_by_parts(assign, k)
+    lo, hi = bounds[rank], bounds[rank + 1]
+    keep = assign[dst.long()] == rank
+    s = old2new[src.long()[keep]]
+    d = old2new[dst.long()[keep]] - lo
+    del keep
+    if exchange == "pull":
+        part = build_device_partition(s, d, bounds, rank, group)
+    elif exchange == "hybrid":
+        part = build_hybrid_partition(s, d, bounds, rank, group, tau=tau)
+    else:
+        raise DGLError("exchange must be 'pull' or 'hybrid'")
+    part.inner_global = new2old[lo:hi]
+    part.halo_global = new2old[part.halo]
+    return part
 
 
 class DevicePartition:
@@ -225,10 +214,14 @@ class DevicePartition:
         self.local_dst = local_dst        # device int32, [0, n_inner)
         self._g = None
         self._split = None
+        self.inner_global = None          # device int64: set when ids were renumbered
+        self.halo_global = None
 
     @property
     def inner(self):
         """Global ids of the owned nodes (as :attr:`Partition.inner`)."""
+        if self.inner_global is not None:
+            return self.inner_global.cpu().numpy().astype(np.int64)
         return np.arange(self.lo, self.hi, dtype=np.int64)
 
     def number_of_edges(self):
@@ -307,6 +300,172 @@ def build_device_partition(src, dst, bounds, rank, group=None):
     del s, remote
     return DevicePartition(rank, world, lo, hi, halo, send_idx, send_counts, recv_counts, local,
                            dst.to(th.int32))
+
+
+class HybridPartition:
+    """A rank's share of a copy_u sum with a HYBRID exchange (pull rows / push
+    partial sums), planned on the device.
+
+    Pull-only halo exchange (:class:`DevicePartition`) moves one row per distinct
+    (remote source u, destination part q).  On power-law graphs many remote
+    sources of a hub destination v sit on the same part p; then p can sum them
+    itself and send ONE partial row for (v, p).  The planner picks, per
+    destination v and source part p, push when p holds >= ``tau`` distinct
+    sources of v, pull otherwise (a greedy vertex cover of the cut edges between
+    every two parts).  C4 at 8 parts: 15.2 M pulled rows -> 9.2 M rows in all
+    (``profiles/r02_halo_probe.json``).
+
+    Blocks (local ids; every edge is summed exactly once over all ranks):
+      * ``g_own``: owned sources -> owned destinations;
+      * ``g_push``: owned sources -> this rank's outgoing partial rows (grouped
+        by destination rank, the send buffer of the partial exchange);
+      * ``g_recv``: [pulled rows | received partial rows] -> owned destinations.
+    The reference's halo subgraphs (``graph_op.cc:403-509``) have no push side;
+    this is the MI355X path's own exchange."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+        self.inner_global = None
+        self.halo_global = None
+
+    @property
+    def inner(self):
+        if self.inner_global is not None:
+            return self.inner_global.cpu().numpy().astype(np.int64)
+        return np.arange(self.lo, self.hi, dtype=np.int64)
+
+    def rows_moved(self):
+        """Rows this rank receives per exchange (pulled + partial)."""
+        return self.n_halo + self.n_pin
+
+
+def _owner_of(ids, bounds_t):
+    return th.bucketize(ids, bounds_t[1:], right=True)
+
+
+def build_hybrid_partition(src, dst, bounds, rank, group=None, tau=8):
+    """Plan rank ``rank``'s hybrid exchange from its in-edges (``src`` GLOBAL
+    source ids, ``dst`` LOCAL destination ids, as :func:`build_device_partition`),
+    all on the device.  Collective over ``group``: one all-to-all of counts, one
+    of pulled ids, one of push-edge lists (each destination owner tells every
+    source owner which of its edges to sum into which partial row)."""
+    world = len(bounds) - 1
+    lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+    n_inner = hi - lo
+    dev = src.device
+    bt = th.tensor([int(b) for b in bounds], dtype=th.int64, device=dev)
+    s = src.long()
+    d = dst.long()
+    p = _owner_of(s, bt)
+    remote = p != rank
+    own_s, own_d = s[~remote] - lo, d[~remote]
+    rs, rd, rp = s[remote], d[remote], p[remote]
+    # distinct remote (u, v) -> c(v, p) = distinct sources of v on part p
+    pair_of_edge = rp * n_inner + rd                              # (p, v) sorted by p then v
+    uv = th.unique(rs * n_inner + rd)
+    uv_pair = _owner_of(uv // n_inner, bt) * n_inner + uv % n_inner
+    pairs, cnt = th.unique(uv_pair, return_counts=True)
+    pushed = pairs[cnt >= tau]                                    # sorted: by part, then v
+    if pushed.numel():
+        pos = th.searchsorted(pushed, pair_of_edge)
+        is_push = pushed[pos.clamp(max=pushed.numel() - 1)] == pair_of_edge
+    else:
+        pos = th.zeros_like(pair_of_edge)
+        is_push = th.zeros_like(pair_of_edge, dtype=th.bool)
+    # pulled rows (pull edges' distinct sources, grouped by owner: ids ascending)
+    ps_, pd_ = rs[~is_push], rd[~is_push]
+    halo = th.unique(ps_)
+    n_halo = int(halo.numel())
+    recv = th.diff(th.searchsorted(halo, bt))
+    # pushed pairs arriving from each peer (they land after the pulled rows)
+    pin_owner = pushed // n_inner
+    pin_counts = th.bincount(pin_owner, minlength=world)
+    n_pin = int(pushed.numel())
+    # receive block: pulled edges -> halo index, one edge per pushed pair -> n_halo + pair index
+    cols = th.cat([th.searchsorted(halo, ps_), n_halo + th.arange(n_pin, device=dev)])
+    rows = th.cat([pd_, pushed % n_inner])
+    g_recv = device_block_gidx(n_halo + n_pin, n_inner, cols.to(th.int32), rows.to(th.int32)) \
+        if cols.numel() else None
+    g_own = device_block_gidx(n_inner, n_inner, own_s.to(th.int32), own_d.to(th.int32))
+    # push-edge lists for every source owner: (u local on p, pair index within p's segment)
+    e_u = rs[is_push]
+    e_pair = pos[is_push]
+    seg_start = th.cumsum(pin_counts, 0) - pin_counts
+    e_owner = _owner_of(e_u, bt)
+    e_msg = (e_u - bt[e_owner]) * (1 << 31) + (e_pair - seg_start[e_owner])
+    e_msg = e_msg[th.argsort(e_owner, stable=True)]
+    e_counts = th.bincount(e_owner, minlength=world)
+    # one all-to-all of all counts: [pulled rows, partial rows, push edges] per peer
+    cnt_out = th.stack([recv, pin_counts, e_counts], 1).reshape(-1).contiguous()
+    cnt_in = th.empty_like(cnt_out)
+    _a2av(cnt_in, cnt_out, [3] * world, [3] * world, group)
+    cnt_in = cnt_in.view(world, 3).cpu().numpy().astype(np.int64)
+    recv_counts = recv.cpu().numpy().astype(np.int64)
+    send_counts = cnt_in[:, 0]
+    pout_counts = cnt_in[:, 1]                                    # partial rows I send to q
+    pin_counts_np = pin_counts.cpu().numpy().astype(np.int64)
+    req = th.empty(int(send_counts.sum()), dtype=th.int64, device=dev)
+    _a2av(req, halo, send_counts.tolist(), recv_counts.tolist(), group)
+    msgs = th.empty(int(cnt_in[:, 2].sum()), dtype=th.int64, device=dev)
+    _a2av(msgs, e_msg, cnt_in[:, 2].tolist(), e_counts.cpu().numpy().astype(np.int64).tolist(),
+          group)
+    # push block: rows = my outgoing partial rows (peer order), cols = owned sources
+    n_pout = int(pout_counts.sum())
+    msg_peer = th.repeat_interleave(th.arange(world, device=dev),
+                                    th.from_numpy(cnt_in[:, 2]).to(dev))
+    pout_start = th.from_numpy(np.cumsum(pout_counts) - pout_counts).to(dev)
+    push_rows = pout_start[msg_peer] + msgs % (1 << 31)
+    push_cols = msgs // (1 << 31)
+    g_push = device_block_gidx(n_inner, n_pout, push_cols.to(th.int32), push_rows.to(th.int32)) \
+        if n_pout else None
+    part = HybridPartition(part_id=rank, num_parts=world, lo=lo, hi=hi, n_inner=n_inner,
+                           halo=halo, n_halo=n_halo, send_idx=req - lo,
+                           send_counts=send_counts, recv_counts=recv_counts,
+                           n_pin=n_pin, pin_counts=pin_counts_np, n_pout=n_pout,
+                           pout_counts=pout_counts, g_own=g_own, g_recv=g_recv, g_push=g_push,
+                           tau=tau, n_push_edges_out=int(msgs.numel()))
+    return part
+
+
+def aggregate_hybrid(x_inner, part, out=None, group=None, bufs=None):
+    """copy_u_sum of a :class:`HybridPartition` (inference / benchmarking, no
+    autograd): the pulled rows' all-to-all-v goes first; the push block sums the
+    owned sources of every outgoing partial row and its all-to-all-v follows;
+    the owned block runs while both are in flight; then ONE pass over [pulled |
+    partial] rows adds onto it through the kernel epilogue's ``addend``.
+    ``bufs`` (from :func:`hybrid_buffers`) avoids per-call allocations."""
+    from . import kernel as K
+    if bufs is None:
+        bufs = hybrid_buffers(x_inner, part)
+    send, recv, pout, tmp = bufs["send"], bufs["recv"], bufs["pout"], bufs["tmp"]
+    if out is None:
+        out = x_inner.new_empty((part.n_inner,) + tuple(x_inner.shape[1:]))
+    th.index_select(x_inner, 0, part.send_idx, out=send)
+    w1 = _a2av_async(recv[:part.n_halo], send, part.recv_counts.tolist(),
+                     part.send_counts.tolist(), group)
+    if part.g_push is not None:
+        K.copy_reduce("sum", part.g_push, 0, x_inner, pout)
+    w2 = _a2av_async(recv[part.n_halo:], pout, part.pin_counts.tolist(),
+                     part.pout_counts.tolist(), group)
+    if part.g_recv is None:
+        K.copy_reduce("sum", part.g_own, 0, x_inner, out)
+        for w in (w1, w2):
+            if w is not None:
+                w.wait()
+        return out
+    K.copy_reduce("sum", part.g_own, 0, x_inner, tmp)
+    for w in (w1, w2):
+        if w is not None:
+            w.wait()
+    K.copy_reduce("sum", part.g_recv, 0, recv, out, epilogue=(None, None, None, tmp))
+    return out
+
+
+def hybrid_buffers(x_inner, part):
+    f = tuple(x_inner.shape[1:])
+    e = x_inner.new_empty
+    return {"send": e((int(part.send_counts.sum()),) + f), "recv": e((part.n_halo + part.n_pin,) + f),
+            "pout": e((part.n_pout,) + f), "tmp": e((part.n_inner,) + f)}
 
 
 # --------------------------------------------------------------------------- #

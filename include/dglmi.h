@@ -263,6 +263,23 @@ int DGLMIEdgeSoftmaxBackward(const DGLMIGraph* graph, const DGLMIArray* out,
 int DGLMIPartitionLDG(int64_t num_nodes, const int64_t* indptr, const int64_t* indices,
                       int32_t num_parts, double slack, int64_t* assign);
 
+/* Balanced label propagation on the device (extension replacing METIS k-way,
+ * metis_partition.cc:19-66, which metis_partition calls on the symmetrised graph,
+ * transform.py:589-630).  The symmetrised adjacency is the union of the graph's
+ * in-CSR and out-CSR (square graphs only; in_csr.rows required).  `assign`
+ * (device int32, num_nodes) holds the initial parts on entry and the final parts
+ * on return; each round every node of one hash half proposes the part most of its
+ * neighbours sit in when that beats its own, and proposals into part p are
+ * accepted with probability min(1, room_p / proposed_weight_p), room_p =
+ * (1 + slack) * total / num_parts - load_p.  node_weight: device int32 per node
+ * (NULL = 1).  Deterministic for a given seed.  part_loads (host, num_parts) and
+ * cut_edges (host; edges whose endpoints sit in different parts) may be NULL.
+ * num_parts <= 64.  Synchronises `stream` before returning. */
+int DGLMIPartitionLabelProp(const DGLMIGraph* graph, int32_t num_parts, int32_t rounds,
+                            double slack, const int32_t* node_weight, uint64_t seed,
+                            int32_t* assign, int64_t* part_loads, int64_t* cut_edges,
+                            void* stream);
+
 /* ---- measurement utility (bench.py; no reference counterpart) -------------
  * dst[i] = src[i] for num_floats fp32 values (a multiple of 4, both 16-B aligned)
  * by a float4 streaming copy: the access pattern MI355X_MICROARCH.md quotes the

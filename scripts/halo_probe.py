@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""How many rows must a C4 layer move at k = 8?  For a node assignment, the
+pull-only exchange moves every distinct (remote source, destination part) row;
+a hybrid exchange may instead push the partial sum of a destination v over the
+sources a part p holds for it (one row per (v, p)) when that replaces >= tau
+pulled rows' worth of edges.  Reports pull-only, push-only and greedy hybrid row
+counts for: contiguous ids (random), device label propagation, and -- for
+scale only -- the RMAT generator's own id-bit blocks (not available to a real
+partitioner: it reads the generator's id map)."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "dgl-hack_amd"))
+
+import torch as th  # noqa: E402
+
+import bench  # noqa: E402
+from dgl import distributed as D  # noqa: E402
+from dgl.graph_index import device_block_gidx  # noqa: E402
+
+
+def volumes(src, dst, a, k, n, taus):
+    s, d = src.long(), dst.long()
+    ps, pd = a[s].long(), a[d].long()
+    x = ps != pd
+    s, d, ps, pd = s[x], d[x], ps[x], pd[x]
+    pairs = th.unique(s * n + d)                  # distinct cross (u, v)
+    u, v = pairs // n, pairs % n
+    pu, pv = a[u].long(), a[v].long()
+    pull = int(th.unique(u * k + pv).numel())     # rows (u -> part of v)
+    vp, cnt = th.unique(v * k + pu, return_counts=True)
+    push = int(vp.numel())                        # partials (v <- part of u)
+    res = {"cross_edges": int(x.sum()), "pull_rows": pull, "push_rows": push, "hybrid": {}}
+    c_of_pair = cnt[th.searchsorted(vp, v * k + pu)]
+    for t in taus:
+        pushed = c_of_pair >= t
+        n_push = int((cnt >= t).sum())
+        rest = th.unique(u[~pushed] * k + pv[~pushed]).numel()
+        res["hybrid"][str(t)] = {"push_rows": n_push, "pull_rows": int(rest), "total": n_push + int(rest)}
+    return res
+
+
+def main():
+    dev = "cuda:0"
+    k, n = 8, bench.C4_NODES
+    src, dst, perm = bench.c4_workload(dev, return_perm=True)
+    taus = [2, 3, 4, 8, 16]
+    out = {}
+    g = device_block_gidx(n, n, src, dst)
+    w = (g.in_csr.degrees() + 1).to(th.int32)
+    ct = D.contiguous_parts_device(w, k).long()
+    out["contiguous"] = volumes(src, dst, ct, k, n, taus)
+    print("contiguous", json.dumps(out["contiguous"]), flush=True)
+    lp, _ = D.partition_labelprop(g, k, rounds=24)
+    out["labelprop"] = volumes(src, dst, lp.long(), k, n, taus)
+    print("labelprop", json.dumps(out["labelprop"]), flush=True)
+    inv = th.empty_like(perm.long())
+    inv[perm.long()] = th.arange(n, device=dev)
+    bits = (inv >> 21).clamp(max=k - 1)          # generator id >> 21: 8 blocks of 2^21
+    out["generator_bits"] = volumes(src, dst, bits, k, n, taus)
+    print("generator_bits", json.dumps(out["generator_bits"]), flush=True)
+    os.makedirs("gpurun_out", exist_ok=True)
+    json.dump(out, open("gpurun_out/halo_probe.json", "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
