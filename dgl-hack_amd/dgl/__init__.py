@@ -16,7 +16,8 @@ from .graph_index import GraphIndex  # noqa: F401
 from .heterograph import (DGLHeteroGraph, heterograph, graph, bipartite,  # noqa: F401
                           hetero_from_relations)
 from .transform import (laplacian_lambda_max, add_self_loop, remove_self_loop,  # noqa: F401
-                        reverse, to_bidirected)
+                        reverse, to_bidirected, metis_partition,
+                        partition_graph_with_halo)
 from . import transform  # noqa: F401
 from . import nn  # noqa: F401
 

@@ -191,6 +191,129 @@ def build_partition_from_assignment(src, dst, assign, rank, group=None, num_part
     return part
 
 
+# --------------------------------------------------------------------------- #
+# halo partitions
+# --------------------------------------------------------------------------- #
+class Partition:
+    """One rank's halo subgraph (``graph_op.cc:403-509`` with num_hops = 1).
+
+    Local source ids: ``[0, n_inner)`` are the owned nodes (``inner``, global ids
+    ascending), ``[n_inner, n_inner + n_halo)`` the halo nodes grouped by owner.
+    Local destination ids: ``[0, n_inner)``.  ``parent_eid`` maps local edges to
+    global edge ids (local edges keep global edge-id order).
+    """
+
+    def __init__(self, part_id, num_parts, inner, halo, halo_owner, local_src, local_dst,
+                 parent_eid, send_idx, send_counts, recv_counts):
+        self.part_id = part_id
+        self.num_parts = num_parts
+        self.inner = inner
+        self.halo = halo
+        self.halo_owner = halo_owner
+        self.n_inner = len(inner)
+        self.n_halo = len(halo)
+        self.local_src = local_src
+        self.local_dst = local_dst
+        self.parent_eid = parent_eid
+        self.send_idx = send_idx          # local inner ids, concatenated in peer order
+        self.send_counts = send_counts    # rows sent to each peer
+        self.recv_counts = recv_counts    # halo rows received from each peer
+        self._gidx = {}
+        self._dev = {}
+
+    def number_of_edges(self):
+        return int(self.local_src.shape[0])
+
+    def gidx(self, device):
+        """In/out CSRs of the local block (rows: n_inner dst, cols: n_inner + n_halo src)."""
+        key = str(device)
+        if key not in self._gidx:
+            n_src = self.n_inner + self.n_halo
+            n_dst = self.n_inner
+            out_csr = host_coo_to_csr(n_src, self.local_src, self.local_dst)
+            in_csr = host_csr_transpose(n_src, n_dst, *out_csr)
+
+            def mk(csr, rows_n, cols_n):
+                indptr, indices, data = csr
+                rows = np.repeat(np.arange(rows_n, dtype=np.int32), np.diff(indptr))
+                t = lambda a: th.from_numpy(np.ascontiguousarray(a, np.int32)).to(device)
+                return DeviceCSR(t(indptr), t(indices), t(data), t(rows), cols_n)
+
+            self._gidx[key] = ImmutableGraphIndex(mk(in_csr, n_dst, n_src), mk(out_csr, n_src, n_dst),
+                                                  n_src, n_dst, th.device(device), eid_perm=True)
+        return self._gidx[key]
+
+    def device_plan(self, device):
+        key = str(device)
+        if key not in self._dev:
+            self._dev[key] = th.from_numpy(self.send_idx).to(device)
+        return self._dev[key]
+
+    def local_graph(self, device):
+        """The local block as a DGLGraph over ``n_inner + n_halo`` nodes (owned
+        rows first; only they have in-edges), local edge k = global edge
+        ``parent_eid[k]`` -- what a whole-graph module (GATConv, RelGraphConv)
+        runs on once the halo rows are present."""
+        key = ("g", str(device))
+        if key not in self._dev:
+            from .graph import DGLGraph
+            t = lambda a: th.from_numpy(np.ascontiguousarray(a, np.int32)).to(device)
+            self._dev[key] = DGLGraph.from_device_coo(t(self.local_src), t(self.local_dst),
+                                                      self.n_inner + self.n_halo)
+        return self._dev[key]
+
+    def local_edge_data(self, edge_data):
+        """Rows of a global per-edge tensor for the local edges (in local order)."""
+        idx = th.from_numpy(self.parent_eid).to(edge_data.device)
+        return edge_data.index_select(0, idx)
+
+
+def build_partitions(src, dst, num_nodes, assign, parts=None, num_parts=None):
+    """Halo subgraphs of every (or the listed) partition, from the global edge list."""
+    src = np.asarray(src, np.int64)
+    dst = np.asarray(dst, np.int64)
+    assign = np.asarray(assign, np.int64)
+    k = num_parts if num_parts is not None else (int(assign.max()) + 1 if assign.size else 1)
+    eid = np.arange(src.shape[0], dtype=np.int64)
+    owner_dst = assign[dst]
+    inner = [np.nonzero(assign == p)[0] for p in range(k)]
+    local_of = np.empty(num_nodes, np.int64)
+    for p in range(k):
+        local_of[inner[p]] = np.arange(len(inner[p]))
+    halos = []
+    for p in range(k):
+        sel = owner_dst == p
+        s = src[sel]
+        remote = np.unique(s[assign[s] != p])
+        order = np.lexsort((remote, assign[remote]))
+        halos.append(remote[order])
+    out = []
+    for p in (range(k) if parts is None else parts):
+        sel = owner_dst == p
+        s, d, e = src[sel], dst[sel], eid[sel]
+        halo = halos[p]
+        loc = np.empty(num_nodes, np.int64)  # global -> local source id for this partition
+        loc[inner[p]] = np.arange(len(inner[p]))
+        loc[halo] = len(inner[p]) + np.arange(len(halo))
+        local_src = loc[s]
+        local_dst = local_of[d]
+        halo_owner = assign[halo]
+        recv_counts = np.bincount(halo_owner, minlength=k).astype(np.int64)
+        send_parts = []
+        send_counts = np.zeros(k, np.int64)
+        for q in range(k):
+            if q == p:
+                send_parts.append(np.empty(0, np.int64))
+                continue
+            need = halos[q][assign[halos[q]] == p]  # my nodes that q needs, in q's halo order
+            send_parts.append(local_of[need])
+            send_counts[q] = len(need)
+        send_idx = np.concatenate(send_parts) if send_parts else np.empty(0, np.int64)
+        out.append(Partition(p, k, inner[p], halo, halo_owner, local_src, local_dst, e, send_idx,
+                             send_counts, recv_counts))
+    return out
+
+
 class DevicePartition:
     """A rank's halo subgraph planned ON THE DEVICE for a contiguous (id-range)
     node partition -- the path for graphs whose edge lists only ever live in

@@ -6,15 +6,17 @@ config C4: synthetic RMAT, 10 M nodes / 200 M edges, feat 64).
   torchrun --nproc-per-node 8 --master-addr 127.0.0.1 examples/dist_gcn.py
 
 One process per GPU.  Every rank generates the same RMAT edge list on its GPU
-(seeded), owns a contiguous block of node ids (ids are randomly permuted, so
-blocks are balanced), keeps the in-edges of its nodes and plans its halo on
-the device (``dgl.distributed.build_device_partition``).  Each layer fetches
+(seeded), partitions it with the device label propagation
+(``dgl.distributed.partition_labelprop``, identical on every rank), keeps the
+in-edges of its nodes and plans its halo on the device
+(``dgl.distributed.build_partition_from_assignment``).  Each layer fetches
 the halo rows with one all-to-all-v (RCCL over xGMI), aggregates locally with
 the load-balanced HIP kernel (``DistGraphConv``); weight gradients go through
 one flattened all-reduce.  The reference keeps these pieces apart
 (METIS partition ``transform.py:589-630``, halo subgraphs ``graph_op.cc:403-509``,
 DDP all-reduce in ``examples/pytorch/graphsage/train_sampling_multi_gpu.py``);
-METIS is not available here, so the partition is by id range.
+METIS is not available here, so label propagation stands in for it
+(``--partition contiguous``: the previous id-range split).
 
 Prints one JSON line (rank 0): epoch time (max over ranks), edges/s, halo sizes.
 """
@@ -65,6 +67,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--dist-backend", default="nccl")
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (rehearsal)")
+    ap.add_argument("--partition", default="labelprop", choices=["labelprop", "contiguous"])
+    ap.add_argument("--lp-rounds", type=int, default=24)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -86,25 +90,30 @@ def main():
     n, m = args.nodes, args.edges
     t0 = time.time()
     src, dst = rmat_graph(n, m, dev)
-    bounds = [n * p // world for p in range(world + 1)]
-    lo, hi = bounds[rank], bounds[rank + 1]
-    # global degrees of the owned nodes: in-degree is local, out-degree is counted
-    # over the whole (identical on every rank) edge list
-    odeg = th.bincount(src[(src >= lo) & (src < hi)].long() - lo, minlength=hi - lo)
-    sel = (dst >= lo) & (dst < hi)
-    lsrc, ldst = src[sel], dst[sel] - lo
-    del src, dst, sel
-    ideg = th.bincount(ldst.long(), minlength=hi - lo)
-    part = D.build_device_partition(lsrc, ldst, bounds, rank)
+    # partition: device label propagation (the METIS stand-in) on the whole graph,
+    # identical on every rank (deterministic kernels); --partition contiguous keeps
+    # the id-range split.  The partition renumbers nodes part by part.
+    if args.partition == "labelprop" and world > 1:
+        from dgl.graph_index import device_block_gidx
+        assign, _ = D.partition_labelprop(device_block_gidx(n, n, src, dst), world,
+                                          rounds=args.lp_rounds)
+    else:
+        assign = D.contiguous_parts_device(th.ones(n, dtype=th.int32, device=dev), world) \
+            if world > 1 else th.zeros(n, dtype=th.int32, device=dev)
+    odeg_all = th.bincount(src.long(), minlength=n)
+    ideg_all = th.bincount(dst.long(), minlength=n)
+    part = D.build_partition_from_assignment(src, dst, assign, rank, None, world)
     part.release_edges()
-    del lsrc, ldst
+    inner = part.inner_global
+    odeg, ideg = odeg_all[inner], ideg_all[inner]
+    del src, dst, odeg_all, ideg_all
     th.cuda.synchronize()
     t_setup = time.time() - t0
 
     gx = th.Generator(device=dev)
     gx.manual_seed(7)
-    x = th.randn(n, args.feat, generator=gx, device=dev)[lo:hi].contiguous()
-    y = th.randint(0, args.classes, (n,), generator=gx, device=dev)[lo:hi]
+    x = th.randn(n, args.feat, generator=gx, device=dev)[inner].contiguous()
+    y = th.randint(0, args.classes, (n,), generator=gx, device=dev)[inner]
     th.manual_seed(0)
     l1 = D.DistGraphConv(args.feat, args.hidden, activation=th.relu).to(dev)
     l2 = D.DistGraphConv(args.hidden, args.classes).to(dev)
@@ -166,7 +175,10 @@ def main():
             "edge_visits_per_s": 3 * edges / (ms * 1e-3),
             "halo_rows_total": halo_rows, "max_halo_rows_per_rank": halo_max,
             "halo_bytes_per_layer_fwd": halo_rows * 4 * args.feat,
-            "loss": loss_v, "partition": "contiguous id ranges (permuted ids), device halo plan",
+            "loss": loss_v,
+            "partition": ("device label propagation, %d rounds" % args.lp_rounds
+                          if args.partition == "labelprop" else "contiguous id ranges")
+                         + ", device halo plan",
             "collectives": dist.get_backend() if dist is not None else "none"}), flush=True)
     if dist is not None:
         dist.barrier()

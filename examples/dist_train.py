@@ -11,9 +11,10 @@ the GPUs of one node:
   torchrun --nproc-per-node 4 --master-addr 127.0.0.1 examples/dist_train.py --model rgcn
 
 One process per GPU.  Every rank draws the same synthetic graph on its GPU
-(Chung-Lu power law, seeded; the datasets need downloads), owns a contiguous
-block of node ids and all their in-edges, plans its halo on the device
-(``dgl.distributed.build_device_partition``) and trains with
+(Chung-Lu power law, seeded; the datasets need downloads), partitions it with
+the device label propagation (``dgl.distributed.partition_labelprop``, the
+METIS stand-in), owns its part's nodes and all their in-edges, plans its halo
+on the device (``build_partition_from_assignment``) and trains with
 ``DistGATConv`` / ``DistRelGraphConv``: one all-to-all-v per layer and
 direction for the halo rows (RCCL over xGMI), the fused GAT kernel or the
 typed gather on the local block, one flattened gradient all-reduce per step.
@@ -88,17 +89,23 @@ def main():
     src, dst = chung_lu(n, m, cfg["alpha"], cfg["seed"], dev)
     gen = th.Generator(device=dev)
     gen.manual_seed(cfg["seed"] + 1)
-    bounds = [n * p // world for p in range(world + 1)]
-    lo, hi = bounds[rank], bounds[rank + 1]
-    sel = (dst >= lo) & (dst < hi)
+    # device label propagation (the METIS stand-in), identical on every rank
+    if world > 1:
+        from dgl.graph_index import device_block_gidx
+        assign, _ = D.partition_labelprop(device_block_gidx(n, n, src, dst), world)
+    else:
+        assign = th.zeros(n, dtype=th.int32, device=dev)
+    sel = assign[dst.long()] == rank   # local edge order = build_partition_from_assignment's
     if args.model == "rgcn":
         et = th.randint(0, cfg["rels"], (m,), generator=gen, device=dev)
         indeg = th.bincount(dst.long(), minlength=n).float().clamp(min=1)
         et_l = et[sel]
         norm_l = (1.0 / indeg)[dst[sel].long()].view(-1, 1)
         del et, indeg
-    part = D.build_device_partition(src[sel], dst[sel] - lo, bounds, rank)
+    part = D.build_partition_from_assignment(src, dst, assign, rank, None, world)
     del src, dst, sel
+    inner = part.inner_global
+    n_own = part.n_inner
     part.gidx()
     part.local_graph()
     th.cuda.synchronize()
@@ -106,15 +113,15 @@ def main():
 
     gx = th.Generator(device=dev)
     gx.manual_seed(7)
-    x = th.randn(hi - lo, cfg["feat"], generator=gx, device=dev)
-    y = th.randint(0, cfg["classes"], (hi - lo,), generator=gx, device=dev)
+    x = th.randn(n, cfg["feat"], generator=gx, device=dev)[inner].contiguous()
+    y = th.randint(0, cfg["classes"], (n,), generator=gx, device=dev)[inner]
     th.manual_seed(0)
     if args.model == "gat":
         l1 = D.DistGATConv(cfg["feat"], cfg["hidden"], cfg["heads"], activation=th.nn.functional.elu)
         l2 = D.DistGATConv(cfg["hidden"] * cfg["heads"], cfg["classes"], 1)
 
         def forward():
-            h = l1(part, x).reshape(hi - lo, -1)
+            h = l1(part, x).reshape(n_own, -1)
             return l2(part, h).mean(1)
     else:
         l1 = D.DistRelGraphConv(cfg["feat"], cfg["hidden"], cfg["rels"], "basis",
