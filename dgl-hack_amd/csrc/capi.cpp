@@ -1173,3 +1173,257 @@ int DGLMIEdgeSoftmaxBackward(const DGLMIGraph* graph, const DGLMIArray* out,
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// The hack's extra PackedFuncs (binary_reduce.cc:398-450): the R-GCN layer
+// kernels and the neighbour-access benchmark.  Relation transforms become dense
+// products over node rows and every edge only gathers (hack_kernels.hip); the
+// gathers run on the load-balanced reduce over relation-expanded column ids.
+// ---------------------------------------------------------------------------
+namespace {
+
+DGLMIGraph plain_graph(const DGLMIGraph* g) {
+  DGLMIGraph p = *g;
+  p.num_col_blocks = 0;
+  p.in_col_blocks = p.out_col_blocks = nullptr;
+  p.in_gather_cols = p.out_gather_cols = nullptr;
+  return p;
+}
+
+DGLMIGraph no_workspace() {
+  DGLMIGraph z;
+  std::memset(&z, 0, sizeof(z));
+  return z;
+}
+
+int64_t edge_values(const DGLMIArray* norm, int64_t E, const char* name) {
+  check_array(norm, name);
+  const int64_t n = norm->shape[0] * feat_numel(norm);
+  DGLMI_CHECK(norm->shape[0] == E && n == E, std::string(name) + " needs one value per edge");
+  return n;
+}
+
+// the out-CSR regrouped by relation-expanded source row (mode 0: t * N + u, mode
+// 1: u * R + t), stable: positions of a row keep their out-CSR order
+struct TypedOutCsr {
+  DGLMIGraph z = no_workspace();
+  Scratch keys, ptr, idx, dat, rows, ws;
+  DGLMICsr csr;
+  TypedOutCsr(const DGLMICsr& out, const int32_t* etypes, int64_t num_typed_rows, int64_t mul,
+              int mode, hipStream_t s)
+      : keys(&z, out.nnz * 4, s), ptr(&z, (num_typed_rows + 1) * 4, s), idx(&z, out.nnz * 4, s),
+        dat(&z, out.nnz * 4, s), rows(&z, out.nnz * 4, s),
+        ws(&z, DGLMICOOToCSRDeviceWorkspaceBytes(num_typed_rows, out.nnz), s) {
+    launch_typed_ids(out.rows, out.data, etypes, out.nnz, mul, mode, static_cast<int32_t*>(keys.ptr),
+                     s);
+    DGLMI_CHECK(DGLMICOOToCSRDevice(num_typed_rows, out.nnz, static_cast<int32_t*>(keys.ptr),
+                                    out.indices, out.data, static_cast<int32_t*>(ptr.ptr),
+                                    static_cast<int32_t*>(idx.ptr), static_cast<int32_t*>(dat.ptr),
+                                    ws.ptr, DGLMICOOToCSRDeviceWorkspaceBytes(num_typed_rows, out.nnz),
+                                    s) == 0,
+                "typed CSR build");
+    DGLMI_CHECK(DGLMICSRExpandRows(static_cast<int32_t*>(ptr.ptr), num_typed_rows, out.nnz,
+                                   static_cast<int32_t*>(rows.ptr), s) == 0,
+                "typed CSR rows");
+    csr.num_rows = num_typed_rows;
+    csr.num_cols = out.num_cols;
+    csr.nnz = out.nnz;
+    csr.indptr = static_cast<int32_t*>(ptr.ptr);
+    csr.indices = static_cast<int32_t*>(idx.ptr);
+    csr.data = static_cast<int32_t*>(dat.ptr);
+    csr.rows = static_cast<int32_t*>(rows.ptr);
+  }
+};
+
+void rgcn_common(const DGLMIGraph* g, const int32_t* etypes, int64_t rows_expanded) {
+  check_graph(g);
+  check_csr(g->in_csr, "in_csr", true);
+  check_csr(g->out_csr, "out_csr", true);
+  DGLMI_CHECK(g->in_csr.nnz == g->out_csr.nnz, "in/out CSR edge counts differ");
+  DGLMI_CHECK(g->in_csr.nnz == 0 || etypes != nullptr, "null etypes");
+  DGLMI_CHECK(rows_expanded < INT32_MAX, "relations x nodes exceeds int32 indexing");
+}
+
+void check_fast_width(int64_t F) {
+  DGLMI_CHECK(fast_supported(FAST_COL_MUL_EDGE_BCAST, F, F),
+              "unsupported feature width " + std::to_string(F));
+}
+
+}  // namespace
+
+extern "C" {
+
+int DGLMIRgcnLayer0(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* weight,
+                    const DGLMIArray* norm, DGLMIArray* ret, void* stream) {
+  API_BEGIN();
+  check_array(weight, "weight");
+  check_array(ret, "ret");
+  DGLMI_CHECK(weight->ndim == 3, "weight must be (num_rels, num_src, F)");
+  const int64_t R = weight->shape[0], N = weight->shape[1], F = weight->shape[2];
+  rgcn_common(graph, etypes, R * N);
+  const DGLMICsr& in = graph->in_csr;
+  DGLMI_CHECK(in.num_cols == N, "weight rows must equal the number of source nodes");
+  DGLMI_CHECK(ret->shape[0] == in.num_rows && feat_numel(ret) == F, "ret must be (num_dst, F)");
+  edge_values(norm, in.nnz, "norm");
+  check_fast_width(F);
+  DeviceGuard guard(graph->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  DGLMIGraph z = no_workspace(), pg = plain_graph(graph);
+  Scratch cols(&z, in.nnz * 4, s);
+  launch_typed_ids(in.indices, in.data, etypes, in.nnz, N, 0, static_cast<int32_t*>(cols.ptr), s);
+  DGLMICsr walk = in;
+  walk.indices = static_cast<int32_t*>(cols.ptr);
+  walk.num_cols = R * N;
+  run_fast(&pg, walk, FAST_COL_MUL_EDGE_BCAST, RED_SUM, weight->data, nullptr, norm->data, nullptr,
+           ret->data, F, F, s);
+  API_END();
+}
+
+int DGLMIRgcnLayer0Backward(const DGLMIGraph* graph, const int32_t* etypes,
+                            const DGLMIArray* grad_out, const DGLMIArray* norm,
+                            DGLMIArray* grad_weight, void* stream) {
+  API_BEGIN();
+  check_array(grad_out, "grad_out");
+  check_array(grad_weight, "grad_weight");
+  DGLMI_CHECK(grad_weight->ndim == 3, "grad_weight must be (num_rels, num_src, F)");
+  const int64_t R = grad_weight->shape[0], N = grad_weight->shape[1], F = grad_weight->shape[2];
+  rgcn_common(graph, etypes, R * N);
+  const DGLMICsr& out = graph->out_csr;
+  DGLMI_CHECK(out.num_rows == N, "grad_weight rows must equal the number of source nodes");
+  DGLMI_CHECK(grad_out->shape[0] == graph->in_csr.num_rows && feat_numel(grad_out) == F,
+              "grad_out must be (num_dst, F)");
+  edge_values(norm, out.nnz, "norm");
+  check_fast_width(F);
+  DeviceGuard guard(graph->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  DGLMIGraph pg = plain_graph(graph);
+  if (out.nnz == 0) {
+    launch_fill(grad_weight->data, R * N * F, 0.0f, s);
+    return 0;
+  }
+  TypedOutCsr typed(out, etypes, R * N, N, 0, s);
+  run_fast(&pg, typed.csr, FAST_COL_MUL_EDGE_BCAST, RED_SUM, grad_out->data, nullptr, norm->data,
+           nullptr, grad_weight->data, F, F, s);
+  API_END();
+}
+
+int DGLMIRgcnLayer1(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* hidden,
+                    const DGLMIArray* weight, const DGLMIArray* norm, DGLMIArray* ret,
+                    void* stream) {
+  API_BEGIN();
+  check_array(hidden, "hidden");
+  check_array(weight, "weight");
+  check_array(ret, "ret");
+  DGLMI_CHECK(weight->ndim == 3, "weight must be (num_rels, F_in, F_out)");
+  const int64_t R = weight->shape[0], K = weight->shape[1], X = weight->shape[2];
+  const DGLMICsr& in = graph ? graph->in_csr : DGLMICsr{};
+  rgcn_common(graph, etypes, R * in.num_cols);
+  DGLMI_CHECK(hidden->shape[0] == in.num_cols && feat_numel(hidden) == K,
+              "hidden must be (num_src, F_in)");
+  DGLMI_CHECK(ret->shape[0] == in.num_rows && feat_numel(ret) == X, "ret must be (num_dst, F_out)");
+  edge_values(norm, in.nnz, "norm");
+  check_fast_width(X);
+  DeviceGuard guard(graph->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t N = in.num_cols, M = R * X;
+  DGLMIGraph z = no_workspace(), pg = plain_graph(graph);
+  Scratch wcat(&z, K * M * 4, s), y(&z, N * M * 4, s), cols(&z, in.nnz * 4, s);
+  launch_permute_rkx(weight->data, R, K, X, true, static_cast<float*>(wcat.ptr), s);
+  // y[u, r * X + x] = sum_k hidden[u, k] w[r, k, x]; row u * R + r of the (N R, X) view
+  launch_gemm(hidden->data, K, 1, static_cast<float*>(wcat.ptr), M, 1, static_cast<float*>(y.ptr), N,
+              M, K, 1, nullptr, s);
+  launch_typed_ids(in.indices, in.data, etypes, in.nnz, R, 1, static_cast<int32_t*>(cols.ptr), s);
+  DGLMICsr walk = in;
+  walk.indices = static_cast<int32_t*>(cols.ptr);
+  walk.num_cols = N * R;
+  run_fast(&pg, walk, FAST_COL_MUL_EDGE_BCAST, RED_SUM, static_cast<float*>(y.ptr), nullptr,
+           norm->data, nullptr, ret->data, X, X, s);
+  API_END();
+}
+
+int DGLMIRgcnLayer1Backward(const DGLMIGraph* graph, const int32_t* etypes,
+                            const DGLMIArray* hidden, const DGLMIArray* weight,
+                            const DGLMIArray* norm, const DGLMIArray* grad_out,
+                            DGLMIArray* grad_hidden, DGLMIArray* grad_weight, void* stream) {
+  API_BEGIN();
+  check_array(hidden, "hidden");
+  check_array(weight, "weight");
+  check_array(grad_out, "grad_out");
+  check_array(grad_hidden, "grad_hidden");
+  check_array(grad_weight, "grad_weight");
+  DGLMI_CHECK(weight->ndim == 3 && grad_weight->ndim == 3, "weights must be (num_rels, F_in, F_out)");
+  const int64_t R = weight->shape[0], K = weight->shape[1], X = weight->shape[2];
+  for (int i = 0; i < 3; ++i) DGLMI_CHECK(grad_weight->shape[i] == weight->shape[i], "grad_weight shape");
+  const DGLMICsr& out = graph ? graph->out_csr : DGLMICsr{};
+  rgcn_common(graph, etypes, R * out.num_rows);
+  const int64_t N = out.num_rows, M = R * X;
+  DGLMI_CHECK(hidden->shape[0] == N && feat_numel(hidden) == K, "hidden must be (num_src, F_in)");
+  DGLMI_CHECK(grad_hidden->shape[0] == N && feat_numel(grad_hidden) == K, "grad_hidden shape");
+  DGLMI_CHECK(grad_out->shape[0] == graph->in_csr.num_rows && feat_numel(grad_out) == X,
+              "grad_out must be (num_dst, F_out)");
+  edge_values(norm, out.nnz, "norm");
+  check_fast_width(X);
+  DeviceGuard guard(graph->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  DGLMIGraph z = no_workspace(), pg = plain_graph(graph);
+  const int64_t splits = gemm_splits(K, M, N);
+  Scratch wcat(&z, K * M * 4, s), gy(&z, N * M * 4, s), gw(&z, K * M * 4, s),
+      parts(&z, splits > 1 ? splits * K * M * 4 : 0, s);
+  launch_permute_rkx(weight->data, R, K, X, true, static_cast<float*>(wcat.ptr), s);
+  // gy[u * R + t] = sum over out-edges of u with type t of norm_e * grad_out[v]
+  if (out.nnz > 0) {
+    TypedOutCsr typed(out, etypes, N * R, R, 1, s);
+    run_fast(&pg, typed.csr, FAST_COL_MUL_EDGE_BCAST, RED_SUM, grad_out->data, nullptr, norm->data,
+             nullptr, static_cast<float*>(gy.ptr), X, X, s);
+  } else {
+    launch_fill(static_cast<float*>(gy.ptr), N * M, 0.0f, s);
+  }
+  // grad_hidden = gy (N x RX) . wcat^T ; grad_wcat = hidden^T (K x N) . gy (split over N)
+  launch_gemm(static_cast<float*>(gy.ptr), M, 1, static_cast<float*>(wcat.ptr), 1, M,
+              grad_hidden->data, N, K, M, 1, nullptr, s);
+  launch_gemm(hidden->data, 1, K, static_cast<float*>(gy.ptr), M, 1, static_cast<float*>(gw.ptr), K,
+              M, N, splits, static_cast<float*>(parts.ptr), s);
+  launch_permute_rkx(static_cast<float*>(gw.ptr), R, K, X, false, grad_weight->data, s);
+  check_hip(hipGetLastError(), "rgcn layer1 backward launch");
+  API_END();
+}
+
+int DGLMINbAccess(const DGLMIGraph* graph, const DGLMIArray* feat, const int32_t* node_map,
+                  const int32_t* deg_inc_node_map, int32_t times, int32_t warm_up_times,
+                  double* avg_us, void* stream) {
+  API_BEGIN();
+  (void)node_map;          // the reference's sharding modes that read them are disabled
+  (void)deg_inc_node_map;  // (binary_reduce_impl.cu:779-900); accepted and ignored
+  check_graph(graph);
+  check_array(feat, "feat");
+  const DGLMICsr& in = graph->in_csr;
+  check_csr(in, "in_csr", true);
+  DGLMI_CHECK(feat->shape[0] == in.num_cols, "feat must have one row per source node");
+  DGLMI_CHECK(times > warm_up_times && warm_up_times >= 0, "need times > warm_up_times >= 0");
+  const int64_t F = feat_numel(feat);
+  DGLMI_CHECK(fast_supported(FAST_COPY_COL, F, 1), "unsupported feature width");
+  DeviceGuard guard(graph->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  DGLMIGraph z = no_workspace();
+  Scratch sink(&z, in.num_rows * F * 4, s);
+  hipEvent_t a, b;
+  check_hip(hipEventCreate(&a), "hipEventCreate");
+  check_hip(hipEventCreate(&b), "hipEventCreate");
+  double total = 0.0;
+  for (int i = 0; i < times; ++i) {
+    check_hip(hipEventRecord(a, s), "hipEventRecord");
+    run_fast(graph, in, FAST_COPY_COL, RED_SUM, feat->data, nullptr, nullptr, nullptr,
+             static_cast<float*>(sink.ptr), F, 1, s);
+    check_hip(hipEventRecord(b, s), "hipEventRecord");
+    check_hip(hipEventSynchronize(b), "hipEventSynchronize");
+    float ms = 0.0f;
+    check_hip(hipEventElapsedTime(&ms, a, b), "hipEventElapsedTime");
+    if (i >= warm_up_times) total += ms * 1e3;
+  }
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  if (avg_us) *avg_us = total / (times - warm_up_times);
+  API_END();
+}
+
+}  // extern "C"

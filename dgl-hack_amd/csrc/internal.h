@@ -279,4 +279,18 @@ void launch_gat_backward_src(const GatArgs& a, hipStream_t s);
 void launch_gat_merge(const float* out_part, const float* m_part, const float* l_part, int nb,
                       int64_t num_rows, int H, int D, float* out, float* m, float* l, hipStream_t s);
 
+// R-GCN C entries (hack_kernels.hip): relation-expanded ids (mode 0: etypes[eid] *
+// mul + id, mode 1: id * mul + etypes[eid]; eids NULL = position), the relation
+// weight layout (R, K, X) <-> (K, R * X), and C (M x N, row-major) = A . B with A,
+// B by (row, col) strides, the reduction split `splits` ways through `partials`
+// (splits * M * N floats) when splits > 1 (gemm_splits picks it).
+void launch_typed_ids(const int32_t* ids, const int32_t* eids, const int32_t* etypes, int64_t nnz,
+                      int64_t mul, int mode, int32_t* out, hipStream_t s);
+void launch_permute_rkx(const float* w, int64_t R, int64_t K, int64_t X, bool to_cat, float* out,
+                        hipStream_t s);
+int64_t gemm_splits(int64_t M, int64_t N, int64_t K);
+void launch_gemm(const float* A, int64_t a_rs, int64_t a_cs, const float* B, int64_t b_rs,
+                 int64_t b_cs, float* C, int64_t M, int64_t N, int64_t K, int64_t splits,
+                 float* partials, hipStream_t s);
+
 }  // namespace dglmi

@@ -158,6 +158,22 @@ _SIGS = {
     "DGLMIPartitionLabelProp": (ctypes.c_int, [
         ctypes.POINTER(Graph), ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_void_p,
         ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "DGLMIRgcnLayer0": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.c_void_p, ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.c_void_p]),
+    "DGLMIRgcnLayer0Backward": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.c_void_p, ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.c_void_p]),
+    "DGLMIRgcnLayer1": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.c_void_p, ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.c_void_p]),
+    "DGLMIRgcnLayer1Backward": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.c_void_p, ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_void_p]),
+    "DGLMINbAccess": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_double), ctypes.c_void_p]),
     "DGLMIStreamCopy": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
 }

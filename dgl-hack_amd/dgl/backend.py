@@ -206,21 +206,12 @@ def nb_access_bench(graph, feat, node_map=None, deg_inc_node_map=None, times=15,
     them (the compiler may drop the loads); here the timed launch is the
     load-balanced in-neighbour gather itself (copy_u_sum), whose result is kept
     so the gathers are real.  The node maps of the reference's disabled
-    sharding modes are accepted and ignored.  Returns (feat, average_us)."""
+    sharding modes are accepted and ignored (``DGLMINbAccess``, the C entry of
+    ``_CAPI_DGLNbAccess``).  Returns (feat, average_us)."""
     import sys
     gidx = graph if hasattr(graph, "in_csr") else graph._graph.get_immutable_gidx(feat.device)
     x = feat.contiguous().view(feat.shape[0], -1)
-    out = x.new_empty((gidx.in_csr.num_rows, x.shape[1]))
-    total = 0.0
-    for i in range(times):
-        a, b = th.cuda.Event(enable_timing=True), th.cuda.Event(enable_timing=True)
-        a.record()
-        K.copy_reduce("sum", gidx, SRC, x, out)
-        b.record()
-        b.synchronize()
-        if i >= warm_up_times:
-            total += a.elapsed_time(b) * 1e3
-    avg = total / max(1, times - warm_up_times)
+    avg = K.nb_access(gidx, x, node_map, deg_inc_node_map, times, warm_up_times)
     print("feat_len:%d num_nodes:%d num_edges:%d -- neighbour gather takes %.1f us on average"
           % (x.shape[1], gidx.in_csr.num_rows, gidx.in_csr.nnz, avg), file=sys.stderr)
     return feat, avg

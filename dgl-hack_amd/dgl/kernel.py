@@ -337,3 +337,62 @@ def edge_softmax_backward(graph, out, grad_out, grad_logits):
                                                    _arr(grad_out, "grad_out"),
                                                    _arr(grad_logits, "grad_logits"), _stream(out)))
     return grad_logits
+
+
+# --------------------------------------------------------------------------- #
+# the hack's extra kernels (kernel.py:156-169 of the reference)
+# --------------------------------------------------------------------------- #
+def _etypes(graph, etypes):
+    if not isinstance(etypes, th.Tensor) or etypes.dtype != th.int32 or etypes.device != graph.device:
+        raise DGLError("etypes must be an int32 tensor on the graph device (one entry per edge id)")
+    if etypes.numel() != graph.in_csr.nnz:
+        raise DGLError("etypes needs one entry per edge")
+    return ctypes.c_void_p(etypes.contiguous().data_ptr())
+
+
+def nb_access(graph, feat, node_map=None, deg_inc_node_map=None, times=15, warm_up_times=5):
+    """_CAPI_DGLNbAccess: time `times` in-neighbour row gathers of ``feat``; returns
+    the mean microseconds of the launches after the warm-ups."""
+    _check_ctx(graph, [("feat", feat)])
+    avg = ctypes.c_double(0.0)
+    check_call(_ffi.lib().DGLMINbAccess(
+        ctypes.byref(graph.cstruct(_workspace(graph, feat[0].numel(), feat.device))),
+        _arr(feat, "feat"), _map(node_map, "node_map"), _map(deg_inc_node_map, "deg_inc_node_map"),
+        int(times), int(warm_up_times), ctypes.byref(avg), _stream(feat)))
+    return avg.value
+
+
+def rgcn_layer0(graph, etypes, weight, norm, ret):
+    """_CAPI_DGLRgcnLayer0: ret[v] = sum_e weight[etypes[e], u] * norm[e]."""
+    _check_ctx(graph, [("weight", weight), ("norm", norm), ("ret", ret)])
+    check_call(_ffi.lib().DGLMIRgcnLayer0(
+        ctypes.byref(graph.cstruct()), _etypes(graph, etypes), _arr(weight, "weight"),
+        _arr(norm, "norm"), _arr(ret, "ret"), _stream(ret)))
+
+
+def rgcn_layer0_backward(graph, etypes, grad_out, norm, grad_weight):
+    """_CAPI_DGLRgcnLayer0Backward (exact sums over repeated (source, relation) pairs)."""
+    _check_ctx(graph, [("grad_out", grad_out), ("norm", norm), ("grad_weight", grad_weight)])
+    check_call(_ffi.lib().DGLMIRgcnLayer0Backward(
+        ctypes.byref(graph.cstruct()), _etypes(graph, etypes), _arr(grad_out, "grad_out"),
+        _arr(norm, "norm"), _arr(grad_weight, "grad_weight"), _stream(grad_out)))
+
+
+def rgcn_layer1(graph, etypes, hidden, weight, norm, ret):
+    """_CAPI_DGLRgcnLayer1: ret[v] = sum_e norm[e] * hidden[u] . weight[etypes[e]]."""
+    _check_ctx(graph, [("hidden", hidden), ("weight", weight), ("norm", norm), ("ret", ret)])
+    check_call(_ffi.lib().DGLMIRgcnLayer1(
+        ctypes.byref(graph.cstruct()), _etypes(graph, etypes), _arr(hidden, "hidden"),
+        _arr(weight, "weight"), _arr(norm, "norm"), _arr(ret, "ret"), _stream(ret)))
+
+
+def rgcn_layer1_backward(graph, etypes, hidden, weight, norm, grad_out, grad_hidden, grad_weight):
+    """_CAPI_DGLRgcnLayer1Backward: both gradients (the hack's wrapper drops the
+    weight gradient, tensor.py:493; it is returned here)."""
+    _check_ctx(graph, [("hidden", hidden), ("weight", weight), ("norm", norm),
+                       ("grad_out", grad_out), ("grad_hidden", grad_hidden),
+                       ("grad_weight", grad_weight)])
+    check_call(_ffi.lib().DGLMIRgcnLayer1Backward(
+        ctypes.byref(graph.cstruct()), _etypes(graph, etypes), _arr(hidden, "hidden"),
+        _arr(weight, "weight"), _arr(norm, "norm"), _arr(grad_out, "grad_out"),
+        _arr(grad_hidden, "grad_hidden"), _arr(grad_weight, "grad_weight"), _stream(grad_out)))

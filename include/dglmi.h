@@ -257,6 +257,47 @@ int DGLMIEdgeSoftmaxForward(const DGLMIGraph* graph, const DGLMIArray* logits, D
 int DGLMIEdgeSoftmaxBackward(const DGLMIGraph* graph, const DGLMIArray* out,
                              const DGLMIArray* grad_out, DGLMIArray* grad_logits, void* stream);
 
+/* ---- the hack's R-GCN layer kernels and neighbour-access benchmark -------------
+ * (_CAPI_DGLRgcnLayer0 / 0Backward / 1 / 1Backward / _CAPI_DGLNbAccess,
+ * binary_reduce.cc:398-450; kernels binary_reduce_impl.cu:779-1250).  The
+ * reference reads the relation of every edge from its graph object
+ * (GetCsrSortedByEdgeType); here it is the device int32 array `etypes`, one entry
+ * per edge id, each in [0, num_rels).  norm: one float per edge id ((E) or (E, 1)).
+ * Every output is overwritten.  Relation transforms run as one dense product over
+ * the node rows and every edge only gathers (the hack multiplies per edge).  The
+ * hack's Layer0Backward overwrites repeated (source, relation) pairs
+ * (binary_reduce_impl.cu:1004) and its Python wrapper drops Layer1's weight
+ * gradient (tensor.py:493); these return the exact sums. */
+/* _CAPI_DGLRgcnLayer0: ret[v, :] = sum_{e=(u->v)} weight[etypes[e], u, :] * norm[e];
+ * weight (R, N_src, F), ret (N_dst, F). */
+int DGLMIRgcnLayer0(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* weight,
+                    const DGLMIArray* norm, DGLMIArray* ret, void* stream);
+/* _CAPI_DGLRgcnLayer0Backward: grad_weight[t, u, :] = sum over the edges e of
+ * relation t out of u of grad_out[v, :] * norm[e]; grad_weight (R, N_src, F). */
+int DGLMIRgcnLayer0Backward(const DGLMIGraph* graph, const int32_t* etypes,
+                            const DGLMIArray* grad_out, const DGLMIArray* norm,
+                            DGLMIArray* grad_weight, void* stream);
+/* _CAPI_DGLRgcnLayer1: ret[v, :] = sum_e norm[e] * hidden[u, :] . weight[etypes[e]];
+ * hidden (N_src, F_in), weight (R, F_in, F_out), ret (N_dst, F_out). */
+int DGLMIRgcnLayer1(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* hidden,
+                    const DGLMIArray* weight, const DGLMIArray* norm, DGLMIArray* ret,
+                    void* stream);
+/* _CAPI_DGLRgcnLayer1Backward: grad_hidden[u] = sum_{e out of u} norm[e] * grad_out[v]
+ * . weight[t]^T; grad_weight[t] = sum_{e of relation t} norm[e] hidden[u]^T grad_out[v]. */
+int DGLMIRgcnLayer1Backward(const DGLMIGraph* graph, const int32_t* etypes,
+                            const DGLMIArray* hidden, const DGLMIArray* weight,
+                            const DGLMIArray* norm, const DGLMIArray* grad_out,
+                            DGLMIArray* grad_hidden, DGLMIArray* grad_weight, void* stream);
+/* _CAPI_DGLNbAccess: the in-neighbour gather benchmark.  Runs `times` in-neighbour
+ * row gathers of feat over the in-CSR (the load-balanced copy_u sum, into scratch;
+ * the reference's timed kernels read rows without using them) and writes the mean
+ * HIP-event time of the launches after the first `warm_up_times` to *avg_us (the
+ * reference logs it).  node_map / deg_inc_node_map feed the reference's disabled
+ * sharding modes and are ignored.  Synchronises `stream`. */
+int DGLMINbAccess(const DGLMIGraph* graph, const DGLMIArray* feat, const int32_t* node_map,
+                  const int32_t* deg_inc_node_map, int32_t times, int32_t warm_up_times,
+                  double* avg_us, void* stream);
+
 /* ---- partitioning (metis_partition.cc:19-66 replacement; METIS is absent) --
  * Linear Deterministic Greedy over a symmetrised host CSR (int64): node v goes
  * to the part maximising |N(v) ∩ P| (1 - |P| / C), C = ceil(n / k)(1 + slack). */

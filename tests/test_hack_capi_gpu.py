@@ -1,0 +1,137 @@
+"""C entries of the hack's extra PackedFuncs (``DGLMIRgcnLayer0/1[Backward]``,
+``DGLMINbAccess``; reference ``src/kernel/binary_reduce.cc:398-450``, kernels
+``src/kernel/cuda/binary_reduce_impl.cu:779-1250``) called through the C ABI,
+against fp64 restatements of the reference kernels' sums and against the Python
+path (``dgl.backend.rgcn_layer0/1``).  Where the hack's kernels are wrong (the
+layer-0 backward overwrites repeated (source, relation) pairs, :1004) the C
+entries return the exact sums; the restatements here are the exact sums."""
+import numpy as np
+import pytest
+import torch as th
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _graph(n, m, R, seed, hub=False):
+    import dgl
+    from graphs import powerlaw
+    rng = np.random.default_rng(seed)
+    if hub:
+        src, dst, n = powerlaw(n, m, seed=seed)
+    else:
+        src, dst = rng.integers(0, n, m), rng.integers(0, n, m)
+    # repeated (source, relation) pairs on purpose: the hack's layer-0 backward loses them
+    src[: m // 10] = src[0]
+    et = rng.integers(0, R, m)
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    gidx = g._graph.get_immutable_gidx(DEV)
+    norm = th.from_numpy(rng.uniform(0.1, 1.0, (m, 1))).float().to(DEV)
+    return g, gidx, th.from_numpy(src).to(DEV), th.from_numpy(dst).to(DEV), \
+        th.from_numpy(et).to(DEV), norm
+
+
+@pytest.mark.parametrize("F,hub", [(16, False), (7, False), (64, True)])
+def test_rgcn_layer0_fwd_bwd(F, hub):
+    from dgl import kernel as K
+    n, m, R = 600, 8000, 3
+    g, gidx, s, d, et, norm = _graph(n, m, R, seed=F, hub=hub)
+    n = g.number_of_nodes()
+    w = th.randn(R, n, F, device=DEV)
+    ret = th.full((n, F), float("nan"), device=DEV)
+    K.rgcn_layer0(gidx, et.int(), w, norm, ret)
+    ref = th.zeros(n, F, dtype=th.float64, device=DEV).index_add_(
+        0, d, w.double()[et, s] * norm.double())
+    mass = th.zeros(n, F, dtype=th.float64, device=DEV).index_add_(
+        0, d, (w.double()[et, s] * norm.double()).abs())
+    assert ((ret.double() - ref).abs() <= 1e-5 + 1e-6 * mass).all()
+    go = th.randn(n, F, device=DEV)
+    gw = th.full((R, n, F), float("nan"), device=DEV)
+    K.rgcn_layer0_backward(gidx, et.int(), go, norm, gw)
+    gref = th.zeros(R * n, F, dtype=th.float64, device=DEV).index_add_(
+        0, et * n + s, go.double()[d] * norm.double()).view(R, n, F)
+    th.testing.assert_close(gw.double(), gref, rtol=1e-5, atol=1e-5)
+    # same as the Python path's autograd (typed gather)
+    from dgl import backend as B
+    g.edata["t"] = et
+    wr = w.clone().requires_grad_()
+    out = B.rgcn_layer0(g, wr, norm, et)
+    out.backward(go)
+    th.testing.assert_close(out.detach(), ret, rtol=1e-5, atol=1e-5)
+    th.testing.assert_close(wr.grad, gw, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("K_in,X,hub", [(16, 16, False), (32, 8, True), (20, 5, False)])
+def test_rgcn_layer1_fwd_bwd(K_in, X, hub):
+    from dgl import kernel as K
+    n, m, R = 700, 9000, 4
+    g, gidx, s, d, et, norm = _graph(n, m, R, seed=K_in + X, hub=hub)
+    n = g.number_of_nodes()
+    h = th.randn(n, K_in, device=DEV)
+    w = th.randn(R, K_in, X, device=DEV) / 4
+    ret = th.full((n, X), float("nan"), device=DEV)
+    K.rgcn_layer1(gidx, et.int(), h, w, norm, ret)
+    msg = th.einsum("ek,ekx->ex", h.double()[s], w.double()[et]) * norm.double()
+    ref = th.zeros(n, X, dtype=th.float64, device=DEV).index_add_(0, d, msg)
+    mass = th.zeros(n, X, dtype=th.float64, device=DEV).index_add_(0, d, msg.abs())
+    assert ((ret.double() - ref).abs() <= 1e-4 + 1e-5 * mass).all()
+    go = th.randn(n, X, device=DEV)
+    gh = th.full((n, K_in), float("nan"), device=DEV)
+    gw = th.full((R, K_in, X), float("nan"), device=DEV)
+    K.rgcn_layer1_backward(gidx, et.int(), h, w, norm, go, gh, gw)
+    gmsg = go.double()[d] * norm.double()                        # (E, X)
+    gh_ref = th.zeros(n, K_in, dtype=th.float64, device=DEV).index_add_(
+        0, s, th.einsum("ex,ekx->ek", gmsg, w.double()[et]))
+    gw_ref = th.zeros(R, K_in, X, dtype=th.float64, device=DEV).index_add_(
+        0, et, th.einsum("ek,ex->ekx", h.double()[s], gmsg))
+    th.testing.assert_close(gh.double(), gh_ref, rtol=1e-4, atol=1e-4)
+    th.testing.assert_close(gw.double(), gw_ref, rtol=1e-4, atol=2e-4)
+    # the Python path (GEMM + typed gather, autograd) agrees
+    from dgl import backend as B
+    hr, wr = h.clone().requires_grad_(), w.clone().requires_grad_()
+    out = B.rgcn_layer1(g, hr, wr, norm, et)
+    out.backward(go)
+    th.testing.assert_close(out.detach(), ret, rtol=1e-4, atol=1e-4)
+    th.testing.assert_close(hr.grad, gh, rtol=1e-4, atol=1e-4)
+    th.testing.assert_close(wr.grad, gw, rtol=1e-4, atol=2e-4)
+
+
+def test_rgcn_gemm_split_k_large_n():
+    """Layer-1 weight gradient over many nodes takes the split-K GEMM path."""
+    from dgl import kernel as K
+    n, m, R, K_in, X = 60000, 200000, 2, 8, 8
+    g, gidx, s, d, et, norm = _graph(n, m, R, seed=3)
+    h = th.randn(n, K_in, device=DEV)
+    w = th.randn(R, K_in, X, device=DEV)
+    go = th.randn(n, X, device=DEV)
+    gh = th.empty(n, K_in, device=DEV)
+    gw = th.empty(R, K_in, X, device=DEV)
+    K.rgcn_layer1_backward(gidx, et.int(), h, w, norm, go, gh, gw)
+    gmsg = go.double()[d] * norm.double()
+    gw_ref = th.zeros(R, K_in, X, dtype=th.float64, device=DEV).index_add_(
+        0, et, th.einsum("ek,ex->ekx", h.double()[s], gmsg))
+    th.testing.assert_close(gw.double(), gw_ref, rtol=1e-4, atol=1e-3)
+
+
+def test_rgcn_rejects_bad_arguments():
+    from dgl import kernel as K
+    from dgl._ffi import DGLError
+    g, gidx, s, d, et, norm = _graph(100, 500, 2, seed=1)
+    w = th.randn(2, 100, 8, device=DEV)
+    ret = th.empty(100, 8, device=DEV)
+    with pytest.raises(DGLError, match="etypes"):
+        K.rgcn_layer0(gidx, et[:10].int(), w, norm, ret)
+    with pytest.raises(DGLError, match="norm"):
+        K.rgcn_layer0(gidx, et.int(), w, norm[:10], ret)
+    with pytest.raises(DGLError, match="source nodes"):
+        K.rgcn_layer0(gidx, et.int(), th.randn(2, 50, 8, device=DEV), norm, ret)
+
+
+def test_nb_access_times_the_gather():
+    from dgl import backend as B
+    g, gidx, s, d, et, norm = _graph(5000, 60000, 2, seed=2)
+    x = th.randn(5000, 64, device=DEV)
+    out, us = B.nb_access_bench(g, x, None, None, times=6, warm_up_times=2)
+    assert out is x and us > 0
