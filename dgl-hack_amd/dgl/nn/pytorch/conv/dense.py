@@ -116,7 +116,14 @@ class DenseChebConv(nn.Module):
         eye = th.eye(n, dtype=A.dtype, device=A.device)
         L = eye - dinv[:, None] * A * dinv[None, :]
         if lambda_max is None:
-            lambda_max = th.linalg.eigvals(L).real.max()
+            # the reference's th.eig takes every eigenvalue of a general matrix; a
+            # symmetric adjacency (undirected graph) gives a symmetric L, whose
+            # spectrum eigvalsh finds far faster (pass lambda_max, e.g. from
+            # dgl.laplacian_lambda_max, to skip the decomposition altogether)
+            if th.equal(A, A.transpose(0, 1)):
+                lambda_max = th.linalg.eigvalsh(L).max()
+            else:
+                lambda_max = th.linalg.eigvals(L).real.max()
         L_hat = 2 * L / lambda_max - eye
         Z = [eye]
         for i in range(1, self._k):
