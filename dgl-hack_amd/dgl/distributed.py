@@ -457,9 +457,23 @@ class HybridPartition:
             return self.inner_global.cpu().numpy().astype(np.int64)
         return np.arange(self.lo, self.hi, dtype=np.int64)
 
+    def number_of_edges(self):
+        """In-edges of the owned nodes (some of them summed by their sources' owners)."""
+        return self.n_in_edges
+
     def rows_moved(self):
         """Rows this rank receives per exchange (pulled + partial)."""
         return self.n_halo + self.n_pin
+
+    def send_graph(self):
+        """Block (sent-row slot -> owned row) of the pull plan: the reverse
+        exchange's gradients are summed per owned row by one SpMM over it."""
+        if getattr(self, "_send_g", None) is None:
+            n = int(self.send_idx.shape[0])
+            self._send_g = device_block_gidx(
+                n, self.n_inner, th.arange(n, device=self.send_idx.device, dtype=th.int32),
+                self.send_idx.to(th.int32))
+        return self._send_g
 
 
 def _owner_of(ids, bounds_t):
@@ -546,7 +560,8 @@ def build_hybrid_partition(src, dst, bounds, rank, group=None, tau=8):
                            send_counts=send_counts, recv_counts=recv_counts,
                            n_pin=n_pin, pin_counts=pin_counts_np, n_pout=n_pout,
                            pout_counts=pout_counts, g_own=g_own, g_recv=g_recv, g_push=g_push,
-                           tau=tau, n_push_edges_out=int(msgs.numel()))
+                           tau=tau, n_push_edges_out=int(msgs.numel()),
+                           n_in_edges=int(s.numel()))
     return part
 
 
@@ -582,6 +597,94 @@ def aggregate_hybrid(x_inner, part, out=None, group=None, bufs=None):
             w.wait()
     K.copy_reduce("sum", part.g_recv, 0, recv, out, epilogue=(None, None, None, tmp))
     return out
+
+
+class HybridAggregate(th.autograd.Function):
+    """Differentiable copy_u sum over a :class:`HybridPartition` with GraphConv's
+    epilogue: out = (sum over the in-edges of x) * row_mul + bias.  Forward as
+    :func:`aggregate_hybrid`.  Backward: the gradient of the received rows is one
+    SpMM over the receive block's out-CSR; pulled-row gradients go back to their
+    owners and partial-row gradients back to their pushers with the reverse
+    all-to-all-v; the owner sums what it gets back per row with one SpMM over the
+    send plan (deterministic, no atomics), the pusher walks its push block
+    backwards.  row_mul is a constant (no gradient)."""
+
+    @staticmethod
+    def forward(ctx, x_inner, bias, part, row_mul, group):
+        from . import kernel as K
+        x = x_inner.contiguous()
+        f = tuple(x.shape[1:])
+        send = x.new_empty((int(part.send_counts.sum()),) + f)
+        recv = x.new_empty((part.n_halo + part.n_pin,) + f)
+        pout = x.new_empty((part.n_pout,) + f)
+        out = x.new_empty((part.n_inner,) + f)
+        th.index_select(x, 0, part.send_idx, out=send)
+        w1 = _a2av_async(recv[:part.n_halo], send, part.recv_counts.tolist(),
+                         part.send_counts.tolist(), group)
+        if part.g_push is not None:
+            K.copy_reduce("sum", part.g_push, 0, x, pout)
+        w2 = _a2av_async(recv[part.n_halo:], pout, part.pin_counts.tolist(),
+                         part.pout_counts.tolist(), group)
+        if part.g_recv is None:
+            K.copy_reduce("sum", part.g_own, 0, x, out, epilogue=(row_mul, None, bias))
+        else:
+            tmp = x.new_empty(out.shape)
+            K.copy_reduce("sum", part.g_own, 0, x, tmp, epilogue=(row_mul, None, None))
+        for w in (w1, w2):
+            if w is not None:
+                w.wait()
+        if part.g_recv is not None:
+            K.copy_reduce("sum", part.g_recv, 0, recv, out, epilogue=(row_mul, None, bias, tmp))
+        ctx.part, ctx.group, ctx.has_bias = part, group, bias is not None
+        ctx.save_for_backward(x, out, recv, row_mul)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        from . import kernel as K
+        x, out, recv, row_mul = ctx.saved_tensors
+        part, group = ctx.part, ctx.group
+        g = grad_out.contiguous()
+        gs = (g * row_mul.view(-1, 1)).contiguous() if row_mul is not None else g
+        f = tuple(x.shape[1:])
+        gx = th.empty_like(x)
+        K.backward_copy_reduce("sum", part.g_own, 0, x, out, gs, gx)
+        if part.g_recv is not None:
+            grecv = th.empty_like(recv)
+            K.backward_copy_reduce("sum", part.g_recv, 0, recv, out, gs, grecv)
+            gpull = x.new_empty((int(part.send_counts.sum()),) + f)
+            gpart = x.new_empty((part.n_pout,) + f)
+            w1 = _a2av_async(gpull, grecv[:part.n_halo], part.send_counts.tolist(),
+                             part.recv_counts.tolist(), group)
+            w2 = _a2av_async(gpart, grecv[part.n_halo:].contiguous(), part.pout_counts.tolist(),
+                             part.pin_counts.tolist(), group)
+        else:
+            w1 = w2 = None
+            gpull = x.new_empty((int(part.send_counts.sum()),) + f)
+            gpart = x.new_empty((part.n_pout,) + f)
+            _a2av(gpull, x.new_empty((0,) + f), part.send_counts.tolist(),
+                  part.recv_counts.tolist(), group)
+            _a2av(gpart, x.new_empty((0,) + f), part.pout_counts.tolist(),
+                  part.pin_counts.tolist(), group)
+        for w in (w1, w2):
+            if w is not None:
+                w.wait()
+        if gpull.shape[0]:
+            back = th.empty_like(x)
+            K.copy_reduce("sum", part.send_graph(), 0, gpull, back)
+            gx += back
+        if part.g_push is not None and gpart.shape[0]:
+            back = th.empty_like(x)
+            K.backward_copy_reduce("sum", part.g_push, 0, x, gpart, gpart, back)
+            gx += back
+        gb = g.reshape(-1, g.shape[-1]).sum(0) if ctx.has_bias and ctx.needs_input_grad[1] else None
+        return gx, gb, None, None, None
+
+
+def hybrid_aggregate(x_inner, part, row_mul=None, bias=None, group=None):
+    """Differentiable :func:`aggregate_hybrid` with GraphConv's norm and bias
+    fused (:class:`HybridAggregate`)."""
+    return HybridAggregate.apply(x_inner, bias, part, row_mul, group)
 
 
 def hybrid_buffers(x_inner, part):
@@ -725,7 +828,9 @@ def allreduce_gradients(params, group=None, average=True):
 class DistGraphConv(th.nn.Module):
     """GraphConv on a halo partition: identical math to
     ``dgl.nn.pytorch.GraphConv`` on the whole graph (``graphconv.py:103-178``),
-    with global degrees for the normaliser and one halo exchange per layer."""
+    with global degrees for the normaliser and one halo exchange per layer (pull
+    for a :class:`DevicePartition` / :class:`Partition`, pull + push-partial for a
+    :class:`HybridPartition`)."""
 
     def __init__(self, in_feats, out_feats, norm="both", bias=True, activation=None):
         super().__init__()
@@ -737,7 +842,8 @@ class DistGraphConv(th.nn.Module):
         out-/in-degrees of the owned nodes."""
         from . import backend as B
         conv = self.conv
-        gidx = part.gidx(feat.device)
+        hybrid = isinstance(part, HybridPartition)
+        gidx = None if hybrid else part.gidx(feat.device)
         if conv._norm == "both":
             norm = th.pow(out_deg_inner.float().clamp(min=1), -0.5)
             feat = feat * norm.reshape(norm.shape + (1,) * (feat.dim() - 1))
@@ -746,7 +852,15 @@ class DistGraphConv(th.nn.Module):
         if conv._norm != "none":
             degs = in_deg_inner.float().clamp(min=1)
             dnorm = th.pow(degs, -0.5) if conv._norm == "both" else 1.0 / degs
-        if feat.dim() == 2 and feat.dtype == th.float32:
+        if hybrid:
+            # pull / push-partial exchange (HybridPartition); norm and bias fused
+            if feat.dim() != 2 or feat.dtype != th.float32:
+                raise DGLError("the hybrid exchange takes 2-D float32 features")
+            if conv._in_feats > conv._out_feats:
+                rst = hybrid_aggregate(B.project(feat, w), part, dnorm, conv.bias, group)
+            else:
+                rst = B.project(hybrid_aggregate(feat, part, dnorm, None, group), w, conv.bias)
+        elif feat.dim() == 2 and feat.dtype == th.float32:
             # norm and bias fused into the aggregation kernel (GraphConv._fused_forward)
             if conv._in_feats > conv._out_feats:
                 full = halo_exchange(B.project(feat, w), part, group)

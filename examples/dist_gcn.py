@@ -9,9 +9,11 @@ One process per GPU.  Every rank generates the same RMAT edge list on its GPU
 (seeded), partitions it with the device label propagation
 (``dgl.distributed.partition_labelprop``, identical on every rank), keeps the
 in-edges of its nodes and plans its halo on the device
-(``dgl.distributed.build_partition_from_assignment``).  Each layer fetches
-the halo rows with one all-to-all-v (RCCL over xGMI), aggregates locally with
-the load-balanced HIP kernel (``DistGraphConv``); weight gradients go through
+(``dgl.distributed.build_partition_from_assignment``).  Each layer exchanges
+halo rows (RCCL all-to-all-v over xGMI; by default the hybrid exchange: pulled
+rows plus partial sums pushed by the parts that hold many sources of a
+destination) and aggregates locally with the load-balanced HIP kernel
+(``DistGraphConv``); weight gradients go through
 one flattened all-reduce.  The reference keeps these pieces apart
 (METIS partition ``transform.py:589-630``, halo subgraphs ``graph_op.cc:403-509``,
 DDP all-reduce in ``examples/pytorch/graphsage/train_sampling_multi_gpu.py``);
@@ -69,6 +71,8 @@ def main():
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (rehearsal)")
     ap.add_argument("--partition", default="labelprop", choices=["labelprop", "contiguous"])
     ap.add_argument("--lp-rounds", type=int, default=24)
+    ap.add_argument("--exchange", default="hybrid", choices=["hybrid", "pull"],
+                    help="halo exchange: pulled rows + pushed partial sums, or pulled rows only")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -102,8 +106,10 @@ def main():
             if world > 1 else th.zeros(n, dtype=th.int32, device=dev)
     odeg_all = th.bincount(src.long(), minlength=n)
     ideg_all = th.bincount(dst.long(), minlength=n)
-    part = D.build_partition_from_assignment(src, dst, assign, rank, None, world)
-    part.release_edges()
+    part = D.build_partition_from_assignment(src, dst, assign, rank, None, world,
+                                             exchange=args.exchange)
+    if args.exchange == "pull":
+        part.release_edges()
     inner = part.inner_global
     odeg, ideg = odeg_all[inner], ideg_all[inner]
     del src, dst, odeg_all, ideg_all
@@ -145,7 +151,8 @@ def main():
     if dist is not None:
         dist.barrier()
     el = time.perf_counter() - t
-    stats = th.tensor([el, float(part.n_halo), float(part.number_of_edges())], dtype=th.float64,
+    moved = part.rows_moved() if args.exchange == "hybrid" else part.n_halo
+    stats = th.tensor([el, float(moved), float(part.number_of_edges())], dtype=th.float64,
                       device=cdev)
     if dist is not None:
         mx = stats.clone()
@@ -178,7 +185,7 @@ def main():
             "loss": loss_v,
             "partition": ("device label propagation, %d rounds" % args.lp_rounds
                           if args.partition == "labelprop" else "contiguous id ranges")
-                         + ", device halo plan",
+                         + ", device halo plan, %s exchange" % args.exchange,
             "collectives": dist.get_backend() if dist is not None else "none"}), flush=True)
     if dist is not None:
         dist.barrier()

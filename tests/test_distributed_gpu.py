@@ -26,6 +26,11 @@ def _worker(rank, world, src, dst, n, q, planner):
     if planner == "host_ldg":
         assign = D.partition_assignment(n, src, dst, world, "ldg")
         part = D.build_partitions(src, dst, n, assign, num_parts=world)[rank]
+    elif planner == "device_lp_hybrid":  # label propagation + pull / push-partial exchange
+        s_d, d_d = th.from_numpy(src).to(dev).int(), th.from_numpy(dst).to(dev).int()
+        assign, _ = D.partition_labelprop(D.device_block_gidx(n, n, s_d, d_d), world, rounds=8)
+        part = D.build_partition_from_assignment(s_d, d_d, assign, rank, None, world,
+                                                 exchange="hybrid", tau=2)
     else:  # contiguous id ranges, halo plan built on the device
         bounds = [n * p // world for p in range(world + 1)]
         lo, hi = bounds[rank], bounds[rank + 1]
@@ -64,7 +69,7 @@ def _worker(rank, world, src, dst, n, q, planner):
         q.put("ok")
 
 
-@pytest.mark.parametrize("planner", ["host_ldg", "device_contiguous"])
+@pytest.mark.parametrize("planner", ["host_ldg", "device_contiguous", "device_lp_hybrid"])
 def test_dist_gcn_matches_single_gpu(planner):
     import torch.multiprocessing as mp
     from dist_util import run_world
@@ -132,6 +137,12 @@ def _gat_rgcn_worker(rank, world, src, dst, et, n, q, planner):
         assign = D.partition_assignment(n, src, dst, world, "ldg")
         part = D.build_partitions(src, dst, n, assign, num_parts=world)[rank]
         et_l, norm_l = part.local_edge_data(et_t), part.local_edge_data(norm)
+    elif planner == "device_lp":  # label propagation, renumbered partition, pull exchange
+        s_d, d_d = th.from_numpy(src).to(dev).int(), th.from_numpy(dst).to(dev).int()
+        assign, _ = D.partition_labelprop(D.device_block_gidx(n, n, s_d, d_d), world, rounds=8)
+        part = D.build_partition_from_assignment(s_d, d_d, assign, rank, None, world)
+        keep = assign[d_d.long()] == rank  # local edge order: the global order, kept edges
+        et_l, norm_l = et_t[keep], norm[keep]
     else:
         bounds = [n * p // world for p in range(world + 1)]
         lo, hi = bounds[rank], bounds[rank + 1]
@@ -173,7 +184,7 @@ def _gat_rgcn_worker(rank, world, src, dst, et, n, q, planner):
         q.put("ok")
 
 
-@pytest.mark.parametrize("planner", ["host_ldg", "device_contiguous"])
+@pytest.mark.parametrize("planner", ["host_ldg", "device_contiguous", "device_lp"])
 def test_dist_gat_and_rgcn_match_single_gpu(planner):
     """DistGATConv (fused GAT on the local block, ft/el halo rows exchanged) and
     DistRelGraphConv (x halo rows exchanged, typed gather on the local block):
