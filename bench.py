@@ -51,6 +51,16 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 def log(*a):
     if int(os.environ.get("RANK", "0")) == 0:
         print(*a, file=sys.stderr, flush=True)
+    trace(*a)
+
+
+def trace(*a):
+    """Per-rank progress file (DGLMI_BENCH_TRACE=dir): where every rank is."""
+    d = os.environ.get("DGLMI_BENCH_TRACE")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "rank%s.log" % os.environ.get("RANK", "0")), "a") as fh:
+            fh.write("%.2f %s\n" % (time.time(), " ".join(str(x) for x in a)))
 
 
 def rmat_edges(scale, num_edges, seed, device, chunk=25_000_000):
@@ -146,13 +156,15 @@ def measure_c4(world, rank, dist, cdev, device, args):
     from dgl import kernel as K
     from dgl.graph_index import device_block_gidx
     t0 = time.time()
-    src, dst, x = c4_workload(device)
-    gidx = device_block_gidx(C4_NODES, C4_NODES, src, dst)
-    out_full = th.empty(C4_NODES, FEAT, device=device)
+    C4_N, C4_E = args.c4_nodes, args.c4_edges
+    src, dst, x = c4_workload(device, C4_N, C4_E)
+    gidx = device_block_gidx(C4_N, C4_N, src, dst)
+    log("C4: graph + CSRs (%.1fs)" % (time.time() - t0))
+    out_full = th.empty(C4_N, FEAT, device=device)
     K.copy_reduce("sum", gidx, 0, x, out_full)
     th.cuda.synchronize()
     res = {"workload": "C4: RMAT scale 24 (ids >= 10M rejected), %d nodes, %d edges, feat %d"
-                       % (C4_NODES, C4_EDGES, FEAT), "scaling": "strong", "n_gpus": world,
+                       % (C4_N, C4_E, FEAT), "scaling": "strong", "n_gpus": world,
            "setup_s": None}
     steps = max(1, args.steps)
     if world == 1:
@@ -163,7 +175,7 @@ def measure_c4(world, rank, dist, cdev, device, args):
         el = _timed(step, steps, None, None)
         if not th.equal(out, out_full):
             raise SystemExit("C4 copy_u_sum not deterministic")
-        res.update({"value": C4_EDGES * steps / el, "unit": "edges/s",
+        res.update({"value": C4_E * steps / el, "unit": "edges/s",
                     "ms_per_step": el * 1e3 / steps, "partitioner": None,
                     "setup_s": time.time() - t0})
         return res
@@ -172,19 +184,24 @@ def measure_c4(world, rank, dist, cdev, device, args):
     th.cuda.synchronize()
     lp_s = time.time() - t1
     # every rank computed the same labels (deterministic kernels); make sure of it
-    h = (assign.long() * th.arange(1, C4_NODES + 1, device=device) % 1000003).sum()
+    h = (assign.long() * th.arange(1, C4_N + 1, device=device) % 1000003).sum()
     hs = th.tensor([float(h.item())], device=cdev, dtype=th.float64)
     hmax, hmin = hs.clone(), hs.clone()
     dist.all_reduce(hmax, op=dist.ReduceOp.MAX)
     dist.all_reduce(hmin, op=dist.ReduceOp.MIN)
     if float(hmax.item()) != float(hmin.item()):
         raise SystemExit("ranks disagree on the partition")
+    trace("C4: hash check done")
+    log("C4: label propagation %.2fs" % lp_s)
+    trace("C4: hash check")
     stats_lp = D.partition_stats(src, dst, assign, world)
     contig = D.contiguous_parts_device((gidx.in_csr.degrees() + 1).to(th.int32), world)
     stats_ct = D.partition_stats(src, dst, contig, world)
     del contig
+    log("C4: partition stats (%.1fs)" % (time.time() - t0))
     part = D.build_partition_from_assignment(src, dst, assign, rank, None, world,
                                              exchange="hybrid", tau=args.c4_tau)
+    log("C4: hybrid plan (%.1fs)" % (time.time() - t0))
     pull = D.build_partition_from_assignment(src, dst, assign, rank, None, world)
     pull.release_edges()
     pull.split_gidx()
@@ -202,9 +219,11 @@ def measure_c4(world, rank, dist, cdev, device, args):
     tmp_p = th.empty(pull.n_inner, f, device=device)
     out_p = th.empty(pull.n_inner, f, device=device)
     pstep = lambda: D.aggregate_with_halo(x_inner, pull, out_p, None, recv_p, send_p, tmp_p)
+    log("C4: pull plan (%.1fs)" % (time.time() - t0))
     step()
     pstep()
     th.cuda.synchronize()
+    log("C4: first steps (%.1fs)" % (time.time() - t0))
     scale = ref.abs().max().clamp(min=1e-30)
     err = _max_over_ranks(float((out - ref).abs().max() / scale), dist, cdev)
     perr = _max_over_ranks(float((out_p - ref).abs().max() / scale), dist, cdev)
@@ -222,24 +241,24 @@ def measure_c4(world, rank, dist, cdev, device, args):
     moved = th.tensor([float(part.rows_moved()), float(pull.n_halo)], device=cdev,
                       dtype=th.float64)
     dist.all_reduce(moved)
-    res.update({"value": C4_EDGES * steps / el, "unit": "edges/s", "ms_per_step": el * 1e3 / steps,
+    res.update({"value": C4_E * steps / el, "unit": "edges/s", "ms_per_step": el * 1e3 / steps,
                 "exchange": "hybrid: pulled rows + pushed partial sums (tau %d), two "
                             "all-to-all-v (%s) overlapped with the owned-source SpMM"
                             % (args.c4_tau, dist.get_backend()),
                 "rows_moved_per_step": int(moved[0].item()),
                 "bytes_moved_per_step": int(moved[0].item()) * 4 * f,
                 "pull_only": {"ms_per_step": pel * 1e3 / steps,
-                              "edges_per_s": C4_EDGES * steps / pel,
+                              "edges_per_s": C4_E * steps / pel,
                               "rows_moved_per_step": int(moved[1].item()),
                               "exchange_only_ms": ex * 1e3 / steps},
                 "partitioner": "device label propagation, %d rounds, edge-balanced, slack 0.05 "
                                "(%.2fs)" % (args.c4_rounds, lp_s),
                 "rel_err_vs_single_gpu": max(err, perr),
                 "halo_rows_pull": stats_lp["halo_rows"], "edges_per_part": stats_lp["edges"],
-                "cut_fraction": stats_lp["cut_edges"] / C4_EDGES,
+                "cut_fraction": stats_lp["cut_edges"] / C4_E,
                 "contiguous_partition": {"halo_rows_pull": stats_ct["halo_rows"],
                                          "edges_per_part": stats_ct["edges"],
-                                         "cut_fraction": stats_ct["cut_edges"] / C4_EDGES},
+                                         "cut_fraction": stats_ct["cut_edges"] / C4_E},
                 "setup_s": time.time() - t0})
     return res
 
@@ -586,6 +605,8 @@ def main():
                     help="N=1: skip the rocprofv3 PMC passes (roofline traffic)")
     ap.add_argument("--no-c4", action="store_true",
                     help="skip the fixed-size C4 (10M / 200M, partitioned, with exchange) line")
+    ap.add_argument("--c4-nodes", type=int, default=C4_NODES, help=argparse.SUPPRESS)
+    ap.add_argument("--c4-edges", type=int, default=C4_EDGES, help=argparse.SUPPRESS)
     ap.add_argument("--c4-rounds", type=int, default=24,
                     help="label-propagation rounds of the C4 partition")
     ap.add_argument("--c4-tau", type=int, default=8,
@@ -726,6 +747,7 @@ def main():
     value = edges_total * args.steps / elapsed
     exch = None
     if part is not None:
+        log("with-exchange line ...")
         try:
             exch = measure_exchange(part, x, out, args, dist, cdev, device, edges_total)
         except SystemExit as exc:

@@ -59,7 +59,7 @@ def main():
     print("labelprop", json.dumps(out["labelprop"]), flush=True)
     inv = th.empty_like(perm.long())
     inv[perm.long()] = th.arange(n, device=dev)
-    bits = (inv >> 21).clamp(max=k - 1)          # generator id >> 21: 8 blocks of 2^21
+    bits = inv * k // n                           # 8 equal ranges of generator ids
     out["generator_bits"] = volumes(src, dst, bits, k, n, taus)
     print("generator_bits", json.dumps(out["generator_bits"]), flush=True)
     os.makedirs("gpurun_out", exist_ok=True)
