@@ -12,6 +12,6 @@ fi
 timeout -k 10 600 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
 rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench.json; tail -12 gpurun_out/bench.err
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-pmc --no-cpu-baseline --no-update-all > gpurun_out/prof.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-pmc --no-cpu-baseline --no-update-all --no-c4 > gpurun_out/prof.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; tail -2 gpurun_out/prof.log
 exit $rc
