@@ -120,3 +120,30 @@ def test_labelprop_partitioned_aggregation_matches_single_gpu(exchange, world):
     q = ctx.Queue()
     run_world(_agg_worker, world, (src, dst, n, q, exchange))
     assert q.get(timeout=5) == "ok"
+
+
+def test_metis_partition_on_gpu_uses_label_propagation():
+    """dgl.transform.metis_partition with a GPU present partitions with the device
+    label propagation (node-balanced like METIS); the reference's structural checks
+    (tests/compute/test_transform.py:245-274) hold, and parts stay within 3 %."""
+    import dgl
+    from dgl import distributed as D
+    rng = np.random.default_rng(0)
+    n = 1000
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(rng.integers(0, n, n * 10), rng.integers(0, n, n * 10))
+    for hops in (0, 1):
+        subgs = dgl.transform.metis_partition(g, 4, hops)
+        inner_total = 0
+        for pid, sub in subgs.items():
+            inner = sub.ndata["inner_node"].numpy()
+            inner_total += int(inner.sum())
+            assert (sub.ndata["part_id"].numpy()[inner == 1] == pid).all()
+            if hops == 0:
+                assert (inner == 1).all() and (sub.edata["inner_edge"].numpy() == 1).all()
+            assert int(inner.sum()) <= 1.03 * n / 4 + 1
+        assert inner_total == n
+    s, d = (t.numpy() for t in g.edges())
+    a = D.partition_assignment(n, s, d, 4, "labelprop")
+    assert a.min() >= 0 and a.max() < 4
