@@ -480,12 +480,16 @@ def _owner_of(ids, bounds_t):
     return th.bucketize(ids, bounds_t[1:], right=True)
 
 
-def build_hybrid_partition(src, dst, bounds, rank, group=None, tau=8):
-    """Plan rank ``rank``'s hybrid exchange from its in-edges (``src`` GLOBAL
-    source ids, ``dst`` LOCAL destination ids, as :func:`build_device_partition`),
-    all on the device.  Collective over ``group``: one all-to-all of counts, one
-    of pulled ids, one of push-edge lists (each destination owner tells every
-    source owner which of its edges to sum into which partial row)."""
+def plan_hybrid(src, dst, bounds, rank, group=None, tau=8):
+    """The hybrid exchange plan of rank ``rank`` as edge lists (no CSRs), on the
+    tensors' device (the GPU, or the CPU in the gloo tests).  ``src``: GLOBAL
+    source ids of the rank's in-edges, ``dst``: their LOCAL destination ids.
+    Collective over ``group``: one all-to-all of counts, one of pulled ids, one of
+    push-edge lists (each destination owner tells every source owner which of its
+    edges to sum into which partial row).  Returns a dict: ``own_src`` /
+    ``own_dst`` (owned -> owned), ``recv_col`` / ``recv_dst`` ([pulled | partial]
+    row -> owned), ``push_src`` / ``push_row`` (owned -> outgoing partial row) and
+    the exchange counts."""
     world = len(bounds) - 1
     lo, hi = int(bounds[rank]), int(bounds[rank + 1])
     n_inner = hi - lo
@@ -521,9 +525,6 @@ def build_hybrid_partition(src, dst, bounds, rank, group=None, tau=8):
     # receive block: pulled edges -> halo index, one edge per pushed pair -> n_halo + pair index
     cols = th.cat([th.searchsorted(halo, ps_), n_halo + th.arange(n_pin, device=dev)])
     rows = th.cat([pd_, pushed % n_inner])
-    g_recv = device_block_gidx(n_halo + n_pin, n_inner, cols.to(th.int32), rows.to(th.int32)) \
-        if cols.numel() else None
-    g_own = device_block_gidx(n_inner, n_inner, own_s.to(th.int32), own_d.to(th.int32))
     # push-edge lists for every source owner: (u local on p, pair index within p's segment)
     e_u = rs[is_push]
     e_pair = pos[is_push]
@@ -553,16 +554,33 @@ def build_hybrid_partition(src, dst, bounds, rank, group=None, tau=8):
     pout_start = th.from_numpy(np.cumsum(pout_counts) - pout_counts).to(dev)
     push_rows = pout_start[msg_peer] + msgs % (1 << 31)
     push_cols = msgs // (1 << 31)
-    g_push = device_block_gidx(n_inner, n_pout, push_cols.to(th.int32), push_rows.to(th.int32)) \
+    return {"lo": lo, "hi": hi, "n_inner": n_inner, "halo": halo, "n_halo": n_halo,
+            "send_idx": req - lo, "send_counts": send_counts, "recv_counts": recv_counts,
+            "n_pin": n_pin, "pin_counts": pin_counts_np, "n_pout": n_pout,
+            "pout_counts": pout_counts, "own_src": own_s, "own_dst": own_d,
+            "recv_col": cols, "recv_dst": rows, "push_src": push_cols, "push_row": push_rows,
+            "n_in_edges": int(s.numel())}
+
+
+def build_hybrid_partition(src, dst, bounds, rank, group=None, tau=8):
+    """Plan rank ``rank``'s hybrid exchange (:func:`plan_hybrid`) and build its
+    three blocks on the device."""
+    pl = plan_hybrid(src, dst, bounds, rank, group, tau)
+    n_inner, n_halo, n_pin, n_pout = pl["n_inner"], pl["n_halo"], pl["n_pin"], pl["n_pout"]
+    i32 = lambda t: t.to(th.int32)
+    g_own = device_block_gidx(n_inner, n_inner, i32(pl["own_src"]), i32(pl["own_dst"]))
+    g_recv = device_block_gidx(n_halo + n_pin, n_inner, i32(pl["recv_col"]), i32(pl["recv_dst"])) \
+        if pl["recv_col"].numel() else None
+    g_push = device_block_gidx(n_inner, n_pout, i32(pl["push_src"]), i32(pl["push_row"])) \
         if n_pout else None
-    part = HybridPartition(part_id=rank, num_parts=world, lo=lo, hi=hi, n_inner=n_inner,
-                           halo=halo, n_halo=n_halo, send_idx=req - lo,
-                           send_counts=send_counts, recv_counts=recv_counts,
-                           n_pin=n_pin, pin_counts=pin_counts_np, n_pout=n_pout,
-                           pout_counts=pout_counts, g_own=g_own, g_recv=g_recv, g_push=g_push,
-                           tau=tau, n_push_edges_out=int(msgs.numel()),
-                           n_in_edges=int(s.numel()))
-    return part
+    return HybridPartition(part_id=rank, num_parts=len(bounds) - 1, lo=pl["lo"], hi=pl["hi"],
+                           n_inner=n_inner, halo=pl["halo"], n_halo=n_halo,
+                           send_idx=pl["send_idx"], send_counts=pl["send_counts"],
+                           recv_counts=pl["recv_counts"], n_pin=n_pin,
+                           pin_counts=pl["pin_counts"], n_pout=n_pout,
+                           pout_counts=pl["pout_counts"], g_own=g_own, g_recv=g_recv,
+                           g_push=g_push, tau=tau, n_push_edges_out=int(pl["push_src"].numel()),
+                           n_in_edges=pl["n_in_edges"])
 
 
 def aggregate_hybrid(x_inner, part, out=None, group=None, bufs=None):

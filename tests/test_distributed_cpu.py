@@ -145,3 +145,44 @@ def test_ldg_partitioned_aggregation_gloo_world2():
     members = [np.nonzero(block == b)[0] for b in range(2)]
     v = np.where(same, np.array([rng.choice(members[block[x]]) for x in u]), rng.integers(0, n, 20000))
     run_world(_ldg_agg_worker, 2, (u.astype(np.int64), v.astype(np.int64), n))
+
+
+def _hybrid_plan_worker(rank, world, src, dst, n, tau):
+    """The hybrid (pull + push-partial) plan, executed with torch index_add on the
+    CPU (stand-in for the HIP SpMMs of aggregate_hybrid): every in-edge of an owned
+    destination is summed exactly once over all ranks, so the result equals the
+    whole-graph sum; x = ones counts the in-degrees exactly."""
+    import torch.distributed as dist
+    bounds = [n * p // world for p in range(world + 1)]
+    lo, hi = bounds[rank], bounds[rank + 1]
+    sel = (dst >= lo) & (dst < hi)
+    pl = D.plan_hybrid(th.from_numpy(src[sel]), th.from_numpy(dst[sel] - lo), bounds, rank,
+                       None, tau)
+    xg = th.randn(n, 3, generator=th.Generator().manual_seed(4), dtype=th.float64)
+    results = []
+    for x in (xg, th.ones(n, 3, dtype=th.float64)):
+        xi = x[lo:hi]
+        send = xi[pl["send_idx"]]
+        recv_pull = th.empty(pl["n_halo"], 3, dtype=th.float64)
+        D._a2av(recv_pull, send, pl["recv_counts"].tolist(), pl["send_counts"].tolist(), None)
+        pout = th.zeros(pl["n_pout"], 3, dtype=th.float64).index_add_(0, pl["push_row"],
+                                                                       xi[pl["push_src"]])
+        recv_part = th.empty(pl["n_pin"], 3, dtype=th.float64)
+        D._a2av(recv_part, pout, pl["pin_counts"].tolist(), pl["pout_counts"].tolist(), None)
+        recv = th.cat([recv_pull, recv_part])
+        out = th.zeros(hi - lo, 3, dtype=th.float64).index_add_(0, pl["own_dst"], xi[pl["own_src"]])
+        out.index_add_(0, pl["recv_dst"], recv[pl["recv_col"]])
+        results.append(out)
+    ref = th.zeros(n, 3, dtype=th.float64).index_add_(0, th.from_numpy(dst), xg[th.from_numpy(src)])
+    assert th.allclose(results[0], ref[lo:hi], atol=1e-9)
+    indeg = th.from_numpy(np.bincount(dst, minlength=n)[lo:hi]).double()
+    assert th.equal(results[1][:, 0], indeg)
+    flags = [None] * world
+    dist.all_gather_object(flags, (pl["n_pin"], pl["n_halo"]))
+    assert sum(f[0] for f in flags) > 0  # partial rows were exercised
+
+
+@pytest.mark.parametrize("world,tau", [(2, 2), (3, 3), (2, 8)])
+def test_hybrid_plan_gloo(world, tau):
+    src, dst, n = powerlaw(3000, 40000, seed=6)
+    run_world(_hybrid_plan_worker, world, (src, dst, n, tau))
