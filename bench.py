@@ -241,11 +241,20 @@ def measure_c4(world, rank, dist, cdev, device, args):
     moved = th.tensor([float(part.rows_moved()), float(pull.n_halo)], device=cdev,
                       dtype=th.float64)
     dist.all_reduce(moved)
+    # per-rank SpMM work of the hybrid step (edges walked: owned block + push block +
+    # receive block) -- the push side moves work to the hub sources' owners
+    nnz = lambda gi: gi.in_csr.nnz if gi is not None else 0
+    work = th.tensor([float(nnz(part.g_own) + nnz(part.g_push) + nnz(part.g_recv))],
+                     device=cdev, dtype=th.float64)
+    works = [th.zeros_like(work) for _ in range(world)]
+    dist.all_gather(works, work)
+    works = [int(w.item()) for w in works]
     res.update({"value": C4_E * steps / el, "unit": "edges/s", "ms_per_step": el * 1e3 / steps,
                 "exchange": "hybrid: pulled rows + pushed partial sums (tau %d), two "
                             "all-to-all-v (%s) overlapped with the owned-source SpMM"
                             % (args.c4_tau, dist.get_backend()),
                 "rows_moved_per_step": int(moved[0].item()),
+                "spmm_edges_per_rank": works,
                 "bytes_moved_per_step": int(moved[0].item()) * 4 * f,
                 "pull_only": {"ms_per_step": pel * 1e3 / steps,
                               "edges_per_s": C4_E * steps / pel,

@@ -1,6 +1,6 @@
 // Helpers of the C entries that replace the hack's R-GCN PackedFuncs
 // (_CAPI_DGLRgcnLayer0/1[Backward], binary_reduce.cc:411-450): relation-expanded
-// column ids, the relation-weight layout change, and a small LDS-tiled fp32
+// column ids, the relation-weight layout change, and an LDS-tiled fp32-input MFMA
 // GEMM for the (N x K) . (K x R*F) transforms.
 //
 // The hack computes one (F_in x F_out) product PER EDGE inside its gather
@@ -17,8 +17,6 @@ namespace dglmi {
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kTile = 64;   // output tile (rows and columns)
-constexpr int kTileK = 16;  // reduction slice per LDS stage
 
 // relation-expanded ids: mode 0: etype * mul + id (type-major), 1: id * mul + etype
 __global__ void k_typed_ids(const int32_t* __restrict__ ids, const int32_t* __restrict__ eids,
@@ -46,54 +44,62 @@ __global__ void k_permute_rkx(const float* __restrict__ w, int64_t R, int64_t K,
 }
 
 // C[z] (M x N, row-major) = sum over k in split z of A[m, k] * B[k, n]; A and B by
-// (row, col) strides.  64 x 64 output tile per workgroup, 4 x 4 per thread, the
-// A and B slices of 16 along k staged in LDS.
+// (row, col) strides.  fp32-input MFMA (v_mfma_f32_32x32x2_f32: exact f32, an
+// fmaf chain per output): a 128 x 64 output tile per workgroup, each of the four
+// waves owning 32 rows x 64 columns (two 32 x 32 accumulators); 32-deep slices of
+// A and B staged in LDS with loads that run along each operand's unit-stride
+// dimension.
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+constexpr int kTM = 128, kTN = 64, kTK = 32;
+
 __global__ void __launch_bounds__(kBlock) k_gemm(const float* __restrict__ A, int64_t a_rs,
                                                  int64_t a_cs, const float* __restrict__ B,
                                                  int64_t b_rs, int64_t b_cs, float* __restrict__ C,
                                                  int64_t M, int64_t N, int64_t K, int64_t k_split) {
-  __shared__ float As[kTileK][kTile + 4];
-  __shared__ float Bs[kTileK][kTile + 4];
-  const int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
-  const int64_t m0 = static_cast<int64_t>(blockIdx.x) * kTile;  // x: the long dimension
-  const int64_t n0 = static_cast<int64_t>(blockIdx.y) * kTile;
+  __shared__ float As[kTM][kTK + 1];
+  __shared__ float Bs[kTK][kTN + 1];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // 1-D grid, column tiles fastest: the blocks that share an A row slice run
+  // back to back, so the slice is read from HBM once and from L2 after that
+  const int64_t n_tiles = (N + kTN - 1) / kTN;
+  const int64_t m0 = static_cast<int64_t>(blockIdx.x) / n_tiles * kTM;
+  const int64_t n0 = static_cast<int64_t>(blockIdx.x) % n_tiles * kTN;
   const int64_t kb = static_cast<int64_t>(blockIdx.z) * k_split;
   const int64_t ke = kb + k_split < K ? kb + k_split : K;
-  float acc[4][4] = {};
-  for (int64_t k0 = kb; k0 < ke; k0 += kTileK) {
-    for (int i = threadIdx.x; i < kTile * kTileK; i += kBlock) {
-      const int kk = i / kTile, mm = i % kTile;
+  f32x16 acc0 = {}, acc1 = {};
+  for (int64_t k0 = kb; k0 < ke; k0 += kTK) {
+    for (int i = threadIdx.x; i < kTM * kTK; i += kBlock) {
+      const int kk = a_cs == 1 ? i % kTK : i / kTM;
+      const int mm = a_cs == 1 ? i / kTK : i % kTM;
       const int64_t m = m0 + mm, k = k0 + kk;
-      As[kk][mm] = (m < M && k < ke) ? A[m * a_rs + k * a_cs] : 0.0f;
-      const int64_t n = n0 + mm;
-      Bs[kk][mm] = (n < N && k < ke) ? B[k * b_rs + n * b_cs] : 0.0f;
+      As[mm][kk] = (m < M && k < ke) ? A[m * a_rs + k * a_cs] : 0.0f;
+    }
+    for (int i = threadIdx.x; i < kTK * kTN; i += kBlock) {
+      const int kk = b_cs == 1 ? i / kTN : i % kTK;
+      const int nn = b_cs == 1 ? i % kTN : i / kTK;
+      const int64_t n = n0 + nn, k = k0 + kk;
+      Bs[kk][nn] = (n < N && k < ke) ? B[k * b_rs + n * b_cs] : 0.0f;
     }
     __syncthreads();
+    const int r = lane & 31, h = lane >> 5;
 #pragma unroll
-    for (int kk = 0; kk < kTileK; ++kk) {
-      float a[4], b[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        a[i] = As[kk][ty * 4 + i];
-        b[i] = Bs[kk][tx * 4 + i];
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] += a[i] * b[j];
+    for (int kk = 0; kk < kTK; kk += 2) {
+      const float a = As[w * 32 + r][kk + h];
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Bs[kk + h][r], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Bs[kk + h][32 + r], acc1, 0, 0, 0);
     }
     __syncthreads();
   }
+  // C/D map: col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
   float* Cz = C + static_cast<int64_t>(blockIdx.z) * M * N;
+  const int col = lane & 31;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t m = m0 + ty * 4 + i;
+  for (int reg = 0; reg < 16; ++reg) {
+    const int64_t m = m0 + w * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
     if (m >= M) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t n = n0 + tx * 4 + j;
-      if (n < N) Cz[m * N + n] = acc[i][j];
-    }
+    const int64_t n = n0 + col;
+    if (n < N) Cz[m * N + n] = acc0[reg];
+    if (n + 32 < N) Cz[m * N + n + 32] = acc1[reg];
   }
 }
 
@@ -131,9 +137,9 @@ void launch_permute_rkx(const float* w, int64_t R, int64_t K, int64_t X, bool to
 
 int64_t gemm_splits(int64_t M, int64_t N, int64_t K) {
   // split the reduction when the output has too few tiles to fill 256 CUs
-  const int64_t tiles = ((M + kTile - 1) / kTile) * ((N + kTile - 1) / kTile);
+  const int64_t tiles = ((M + kTM - 1) / kTM) * ((N + kTN - 1) / kTN);
   int64_t splits = 1;
-  while (tiles * splits < 512 && K / (splits * 2) >= 1024 && splits < 256) splits *= 2;
+  while (tiles * splits < 4096 && K / (splits * 2) >= 512 && splits < 2048) splits *= 2;
   return splits;
 }
 
@@ -145,10 +151,10 @@ void launch_gemm(const float* A, int64_t a_rs, int64_t a_cs, const float* B, int
     launch_fill(C, M * N, 0.0f, s);
     return;
   }
-  const int64_t k_split = ((K + splits - 1) / splits + kTileK - 1) / kTileK * kTileK;
+  const int64_t k_split = ((K + splits - 1) / splits + kTK - 1) / kTK * kTK;
   const int64_t used = (K + k_split - 1) / k_split;
-  const dim3 grid(static_cast<unsigned>((M + kTile - 1) / kTile),
-                  static_cast<unsigned>((N + kTile - 1) / kTile), static_cast<unsigned>(used));
+  const dim3 grid(static_cast<unsigned>(((M + kTM - 1) / kTM) * ((N + kTN - 1) / kTN)), 1,
+                  static_cast<unsigned>(used));
   if (used == 1) {
     hipLaunchKernelGGL(k_gemm, grid, dim3(kBlock), 0, s, A, a_rs, a_cs, B, b_rs, b_cs, C, M, N, K,
                        k_split);

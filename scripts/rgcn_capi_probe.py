@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""C5 (5 M nodes, 80 M typed edges, 4 relations, 64 -> 64): the R-GCN C entries
+(DGLMIRgcnLayer1 / 1Backward: the library's tiled GEMM + relation-expanded gather,
+typed out-CSR re-sorted per call) against the Python path (RelGraphConv: hipBLASLt
+GEMM via torch + the cached typed gather).  HIP-event medians."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "dgl-hack_amd"))
+
+import numpy as np  # noqa: E402
+import torch as th  # noqa: E402
+
+
+def ktime(fn, steps=10):
+    fn()
+    ev = [(th.cuda.Event(enable_timing=True), th.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for a, b in ev:
+        a.record()
+        fn()
+        b.record()
+    th.cuda.synchronize()
+    return float(np.median([a.elapsed_time(b) for a, b in ev]))
+
+
+def main():
+    import dgl
+    from dgl import kernel as K
+    from dgl.nn.pytorch import RelGraphConv
+    dev = "cuda:0"
+    n, m, R, F = 5_000_000, 80_000_000, 4, 64
+    g0 = th.Generator(device=dev)
+    g0.manual_seed(8)
+    src = th.randint(0, n, (m,), device=dev, generator=g0, dtype=th.int32)
+    dst = th.randint(0, n, (m,), device=dev, generator=g0, dtype=th.int32)
+    et = th.randint(0, R, (m,), device=dev, generator=g0)
+    g = dgl.DGLGraph.from_device_coo(src, dst, n)
+    gidx = g._graph.get_immutable_gidx(dev)
+    norm = (1.0 / th.bincount(dst.long(), minlength=n).clamp(min=1).float())[dst.long()].view(-1, 1)
+    conv = RelGraphConv(F, F, R, "basis", num_bases=R, bias=False).to(dev)
+    h = th.randn(n, F, device=dev)
+    W = conv._relation_weights().detach().contiguous()
+    et32 = et.int()
+    ret = th.empty(n, F, device=dev)
+    go = th.randn(n, F, device=dev)
+    gh, gw = th.empty(n, F, device=dev), th.empty_like(W)
+    res = {"config": "C5 R-GCN layer 64->64, 4 relations, 5M nodes / 80M edges"}
+    if "--capi-only" in sys.argv:  # for rocprofv3 kernel statistics
+        for _ in range(3):
+            K.rgcn_layer1(gidx, et32, h, W, norm, ret)
+            K.rgcn_layer1_backward(gidx, et32, h, W, norm, go, gh, gw)
+        th.cuda.synchronize()
+        return
+    res["python_fwd_ms"] = ktime(lambda: conv(g, h, et, norm))
+    hr = h.clone().requires_grad_()
+
+    def py_fb():
+        out = conv(g, hr, et, norm)
+        out.backward(go)
+    res["python_fwd_bwd_ms"] = ktime(py_fb)
+    res["capi_layer1_ms"] = ktime(lambda: K.rgcn_layer1(gidx, et32, h, W, norm, ret))
+    res["capi_layer1_backward_ms"] = ktime(
+        lambda: K.rgcn_layer1_backward(gidx, et32, h, W, norm, go, gh, gw))
+    w0 = th.randn(R, n, 16, device=dev)
+    r0 = th.empty(n, 16, device=dev)
+    res["capi_layer0_F16_ms"] = ktime(lambda: K.rgcn_layer0(gidx, et32, w0, norm, r0))
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
