@@ -40,6 +40,15 @@ def volumes(src, dst, a, k, n, taus):
         n_push = int((cnt >= t).sum())
         rest = th.unique(u[~pushed] * k + pv[~pushed]).numel()
         res["hybrid"][str(t)] = {"push_rows": n_push, "pull_rows": int(rest), "total": n_push + int(rest)}
+    # edge-level rule: cover each cut edge by its heavier endpoint in the bipartite
+    # cut graph between the two parts (push v when c(v, p) > d(u, q), d = distinct
+    # destinations of u on q), a vertex-cover heuristic
+    up, dcnt = th.unique(u * k + pv, return_counts=True)
+    d_of = dcnt[th.searchsorted(up, u * k + pv)]
+    for name, push in (("cover_gt", c_of_pair > d_of), ("cover_ge", c_of_pair >= d_of)):
+        n_push = int(th.unique((v * k + pu)[push]).numel())
+        n_pull = int(th.unique((u * k + pv)[~push]).numel())
+        res["hybrid"][name] = {"push_rows": n_push, "pull_rows": n_pull, "total": n_push + n_pull}
     return res
 
 
