@@ -30,6 +30,9 @@ def summary(st, n_edges):
             "halo_rows": st["halo_rows"], "edges": st["edges"]}
 
 
+SLACK = 0.05
+
+
 def probe(src, dst, n, ks, rounds_list, tag, out):
     gidx = device_block_gidx(n, n, src, dst)
     m = int(src.shape[0])
@@ -41,7 +44,7 @@ def probe(src, dst, n, ks, rounds_list, tag, out):
         for r in rounds_list:
             th.cuda.synchronize()
             t0 = time.time()
-            a, info = D.partition_labelprop(gidx, k, rounds=r)
+            a, info = D.partition_labelprop(gidx, k, rounds=r, slack=SLACK)
             th.cuda.synchronize()
             dt = time.time() - t0
             rec = summary(D.partition_stats(src, dst, a, k), m)
@@ -57,10 +60,13 @@ def main():
     ap.add_argument("--rounds", default="8,24,48")
     ap.add_argument("--ks", default="2,4,8")
     ap.add_argument("--ldg", action="store_true")
+    ap.add_argument("--slack", type=float, default=0.05)
     ap.add_argument("--out", default="gpurun_out/partition_probe.json")
     args = ap.parse_args()
     dev = "cuda:0"
     rounds = [int(r) for r in args.rounds.split(",")]
+    global SLACK
+    SLACK = args.slack
     ks = [int(k) for k in args.ks.split(",")]
     out = {}
     t0 = time.time()
