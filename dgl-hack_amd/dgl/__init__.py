@@ -19,6 +19,7 @@ from .transform import (laplacian_lambda_max, add_self_loop, remove_self_loop,  
                         reverse, to_bidirected, metis_partition,
                         partition_graph_with_halo)
 from . import transform  # noqa: F401
+from . import data  # noqa: F401
 from . import nn  # noqa: F401
 
 __version__ = "0.4"

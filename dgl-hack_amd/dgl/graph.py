@@ -287,6 +287,10 @@ class DGLGraph(object):
     def is_readonly(self):
         return self._readonly
 
+    def readonly(self, readonly_state=True):
+        """Set the read-only state in place (``graph.py:3819-3860``)."""
+        self._readonly = bool(readonly_state)
+
     def nodes(self):
         return th.arange(self.number_of_nodes(), dtype=th.int64)
 

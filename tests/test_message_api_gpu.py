@@ -250,3 +250,17 @@ def test_missing_functions_raise():
     g.register_message_func(fn.copy_src("h", "m"))
     with pytest.raises(DGLError):
         g.update_all()
+
+
+def test_saved_graph_runs_update_all(tmp_path):
+    """save_graphs of device features (written as CPU arrays, ndarray.h:415-427), then
+    load_graphs -> update_all on the GPU: the known answers of the star graph again."""
+    from dgl.data.utils import save_graphs, load_graphs
+    g = star_graph()
+    path = str(tmp_path / "star.bin")
+    save_graphs(path, [g], {"y": th.ones(1, device=DEV)})
+    (h,), labels = load_graphs(path)
+    assert h.ndata["h"].device.type == "cpu" and labels["y"].device.type == "cpu"
+    h = h.to(DEV)
+    h.update_all(fn.src_mul_edge(src="h", edge="h", out="m"), fn.sum(msg="m", out="out"))
+    assert th.equal(h.ndata["out"].cpu(), th.tensor(STAR_MUL))
