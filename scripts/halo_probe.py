@@ -35,6 +35,21 @@ def volumes(src, dst, a, k, n, taus):
     push = int(vp.numel())                        # partials (v <- part of u)
     res = {"cross_edges": int(x.sum()), "pull_rows": pull, "push_rows": push, "hybrid": {}}
     c_of_pair = cnt[th.searchsorted(vp, v * k + pu)]
+    # per-part SpMM work of the hybrid step at tau = 8 (what bench's
+    # spmm_edges_per_rank counts): owned block + push block + receive block
+    # (edges of pulled rows, one entry per incoming partial row)
+    pos = th.searchsorted(vp, d * k + ps)            # (v, part of u) of every cut edge
+    pushed_e = cnt[pos] >= 8
+    a_all = a.long()
+    a_src, a_dst = a_all[src.long()], a_all[dst.long()]
+    own = th.bincount(a_dst[a_src == a_dst], minlength=k)
+    push_w = th.bincount(ps[pushed_e], minlength=k)
+    partials_in = th.bincount(a_all[vp[cnt >= 8] // k], minlength=k)
+    recv_w = th.bincount(pd[~pushed_e], minlength=k) + partials_in
+    work = (own + push_w + recv_w).tolist()
+    res["hybrid_tau8_work_per_part"] = work
+    res["hybrid_tau8_work_imbalance"] = max(work) / (sum(work) / k)
+    res["edges_per_part"] = th.bincount(a_dst, minlength=k).tolist()
     for t in taus:
         pushed = c_of_pair >= t
         n_push = int((cnt >= t).sum())
@@ -54,7 +69,7 @@ def volumes(src, dst, a, k, n, taus):
 
 def main():
     dev = "cuda:0"
-    k, n = 8, bench.C4_NODES
+    k, n = int(os.environ.get("K", "8")), bench.C4_NODES
     src, dst, perm = bench.c4_workload(dev, return_perm=True)
     taus = [2, 3, 4, 8, 16]
     out = {}
@@ -63,7 +78,7 @@ def main():
     ct = D.contiguous_parts_device(w, k).long()
     out["contiguous"] = volumes(src, dst, ct, k, n, taus)
     print("contiguous", json.dumps(out["contiguous"]), flush=True)
-    lp, _ = D.partition_labelprop(g, k, rounds=24)
+    lp, _ = D.partition_labelprop(g, k, rounds=24, slack=float(os.environ.get("SLACK", "0.02")))
     out["labelprop"] = volumes(src, dst, lp.long(), k, n, taus)
     print("labelprop", json.dumps(out["labelprop"]), flush=True)
     inv = th.empty_like(perm.long())
@@ -72,7 +87,7 @@ def main():
     out["generator_bits"] = volumes(src, dst, bits, k, n, taus)
     print("generator_bits", json.dumps(out["generator_bits"]), flush=True)
     os.makedirs("gpurun_out", exist_ok=True)
-    json.dump(out, open("gpurun_out/halo_probe.json", "w"), indent=1)
+    json.dump(out, open("gpurun_out/halo_probe_k%d.json" % k, "w"), indent=1)
 
 
 if __name__ == "__main__":
