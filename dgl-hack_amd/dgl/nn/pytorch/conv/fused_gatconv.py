@@ -6,10 +6,8 @@ unfused GATConv composition when the head size is not supported by the fused
 kernel or attention dropout is active (the fused kernel has no per-edge
 buffer to drop out).  The reference's timing prints are not reproduced.
 """
-import torch as th
 
 from .... import backend as B
-from .... import kernel as K
 from .gatconv import GATConv
 
 

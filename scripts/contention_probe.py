@@ -3,7 +3,6 @@
 175 M int64 keys (what partition_stats does at C4 size) and log progress per
 process; a sort whose tiles spin on their predecessors can stall when other
 processes' kernels hold the CUs."""
-import os
 import sys
 import time
 

@@ -3,7 +3,6 @@ per source block (destination block for the source-side gradient), partial sums
 chained through the epilogue addend.  Forced block counts on small graphs and
 the automatic rule on a graph that triggers it, against the unblocked kernels
 and fp64 restatements; the caller's epilogue (row scale, bias, addend) is kept."""
-import numpy as np
 import pytest
 import torch as th
 

@@ -7,7 +7,6 @@ code paths of the engine against each other (fused vs unfused GAT, the Python
 R-GCN path vs the C entry with its own GEMM), a checksum of checksums, and
 fp64 recomputation of sampled destination rows with a bound scaled by the row's
 absolute mass (fp32 summation order differs from any reference order)."""
-import numpy as np
 import pytest
 import torch as th
 

@@ -19,7 +19,6 @@ import scipy.sparse  # noqa: F401
 import torch as th
 
 import dgl
-import dgl.function as fn
 import dgl.nn.pytorch as nn
 
 pytestmark = pytest.mark.gpu

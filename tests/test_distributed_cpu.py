@@ -4,7 +4,7 @@ import pytest
 import torch as th
 
 from dgl import distributed as D
-from graphs import powerlaw, er_graph
+from graphs import powerlaw
 from dist_util import run_world
 
 

@@ -1,5 +1,4 @@
 """Heterograph construction and bookkeeping (host side, no kernels)."""
-import numpy as np
 import pytest
 import scipy.sparse as sp
 

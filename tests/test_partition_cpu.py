@@ -4,7 +4,6 @@ reference's own ``tests/compute/test_transform.py:224-276``), and to_bidirected
 (vectorised) against a loop restatement of ``graph_op.cc:332-401``."""
 import numpy as np
 import pytest
-import torch as th
 
 import dgl
 
