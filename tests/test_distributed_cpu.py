@@ -147,13 +147,14 @@ def test_ldg_partitioned_aggregation_gloo_world2():
     run_world(_ldg_agg_worker, 2, (u.astype(np.int64), v.astype(np.int64), n))
 
 
-def _hybrid_plan_worker(rank, world, src, dst, n, tau):
+def _hybrid_plan_worker(rank, world, src, dst, n, tau, bounds=None):
     """The hybrid (pull + push-partial) plan, executed with torch index_add on the
     CPU (stand-in for the HIP SpMMs of aggregate_hybrid): every in-edge of an owned
     destination is summed exactly once over all ranks, so the result equals the
     whole-graph sum; x = ones counts the in-degrees exactly."""
     import torch.distributed as dist
-    bounds = [n * p // world for p in range(world + 1)]
+    if bounds is None:
+        bounds = [n * p // world for p in range(world + 1)]
     lo, hi = bounds[rank], bounds[rank + 1]
     sel = (dst >= lo) & (dst < hi)
     pl = D.plan_hybrid(th.from_numpy(src[sel]), th.from_numpy(dst[sel] - lo), bounds, rank,
@@ -186,3 +187,10 @@ def _hybrid_plan_worker(rank, world, src, dst, n, tau):
 def test_hybrid_plan_gloo(world, tau):
     src, dst, n = powerlaw(3000, 40000, seed=6)
     run_world(_hybrid_plan_worker, world, (src, dst, n, tau))
+
+
+def test_hybrid_plan_gloo_empty_part():
+    """A rank that owns no nodes (bounds [0, n/2, n/2, n]) sends and receives
+    nothing, and the two others still sum every in-edge exactly once."""
+    src, dst, n = powerlaw(2000, 30000, seed=9)
+    run_world(_hybrid_plan_worker, 3, (src, dst, n, 4, [0, n // 2, n // 2, n]))

@@ -69,13 +69,17 @@ def test_labelprop_rejects_bad_input():
         D.partition_labelprop(g, 2, init=bad)
 
 
-def _agg_worker(rank, world, src, dst, n, q, exchange="pull"):
+def _agg_worker(rank, world, src, dst, n, q, exchange="pull", empty_part=False):
     import torch.distributed as dist
     from dgl import distributed as D
     from dgl import kernel as K
     s, d = th.from_numpy(src).to(DEV).int(), th.from_numpy(dst).to(DEV).int()
     g = D.device_block_gidx(n, n, s, d)
-    assign, _ = D.partition_labelprop(g, world, rounds=10)
+    if empty_part:  # parts {0, world-1} only: the middle ranks own nothing
+        assign, _ = D.partition_labelprop(g, 2, rounds=10)
+        assign = assign * (world - 1)
+    else:
+        assign, _ = D.partition_labelprop(g, world, rounds=10)
     part = D.build_partition_from_assignment(s, d, assign, rank, None, world, exchange=exchange,
                                              tau=2)
     x = th.from_numpy(np.random.RandomState(0).randn(n, 32).astype(np.float32)).to(DEV)
@@ -95,7 +99,8 @@ def _agg_worker(rank, world, src, dst, n, q, exchange="pull"):
         full_exact = bool(th.equal(full, th.cat([x_inner, x[part.halo_global]])))
         n_push = 0
     bound = 1e-5 + 2e-6 * mass[part.inner_global]
-    res = {"err": float(((out - ref[part.inner_global]).abs() / bound).max()),
+    rel = (out - ref[part.inner_global]).abs() / bound
+    res = {"err": float(rel.max()) if rel.numel() else 0.0,
            "full_exact": full_exact, "inner": part.inner, "n_halo": part.n_halo,
            "n_push": n_push}
     objs = [None] * world
@@ -110,15 +115,17 @@ def _agg_worker(rank, world, src, dst, n, q, exchange="pull"):
         q.put("ok")
 
 
-@pytest.mark.parametrize("exchange,world", [("pull", 2), ("hybrid", 2), ("hybrid", 3)])
-def test_labelprop_partitioned_aggregation_matches_single_gpu(exchange, world):
+@pytest.mark.parametrize("exchange,world,empty", [("pull", 2, False), ("hybrid", 2, False),
+                                                  ("hybrid", 3, False), ("hybrid", 3, True),
+                                                  ("pull", 3, True)])
+def test_labelprop_partitioned_aggregation_matches_single_gpu(exchange, world, empty):
     import torch.multiprocessing as mp
     from dist_util import run_world
     from graphs import powerlaw
     src, dst, n = powerlaw(5000, 60000, seed=5)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    run_world(_agg_worker, world, (src, dst, n, q, exchange))
+    run_world(_agg_worker, world, (src, dst, n, q, exchange, empty))
     assert q.get(timeout=5) == "ok"
 
 
