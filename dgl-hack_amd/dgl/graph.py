@@ -39,6 +39,7 @@ from .function.base import TargetCode
 from .function.message import MessageFunction
 from .function.reducer import ReduceFunction
 from .graph_index import GraphIndex
+from .init import zero_initializer
 
 ALL = "__ALL__"
 
@@ -54,11 +55,25 @@ def _to_index_array(x, name):
 
 
 class Frame(MutableMapping):
-    """Columns of per-node or per-edge features (``python/dgl/frame.py``)."""
+    """Columns of per-node or per-edge features (``python/dgl/frame.py``), with the
+    per-column initializers of ``frame.py:219-260`` (default: zeros)."""
 
-    def __init__(self, num_rows_fn, data=None):
+    def __init__(self, num_rows_fn, data=None, initializers=None):
         self._num_rows = num_rows_fn
         self._cols = dict(data) if data else {}
+        self._inits = dict(initializers) if initializers else {}
+
+    def set_initializer(self, initializer, column=None):
+        self._inits[column] = initializer
+
+    def get_initializer(self, column=None):
+        return self._inits.get(column, self._inits.get(None, zero_initializer))
+
+    def init_rows(self, column, like, ids):
+        """Rows ``ids`` (a device id tensor) of ``column`` from its initializer, shaped
+        and typed like ``like`` (a tensor with the column's row shape)."""
+        shape = (int(ids.shape[0]),) + tuple(like.shape[1:])
+        return self.get_initializer(column)(shape, like.dtype, like.device, ids)
 
     def __getitem__(self, key):
         return self._cols[key]
@@ -85,7 +100,7 @@ class Frame(MutableMapping):
         return repr({k: tuple(v.shape) for k, v in self._cols.items()})
 
     def clone(self):
-        return Frame(self._num_rows, self._cols)
+        return Frame(self._num_rows, self._cols, self._inits)
 
 
 class EdgeBatch(object):
@@ -124,6 +139,83 @@ class NodeBatch(object):
 
     def __len__(self):
         return self.batch_size()
+
+
+class _Space(object):
+    __slots__ = ["data"]
+
+    def __init__(self, data):
+        self.data = data
+
+
+class _RowView(MutableMapping):
+    """``G.nodes[ids].data`` / ``G.edges[ids].data`` (view.py:46-81, 114-150)."""
+
+    def __init__(self, graph, sel, node):
+        self._g, self._sel, self._node = graph, sel, node
+
+    def _frame(self):
+        return self._g._node_frame if self._node else self._g._edge_frame
+
+    def __getitem__(self, key):
+        get = self._g.get_n_repr if self._node else self._g.get_e_repr
+        return get(self._sel)[key]
+
+    def __setitem__(self, key, val):
+        put = self._g.set_n_repr if self._node else self._g.set_e_repr
+        put({key: val}, self._sel)
+
+    def __delitem__(self, key):
+        if not is_all(self._sel):
+            raise DGLError("Delete feature data is not supported on only a subset of rows")
+        del self._frame()[key]
+
+    def __iter__(self):
+        return iter(self._frame())
+
+    def __len__(self):
+        return len(self._frame())
+
+
+class NodeView(object):
+    """``G.nodes`` (view.py:15-44): call for all node ids, index for row data."""
+
+    def __init__(self, graph):
+        self._g = graph
+
+    def __len__(self):
+        return self._g.number_of_nodes()
+
+    def __getitem__(self, nodes):
+        if isinstance(nodes, slice):
+            if not (nodes.start is None and nodes.stop is None and nodes.step is None):
+                raise DGLError('Currently only full slice ":" is supported')
+            return _Space(_RowView(self._g, ALL, True))
+        return _Space(_RowView(self._g, nodes, True))
+
+    def __call__(self):
+        return th.arange(self._g.number_of_nodes(), dtype=th.int64)
+
+
+class EdgeView(object):
+    """``G.edges`` (view.py:83-112): call for the edge list, index (edge ids or a
+    (u, v) pair of id lists) for row data."""
+
+    def __init__(self, graph):
+        self._g = graph
+
+    def __len__(self):
+        return self._g.number_of_edges()
+
+    def __getitem__(self, edges):
+        if isinstance(edges, slice):
+            if not (edges.start is None and edges.stop is None and edges.step is None):
+                raise DGLError('Currently only full slice ":" is supported')
+            return _Space(_RowView(self._g, ALL, False))
+        return _Space(_RowView(self._g, edges, False))
+
+    def __call__(self, *args, **kwargs):
+        return self._g.all_edges(*args, **kwargs)
 
 
 class DGLGraph(object):
@@ -188,6 +280,8 @@ class DGLGraph(object):
     # ---- conversion (graph_index.py:1078-1135, :1138-1163) -------------------------
     def from_networkx(self, nx_graph):
         import networkx as nx
+        if self.number_of_nodes() or self.number_of_edges():
+            self.clear()
         if not nx_graph.is_directed():
             nx_graph = nx_graph.to_directed()
         n = nx_graph.number_of_nodes()
@@ -207,6 +301,10 @@ class DGLGraph(object):
         self._graph.add_edges(src, dst)
 
     def from_scipy_sparse_matrix(self, spmat):
+        """Replace the graph by ``spmat``'s edges in COO order (graph.py:1870-1901:
+        clear, then build)."""
+        if self.number_of_nodes() or self.number_of_edges():
+            self.clear()
         coo = spmat.tocoo()
         self._graph.add_nodes(coo.shape[0])
         self._graph.add_edges(coo.row.astype(np.int64), coo.col.astype(np.int64))
@@ -230,6 +328,18 @@ class DGLGraph(object):
         old = self.number_of_edges()
         self._graph.add_edges(_to_index_array(u, "u"), _to_index_array(v, "v"))
         self._extend_frame(self._edge_frame, old, self.number_of_edges() - old, data)
+        self._extend_messages(old)
+
+    def _extend_messages(self, old):
+        """New edges carry no pending message; earlier pending ones stay
+        (graph.py:1044-1047, msg_index.append_zeros / msg_frame.add_rows)."""
+        m = self.number_of_edges()
+        ind = getattr(self, "_msg_ind", None)
+        if ind is not None and ind.shape[0] == old:
+            self._msg_ind = np.concatenate([ind, np.zeros(m - old, bool)])
+        for k, t in (getattr(self, "_msg_frame", None) or {}).items():
+            if t.shape[0] == old:
+                self._msg_frame[k] = th.cat([t, t.new_zeros((m - old,) + tuple(t.shape[1:]))])
 
     def add_edges_with_type(self, u, v, etypes, data=None):
         """Add typed edges (the hack's graph.py:1229); types feed R-GCN kernels."""
@@ -238,6 +348,7 @@ class DGLGraph(object):
         self._graph.add_edges_with_type(_to_index_array(u, "u"), _to_index_array(v, "v"),
                                         _to_index_array(etypes, "etypes"))
         self._extend_frame(self._edge_frame, old, self.number_of_edges() - old, data)
+        self._extend_messages(old)
 
     @staticmethod
     def _extend_frame(frame, old, num, data):
@@ -246,7 +357,7 @@ class DGLGraph(object):
             if data is not None and k in data:
                 ext = data[k]
             else:
-                ext = col.new_zeros((num,) + tuple(col.shape[1:]))
+                ext = frame.init_rows(k, col, th.arange(old, old + num, device=col.device))
             frame._cols[k] = th.cat([col, ext.to(col.device, col.dtype)], 0)
         if data is not None:
             for k, v in data.items():
@@ -291,10 +402,119 @@ class DGLGraph(object):
         """Set the read-only state in place (``graph.py:3819-3860``)."""
         self._readonly = bool(readonly_state)
 
+    @property
     def nodes(self):
-        return th.arange(self.number_of_nodes(), dtype=th.int64)
+        """``G.nodes()`` (all node ids) and ``G.nodes[ids].data`` (view.py:15-81)."""
+        return NodeView(self)
 
-    def edges(self, form="uv", order=None):
+    @property
+    def edges(self):
+        """``G.edges(form, order)`` and ``G.edges[eids or (u, v)].data`` (view.py:83-150)."""
+        return EdgeView(self)
+
+    def edge_ids(self, u, v, force_multi=None, return_uv=False):
+        """Ids of the edges u[i] -> v[i] (graph.py:399-470); a scalar side broadcasts.
+        Every edge of a pair is returned, in id order, pair after pair; with
+        ``return_uv`` also their endpoints."""
+        us, vs = _to_index_array(u, "u"), _to_index_array(v, "v")
+        if us.shape[0] == 1 and vs.shape[0] > 1:
+            us = np.full(vs.shape, us[0], np.int64)
+        if vs.shape[0] == 1 and us.shape[0] > 1:
+            vs = np.full(us.shape, vs[0], np.int64)
+        if us.shape != vs.shape:
+            raise DGLError("u and v must have the same length")
+        src, dst, _ = self._graph.edges()
+        n = max(self.number_of_nodes(), 1)
+        key = src * n + dst
+        order = np.argsort(key, kind="stable")
+        q = us * n + vs
+        lo = np.searchsorted(key[order], q, "left")
+        hi = np.searchsorted(key[order], q, "right")
+        if np.any(hi == lo):
+            i = int(np.nonzero(hi == lo)[0][0])
+            raise DGLError("Edge (%d, %d) does not exist" % (us[i], vs[i]))
+        eids = np.concatenate([order[a:b] for a, b in zip(lo, hi)]) if len(q) else \
+            np.empty(0, np.int64)
+        e = th.from_numpy(eids.astype(np.int64))
+        if return_uv:
+            return th.from_numpy(src[eids].copy()), th.from_numpy(dst[eids].copy()), e
+        return e
+
+    def edge_id(self, u, v, force_multi=None, return_array=False):
+        e = self.edge_ids([u], [v])
+        return e if return_array or e.shape[0] != 1 else int(e[0])
+
+    # ---- feature access by rows (graph.py:1870-2060) -----------------------------
+    def _rows(self, frame, sel, data, num_rows, inplace):
+        for k, val in data.items():
+            if not isinstance(val, th.Tensor):
+                raise DGLError("Feature %s must be a torch tensor" % k)
+            if is_all(sel):
+                frame[k] = val
+                continue
+            idx = th.as_tensor(sel, device=val.device)
+            if val.shape[0] != idx.shape[0]:
+                raise DGLError("Expected %d rows for feature %s, got %d"
+                               % (idx.shape[0], k, val.shape[0]))
+            if k in frame:
+                base = frame[k]
+                if inplace:
+                    base.index_copy_(0, idx.to(base.device), val.to(base.device, base.dtype))
+                    continue
+                frame._cols[k] = base.index_copy(0, idx.to(base.device), val.to(base.device, base.dtype))
+            else:
+                ids = th.arange(num_rows, device=val.device)
+                frame._cols[k] = frame.init_rows(k, val, ids).index_copy(0, idx, val)
+
+    def get_n_repr(self, u=ALL):
+        if is_all(u):
+            return dict(self._node_frame)
+        idx = _to_index_array(u, "u")
+        return {k: v[th.as_tensor(idx, device=v.device)] for k, v in self._node_frame.items()}
+
+    def set_n_repr(self, data, u=ALL, inplace=False):
+        self._rows(self._node_frame, u if is_all(u) else _to_index_array(u, "u"), data,
+                   self.number_of_nodes(), inplace)
+
+    def pop_n_repr(self, key):
+        return self._node_frame.pop(key)
+
+    def get_e_repr(self, edges=ALL):
+        if is_all(edges):
+            return dict(self._edge_frame)
+        eid = self._resolve_edges(edges)[2]
+        return {k: v[th.as_tensor(eid, device=v.device)] for k, v in self._edge_frame.items()}
+
+    def set_e_repr(self, data, edges=ALL, inplace=False):
+        sel = edges if is_all(edges) else self._resolve_edges(edges)[2]
+        self._rows(self._edge_frame, sel, data, self.number_of_edges(), inplace)
+
+    def pop_e_repr(self, key):
+        return self._edge_frame.pop(key)
+
+    def set_n_initializer(self, initializer, field=None):
+        """Initializer of node features (graph.py:1700-1730): ``field`` None sets the
+        default of every column."""
+        self._node_frame.set_initializer(initializer, field)
+
+    def set_e_initializer(self, initializer, field=None):
+        self._edge_frame.set_initializer(initializer, field)
+
+    def clear(self):
+        """Remove every node, edge, feature and pending message (graph.py:1190)."""
+        self._graph = GraphIndex(0)
+        self._node_frame = Frame(self.number_of_nodes, None, self._node_frame._inits)
+        self._edge_frame = Frame(self.number_of_edges, None, self._edge_frame._inits)
+        self._msg_frame, self._msg_ind = {}, None
+
+    def _get_msg_index(self):
+        """Pending-message indicator per edge id (graph.py:_get_msg_index), as int64."""
+        ind = getattr(self, "_msg_ind", None)
+        if ind is None or ind.shape[0] != self.number_of_edges():
+            return np.zeros(self.number_of_edges(), np.int64)
+        return ind.astype(np.int64)
+
+    def all_edges(self, form="uv", order=None):
         src, dst, eid = self._graph.edges()
         s, d, e = th.from_numpy(src.copy()), th.from_numpy(dst.copy()), th.from_numpy(eid.copy())
         if form == "uv":
@@ -304,9 +524,6 @@ class DGLGraph(object):
         if form == "all":
             return s, d, e
         raise DGLError("Invalid form: %s" % form)
-
-    def all_edges(self, form="uv", order=None):
-        return self.edges(form, order)
 
     def in_degrees(self, v=ALL):
         d = th.from_numpy(self._graph.in_degrees())
@@ -386,8 +603,8 @@ class DGLGraph(object):
         g = DGLGraph.__new__(DGLGraph)
         g._graph = self._graph
         g._readonly = self._readonly
-        g._node_frame = Frame(g.number_of_nodes, self._node_frame._cols)
-        g._edge_frame = Frame(g.number_of_edges, self._edge_frame._cols)
+        g._node_frame = Frame(g.number_of_nodes, self._node_frame._cols, self._node_frame._inits)
+        g._edge_frame = Frame(g.number_of_edges, self._edge_frame._cols, self._edge_frame._inits)
         for attr in ("_message_func", "_reduce_func", "_apply_node_func", "_apply_edge_func"):
             if hasattr(self, attr):
                 setattr(g, attr, getattr(self, attr))
@@ -538,6 +755,12 @@ class DGLGraph(object):
                 if k not in out:
                     out[k] = t.new_zeros((n,) + tuple(t.shape[1:]))
                 out[k] = out[k].index_copy(0, nodes, t)
+        zero = th.nonzero(deg == 0).squeeze(1)
+        if out and zero.numel():
+            # zero-degree rows: the node frame's initializer for the field
+            # (degree_bucketing.py:73-79, ir NEW_DICT)
+            for k in out:
+                out[k] = out[k].index_copy(0, zero, self._node_frame.init_rows(k, out[k], zero))
         return out
 
     # ---- registered defaults (graph.py:2458-2548) -------------------------------------
@@ -591,6 +814,10 @@ class DGLGraph(object):
         self._check_builtin(mfuncs, rfuncs)
         if self.number_of_nodes() == 0:
             return
+        if self.number_of_edges() == 0:  # scheduler.py:214-219: every node has zero
+            if apply_node_func is not None:  # in-degree, downgrade to apply_nodes
+                self.apply_nodes(apply_node_func)
+            return
         dev = self._device(self._node_frame, self._edge_frame)
         gidx = self._gidx(dev)
         res = self._reduce(gidx, mfuncs, rfuncs, lambda: self._edge_tensors(ALL, dev), dev)
@@ -607,9 +834,10 @@ class DGLGraph(object):
         sub._parent_eid = eid
         return sub
 
-    def _write_partial(self, res, recv_nodes, apply_node_func, dev):
+    def _write_partial(self, res, recv_nodes, apply_node_func, dev, inplace=False):
         """Write reduced rows of ``recv_nodes`` (sorted, unique) into the node frame,
-        after the optional apply function (scheduler.py:_apply_with_accum)."""
+        after the optional apply function (scheduler.py:_apply_with_accum); with
+        ``inplace`` into the frame's existing tensors (WRITE_ROW_INPLACE_)."""
         v = th.as_tensor(np.unique(recv_nodes), device=dev)
         if apply_node_func is not None:
             data = {k: t[v] for k, t in self._node_frame.items()}
@@ -618,15 +846,11 @@ class DGLGraph(object):
             for k, t in apply_node_func(nb).items():
                 res[k] = th.zeros((self.number_of_nodes(),) + tuple(t.shape[1:]), dtype=t.dtype,
                                   device=dev).index_copy(0, v, t)
-        for k, t in res.items():
-            if k in self._node_frame:
-                base = self._node_frame[k]
-            else:
-                base = th.zeros_like(t)
-            self._node_frame[k] = base.index_copy(0, v, t[v])
+        self._rows(self._node_frame, v.cpu().numpy(), {k: t[v] for k, t in res.items()},
+                   self.number_of_nodes(), inplace)
 
     def _partial_reduce(self, src, dst, eid, message_func, reduce_func, apply_node_func,
-                        recv_nodes):
+                        recv_nodes, inplace=False):
         message_func, reduce_func, apply_node_func = self._defaults(
             message_func, reduce_func, apply_node_func)
         mfuncs, rfuncs = self._as_list(message_func), self._as_list(reduce_func)
@@ -637,7 +861,7 @@ class DGLGraph(object):
         res = self._reduce(gidx, mfuncs, rfuncs,
                            lambda: (th.as_tensor(src, device=dev), th.as_tensor(dst, device=dev),
                                     th.as_tensor(eid, device=dev)), dev)
-        self._write_partial(res, recv_nodes, apply_node_func, dev)
+        self._write_partial(res, recv_nodes, apply_node_func, dev, inplace)
 
     def pull(self, v, message_func="default", reduce_func="default", apply_node_func="default",
              inplace=False):
@@ -648,10 +872,10 @@ class DGLGraph(object):
         if not mask.any():  # scheduler.py:472-476: downgrade to apply_nodes
             apply_node_func = self._default(apply_node_func, "_apply_node_func")
             if apply_node_func is not None:
-                self.apply_nodes(apply_node_func, vs)
+                self.apply_nodes(apply_node_func, vs, inplace)
             return
         self._partial_reduce(src[mask], dst[mask], eid[mask], message_func, reduce_func,
-                             apply_node_func, vs)
+                             apply_node_func, vs, inplace)
 
     def send_and_recv(self, edges, message_func="default", reduce_func="default",
                       apply_node_func="default", inplace=False):
@@ -659,7 +883,8 @@ class DGLGraph(object):
         src, dst, eid = self._resolve_edges(edges)
         if len(eid) == 0:
             return
-        self._partial_reduce(src, dst, eid, message_func, reduce_func, apply_node_func, dst)
+        self._partial_reduce(src, dst, eid, message_func, reduce_func, apply_node_func, dst,
+                             inplace)
 
     def push(self, u, message_func="default", reduce_func="default", apply_node_func="default",
              inplace=False):
@@ -671,7 +896,7 @@ class DGLGraph(object):
         if not mask.any():
             return
         self._partial_reduce(src[mask], dst[mask], eid[mask], message_func, reduce_func,
-                             apply_node_func, dst[mask])
+                             apply_node_func, dst[mask], inplace)
 
     # ---- two-phase send / recv (graph.py:2749-2960, scheduler.py:31-129) ---------------
     def send(self, edges=ALL, message_func="default"):
@@ -729,7 +954,7 @@ class DGLGraph(object):
             mask[:] = False
         if not mask.any():  # scheduler.py:101-107: downgrade to apply_nodes
             if apply_node_func is not None:
-                self.apply_nodes(apply_node_func, vs)
+                self.apply_nodes(apply_node_func, vs, inplace)
             return
         dev = self._device(self._node_frame, self._edge_frame)
         gidx = _PartialIndex(self.number_of_nodes(), src[mask], dst[mask],
@@ -739,7 +964,7 @@ class DGLGraph(object):
                                     th.as_tensor(dst[mask], device=dev),
                                     th.as_tensor(eid[mask], device=dev)), dev,
                            msgs=self._msg_frame)
-        self._write_partial(res, vs, apply_node_func, dev)
+        self._write_partial(res, vs, apply_node_func, dev, inplace)
         ind[eid[mask]] = False
         if not ind.any():
             self._msg_frame = {}
@@ -748,18 +973,14 @@ class DGLGraph(object):
         src, dst, eid = self._graph.edges()
         if is_all(edges):
             return src, dst, eid
+        nested = getattr(edges, "ndim", 1) > 1 or (
+            isinstance(edges, list) and any(isinstance(x, (list, tuple, np.ndarray, th.Tensor))
+                                            for x in edges))
+        if nested:  # graph.py:2780 (utils.toindex rejects 2-D input)
+            raise DGLError("Edges must be edge ids or a (u, v) tuple, got a nested sequence")
         if isinstance(edges, tuple) and len(edges) == 2:
-            u = _to_index_array(edges[0], "u")
-            v = _to_index_array(edges[1], "v")
-            lookup = {}
-            for i in range(len(src)):
-                lookup.setdefault((int(src[i]), int(dst[i])), []).append(i)
-            sel = []
-            for a, b in zip(u, v):
-                if (int(a), int(b)) not in lookup:
-                    raise DGLError("Edge (%d, %d) does not exist" % (a, b))
-                sel.extend(lookup[(int(a), int(b))])
-            sel = np.array(sel, np.int64)
+            # every edge of each (u, v) pair, a length-1 side broadcast (utils.py:toindex)
+            sel = self.edge_ids(edges[0], edges[1]).numpy()
         else:
             sel = _to_index_array(edges, "eid")
         return src[sel], dst[sel], eid[sel]
@@ -794,35 +1015,36 @@ class DGLGraph(object):
                 res = func._invoke(gidx, self._node_frame, self._node_frame, self._edge_frame, m,
                                    reducer="none")
                 sel = th.as_tensor(eid, device=dev)
-                base = self._edge_frame[func.out_field] if func.out_field in self._edge_frame \
-                    else th.zeros_like(res)
-                res = base.index_copy(0, sel, res[sel])
-            self._edge_frame[func.out_field] = res
+                self._rows(self._edge_frame, np.asarray(eid), {func.out_field: res[sel]}, m,
+                           inplace)
+                return
+            self._edge_frame[func.out_field] = res  # all edges: a new column, never in place
             return
         s, d, e = self._edge_tensors(edges, dev)
         eb = EdgeBatch(s, d, e, {k: v[s] for k, v in self._node_frame.items()},
                        {k: v[d] for k, v in self._node_frame.items()},
                        {k: v[e] for k, v in self._edge_frame.items()})
         out = func(eb)
-        for k, v in out.items():
-            if is_all(edges):
+        if is_all(edges):  # scheduler.py:334-375: all edges are written as new columns
+            for k, v in out.items():
                 self._edge_frame[k] = v
-            else:
-                base = self._edge_frame[k] if k in self._edge_frame else \
-                    v.new_zeros((self.number_of_edges(),) + tuple(v.shape[1:]))
-                self._edge_frame[k] = base.index_copy(0, e, v)
+            return
+        self._rows(self._edge_frame, e.cpu().numpy(), out, self.number_of_edges(), inplace)
 
-    def apply_nodes(self, func, v=ALL, inplace=False):
+    def apply_nodes(self, func="default", v=ALL, inplace=False):
+        func = self._default(func, "_apply_node_func")
+        if func is None:
+            raise DGLError("A node function is required (pass one or call "
+                           "register_apply_node_func)")
         dev = self._device(self._node_frame)
         nodes = self.nodes().to(dev) if is_all(v) else th.as_tensor(_to_index_array(v, "v"), device=dev)
         nb = NodeBatch(nodes, {k: t[nodes] for k, t in self._node_frame.items()})
-        for k, t in func(nb).items():
-            if is_all(v):
+        out = func(nb)
+        if is_all(v):  # all nodes: new columns, never in place (test_inplace_update.py:267)
+            for k, t in out.items():
                 self._node_frame[k] = t
-            else:
-                base = self._node_frame[k] if k in self._node_frame else \
-                    t.new_zeros((self.number_of_nodes(),) + tuple(t.shape[1:]))
-                self._node_frame[k] = base.index_copy(0, nodes, t)
+            return
+        self._rows(self._node_frame, nodes.cpu().numpy(), out, self.number_of_nodes(), inplace)
 
 
 class _PartialIndex(GraphIndex):

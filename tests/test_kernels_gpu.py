@@ -299,13 +299,28 @@ def test_single_hub_and_gaps():
 
 
 def test_empty_graph_and_isolated():
+    """Edgeless graph: update_all downgrades to apply_nodes and writes no reduce
+    field (scheduler.py:216-222); the kernel itself still identity-fills every row
+    (binary_reduce_common.h:444-485), and so do isolated rows of a graph with edges."""
     g = dgl.DGLGraph()
     g.add_nodes(7)
     g.ndata["h"] = th.ones(7, 16, device=DEV)
     g.update_all(fn.copy_u("h", "m"), fn.sum("m", "s"))
-    assert th.equal(g.ndata["s"], th.zeros(7, 16, device=DEV))
+    assert "s" not in g.ndata
+    gidx = g._graph.get_immutable_gidx(DEV)
+    assert th.equal(dgl.backend.copy_reduce("sum", gidx, 0, g.ndata["h"], 7),
+                    th.zeros(7, 16, device=DEV))
+    assert (dgl.backend.copy_reduce("max", gidx, 0, g.ndata["h"], 7)
+            == -3.4028234663852886e38).all()
+    g = dgl.DGLGraph()
+    g.add_nodes(7)
+    g.add_edges([0], [1])
+    g.ndata["h"] = th.ones(7, 16, device=DEV)
+    g.update_all(fn.copy_u("h", "m"), fn.sum("m", "s"))
+    assert th.equal(g.ndata["s"][1], th.ones(16, device=DEV))
+    assert th.equal(g.ndata["s"][th.tensor([0, 2, 3, 4, 5, 6])], th.zeros(6, 16, device=DEV))
     g.update_all(fn.copy_u("h", "m"), fn.max("m", "s"))
-    assert (g.ndata["s"] == -3.4028234663852886e38).all()
+    assert (g.ndata["s"][th.tensor([0, 2, 3, 4, 5, 6])] == -3.4028234663852886e38).all()
 
 
 def test_rejects_cpu_tensors():
