@@ -858,6 +858,10 @@ def main():
             res["c4"] = measure_c4(world, rank, dist, cdev, device, args)
         except SystemExit as exc:  # parity checks agree across ranks before exiting
             res["c4"] = {"error": str(exc)}
+        except Exception as exc:  # noqa: BLE001
+            if world > 1:  # peers may sit in a collective: fail the job rather than hang
+                raise
+            res["c4"] = {"error": repr(exc)}  # one process: keep the headline line
         log("C4: %s" % json.dumps(res["c4"]))
     if rank == 0:
         print(json.dumps(res), flush=True)
