@@ -8,9 +8,11 @@ The subset a heterogeneous GNN needs on the message-passing path:
   ``edata`` for single-type graphs, counts, degrees, ``to_canonical_etype``;
 * relation views ``g[etype]`` / ``g[stype, etype, dtype]`` that behave like a
   (bipartite) DGLGraph -- ``srcdata`` / ``dstdata`` / ``edata``, ``update_all``,
-  ``apply_edges``, ``local_var`` -- so GraphConv / GATConv / edge_softmax run on
-  one relation and ``nn.pytorch.HeteroGraphConv`` composes them
-  (``nn/pytorch/hetero.py:112-170``);
+  ``send_and_recv``, ``pull``, ``push``, ``send`` / ``recv``, ``apply_nodes``,
+  ``apply_edges``, ``local_var``, with builtin or user-defined message / reduce
+  functions (UDF reducers by degree bucketing) -- so GraphConv / GATConv /
+  edge_softmax run on one relation and ``nn.pytorch.HeteroGraphConv`` composes
+  them (``nn/pytorch/hetero.py:112-170``);
 * ``update_all(..., etype=)`` and ``multi_update_all(etype_dict, cross_reducer)``
   (``heterograph.py:3570-3656``).
 
@@ -137,15 +139,6 @@ def _as_list(f):
     return list(f) if isinstance(f, (list, tuple)) else [f]
 
 
-def _check_builtin(mfuncs, rfuncs):
-    for f in mfuncs:
-        if not isinstance(f, MessageFunction):
-            raise DGLError("message passing takes builtin message functions (dgl.function.*)")
-    for f in rfuncs:
-        if not isinstance(f, ReduceFunction):
-            raise DGLError("user-defined reduce functions are not supported by the MI355X engine")
-
-
 def _reduce(rel, gidx, mfuncs, rfuncs, srcf, dstf, edgef):
     fld2m = {f.out_field: f for f in mfuncs}
     out = {}
@@ -164,6 +157,129 @@ def _device_of(*frames):
             if isinstance(v, th.Tensor):
                 return v.device
     return th.device("cuda", th.cuda.current_device())
+
+
+def _is_udf(funcs):
+    return len(funcs) == 1 and not isinstance(funcs[0], (MessageFunction, ReduceFunction))
+
+
+def _check_funcs(mfuncs, rfuncs):
+    """Builtins (one kernel per message / reduce pair) or ONE user-defined message
+    and / or reduce function (heterograph.py:3400-3470 accepts both)."""
+    if not _is_udf(mfuncs):
+        for f in mfuncs:
+            if not isinstance(f, MessageFunction):
+                raise DGLError("a list of message functions must hold builtins only")
+    if not _is_udf(rfuncs):
+        for f in rfuncs:
+            if not isinstance(f, ReduceFunction):
+                raise DGLError("a list of reduce functions must hold builtins only")
+
+
+def _rel_edge_ids(rel, u, v):
+    """Every edge u[i] -> v[i] of one relation, in id order per pair; a length-1
+    side broadcasts (heterograph.py:edge_ids)."""
+    us, vs = _ids(u), _ids(v)
+    if us.shape[0] == 1 and vs.shape[0] > 1:
+        us = np.full(vs.shape, us[0], np.int64)
+    if vs.shape[0] == 1 and us.shape[0] > 1:
+        vs = np.full(us.shape, vs[0], np.int64)
+    if us.shape != vs.shape:
+        raise DGLError("u and v must have the same length")
+    key = rel.src * max(rel.n_dst, 1) + rel.dst
+    order = np.argsort(key, kind="stable")
+    q = us * max(rel.n_dst, 1) + vs
+    lo, hi = np.searchsorted(key[order], q, "left"), np.searchsorted(key[order], q, "right")
+    if np.any(hi == lo):
+        i = int(np.nonzero(hi == lo)[0][0])
+        raise DGLError("Edge (%d, %d) does not exist" % (us[i], vs[i]))
+    return np.concatenate([order[a:b] for a, b in zip(lo, hi)]) if len(q) else \
+        np.empty(0, np.int64)
+
+
+def _select(rel, edges):
+    """Edge ids of ``edges``: ALL, ids, or a (u, v) pair of id sequences."""
+    if is_all(edges):
+        return None
+    if isinstance(edges, tuple) and len(edges) == 2:
+        return _rel_edge_ids(rel, edges[0], edges[1])
+    return _ids(edges)
+
+
+def _rel_messages(mfuncs, gidx, s, d, srcf, dstf, edgef, m):
+    """Messages of the walked edges, one row per edge in the block's edge order."""
+    if _is_udf(mfuncs):
+        eb = EdgeBatch(s, d, th.arange(m, device=s.device), {k: v[s] for k, v in srcf.items()},
+                       {k: v[d] for k, v in dstf.items()}, dict(edgef))
+        return dict(mfuncs[0](eb))
+    return {f.out_field: f._invoke(gidx, srcf, dstf, edgef, m, reducer="none") for f in mfuncs}
+
+
+def _bucket_reduce(rfunc, msgs, d, n_dst, dstf):
+    """Degree bucketing (runtime/degree_bucketing.py) on the destination side of one
+    relation: one UDF call per in-degree on a (nodes, degree, ...) mailbox in edge
+    order; rows of nodes without messages are zero."""
+    d = d.long()
+    order = th.argsort(d, stable=True)
+    deg = th.bincount(d, minlength=n_dst)
+    starts = th.cumsum(deg, 0) - deg
+    out = {}
+    for dv in th.unique(deg).tolist():
+        if dv == 0:
+            continue
+        nodes = th.nonzero(deg == dv).squeeze(1)
+        mids = order[starts[nodes].unsqueeze(1) + th.arange(dv, device=d.device)]
+        nb = NodeBatch(nodes, {k: t[nodes] for k, t in dstf.items()},
+                       {k: t[mids] for k, t in msgs.items()})
+        for k, t in rfunc(nb).items():
+            if k not in out:
+                out[k] = t.new_zeros((n_dst,) + tuple(t.shape[1:]))
+            out[k] = out[k].index_copy(0, nodes, t)
+    return out
+
+
+def _rel_reduce(rel, mfuncs, rfuncs, srcf, dstf, edgef, sel=None, msgs=None):
+    """Reduce the messages of one relation's edges (all, or the ids ``sel``) onto
+    its destination nodes: builtin pairs as one HIP kernel each, a UDF message as
+    materialised rows reduced by ``copy_e`` kernels, a UDF reducer by degree
+    bucketing.  ``msgs`` (rows in ``sel`` order) replaces the message function."""
+    from . import backend as B
+    dev = _device_of(srcf, dstf, edgef)
+    if sel is None:
+        gidx = rel.get_immutable_gidx(dev)
+        s = th.from_numpy(rel.src).to(dev)
+        d = th.from_numpy(rel.dst).to(dev)
+        ef = edgef
+    else:
+        s = th.from_numpy(rel.src[sel]).to(dev)
+        d = th.from_numpy(rel.dst[sel]).to(dev)
+        gidx = device_block_gidx(rel.n_src, rel.n_dst, s.int(), d.int())
+        st = th.from_numpy(sel).to(dev)
+        ef = {k: v[st] for k, v in edgef.items()}
+    m = int(s.shape[0])
+    if _is_udf(rfuncs):
+        if msgs is None:
+            msgs = _rel_messages(mfuncs, gidx, s, d, srcf, dstf, ef, m)
+        return _bucket_reduce(rfuncs[0], msgs, d, rel.n_dst, dstf)
+    if msgs is None and _is_udf(mfuncs):
+        msgs = _rel_messages(mfuncs, gidx, s, d, srcf, dstf, ef, m)
+    if msgs is not None:
+        out = {}
+        for r in rfuncs:
+            if r.msg_field not in msgs:
+                raise DGLError('Reduce function requires message field "%s", but the '
+                               'message function does not generate it.' % r.msg_field)
+            out[r.out_field] = B.copy_reduce(r.name, gidx, TargetCode.EDGE,
+                                             msgs[r.msg_field].contiguous(), rel.n_dst)
+        return out
+    return _reduce(rel, gidx, mfuncs, rfuncs, srcf, dstf, ef)
+
+
+def _write_rows(frame, v, res, n):
+    """Rows ``v`` (device ids) of ``res`` into a node frame (a dict of columns)."""
+    for k, t in res.items():
+        base = frame[k] if k in frame else t.new_zeros((n,) + tuple(t.shape[1:]))
+        frame[k] = base.index_copy(0, v, t[v].to(base.dtype))
 
 
 class DGLHeteroGraph:
@@ -350,11 +466,10 @@ class DGLHeteroGraph:
                 per_field = OrderedDict()
                 for c, mfunc, rfunc, afunc in sorted(items, key=lambda it: self._cetypes.index(it[0])):
                     mfs, rfs = _as_list(mfunc), _as_list(rfunc)
-                    _check_builtin(mfs, rfs)
+                    _check_funcs(mfs, rfs)
                     rel = self._rels[c]
                     srcf, dstf, edgef = self._nframes[c[0]], self._nframes[c[2]], self._eframes[c]
-                    gidx = rel.get_immutable_gidx(_device_of(srcf, dstf, edgef))
-                    out = _reduce(rel, gidx, mfs, rfs, srcf, dstf, edgef)
+                    out = _rel_reduce(rel, mfs, rfs, srcf, dstf, edgef)
                     if afunc is not None:
                         nb = NodeBatch(th.arange(rel.n_dst), dict(dstf, **out))
                         out.update(afunc(nb))
@@ -475,29 +590,144 @@ class _RelationGraph:
 
     def update_all(self, message_func, reduce_func, apply_node_func=None):
         mfs, rfs = _as_list(message_func), _as_list(reduce_func)
-        _check_builtin(mfs, rfs)
-        gidx = self._graph.get_immutable_gidx(_device_of(self.srcdata, self.dstdata, self.edata))
-        out = _reduce(self._graph, gidx, mfs, rfs, self.srcdata, self.dstdata, self.edata)
+        _check_funcs(mfs, rfs)
+        rel = self._graph
+        if rel.number_of_edges() == 0:  # scheduler.py:216-222: downgrade to apply
+            if apply_node_func is not None:
+                self.apply_nodes(apply_node_func)
+            return
+        out = _rel_reduce(rel, mfs, rfs, self.srcdata, self.dstdata, self.edata)
         if apply_node_func is not None:
-            nb = NodeBatch(th.arange(self._graph.n_dst), dict(self.dstdata, **out))
+            nb = NodeBatch(th.arange(rel.n_dst), dict(self.dstdata, **out))
             out.update(apply_node_func(nb))
         self.dstdata.update(out)
 
+    def apply_nodes(self, func, v=ALL):
+        """On the destination nodes of the relation."""
+        dev = _device_of(self.dstdata)
+        nodes = th.arange(self._graph.n_dst, device=dev) if is_all(v) else \
+            th.as_tensor(_ids(v), device=dev)
+        out = func(NodeBatch(nodes, {k: t[nodes] for k, t in self.dstdata.items()}))
+        if is_all(v):
+            self.dstdata.update(out)
+        else:
+            _write_rows(self.dstdata, nodes, {k: t.new_zeros((self._graph.n_dst,) +
+                                                             tuple(t.shape[1:])).index_copy(0, nodes, t)
+                                              for k, t in out.items()}, self._graph.n_dst)
+
+    def _partial(self, sel, recv, mfs, rfs, afunc, msgs=None):
+        """Reduce the edges ``sel`` onto the destination nodes ``recv`` (sorted,
+        unique numpy ids), apply, write their rows (scheduler.py:_apply_with_accum)."""
+        rel = self._graph
+        dev = _device_of(self.srcdata, self.dstdata, self.edata)
+        out = _rel_reduce(rel, mfs, rfs, self.srcdata, self.dstdata, self.edata, sel, msgs)
+        v = th.as_tensor(recv, device=dev)
+        if afunc is not None:
+            data = {k: t[v] for k, t in self.dstdata.items()}
+            data.update({k: t[v] for k, t in out.items()})
+            for k, t in afunc(NodeBatch(v, data)).items():
+                out[k] = t.new_zeros((rel.n_dst,) + tuple(t.shape[1:])).index_copy(0, v, t)
+        _write_rows(self.dstdata, v, out, rel.n_dst)
+
+    def send_and_recv(self, edges, message_func, reduce_func, apply_node_func=None):
+        mfs, rfs = _as_list(message_func), _as_list(reduce_func)
+        _check_funcs(mfs, rfs)
+        sel = _select(self._graph, edges)
+        sel = np.arange(self._graph.number_of_edges()) if sel is None else sel
+        if sel.size == 0:
+            return
+        self._partial(sel, np.unique(self._graph.dst[sel]), mfs, rfs, apply_node_func)
+
+    def pull(self, v, message_func, reduce_func, apply_node_func=None):
+        mfs, rfs = _as_list(message_func), _as_list(reduce_func)
+        _check_funcs(mfs, rfs)
+        vs = np.unique(_ids(v))
+        sel = np.nonzero(np.isin(self._graph.dst, vs))[0]
+        if sel.size == 0:  # scheduler.py:472-476
+            if apply_node_func is not None:
+                self.apply_nodes(apply_node_func, vs)
+            return
+        self._partial(sel, vs, mfs, rfs, apply_node_func)
+
+    def push(self, u, message_func, reduce_func, apply_node_func=None):
+        mfs, rfs = _as_list(message_func), _as_list(reduce_func)
+        _check_funcs(mfs, rfs)
+        sel = np.nonzero(np.isin(self._graph.src, _ids(u)))[0]
+        if sel.size == 0:
+            return
+        self._partial(sel, np.unique(self._graph.dst[sel]), mfs, rfs, apply_node_func)
+
+    def send(self, edges=ALL, message_func=None):
+        """Messages of ``edges`` kept on the relation until ``recv`` consumes them."""
+        rel = self._graph
+        mfs = _as_list(message_func)
+        _check_funcs(mfs, [])
+        sel = _select(rel, edges)
+        sel = np.arange(rel.number_of_edges()) if sel is None else sel
+        if sel.size == 0:
+            return
+        dev = _device_of(self.srcdata, self.dstdata, self.edata)
+        s = th.from_numpy(rel.src[sel]).to(dev)
+        d = th.from_numpy(rel.dst[sel]).to(dev)
+        gidx = device_block_gidx(rel.n_src, rel.n_dst, s.int(), d.int())
+        st = th.from_numpy(sel).to(dev)
+        msgs = _rel_messages(mfs, gidx, s, d, self.srcdata, self.dstdata,
+                             {k: t[st] for k, t in self.edata.items()}, int(sel.size))
+        m = rel.number_of_edges()
+        if getattr(rel, "_msg_ind", None) is None:
+            rel._msg_ind, rel._msg_frame = np.zeros(m, bool), {}
+        for k, t in msgs.items():
+            old = rel._msg_frame.get(k)
+            if old is None or old.shape[1:] != t.shape[1:]:
+                old = t.new_zeros((m,) + tuple(t.shape[1:]))
+            rel._msg_frame[k] = old.index_copy(0, st, t)
+        rel._msg_ind[sel] = True
+
+    def recv(self, v=ALL, reduce_func=None, apply_node_func=None):
+        rel = self._graph
+        rfs = _as_list(reduce_func)
+        _check_funcs([], rfs)
+        vs = np.arange(rel.n_dst) if is_all(v) else np.unique(_ids(v))
+        ind = getattr(rel, "_msg_ind", None)
+        sel = np.empty(0, np.int64) if ind is None else \
+            np.nonzero(ind & np.isin(rel.dst, vs))[0]
+        if sel.size == 0:  # scheduler.py:101-107
+            if apply_node_func is not None:
+                self.apply_nodes(apply_node_func, vs)
+            return
+        dev = _device_of(self.srcdata, self.dstdata, self.edata)
+        st = th.from_numpy(sel).to(dev)
+        msgs = {k: t[st] for k, t in rel._msg_frame.items()}
+        self._partial(sel, vs, [], rfs, apply_node_func, msgs)
+        ind[sel] = False
+
     def apply_edges(self, func, edges=ALL):
         dev = _device_of(self.srcdata, self.dstdata, self.edata)
-        if not is_all(edges):
-            raise DGLError("apply_edges on a relation view takes all edges")
+        rel = self._graph
+        sel = _select(rel, edges)
+        m = rel.number_of_edges()
+        if sel is None:
+            s, d = th.from_numpy(rel.src).to(dev), th.from_numpy(rel.dst).to(dev)
+            gidx, ef, k = rel.get_immutable_gidx(dev), self.edata, m
+        else:
+            s, d = th.from_numpy(rel.src[sel]).to(dev), th.from_numpy(rel.dst[sel]).to(dev)
+            gidx = device_block_gidx(rel.n_src, rel.n_dst, s.int(), d.int())
+            st = th.from_numpy(sel).to(dev)
+            ef, k = {kk: t[st] for kk, t in self.edata.items()}, int(sel.size)
         if isinstance(func, MessageFunction):
-            gidx = self._graph.get_immutable_gidx(dev)
-            self.edata[func.out_field] = func._invoke(gidx, self.srcdata, self.dstdata, self.edata,
-                                                      self._graph.number_of_edges(), reducer="none")
+            out = {func.out_field: func._invoke(gidx, self.srcdata, self.dstdata, ef, k,
+                                                reducer="none")}
+        else:
+            eb = EdgeBatch(s, d, th.arange(k, device=dev), {kk: t[s] for kk, t in self.srcdata.items()},
+                           {kk: t[d] for kk, t in self.dstdata.items()}, dict(ef))
+            out = func(eb)
+        if sel is None:
+            self.edata.update(out)
             return
-        s = th.from_numpy(self._graph.src).to(dev)
-        d = th.from_numpy(self._graph.dst).to(dev)
-        e = th.arange(self._graph.number_of_edges(), device=dev)
-        eb = EdgeBatch(s, d, e, {k: v[s] for k, v in self.srcdata.items()},
-                       {k: v[d] for k, v in self.dstdata.items()}, dict(self.edata))
-        self.edata.update(func(eb))
+        st = th.from_numpy(sel).to(dev)
+        for kk, t in out.items():
+            base = self.edata[kk] if kk in self.edata else t.new_zeros((m,) + tuple(t.shape[1:]))
+            self.edata[kk] = base.index_copy(0, st, t.to(base.dtype))
 
 
 def heterograph(data_dict, num_nodes_dict=None):

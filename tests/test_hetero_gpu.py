@@ -143,3 +143,88 @@ def test_gat_conv_on_bipartite_relation(use_fused):
     gat.use_fused = not use_fused
     out2 = gat(rel, (g.nodes["user"].data["h"], g.nodes["game"].data["h"]))
     assert th.allclose(out, out2, rtol=1e-4, atol=1e-5)
+
+
+def _test_heterograph():
+    """tests/compute/test_heterograph.py:12-32 (the wishes relation from its edge
+    list: networkx is not installed here)."""
+    import scipy.sparse as ssp
+    plays = ssp.coo_matrix(([1, 1, 1, 1], ([0, 1, 2, 1], [0, 0, 1, 1])))
+    follows_g = dgl.graph([(0, 1), (1, 2)], "user", "follows")
+    plays_g = dgl.bipartite(plays, "user", "plays", "game")
+    wishes_g = dgl.bipartite([(0, 1), (2, 0)], "user", "wishes", "game")
+    develops_g = dgl.bipartite([(0, 0), (1, 1)], "developer", "develops", "game")
+    return dgl.hetero_from_relations([follows_g, plays_g, wishes_g, develops_g])
+
+
+def test_relation_updates_known_answers():
+    """test_heterograph.py:1313-1359: update_all / send_and_recv / send + recv / pull
+    / push on the (user, plays, game) relation, builtin and UDF message / reduce,
+    with and without an apply function."""
+    import itertools
+
+    def msg_func(edges):
+        return {"m": edges.src["h"]}
+
+    def reduce_func(nodes):
+        return {"y": nodes.mailbox["m"].sum(1)}
+
+    def apply_func(nodes):
+        return {"y": nodes.data["y"] * 2}
+    g = _test_heterograph()
+    x = th.randn(3, 5, device=DEV)
+    g.nodes["user"].data["h"] = x
+    close = lambda a, b: th.allclose(a, b, rtol=1e-6, atol=1e-6)  # noqa: E731
+    for msg, red, apply in itertools.product([fn.copy_u("h", "m"), msg_func],
+                                             [fn.sum("m", "y"), reduce_func],
+                                             [None, apply_func]):
+        k = 1 if apply is None else 2
+        g["user", "plays", "game"].update_all(msg, red, apply)
+        y = g.nodes["game"].data["y"]
+        assert close(y[0], (x[0] + x[1]) * k) and close(y[1], (x[1] + x[2]) * k)
+        del g.nodes["game"].data["y"]
+        g["user", "plays", "game"].send_and_recv(([0, 1, 2], [0, 1, 1]), msg, red, apply)
+        y = g.nodes["game"].data["y"]
+        assert close(y[0], x[0] * k) and close(y[1], (x[1] + x[2]) * k)
+        del g.nodes["game"].data["y"]
+        plays_g = g["user", "plays", "game"]
+        plays_g.send(([0, 1, 2], [0, 1, 1]), msg)
+        plays_g.recv([0, 1], red, apply)
+        y = g.nodes["game"].data["y"]
+        assert close(y[0], x[0] * k) and close(y[1], (x[1] + x[2]) * k)
+        del g.nodes["game"].data["y"]
+        g["user", "plays", "game"].pull(0, msg, red, apply)
+        y = g.nodes["game"].data["y"]
+        assert close(y[0], (x[0] + x[1]) * k)
+        del g.nodes["game"].data["y"]
+        g["user", "plays", "game"].push(0, msg, red, apply)
+        y = g.nodes["game"].data["y"]
+        assert close(y[0], x[0] * k)
+        del g.nodes["game"].data["y"]
+
+
+def test_multi_update_all_backward_known_answer():
+    """test_heterograph.py:1361-1376: plays + wishes summed into games, ones as the
+    upstream gradient -> every user row gets 2."""
+    g = _test_heterograph()
+    x = th.randn(3, 5, device=DEV, requires_grad=True)
+    g.nodes["user"].data["h"] = x
+    g.multi_update_all({"plays": (fn.copy_u("h", "m"), fn.sum("m", "y")),
+                        "wishes": (fn.copy_u("h", "m"), fn.sum("m", "y"))}, "sum")
+    y = g.nodes["game"].data["y"]
+    y.backward(th.ones_like(y))
+    assert th.equal(x.grad.cpu(), th.full((3, 5), 2.))
+
+
+def test_stack_reduce_shapes():
+    """test_heterograph.py:1463-1487."""
+    g = _test_heterograph()
+    g.nodes["user"].data["h"] = th.randn(3, 200, device=DEV)
+
+    def mfunc(edges):
+        return {"m": edges.src["h"]}
+    g.multi_update_all({"plays": (mfunc, lambda n: {"y": n.mailbox["m"].sum(1)}),
+                        "wishes": (mfunc, lambda n: {"y": n.mailbox["m"].max(1)[0]})}, "stack")
+    assert tuple(g.nodes["game"].data["y"].shape) == (g.number_of_nodes("game"), 2, 200)
+    g.multi_update_all({"plays": (mfunc, lambda n: {"y": n.mailbox["m"].sum(1)})}, "stack")
+    assert tuple(g.nodes["game"].data["y"].shape) == (g.number_of_nodes("game"), 1, 200)
