@@ -545,19 +545,25 @@ class DGLGraph(object):
     def out_degree(self, v):
         return int(self.out_degrees([v])[0])
 
-    def in_edges(self, v, form="uv"):
-        vs = _to_index_array(v, "v")
+    def _incident(self, nodes, by_dst, form):
+        """Edges of each queried node in query order, each node's edges in id order
+        (graph_index.py in_edges / out_edges: one CSR row per node)."""
+        q = _to_index_array(nodes, "v")
         src, dst, eid = self._graph.edges()
-        mask = np.isin(dst, vs)
-        s, d, e = (th.from_numpy(a[mask].copy()) for a in (src, dst, eid))
+        key = dst if by_dst else src
+        order = np.argsort(key, kind="stable")
+        lo = np.searchsorted(key[order], q, "left")
+        hi = np.searchsorted(key[order], q, "right")
+        sel = np.concatenate([order[a:b] for a, b in zip(lo, hi)]) if len(q) else \
+            np.empty(0, np.int64)
+        s, d, e = (th.from_numpy(a[sel].copy()) for a in (src, dst, eid))
         return {"uv": (s, d), "eid": e, "all": (s, d, e)}[form]
 
+    def in_edges(self, v, form="uv"):
+        return self._incident(v, True, form)
+
     def out_edges(self, u, form="uv"):
-        us = _to_index_array(u, "u")
-        src, dst, eid = self._graph.edges()
-        mask = np.isin(src, us)
-        s, d, e = (th.from_numpy(a[mask].copy()) for a in (src, dst, eid))
-        return {"uv": (s, d), "eid": e, "all": (s, d, e)}[form]
+        return self._incident(u, False, form)
 
     def adjacency_matrix_scipy(self, transpose=False, fmt="csr", return_edge_ids=None):
         """(graph.py:3567-3599) A row is a destination and a column a source by
@@ -1030,6 +1036,41 @@ class DGLGraph(object):
                 self._edge_frame[k] = v
             return
         self._rows(self._edge_frame, e.cpu().numpy(), out, self.number_of_edges(), inplace)
+
+    def group_apply_edges(self, group_by, func, edges=ALL, inplace=False):
+        """Edges grouped by their source (``group_by='src'``) or destination node,
+        one UDF call per degree bucket on (nodes, degree, ...) shaped data, edges of
+        a node in edge-id order (graph.py:2667-2760, scheduler.py:377-415)."""
+        if group_by not in ("src", "dst"):
+            raise DGLError("Group_by should be either src or dst")
+        dev = self._device(self._node_frame, self._edge_frame)
+        s, d, e = self._edge_tensors(edges, dev)
+        key = (s if group_by == "src" else d).long()
+        order = th.argsort(key, stable=True)
+        n = self.number_of_nodes()
+        deg = th.bincount(key, minlength=n)
+        starts = th.cumsum(deg, 0) - deg
+        out = {}
+        for dv in th.unique(deg).tolist():
+            if dv == 0:
+                continue
+            nodes = th.nonzero(deg == dv).squeeze(1)
+            pos = order[starts[nodes].unsqueeze(1) + th.arange(dv, device=dev)]   # (b, dv)
+            bs, bd, be = s[pos], d[pos], e[pos]
+            eb = EdgeBatch(bs, bd, be, {k: t[bs] for k, t in self._node_frame.items()},
+                           {k: t[bd] for k, t in self._node_frame.items()},
+                           {k: t[be] for k, t in self._edge_frame.items()})
+            for k, t in func(eb).items():
+                if k not in out:
+                    out[k] = t.new_zeros((self.number_of_edges(),) + tuple(t.shape[2:]))
+                out[k] = out[k].index_copy(0, be.reshape(-1), t.reshape((-1,) + tuple(t.shape[2:])))
+        sel = e.cpu().numpy()
+        if is_all(edges) and not inplace:
+            for k, t in out.items():
+                self._edge_frame[k] = t
+            return
+        self._rows(self._edge_frame, sel, {k: t[e] for k, t in out.items()},
+                   self.number_of_edges(), inplace)
 
     def apply_nodes(self, func="default", v=ALL, inplace=False):
         func = self._default(func, "_apply_node_func")

@@ -595,3 +595,43 @@ def test_inplace_apply():
     assert allclose(ef, new_ef)
     g.apply_edges(lambda e: {"e": e.data["e"] * 2}, inplace=True)
     assert not allclose(ef, g.edata["e"])
+
+
+# ---- group_apply_edges (test_basics.py:628-680) ---------------------------------
+@pytest.mark.parametrize("group_by", ["src", "dst"])
+def test_group_apply_edges(group_by):
+    def edge_udf(edges):
+        h = (edges.data["feat"] * (edges.src["h"] + edges.dst["h"])).sum(2)
+        return {"norm_feat": th.softmax(h, dim=1)}
+    g = DGLGraph()
+    g.add_nodes(10)
+    g.add_edges(0, [1, 2, 3, 4, 5, 6, 7, 8])
+    g.add_edges(1, [2, 3, 4, 6, 7, 8])
+    g.add_edges(2, [2, 3, 4, 5, 6, 7, 8])
+    g.ndata["h"] = randn(g.number_of_nodes(), D)
+    g.edata["feat"] = randn(g.number_of_edges(), D)
+    g.group_apply_edges(group_by=group_by, func=edge_udf)
+    u, v, eid = g.out_edges(1, form="all") if group_by == "src" else g.in_edges(5, form="all")
+    out = g.edges[eid].data["norm_feat"]
+    ref = (g.nodes[u].data["h"] + g.nodes[v].data["h"]) * g.edges[eid].data["feat"]
+    assert allclose(out, th.softmax(ref.sum(1), dim=0))
+
+
+def test_group_apply_edges_bucket_ids():
+    """test_basics.py:661-680 (GitHub issue 1036): every bucket row holds exactly
+    the in-edges of its destination."""
+    m = sp.random(10, 10, 0.2, random_state=np.random.RandomState(3))
+    g = DGLGraph(m, readonly=True)
+    g.ndata["id"] = th.arange(g.number_of_nodes(), device=DEV)
+    g.edata["id"] = th.arange(g.number_of_edges(), device=DEV)
+
+    def apply(edges):
+        w = edges.data["id"]
+        n_nodes, deg = w.shape
+        dst = edges.dst["id"][:, 0].cpu()
+        eid1 = np.sort(g.in_edges(dst, "eid").numpy().reshape(n_nodes, deg), 1)
+        eid2 = np.sort(w.cpu().numpy(), 1)
+        assert np.array_equal(eid1, eid2)
+        return {"id2": w}
+    g.group_apply_edges("dst", apply, inplace=True)
+    assert th.equal(g.edata["id2"], g.edata["id"])
