@@ -294,16 +294,19 @@ void launch_mark_cold(const int32_t* cols, int64_t nnz, const int32_t* deg_indpt
 int64_t fast_chunk_edges(int64_t nnz, int64_t F) {
   // Enough chunks to give every CU several groups; long chunks otherwise so
   // that fewer rows are cut (each cut row costs one carry write + read).
-  // DGLMI_CHUNK_EDGES overrides (tuning experiments; power of two >= 16).
+  // DGLMI_CHUNK_EDGES overrides (tuning experiments; power of two >= 4).
   if (const char* env = std::getenv("DGLMI_CHUNK_EDGES")) {
     const long v = std::atol(env);
-    if (v >= 16 && (v & (v - 1)) == 0) return v;
+    if (v >= 4 && (v & (v - 1)) == 0) return v;
   }
   // Measured on M1 (F = 16..256): 512 is best or within 1% (scripts/tune_spmm.py).
   // Narrow rows (F < 16) use one lane per chunk: shorter chunks, more lanes.
+  // Small graphs go down to 8 edges per chunk: a launch-bound Cora-size copy_u
+  // sum is a chain of dependent loads per chunk, k_chunk_reduce 13.9 us at 32,
+  // 8.5 at 16, 7.1 at 8, 6.1 at 4 (scripts/overhead_probe.py under rocprofv3).
   int64_t k = F < 16 ? 128 : 512;
   const int64_t groups_wanted = F < 16 ? 256 /*CUs*/ * 64 * 16 : 256 * 64;
-  while (k > 32 && nnz / k < groups_wanted) k >>= 1;
+  while (k > 8 && nnz / k < groups_wanted) k >>= 1;
   (void)F;
   return k;
 }

@@ -46,6 +46,12 @@ class DeviceCSR:
         self.nnz = int(indices.shape[0])
 
     def cstruct(self):
+        """The C struct of this CSR (arrays are immutable: built once, then copied)."""
+        if getattr(self, "_c", None) is None:
+            self._c = self._make_cstruct()
+        return _ffi.CSR.from_buffer_copy(self._c)
+
+    def _make_cstruct(self):
         c = _ffi.CSR()
         c.num_rows = self.num_rows
         c.num_cols = self.num_cols
@@ -214,6 +220,20 @@ class ImmutableGraphIndex:
         return g
 
     def cstruct(self, workspace=None, coo=False, col_blocks=0):
+        """The DGLMIGraph of a call: a cached template per (coo, col_blocks) -- every
+        pointer in it is fixed for the graph's life -- copied, plus the call's
+        workspace (cuts the host cost of a launch-bound call, C1-size graphs)."""
+        key = (bool(coo), int(col_blocks))
+        tmpls = self.__dict__.setdefault("_ctmpl", {})
+        if key not in tmpls:
+            tmpls[key] = self._make_cstruct(coo, col_blocks)
+        g = _ffi.Graph.from_buffer_copy(tmpls[key])
+        if workspace is not None:
+            g.workspace = workspace.data_ptr()
+            g.workspace_bytes = workspace.numel() * workspace.element_size()
+        return g
+
+    def _make_cstruct(self, coo, col_blocks):
         g = _ffi.Graph()
         if col_blocks > 1:
             ib, ob = self.col_blocks(col_blocks)
@@ -233,19 +253,18 @@ class ImmutableGraphIndex:
         g.out_gather_cols = oc.data_ptr() if oc is not None else None
         g.num_bits = 32
         g.device = self.device.index if self.device.index is not None else th.cuda.current_device()
-        if workspace is not None:
-            g.workspace = workspace.data_ptr()
-            g.workspace_bytes = workspace.numel() * workspace.element_size()
-        else:
-            g.workspace = None
-            g.workspace_bytes = 0
+        g.workspace = None
+        g.workspace_bytes = 0
         return g
 
     def workspace_bytes(self, feat_len):
-        L = _ffi.lib()
-        a = L.DGLMIKernelWorkspaceBytes(ctypes.byref(self.in_csr.cstruct()), int(feat_len))
-        b = L.DGLMIKernelWorkspaceBytes(ctypes.byref(self.out_csr.cstruct()), int(feat_len))
-        return max(a, b)
+        cache = self.__dict__.setdefault("_ws_bytes", {})
+        if feat_len not in cache:
+            L = _ffi.lib()
+            a = L.DGLMIKernelWorkspaceBytes(ctypes.byref(self.in_csr.cstruct()), int(feat_len))
+            b = L.DGLMIKernelWorkspaceBytes(ctypes.byref(self.out_csr.cstruct()), int(feat_len))
+            cache[feat_len] = max(a, b)
+        return cache[feat_len]
 
 
 def host_coo_to_csr(num_rows, row, col, data=None):

@@ -95,8 +95,11 @@ def _overlap_worker(rank, world, src, dst, n, q):
     g = dgl.DGLGraph()
     g.add_nodes(n)
     g.add_edges(src, dst)
-    ref = dgl.backend.copy_reduce("sum", g._graph.get_immutable_gidx(dev), 0, x, n)[lo:hi]
-    ok = th.allclose(out, ref, rtol=1e-5, atol=1e-5)
+    gi = g._graph.get_immutable_gidx(dev)
+    ref = dgl.backend.copy_reduce("sum", gi, 0, x, n)[lo:hi]
+    # fp32 reorder bound: the two sums add the same terms in different orders
+    mass = dgl.backend.copy_reduce("sum", gi, 0, x.abs(), n)[lo:hi]
+    ok = bool(((out - ref).abs() <= 1e-5 + 2e-6 * mass).all())
     import torch.distributed as dist
     flags = [None] * world
     dist.all_gather_object(flags, bool(ok))
