@@ -20,6 +20,7 @@ from __future__ import annotations
 import torch as th
 
 from . import kernel as K
+from ._ffi import DGLError
 
 SRC, DST, EDGE, NONE = 0, 1, 2, 3
 _NOMAP = (None, None)
@@ -325,6 +326,48 @@ def gcn_aggregate(gidx, x, row_mul=None, bias=None, n_dst=None, row_div=None, ad
     if addend is not None:
         addend = addend.contiguous()
     return _GcnAggregate.apply(gidx, x.contiguous(), row_mul, bias, n_dst, row_div, addend)
+
+
+class _GcnNormAggregate(th.autograd.Function):
+    """GraphConv's normalised aggregation with BOTH norms folded into one constant
+    per-edge weight w_e (``ImmutableGraphIndex.gcn_edge_weights``, streamed in walk
+    order): out[v] = sum_{u->v} w_e X[u] + bias in one launch, and the gradient
+    dX[u] = sum_{u->v} w_e dOut[v] in one out-CSR launch -- no elementwise passes
+    for the source-side scaling of X, its gradient, or the destination-side scaling
+    of the incoming gradient (three (N, F) read + write passes per layer)."""
+
+    @staticmethod
+    def forward(ctx, gidx, x, norm, bias, n_dst):
+        vin, w_in, _, _ = gidx.gcn_edge_weights(norm)
+        out = x.new_empty((n_dst, x.shape[1]))
+        epi = None if bias is None else (None, None, bias, None)
+        K.binary_op_reduce("sum", "mul", vin, SRC, EDGE, x, w_in, out, epilogue=epi)
+        ctx.gidx, ctx.norm, ctx.has_bias = gidx, norm, bias is not None
+        ctx.save_for_backward(x, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        x, out = ctx.saved_tensors
+        g = grad_out.contiguous()
+        gx = gb = None
+        if ctx.needs_input_grad[1]:
+            _, _, vout, w_out = ctx.gidx.gcn_edge_weights(ctx.norm)
+            gx = th.empty_like(x)
+            K.backward_lhs_binary_op_reduce("sum", "mul", vout, SRC, EDGE, x, w_out, out, g, gx)
+        if ctx.has_bias and ctx.needs_input_grad[3]:
+            gb = g.sum(0)
+        return None, gx, None, gb, None
+
+
+def gcn_norm_aggregate(gidx, x, norm, bias=None, n_dst=None):
+    """GraphConv aggregation of the UNnormalised features ``x`` (N_src, F) with
+    norm ``"both"`` or ``"right"`` applied through per-edge weights (see
+    _GcnNormAggregate).  Needs a whole graph (edge ids a permutation)."""
+    if norm not in ("both", "right"):
+        raise DGLError("gcn_norm_aggregate: norm must be 'both' or 'right'")
+    n_dst = gidx.in_csr.num_rows if n_dst is None else n_dst
+    return _GcnNormAggregate.apply(gidx, x.contiguous(), norm, bias, n_dst)
 
 
 class FusedGat(th.autograd.Function):

@@ -176,6 +176,21 @@ class ImmutableGraphIndex:
         permuted copy is cached per direction for the last (tensor, version)
         seen."""
         ic, oc = self.in_csr, self.out_csr
+        view = self.position_view(direction)
+        walk = ic if direction == "in" else oc
+        # the cache holds `w` itself: while it is alive no other tensor can take its
+        # address, so (address, version counter, layout) identifies its contents
+        key = (w.data_ptr(), w._version, tuple(w.shape), tuple(w.stride()), w.dtype)
+        cached = self._pos_operands.get(direction)
+        if cached is None or cached[0] != key:
+            cached = (key, w, w[walk.data.long()].contiguous())
+            self._pos_operands[direction] = cached
+        return view, cached[2]
+
+    def position_view(self, direction):
+        """This graph with edge ids = positions of its in-CSR (``"in"``) or out-CSR
+        (``"out"``), so a per-edge operand in that walk's order is streamed."""
+        ic, oc = self.in_csr, self.out_csr
         if getattr(self, "_pos_views", None) is None:
             self._pos_views, self._pos_operands = {}, {}
         if direction not in self._pos_views:
@@ -190,15 +205,29 @@ class ImmutableGraphIndex:
             self._pos_views[direction] = ImmutableGraphIndex(
                 wv if direction == "in" else ov, ov if direction == "in" else wv,
                 self.num_src, self.num_dst, self.device, eid_perm=True)
-        walk = ic if direction == "in" else oc
-        # the cache holds `w` itself: while it is alive no other tensor can take its
-        # address, so (address, version counter, layout) identifies its contents
-        key = (w.data_ptr(), w._version, tuple(w.shape), tuple(w.stride()), w.dtype)
-        cached = self._pos_operands.get(direction)
-        if cached is None or cached[0] != key:
-            cached = (key, w, w[walk.data.long()].contiguous())
-            self._pos_operands[direction] = cached
-        return self._pos_views[direction], cached[2]
+        return self._pos_views[direction]
+
+    def gcn_edge_weights(self, norm):
+        """GraphConv's normalisation as one constant weight per edge, in the walk
+        order of each direction (built once, cached): ``"both"`` w = d_out(u)^-1/2 *
+        d_in(v)^-1/2, ``"right"`` w = 1 / d_in(v) (degrees clamped at 1,
+        graphconv.py:150-170).  Returns (in-view, w_in, out-view, w_out)."""
+        cache = self.__dict__.setdefault("_gcn_w", {})
+        if norm not in cache:
+            ic, oc = self.in_csr, self.out_csr
+            d_in = ic.degrees().float().clamp(min=1)
+            d_out = oc.degrees().float().clamp(min=1)
+            if norm == "both":
+                ns, nd = th.pow(d_out, -0.5), th.pow(d_in, -0.5)
+                w_in = ns[ic.indices.long()] * nd[ic.rows.long()]
+                w_out = ns[oc.rows.long()] * nd[oc.indices.long()]
+            else:
+                nd = 1.0 / d_in
+                w_in = nd[ic.rows.long()]
+                w_out = nd[oc.indices.long()]
+            cache[norm] = (self.position_view("in"), w_in.reshape(-1, 1).contiguous(),
+                           self.position_view("out"), w_out.reshape(-1, 1).contiguous())
+        return cache[norm]
 
     def col_blocks(self, nb):
         """(in_blocks, out_blocks): the in-CSR split by source range and the

@@ -13,6 +13,12 @@ in_feats > out_feats ``out = (A X W) * norm + bias`` in one launch; otherwise
 (``project(..., bias)``, hipBLASLt addmm) -- the row scaling commutes with the
 right-multiplication by W.  ``fused = False`` on the module restores the
 reference's separate steps.
+
+With ``norm`` 'both' or 'right' on a whole graph, both norms become one constant
+weight per edge streamed in the kernel's walk order (``dgl.backend
+.gcn_norm_aggregate``): the forward and the gradient of the features are one
+launch each, without the three elementwise (N, F) passes of the source-side
+scaling, its gradient and the scaled incoming gradient.
 """
 import torch as th
 from torch import nn
@@ -59,6 +65,8 @@ class GraphConv(nn.Module):
                                " create the module with flag weight=False.")
         else:
             weight = self.weight
+        if self._norm != "none" and self._edge_weight_path(graph, feat):
+            return self._edge_weight_forward(graph, feat, weight)
         if self._norm == "both":
             degs = graph._device_degrees(feat.device, "out").float().clamp(min=1)
             norm = th.pow(degs, -0.5)
@@ -68,6 +76,36 @@ class GraphConv(nn.Module):
             rst = self._fused_forward(graph, feat, weight)
         else:
             rst = self._reference_forward(graph, feat, weight)
+        if self._activation is not None:
+            rst = self._activation(rst)
+        return rst
+
+    def _edge_weight_path(self, graph, feat):
+        """Both norms as one streamed per-edge weight (dgl.backend
+        .gcn_norm_aggregate): whole graphs whose aggregation runs as one pass (no
+        column blocks, which only the unweighted copy_u sum takes)."""
+        if not getattr(self, "fused", True) or feat.dim() != 2 or feat.dtype != th.float32:
+            return False
+        if not hasattr(graph._graph, "get_immutable_gidx") or not feat.is_cuda:
+            return False
+        gidx = graph._graph.get_immutable_gidx(feat.device)
+        f = self._out_feats if self._in_feats > self._out_feats else self._in_feats
+        from .... import kernel as K
+        return bool(gidx.eid_perm) and K.spmm_col_blocks(gidx, f) == 1
+
+    def _edge_weight_forward(self, graph, feat, weight):
+        gidx = graph._graph.get_immutable_gidx(feat.device)
+        n_dst = graph.number_of_dst_nodes()
+        if self._in_feats > self._out_feats:
+            if weight is not None:
+                feat = B.project(feat, weight)
+            rst = B.gcn_norm_aggregate(gidx, feat, self._norm, self.bias, n_dst)
+        else:
+            rst = B.gcn_norm_aggregate(gidx, feat, self._norm, None, n_dst)
+            if weight is not None:
+                rst = B.project(rst, weight, self.bias)
+            elif self.bias is not None:
+                rst = rst + self.bias
         if self._activation is not None:
             rst = self._activation(rst)
         return rst
