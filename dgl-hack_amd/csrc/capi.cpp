@@ -778,6 +778,7 @@ GatArgs gat_args(const DGLMIGraph* g, const DGLMIArray* ft, const DGLMIArray* el
   a.m = mx->data;
   a.l = sm->data;
   a.chunk = gat_chunk_edges(std::max<int64_t>(in.nnz, 1));
+  a.o32 = std::max(ft->shape[0], in.num_rows) * a.F < (int64_t(1) << 31);
   return a;
 }
 

@@ -268,6 +268,7 @@ struct GatArgs {
   int raw;          // forward: leave (m, l, acc) unnormalised (merged afterwards)
   int accumulate;   // backward: add into g_er / g_ft / g_el instead of overwriting
   int skip_stats;   // backward (dst side): stats already written by an earlier block
+  int o32;          // every gathered row offset (ft, el, grad_out, stats) < 2^31 elements
 };
 bool gat_supported(int64_t H, int64_t D);
 int64_t gat_chunk_edges(int64_t nnz);

@@ -42,19 +42,45 @@ __device__ __forceinline__ float4 ld4g(const float* p) { return *reinterpret_cas
 __device__ __forceinline__ void st4g(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 __device__ __forceinline__ float leaky(float x, float s) { return x > 0.0f ? x : s * x; }
 __device__ __forceinline__ float dleaky(float x, float s) { return x > 0.0f ? 1.0f : s; }
+// e^x as one v_exp_f32 (2^(x log2 e)): the walks evaluate it once or twice per
+// edge and lane, where the accurate expf's range reduction cost ~12 VALU each.
+// Relative error ~|x| 2^-24 (< 2e-6 for the logits a softmax sees), far inside
+// the 1e-4 budget; forward and backward use the same function, so the
+// attention weights the backward recomputes are the forward's.
+__device__ __forceinline__ float fexp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
+// Element offset of (row, off) in a table of rows `w` floats wide: 32-bit
+// arithmetic when every offset of the gathered tables fits (GatArgs::o32), one
+// v_mul_lo_u32 instead of a 64-bit multiply per gather.
+template <bool O32>
+__device__ __forceinline__ int64_t roff(int64_t row, int64_t w, int off) {
+  if constexpr (O32)
+    return static_cast<int64_t>(static_cast<uint32_t>(row) * static_cast<uint32_t>(w) +
+                                static_cast<uint32_t>(off));
+  else
+    return row * w + off;
+}
 __device__ __forceinline__ float dot4(float4 a, float4 b) {
   return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
 }
-// sum over the D4 lanes of one head (D4 = D / 4, a power of two <= L)
+// sum over the D4 lanes of one head (D4 = D / 4, a power of two <= L).  Lanes
+// 1 and 2 apart swap through DPP quad permutations (no LDS round trip, unlike
+// the ds_bpermute of __shfl_xor); wider heads finish with __shfl_xor.  Every
+// lane of the head ends with the same sum (a + b == b + a).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
 __device__ __forceinline__ float head_sum(float x, int d4) {
-  for (int off = 1; off < d4; off <<= 1) x += __shfl_xor(x, off);
+  if (d4 >= 2) x += dpp_f<0xB1>(x);  // quad_perm [1, 0, 3, 2]: lane ^ 1
+  if (d4 >= 4) x += dpp_f<0x4E>(x);  // quad_perm [2, 3, 0, 1]: lane ^ 2
+  for (int off = 4; off < d4; off <<= 1) x += __shfl_xor(x, off);
   return x;
 }
 
 // ---------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------
-template <int L, int NV>
+template <int L, int NV, bool O32>
 __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
   constexpr int G = kBlock / L;
   constexpr int B = L > 16 ? L : 16;
@@ -71,12 +97,13 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
   const int F4 = static_cast<int>(a.F / 4);
   const int H = a.H, D = a.D;
   const int64_t CW = a.F + 2 * H;  // carry record: acc[F], m[H], l[H]
-  int hd[NV];
+  int hd[NV], fl[NV];
   bool ok4[NV], lead[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int f4 = lane + v * L;
     ok4[v] = f4 < F4;
+    fl[v] = 4 * (ok4[v] ? f4 : F4 - 1);  // gathers of idle slots re-read the last one
     hd[v] = ok4[v] ? (4 * f4) / D : 0;
     lead[v] = ok4[v] && ((4 * f4) % D == 0);
   }
@@ -149,13 +176,13 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
       float elv[U][NV];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
+        // unconditional: positions past the chunk carry column 0 (a valid row),
+        // and the loop below stops at them
         const int64_t col = s_col[g][ub + u];
-        const bool ok = s_row[g][ub + u] != INT_MAX;
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
-          const int f4 = lane + v * L;
-          val[u][v] = (ok && ok4[v]) ? ld4g(a.ft + col * a.F + 4 * f4) : Z;
-          elv[u][v] = (ok && ok4[v]) ? a.el[col * H + hd[v]] : 0.0f;
+          val[u][v] = ld4g(a.ft + roff<O32>(col, a.F, fl[v]));
+          elv[u][v] = a.el[roff<O32>(col, H, hd[v])];
         }
       }
 #pragma unroll
@@ -179,12 +206,12 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
         for (int v = 0; v < NV; ++v) {
           const float s = leaky(elv[u][v] + erv[v], a.slope);
           if (s > mx[v]) {
-            const float sc = expf(mx[v] - s);
+            const float sc = fexp(mx[v] - s);
             acc[v] = make_float4(acc[v].x * sc, acc[v].y * sc, acc[v].z * sc, acc[v].w * sc);
             sm[v] *= sc;
             mx[v] = s;
           }
-          const float pe = expf(s - mx[v]);
+          const float pe = fexp(s - mx[v]);
           const float4 x = val[u][v];
           acc[v] = make_float4(acc[v].x + pe * x.x, acc[v].y + pe * x.y, acc[v].z + pe * x.z,
                                acc[v].w + pe * x.w);
@@ -246,7 +273,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_fixup(GatArgs a) {
 // ---------------------------------------------------------------------------
 // backward, destination side (in-CSR): grad_er, delta, packed stats
 // ---------------------------------------------------------------------------
-template <int L, int NV>
+template <int L, int NV, bool O32>
 __global__ void __launch_bounds__(kBlock) k_gat_bwd_dst(GatArgs a) {
   constexpr int G = kBlock / L;
   constexpr int B = L > 16 ? L : 16;
@@ -262,12 +289,13 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_dst(GatArgs a) {
   const int64_t p1 = p0 + K < a.nnz ? p0 + K : a.nnz;
   const int F4 = static_cast<int>(a.F / 4);
   const int H = a.H, D = a.D, D4 = a.D / 4;
-  int hd[NV];
+  int hd[NV], fl[NV];
   bool ok4[NV], lead[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int f4 = lane + v * L;
     ok4[v] = f4 < F4;
+    fl[v] = 4 * (ok4[v] ? f4 : F4 - 1);  // gathers of idle slots re-read the last one
     hd[v] = ok4[v] ? (4 * f4) / D : 0;
     lead[v] = ok4[v] && ((4 * f4) % D == 0);
   }
@@ -341,13 +369,11 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_dst(GatArgs a) {
       float elv[U][NV];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t col = s_col[g][ub + u];
-        const bool ok = s_row[g][ub + u] != INT_MAX;
+        const int64_t col = s_col[g][ub + u];  // 0 (a valid row) past the chunk
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
-          const int f4 = lane + v * L;
-          ftv[u][v] = (ok && ok4[v]) ? ld4g(a.ft + col * a.F + 4 * f4) : Z;
-          elv[u][v] = (ok && ok4[v]) ? a.el[col * H + hd[v]] : 0.0f;
+          ftv[u][v] = ld4g(a.ft + roff<O32>(col, a.F, fl[v]));
+          elv[u][v] = a.el[roff<O32>(col, H, hd[v])];
         }
       }
 #pragma unroll
@@ -364,7 +390,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_dst(GatArgs a) {
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
           const float pre = elv[u][v] + erv[v];
-          const float att = expf(leaky(pre, a.slope) - mv[v]) * linv[v];
+          const float att = fexp(leaky(pre, a.slope) - mv[v]) * linv[v];
           const float ge = head_sum(dot4(gov[v], ftv[u][v]), D4);
           acc[v] += att * (ge - dlt[v]) * dleaky(pre, a.slope);
         }
@@ -380,7 +406,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_dst(GatArgs a) {
 // ---------------------------------------------------------------------------
 // backward, source side (out-CSR): grad_ft, grad_el
 // ---------------------------------------------------------------------------
-template <int L, int NV>
+template <int L, int NV, bool O32>
 __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
   constexpr int G = kBlock / L;
   constexpr int B = L > 16 ? L : 16;
@@ -397,12 +423,13 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
   const int F4 = static_cast<int>(a.F / 4);
   const int H = a.H, D = a.D, D4 = a.D / 4;
   const int64_t CW = a.F + H;
-  int hd[NV];
+  int hd[NV], fl[NV];
   bool ok4[NV], lead[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int f4 = lane + v * L;
     ok4[v] = f4 < F4;
+    fl[v] = 4 * (ok4[v] ? f4 : F4 - 1);  // gathers of idle slots re-read the last one
     hd[v] = ok4[v] ? (4 * f4) / D : 0;
     lead[v] = ok4[v] && ((4 * f4) % D == 0);
   }
@@ -468,13 +495,11 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
       float4 gov[U][NV], st[U][NV];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t col = s_col[g][ub + u];
-        const bool ok = s_row[g][ub + u] != INT_MAX;
+        const int64_t col = s_col[g][ub + u];  // 0 (a valid row) past the chunk
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
-          const int f4 = lane + v * L;
-          gov[u][v] = (ok && ok4[v]) ? ld4g(a.go + col * a.F + 4 * f4) : Z;
-          st[u][v] = (ok && ok4[v]) ? a.stats[col * H + hd[v]] : Z;
+          gov[u][v] = ld4g(a.go + roff<O32>(col, a.F, fl[v]));
+          st[u][v] = a.stats[roff<O32>(col, H, hd[v])];
         }
       }
 #pragma unroll
@@ -492,7 +517,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
         for (int v = 0; v < NV; ++v) {
           const float4 sv = st[u][v];  // {er, m, 1/l, delta} of the destination
           const float pre = elv[v] + sv.x;
-          const float att = expf(leaky(pre, a.slope) - sv.y) * sv.z;
+          const float att = fexp(leaky(pre, a.slope) - sv.y) * sv.z;
           const float4 gv = gov[u][v];
           const float ge = head_sum(dot4(gv, ftv[v]), D4);
           acce[v] += att * (ge - sv.w) * dleaky(pre, a.slope);
@@ -608,7 +633,10 @@ void fwd_cfg(const GatArgs& a, hipStream_t s) {
   constexpr int G = kBlock / L;
   const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
   const unsigned blocks = static_cast<unsigned>((chunks + G - 1) / G);
-  hipLaunchKernelGGL((k_gat_fwd<L, NV>), dim3(blocks), dim3(kBlock), 0, s, a);
+  if (a.o32)
+    hipLaunchKernelGGL((k_gat_fwd<L, NV, true>), dim3(blocks), dim3(kBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_gat_fwd<L, NV, false>), dim3(blocks), dim3(kBlock), 0, s, a);
   if (chunks > 1) hipLaunchKernelGGL((k_gat_fwd_fixup<L, NV>), dim3(blocks), dim3(kBlock), 0, s, a);
 }
 
@@ -617,7 +645,10 @@ void bwd_dst_cfg(const GatArgs& a, hipStream_t s) {
   constexpr int G = kBlock / L;
   const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
   const unsigned blocks = static_cast<unsigned>((chunks + G - 1) / G);
-  hipLaunchKernelGGL((k_gat_bwd_dst<L, NV>), dim3(blocks), dim3(kBlock), 0, s, a);
+  if (a.o32)
+    hipLaunchKernelGGL((k_gat_bwd_dst<L, NV, true>), dim3(blocks), dim3(kBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_gat_bwd_dst<L, NV, false>), dim3(blocks), dim3(kBlock), 0, s, a);
   if (chunks > 1)
     hipLaunchKernelGGL((k_gat_bwd_fixup<L, NV>), dim3(blocks), dim3(kBlock), 0, s, a,
                        static_cast<float*>(nullptr), a.g_er, 0);
@@ -628,7 +659,10 @@ void bwd_src_cfg(const GatArgs& a, hipStream_t s) {
   constexpr int G = kBlock / L;
   const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
   const unsigned blocks = static_cast<unsigned>((chunks + G - 1) / G);
-  hipLaunchKernelGGL((k_gat_bwd_src<L, NV>), dim3(blocks), dim3(kBlock), 0, s, a);
+  if (a.o32)
+    hipLaunchKernelGGL((k_gat_bwd_src<L, NV, true>), dim3(blocks), dim3(kBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_gat_bwd_src<L, NV, false>), dim3(blocks), dim3(kBlock), 0, s, a);
   if (chunks > 1)
     hipLaunchKernelGGL((k_gat_bwd_fixup<L, NV>), dim3(blocks), dim3(kBlock), 0, s, a, a.g_ft,
                        a.g_el, 1);

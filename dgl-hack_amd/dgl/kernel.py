@@ -266,12 +266,12 @@ def gat_col_blocks(graph, feat_src, backward=False):
     """Column blocks for the fused GAT kernels (DGLMIGraph.num_col_blocks): when the
     gathered ft + el table fits the Infinity Cache but not L2 (>= 32 MiB) and rows
     are long (average in-degree >= 64, so merging per-block row partials is cheap),
-    cut the sources into blocks of 6-12 MiB of table each for the forward and twice
-    that for the backward, whose per-block row work (grad_out / out rows loaded,
-    gradient rows read-modified-written) is heavier (a power of two <= 16).
-    C3 (67 MB table; scripts/gat_probe.py, profiles/r01_gat_blocks.json): forward
-    5.65 ms whole / 4.54 (4 blocks) / 4.13 (8) / 4.53 (16); backward 11.98 /
-    10.63 (4) / 11.04 (8) / 12.61 (16).  DGLMI_GAT_BLOCKS overrides (1 = off)."""
+    cut the sources into blocks of 6-12 MiB of table each (a power of two <= 16),
+    the same count for the forward and both backward walks (one set of block CSRs).
+    C3 (67 MB table; scripts/gat_ab.py + scripts/gpu_gat_prof.sh,
+    profiles/r02_gat_blocks.json): forward 5.8 ms whole / 4.38 (4 blocks) / 3.43 (8)
+    / 3.66 (16); backward 12.0 / 9.86 (4) / 9.00 (8) / 9.59 (16).
+    DGLMI_GAT_BLOCKS overrides (1 = off).  `backward` is kept for callers."""
     env = os.environ.get("DGLMI_GAT_BLOCKS")
     if env is not None:
         return max(1, int(env))
@@ -281,7 +281,7 @@ def gat_col_blocks(graph, feat_src, backward=False):
     nnz, rows = graph.in_csr.nnz, max(1, graph.in_csr.num_rows)
     if table < (32 << 20) or nnz < (1 << 22) or nnz < 64 * rows:
         return 1
-    target = (12 << 20) if backward else (6 << 20)
+    target = 6 << 20
     nb = 1
     while nb < 16 and table / (nb * 2) >= target:
         nb *= 2
