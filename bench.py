@@ -491,6 +491,87 @@ def _timed(fn, steps, dist, cdev):
     return el
 
 
+class SideLineGuard:
+    """N > 1 only.  The side lines after the headline (with-exchange, C4) run
+    collectives.  If one rank raises or stalls there, its peers wait inside RCCL,
+    and torchrun would end the job without the headline line.  So a failing rank
+    posts its error in the job's TCP store; rank 0's watchdog thread then prints
+    the line with the error recorded under the phase that failed, and every rank
+    leaves with status 0.  A phase that exceeds `budget_s` counts as failed."""
+
+    KEY_ERR = "dglmi_bench_side_error"
+    KEY_DONE = "dglmi_bench_line_printed"
+
+    def __init__(self, dist, rank, res, budget_s=300.0, poll_s=0.25):
+        import threading
+        self.store = dist.distributed_c10d._get_default_store()
+        self.rank, self.res, self.budget_s, self.poll_s = rank, res, budget_s, poll_s
+        self.phase = None
+        self.t_phase = time.time()
+        self.lock = threading.Lock()
+        self.printed = False
+        self.thread = threading.Thread(target=self._watch, daemon=True)
+        self.thread.start()
+
+    def start(self, phase):
+        self.phase, self.t_phase = phase, time.time()
+
+    def _emit_and_exit(self, err):
+        with self.lock:
+            if not self.printed:
+                self.printed = True
+                self.res[self.phase or "side_line"] = {"error": err}
+                print(json.dumps(self.res), flush=True)
+            try:
+                self.store.set(self.KEY_DONE, "1")
+            except Exception:  # noqa: BLE001
+                pass
+            os._exit(0)
+
+    def _watch(self):
+        seen = None
+        while True:
+            time.sleep(self.poll_s)
+            if self.printed:
+                return
+            try:
+                if (self.rank == 0 and self.phase is not None
+                        and time.time() - self.t_phase > self.budget_s):
+                    self.store.set(self.KEY_ERR, "%s exceeded %.0f s" % (self.phase, self.budget_s))
+                if seen is None and self.store.check([self.KEY_ERR]):
+                    seen = time.time()
+                if seen is not None and self.rank == 0:
+                    self._emit_and_exit(self.store.get(self.KEY_ERR).decode())
+                if seen is not None and self.store.check([self.KEY_DONE]):
+                    os._exit(0)
+            except Exception:  # noqa: BLE001  (store gone: rank 0 has printed and left)
+                if seen is not None or self.rank != 0:
+                    os._exit(0)
+            if seen is not None and time.time() - seen > 60:
+                os._exit(0)
+
+    def fail(self, exc):
+        err = "rank %d: %s" % (self.rank, exc if isinstance(exc, SystemExit) else repr(exc))
+        log("side line %s failed: %s" % (self.phase, err))
+        if self.rank == 0:
+            self._emit_and_exit(err)
+        try:
+            self.store.set(self.KEY_ERR, err)
+        except Exception:  # noqa: BLE001
+            os._exit(1)
+        time.sleep(120)  # the watchdog leaves once rank 0 has printed
+        os._exit(1)
+
+    def finish(self):
+        """Normal end: rank 0 prints the line (the watchdog can no longer)."""
+        with self.lock:
+            if self.printed:
+                os._exit(0)  # pragma: no cover (the watchdog already printed and is exiting)
+            self.printed = True
+            if self.rank == 0:
+                print(json.dumps(self.res), flush=True)
+
+
 def measure_exchange(part, x, out_ref, args, dist, cdev, device, edges_total):
     """copy_u_sum with the source rows NOT replicated: each step first fetches
     the halo rows with one all-to-all-v (RCCL over xGMI), then aggregates over
@@ -757,15 +838,6 @@ def main():
 
     ms_per_step = elapsed * 1000.0 / args.steps
     value = edges_total * args.steps / elapsed
-    exch = None
-    if part is not None:
-        log("with-exchange line ...")
-        try:
-            exch = measure_exchange(part, x, out, args, dist, cdev, device, edges_total)
-        except SystemExit as exc:
-            # its parity checks agree across ranks (max over ranks) before exiting, so
-            # every rank lands here together; the replicated headline still reports
-            exch = {"error": str(exc)}
     upd_res = None
     if upd is not None:
         upd_res = measure_update_all(upd, x, out, args)
@@ -836,8 +908,6 @@ def main():
     except RuntimeError as exc:  # out of memory on a crowded device: report, don't fail
         res["roofline"]["measured_stream_copy_GBps"] = None
         log("stream copy peak skipped: %r" % exc)
-    if exch is not None:
-        res["with_exchange"] = exch
     if upd_res is not None:
         res["update_all"] = upd_res
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -845,6 +915,31 @@ def main():
             res["cpu_baseline"] = cpu_baseline(o_ptr, o_idx, x, n_dst)
         except Exception as exc:  # the baseline must never take the GPU line down
             res["cpu_baseline"] = {"value": None, "error": repr(exc)}
+    # Side lines.  At N > 1 they run collectives under the guard, so a rank that
+    # fails or stalls in one cannot take the headline line down with it.
+    guard = SideLineGuard(dist, rank, res) if dist is not None else None
+
+    def side(key, fn):
+        if guard is not None:
+            guard.start(key)
+        try:
+            res[key] = fn()
+        except SystemExit as exc:
+            # parity checks agree across ranks (max over ranks) before exiting, so
+            # every rank lands here together
+            res[key] = {"error": str(exc)}
+        except Exception as exc:  # noqa: BLE001
+            if guard is not None:
+                guard.fail(exc)  # does not return
+            res[key] = {"error": repr(exc)}  # one process: keep the headline line
+        if guard is not None:
+            guard.phase = None
+        log("%s: %s" % (key, json.dumps(res[key])))
+
+    if part is not None:
+        log("with-exchange line ...")
+        side("with_exchange",
+             lambda: measure_exchange(part, x, out, args, dist, cdev, device, edges_total))
     if under_profiler and not args.no_c4:
         # under rocprofv3 the kernel statistics must describe the M1 launch alone
         # (C4 runs the same kernel on a 200 M-edge graph): skip the C4 line
@@ -854,16 +949,10 @@ def main():
         if part is not None:
             del part
         th.cuda.empty_cache()
-        try:
-            res["c4"] = measure_c4(world, rank, dist, cdev, device, args)
-        except SystemExit as exc:  # parity checks agree across ranks before exiting
-            res["c4"] = {"error": str(exc)}
-        except Exception as exc:  # noqa: BLE001
-            if world > 1:  # peers may sit in a collective: fail the job rather than hang
-                raise
-            res["c4"] = {"error": repr(exc)}  # one process: keep the headline line
-        log("C4: %s" % json.dumps(res["c4"]))
-    if rank == 0:
+        side("c4", lambda: measure_c4(world, rank, dist, cdev, device, args))
+    if guard is not None:
+        guard.finish()
+    elif rank == 0:
         print(json.dumps(res), flush=True)
     if dist is not None:
         dist.barrier()

@@ -1,0 +1,50 @@
+"""bench.py at N > 1: a side line (with-exchange, C4) that fails or stalls on one
+rank must not take the headline line down (SideLineGuard).  gloo, two CPU ranks."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _run(mode, budget=300):
+    env = dict(os.environ, BUDGET=str(budget), OMP_NUM_THREADS="1")
+    env.pop("RANK", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(HERE, "guard_worker.py"), mode]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, lines, p.stderr
+
+
+@pytest.mark.parametrize("mode", ["ok", "raise", "raise0"])
+def test_side_line_failure_keeps_headline(mode):
+    code, lines, err = _run(mode)
+    assert code == 0, err[-2000:]
+    assert len(lines) == 1, (lines, err[-2000:])
+    res = json.loads(lines[0])
+    assert res["value"] == 1.0
+    if mode == "ok":
+        assert res["c4"] == {"value": 2.0}
+    else:
+        assert "injected failure" in res["c4"]["error"]
+
+
+def test_side_line_stall_hits_budget():
+    code, lines, err = _run("stall", budget=3)
+    assert code == 0, err[-2000:]
+    assert len(lines) == 1
+    assert "exceeded" in json.loads(lines[0])["c4"]["error"]
