@@ -91,6 +91,38 @@ __device__ __forceinline__ float red_backward(float val, float accum) {
   else return 1.0f;
 }
 
+// Rows without positions (zero in-degree) take the reducer identity.  They are
+// written by a row-parallel share, not by the chunk that sees the gap: the group
+// of chunk c checks rows [c·R, (c+1)·R), R = ceil(num_rows / num_chunks), and
+// calls put(r) for each empty one (group-uniform; L lanes per group, L ≤ 64).
+// One group filling a whole gap serialised contiguous empty rows: the ~3 M
+// trailing zero-in-degree rows of M1 renumbered by degree took one group 160 ms
+// (scripts/locality_probe.py).  Cost: one coalesced read of indptr per launch.
+template <typename Put>
+__device__ __forceinline__ void fill_empty_rows(const int32_t* __restrict__ indptr, int64_t num_rows,
+                                                int64_t chunk, int64_t num_chunks, int L, int lane,
+                                                Put&& put) {
+  const int64_t R = (num_rows + num_chunks - 1) / num_chunks;
+  const int64_t r0 = chunk * R;
+  const int64_t r1 = r0 + R < num_rows ? r0 + R : num_rows;
+  for (int64_t base = r0; base < r1; base += L) {
+    const int64_t r = base + lane;
+    const bool empty = r < r1 && indptr[r] == indptr[r + 1];
+    uint64_t m;
+    if (L == 1) {
+      m = empty ? 1u : 0u;
+    } else {
+      m = __ballot(empty);  // the group's lanes are converged here
+      if (L < 64) m = (m >> (((threadIdx.x & 63) / L) * L)) & ((1ull << L) - 1);
+    }
+    while (m) {
+      const int j = __builtin_ctzll(m);
+      m &= m - 1;
+      put(base + j);
+    }
+  }
+}
+
 // binary_reduce_common.h:131-213
 template <int OP>
 __device__ __forceinline__ float op_apply(const float* l, const float* r, int64_t len) {

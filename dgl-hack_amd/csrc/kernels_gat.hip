@@ -120,10 +120,6 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
   };
   int64_t cur = a.rows[p0];
   bool cont = p0 > 0 && a.rows[p0 - 1] == cur;
-  if (!cont) {
-    const int64_t first_gap = p0 > 0 ? (int64_t)a.rows[p0 - 1] + 1 : 0;
-    for (int64_t r = first_gap; r < cur; ++r) zero_row(r);
-  }
   float mx[NV], sm[NV], erv[NV];
   float4 acc[NV];
 #pragma unroll
@@ -191,7 +187,6 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
         if (r == INT_MAX) break;
         if (r != cur) {
           flush(cur, cont, true);
-          for (int64_t e = cur + 1; e < r; ++e) zero_row(e);
           cur = r;
           cont = false;
 #pragma unroll
@@ -223,8 +218,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
   }
   const bool continues = p1 < a.nnz && a.rows[p1] == cur;
   flush(cur, cont, !continues);
-  if (p1 == a.nnz)
-    for (int64_t r = cur + 1; r < a.num_rows; ++r) zero_row(r);
+  fill_empty_rows(a.indptr, a.num_rows, chunk, (a.nnz + K - 1) / K, L, lane, zero_row);
 }
 
 template <int L, int NV>
@@ -348,10 +342,6 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_dst(GatArgs a) {
   };
   int64_t cur = a.rows[p0];
   bool cont = p0 > 0 && a.rows[p0 - 1] == cur;
-  if (!cont) {
-    const int64_t first_gap = p0 > 0 ? (int64_t)a.rows[p0 - 1] + 1 : 0;
-    for (int64_t r = first_gap; r < cur; ++r) zero_row(r);
-  }
   load_row(cur);
   for (int64_t base = p0; base < p1; base += B) {
     for (int q = lane; q < B; q += L) {
@@ -382,7 +372,6 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_dst(GatArgs a) {
         if (r == INT_MAX) break;
         if (r != cur) {
           flush(cur, cont);
-          for (int64_t e = cur + 1; e < r; ++e) zero_row(e);
           cur = r;
           cont = false;
           load_row(cur);
@@ -399,8 +388,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_dst(GatArgs a) {
     __builtin_amdgcn_wave_barrier();
   }
   flush(cur, cont);
-  if (p1 == a.nnz)
-    for (int64_t r = cur + 1; r < a.num_rows; ++r) zero_row(r);
+  fill_empty_rows(a.indptr, a.num_rows, chunk, (a.nnz + K - 1) / K, L, lane, zero_row);
 }
 
 // ---------------------------------------------------------------------------
@@ -475,10 +463,6 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
   };
   int64_t cur = a.rows[p0];
   bool cont = p0 > 0 && a.rows[p0 - 1] == cur;
-  if (!cont) {
-    const int64_t first_gap = p0 > 0 ? (int64_t)a.rows[p0 - 1] + 1 : 0;
-    for (int64_t r = first_gap; r < cur; ++r) zero_row(r);
-  }
   load_row(cur);
   for (int64_t base = p0; base < p1; base += B) {
     for (int q = lane; q < B; q += L) {
@@ -508,7 +492,6 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
         if (r == INT_MAX) break;
         if (r != cur) {
           flush(cur, cont);
-          for (int64_t e = cur + 1; e < r; ++e) zero_row(e);
           cur = r;
           cont = false;
           load_row(cur);
@@ -529,8 +512,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
     __builtin_amdgcn_wave_barrier();
   }
   flush(cur, cont);
-  if (p1 == a.nnz)
-    for (int64_t r = cur + 1; r < a.num_rows; ++r) zero_row(r);
+  fill_empty_rows(a.indptr, a.num_rows, chunk, (a.nnz + K - 1) / K, L, lane, zero_row);
 }
 
 // carries of the backward walks: plain sums (W floats per chunk record, the first

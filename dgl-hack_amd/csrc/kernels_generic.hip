@@ -184,8 +184,6 @@ __global__ void __launch_bounds__(kBlock) k_lb_reduce(EdgeArgs a, int lane_bits)
   };
   int64_t cur = a.rows[p0];
   bool cont = p0 > 0 && a.rows[p0 - 1] == cur;
-  if (!cont)
-    for (int64_t r = p0 > 0 ? (int64_t)a.rows[p0 - 1] + 1 : 0; r < cur; ++r) fill_row(r);
   float acc[kNV];
 #pragma unroll
   for (int v = 0; v < kNV; ++v) acc[v] = I;
@@ -224,7 +222,6 @@ __global__ void __launch_bounds__(kBlock) k_lb_reduce(EdgeArgs a, int lane_bits)
       if (base + u >= p1) break;
       if (rr[u] != cur) {
         flush();
-        for (int64_t r = cur + 1; r < rr[u]; ++r) fill_row(r);
         cur = rr[u];
         cont = false;
       }
@@ -233,8 +230,7 @@ __global__ void __launch_bounds__(kBlock) k_lb_reduce(EdgeArgs a, int lane_bits)
     }
   }
   flush();
-  if (p1 == a.nnz)
-    for (int64_t r = cur + 1; r < a.num_rows; ++r) fill_row(r);
+  fill_empty_rows(a.indptr, a.num_rows, chunk, (a.nnz + K - 1) / K, L, lane, fill_row);
 }
 
 template <int RED, bool BWD>

@@ -26,8 +26,9 @@
 //    and each continuing chunk writes one partial to the carry workspace; a
 //    fixup pass folds the carries into out in chunk order, so results are
 //    deterministic and independent of scheduling.
-//  * Zero-in-degree rows get the reducer identity from the group that sees
-//    the gap in the row sequence (no separate fill pass over `out`).
+//  * Zero-in-degree rows get the reducer identity from a row-parallel share
+//    of every group (fill_empty_rows, internal.h): no separate fill pass over
+//    `out`, and runs of empty rows are spread over the whole grid.
 #include "spmm_chunk.h"
 
 namespace dglmi {
@@ -143,10 +144,6 @@ __global__ void __launch_bounds__(kBlock) k_lane_reduce(FastArgs a) {
   };
   int64_t cur = a.rows[p0];
   bool cont = p0 > 0 && a.rows[p0 - 1] == cur;
-  if (!cont) {
-    const int64_t first_gap = p0 > 0 ? (int64_t)a.rows[p0 - 1] + 1 : 0;
-    for (int64_t r = first_gap; r < cur; ++r) put_gap(r);
-  }
   float acc[F];
 #pragma unroll
   for (int i = 0; i < F; ++i) acc[i] = I;
@@ -184,7 +181,6 @@ __global__ void __launch_bounds__(kBlock) k_lane_reduce(FastArgs a) {
       if (r[u] != cur) {
         if (!cont) epi_row<EPI, F>(a, cur, acc);
         store_row<F>(cont ? a.carry + chunk * F : a.out + cur * F, acc);
-        for (int64_t g = cur + 1; g < r[u]; ++g) put_gap(g);
 #pragma unroll
         for (int i = 0; i < F; ++i) acc[i] = I;
         cur = r[u];
@@ -196,8 +192,7 @@ __global__ void __launch_bounds__(kBlock) k_lane_reduce(FastArgs a) {
   }
   if (!cont && !(EPI && p1 < a.nnz && a.rows[p1] == cur)) epi_row<EPI, F>(a, cur, acc);
   store_row<F>(cont ? a.carry + chunk * F : a.out + cur * F, acc);
-  if (p1 == a.nnz)
-    for (int64_t g = cur + 1; g < a.num_rows; ++g) put_gap(g);
+  fill_empty_rows(a.indptr, a.num_rows, chunk, (a.nnz + K - 1) / K, 1, 0, put_gap);
 }
 
 template <int RED, int F, bool EPI = false>

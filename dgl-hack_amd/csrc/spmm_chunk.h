@@ -209,16 +209,6 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
 
   int64_t cur = a.rows[p0];
   bool cont = p0 > 0 && a.rows[p0 - 1] == cur;
-  // leading empty rows: those after the previous chunk's last row (or from 0)
-  if (!cont) {
-    const int64_t first_gap = p0 > 0 ? (int64_t)a.rows[p0 - 1] + 1 : 0;
-    for (int64_t r = first_gap; r < cur; ++r)
-#pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        const int f4 = lane + v * L;
-        if (f4 < F4) st_out<VAR>(a.out + r * a.F + VW * f4, epiv<EPI, VW>(a, I, r, f4));
-      }
-  }
   V acc[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) acc[v] = I;
@@ -275,7 +265,7 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
         const int32_t r = s_row[g][ub + u];
         if (r == INT_MAX) break;
         if (r != cur) {
-          // flush the finished row, fill the empty rows in between
+          // flush the finished row (empty rows in between: fill_empty_rows)
           float* dst = cont ? a.carry + chunk * a.F : a.out + cur * a.F;
 #pragma unroll
           for (int v = 0; v < NV; ++v) {
@@ -283,12 +273,6 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
             if (f4 < F4) st_out<VAR>(dst + VW * f4, cont ? acc[v] : epiv<EPI, VW>(a, acc[v], cur, f4));
             acc[v] = I;
           }
-          for (int64_t e = cur + 1; e < r; ++e)
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-              const int f4 = lane + v * L;
-              if (f4 < F4) st_out<VAR>(a.out + e * a.F + VW * f4, epiv<EPI, VW>(a, I, e, f4));
-            }
           cur = r;
           cont = false;
         }
@@ -308,15 +292,13 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
       if (f4 < F4) st_out<VAR>(dst + VW * f4, done ? epiv<EPI, VW>(a, acc[v], cur, f4) : acc[v]);
     }
   }
-  if (p1 == a.nnz) {  // trailing empty rows
-    for (int64_t r = cur + 1; r < a.num_rows; ++r)
+  fill_empty_rows(indptr, a.num_rows, chunk, (a.nnz + K - 1) / K, L, lane, [&](int64_t r) {
 #pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        const int f4 = lane + v * L;
-        if (f4 < F4) st_out<VAR>(a.out + r * a.F + VW * f4, epiv<EPI, VW>(a, I, r, f4));
-      }
-  }
-  (void)indptr;
+    for (int v = 0; v < NV; ++v) {
+      const int f4 = lane + v * L;
+      if (f4 < F4) st_out<VAR>(a.out + r * a.F + VW * f4, epiv<EPI, VW>(a, I, r, f4));
+    }
+  });
 }
 
 // Fold the carries of every row cut by chunk boundaries into its head, in
