@@ -369,6 +369,9 @@ def device_block_gidx(num_src, num_dst, src, dst):
     """
     dev = src.device
     m = int(src.shape[0])
+    if max(int(num_src), int(num_dst), m) >= 0x7FFFFFFF:
+        # the reference's GPU kernels are int32-only too (common.h:61-68)
+        raise DGLError("Unsupported idx bits: 64 (graphs need < 2^31 nodes and edges)")
     src = src.to(th.int32).contiguous()
     dst = dst.to(th.int32).contiguous()
     o_ptr, o_idx, o_dat = device_coo_to_csr(num_src, src, dst)

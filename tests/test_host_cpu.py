@@ -187,3 +187,18 @@ def test_ctypes_structs_match_header_layout(tmp_path):
         assert int(got[cname]) == ctypes.sizeof(cls), cname
         for f in names:
             assert int(got["%s.%s" % (cname, f)]) == getattr(cls, f).offset, (cname, f)
+
+
+def test_64bit_graphs_rejected_loudly():
+    """graph_index.py:941-952 switches to int64 ids at 2^31 nodes or edges; the
+    reference's GPU kernels are int32-only (common.h:61-68), and so are these:
+    such graphs raise DGLError instead of wrapping indices."""
+    from dgl.graph_index import device_block_gidx
+    g = GraphIndex(2 ** 31)
+    assert g.bits_needed() == 64
+    with pytest.raises(dgl.DGLError, match="idx bits: 64"):
+        g.get_immutable_gidx("cuda:0")
+    tiny = th.zeros(1, dtype=th.int32)
+    with pytest.raises(dgl.DGLError, match="idx bits: 64"):
+        device_block_gidx(2 ** 31, 4, tiny, tiny)
+    assert GraphIndex(2 ** 31 - 2).bits_needed() == 32
