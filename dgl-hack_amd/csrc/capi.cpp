@@ -365,6 +365,7 @@ void run_fast(const DGLMIGraph* g, const DGLMICsr& walk, int kind, int red, cons
   }
   Scratch carry(g, fast_workspace_bytes(walk.nnz, F), s);
   a.carry = static_cast<float*>(carry.ptr);
+  a.seg_cnt = reinterpret_cast<int32_t*>(static_cast<char*>(carry.ptr) + fast_carry_bytes(walk.nnz, F));
   launch_fast_reduce(kind, red, a, s);
   check_hip(hipGetLastError(), "fast reduce launch");
 }
@@ -939,7 +940,8 @@ int DGLMIFusedGatForward(const DGLMIGraph* graph, const DGLMIArray* feat_src, co
                                             gat_chunk_edges(std::max<int64_t>(c, 1)));
     }
     const int64_t part_bytes = (part_floats * static_cast<int64_t>(sizeof(float)) + 255) & ~int64_t(255);
-    Scratch ws(graph, part_bytes + max_chunks * (a.F + 2 * a.H) * static_cast<int64_t>(sizeof(float)), s);
+    const int64_t carry_bytes = (max_chunks * (a.F + 2 * a.H) * static_cast<int64_t>(sizeof(float)) + 15) & ~int64_t(15);
+    Scratch ws(graph, part_bytes + carry_bytes + max_chunks * static_cast<int64_t>(sizeof(int32_t)), s);
     float* out_part = static_cast<float*>(ws.ptr);
     float* m_part = out_part + nb * N * a.F;
     float* l_part = m_part + nb * N * a.H;
@@ -956,6 +958,7 @@ int DGLMIFusedGatForward(const DGLMIGraph* graph, const DGLMIArray* feat_src, co
       ab.l = l_part + b * N * a.H;
       ab.raw = 1;
       ab.carry = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + part_bytes);
+      ab.seg_cnt = reinterpret_cast<int32_t*>(static_cast<char*>(ws.ptr) + part_bytes + carry_bytes);
       launch_gat_forward(ab, s);
     }
     launch_gat_merge(out_part, m_part, l_part, nb, N, a.H, a.D, out->data, max_out->data,
@@ -964,8 +967,10 @@ int DGLMIFusedGatForward(const DGLMIGraph* graph, const DGLMIArray* feat_src, co
     return 0;
   }
   const int64_t chunks = (walk.nnz + a.chunk - 1) / a.chunk;
-  Scratch carry(graph, chunks * (a.F + 2 * a.H) * static_cast<int64_t>(sizeof(float)), s);
+  const int64_t carry_bytes = (chunks * (a.F + 2 * a.H) * static_cast<int64_t>(sizeof(float)) + 15) & ~int64_t(15);
+  Scratch carry(graph, carry_bytes + chunks * static_cast<int64_t>(sizeof(int32_t)), s);
   a.carry = static_cast<float*>(carry.ptr);
+  a.seg_cnt = reinterpret_cast<int32_t*>(static_cast<char*>(carry.ptr) + carry_bytes);
   launch_gat_forward(a, s);
   check_hip(hipGetLastError(), "fused GAT forward launch");
   API_END();
@@ -1016,10 +1021,11 @@ int DGLMIFusedGatBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src, c
       chunks = std::max(chunks, (c->nnz + k - 1) / k);
     }
   const int64_t stats_bytes = a.num_rows * a.H * 16;
-  const int64_t carry_bytes = chunks * (a.F + a.H) * static_cast<int64_t>(sizeof(float));
-  Scratch ws(graph, stats_bytes + carry_bytes + 256, s);
+  const int64_t carry_bytes = (chunks * (a.F + a.H) * static_cast<int64_t>(sizeof(float)) + 15) & ~int64_t(15);
+  Scratch ws(graph, stats_bytes + carry_bytes + chunks * static_cast<int64_t>(sizeof(int32_t)) + 256, s);
   a.stats = static_cast<float4*>(ws.ptr);
   a.carry = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + ((stats_bytes + 255) & ~int64_t(255)));
+  a.seg_cnt = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(a.carry) + carry_bytes);
   if (nb > 1) {
     // column-blocked: block 0 writes every row's stats and the first gradient
     // terms, later blocks add theirs (block order), first the destination side

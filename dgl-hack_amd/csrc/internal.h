@@ -123,6 +123,27 @@ __device__ __forceinline__ void fill_empty_rows(const int32_t* __restrict__ indp
   }
 }
 
+// Segmented fixups.  A row cut into more than kFixSeg continuation chunks (a
+// hub with ~10^4+ in-edges) is not folded by one group: the group of every
+// kFixSeg-th continuation chunk folds its segment's carries in chunk order,
+// stores the segment's partial in its own (already consumed) carry record and
+// counts itself in at a per-row counter; the group that arrives last folds the
+// row head and the segment partials in segment order.  Deterministic (the same
+// association on every run), and no group waits on another.  One group folding
+// 39 K carries made a 20 M-edge star's copy_u sum 5.4 ms (0.8 ms spread over
+// 1 M rows; scripts/hub_probe.py).  Counters live after the carries in the
+// workspace, one per chunk, zeroed by the reduce kernel that precedes the fixup.
+constexpr int64_t kFixSeg = 32;
+__device__ __forceinline__ bool seg_arrive_last(int32_t* cnt, int64_t nseg, int L, int lane) {
+  __threadfence();  // release: this group's partial, past its XCD's L2
+  int old = 0;
+  if (lane == 0) old = atomicAdd(cnt, 1);
+  if (L > 1) old = __shfl(old, 0, L);
+  const bool last = old == static_cast<int>(nseg - 1);
+  if (last) __threadfence();  // acquire: the other segments' partials
+  return last;
+}
+
 // binary_reduce_common.h:131-213
 template <int OP>
 __device__ __forceinline__ float op_apply(const float* l, const float* r, int64_t len) {
@@ -245,6 +266,7 @@ struct FastArgs {
   int64_t F;            // features per output row
   int64_t head_dim;     // bcast: features per head (E has F / head_dim values per edge)
   float* carry;         // workspace: num_chunks * F floats
+  int32_t* seg_cnt;     // num_chunks counters after the carries (segmented fixup), or null
   int64_t chunk;        // edges per chunk
   // optional fused epilogue (sum only): out = acc * row_mul[r] / row_div[r] + bias + addend[r]
   const float* row_mul;
@@ -258,7 +280,8 @@ struct FastArgs {
   int64_t num_cols;     // rows of the gathered table (policy-probe bound check)
 };
 int64_t fast_chunk_edges(int64_t nnz, int64_t F);
-int64_t fast_workspace_bytes(int64_t nnz, int64_t F);
+int64_t fast_workspace_bytes(int64_t nnz, int64_t F);  // carries + counters
+int64_t fast_carry_bytes(int64_t nnz, int64_t F);      // offset of the counters
 // Returns false if the shape is not supported by the fast path.
 bool fast_supported(int kind, int64_t F, int64_t head_dim);
 void launch_fast_reduce(int kind, int red, const FastArgs& a, hipStream_t s);  // needs a.indptr
@@ -295,6 +318,7 @@ struct GatArgs {
   float* g_el;
   float* g_ft;
   float* carry;
+  int32_t* seg_cnt;  // num_chunks counters after the carries (segmented fixup), or null
   int64_t chunk;
   // column-blocked launches (one launch per block of gathered rows):
   int raw;          // forward: leave (m, l, acc) unnormalised (merged afterwards)

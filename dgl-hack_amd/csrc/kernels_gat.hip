@@ -94,6 +94,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
   const int64_t p0 = chunk * K;
   if (p0 >= a.nnz) return;
   const int64_t p1 = p0 + K < a.nnz ? p0 + K : a.nnz;
+  if (a.seg_cnt != nullptr && lane == 0) a.seg_cnt[chunk] = 0;  // the fixup's counters
   const int F4 = static_cast<int>(a.F / 4);
   const int H = a.H, D = a.D;
   const int64_t CW = a.F + 2 * H;  // carry record: acc[F], m[H], l[H]
@@ -232,11 +233,46 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_fixup(GatArgs a) {
   if (chunk == 0 || p0 >= a.nnz) return;
   const int64_t r = a.rows[p0];
   const int64_t start = a.indptr[r];
-  if (start >= p0 || start < p0 - K) return;
+  if (start >= p0) return;  // not a continuation
+  // segmented for long rows (internal.h, kFixSeg)
+  const int64_t first = start / K + 1;
   const int64_t last = (a.indptr[r + 1] - 1) / K;
+  const int64_t nseg = a.seg_cnt != nullptr ? (last - first + kFixSeg) / kFixSeg : 1;
+  if (nseg == 1 ? chunk != first : (chunk - first) % kFixSeg != 0) return;
+  const int64_t cend = nseg == 1 ? last : (chunk + kFixSeg - 1 < last ? chunk + kFixSeg - 1 : last);
   const int F4 = static_cast<int>(a.F / 4);
   const int H = a.H;
   const int64_t CW = a.F + 2 * H;
+  // online-softmax merge of carry record c into (acc, mx, sm)
+  auto merge = [&](float4& acc, float& mx, float& sm, int64_t c, int f4, int h) {
+    const float* cr = a.carry + c * CW;
+    const float4 ca = ld4g(cr + 4 * f4);
+    const float cm = cr[a.F + h], cl = cr[a.F + H + h];
+    const float mn = fmaxf(mx, cm);
+    const float f1 = expf(mx - mn), f2 = expf(cm - mn);
+    acc = make_float4(acc.x * f1 + ca.x * f2, acc.y * f1 + ca.y * f2, acc.z * f1 + ca.z * f2,
+                      acc.w * f1 + ca.w * f2);
+    sm = sm * f1 + cl * f2;
+    mx = mn;
+  };
+  if (nseg > 1) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int f4 = lane + v * L;
+      if (f4 >= F4) continue;
+      const int h = (4 * f4) / a.D;
+      float* cr = a.carry + chunk * CW;
+      float4 acc = ld4g(cr + 4 * f4);
+      float mx = cr[a.F + h], sm = cr[a.F + H + h];
+      for (int64_t c = chunk + 1; c <= cend; ++c) merge(acc, mx, sm, c, f4, h);
+      st4g(cr + 4 * f4, acc);
+      if ((4 * f4) % a.D == 0) {
+        cr[a.F + h] = mx;
+        cr[a.F + H + h] = sm;
+      }
+    }
+    if (!seg_arrive_last(a.seg_cnt + first, nseg, L, lane)) return;
+  }
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int f4 = lane + v * L;
@@ -244,17 +280,10 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_fixup(GatArgs a) {
     const int h = (4 * f4) / a.D;
     float4 acc = ld4g(a.out + r * a.F + 4 * f4);
     float mx = a.m[r * H + h], sm = a.l[r * H + h];
-    for (int64_t c = chunk; c <= last; ++c) {
-      const float* cr = a.carry + c * CW;
-      const float4 ca = ld4g(cr + 4 * f4);
-      const float cm = cr[a.F + h], cl = cr[a.F + H + h];
-      const float mn = fmaxf(mx, cm);
-      const float f1 = expf(mx - mn), f2 = expf(cm - mn);
-      acc = make_float4(acc.x * f1 + ca.x * f2, acc.y * f1 + ca.y * f2, acc.z * f1 + ca.z * f2,
-                        acc.w * f1 + ca.w * f2);
-      sm = sm * f1 + cl * f2;
-      mx = mn;
-    }
+    if (nseg > 1)
+      for (int64_t sg = 0; sg < nseg; ++sg) merge(acc, mx, sm, first + sg * kFixSeg, f4, h);
+    else
+      for (int64_t c = first; c <= last; ++c) merge(acc, mx, sm, c, f4, h);
     const float inv = a.raw ? 1.0f : (sm > 0.0f ? 1.0f / sm : 0.0f);
     st4g(a.out + r * a.F + 4 * f4, make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv));
     if ((4 * f4) % a.D == 0) {
@@ -281,6 +310,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_dst(GatArgs a) {
   const int64_t p0 = chunk * K;
   if (p0 >= a.nnz) return;
   const int64_t p1 = p0 + K < a.nnz ? p0 + K : a.nnz;
+  if (a.seg_cnt != nullptr && lane == 0) a.seg_cnt[chunk] = 0;  // the fixup's counters
   const int F4 = static_cast<int>(a.F / 4);
   const int H = a.H, D = a.D, D4 = a.D / 4;
   int hd[NV], fl[NV];
@@ -408,6 +438,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
   const int64_t p0 = chunk * K;
   if (p0 >= a.nnz) return;
   const int64_t p1 = p0 + K < a.nnz ? p0 + K : a.nnz;
+  if (a.seg_cnt != nullptr && lane == 0) a.seg_cnt[chunk] = 0;  // the fixup's counters
   const int F4 = static_cast<int>(a.F / 4);
   const int H = a.H, D = a.D, D4 = a.D / 4;
   const int64_t CW = a.F + H;
@@ -529,28 +560,54 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_fixup(GatArgs a, float* vec_
   if (chunk == 0 || p0 >= a.nnz) return;
   const int64_t r = a.rows[p0];
   const int64_t start = a.indptr[r];
-  if (start >= p0 || start < p0 - K) return;
+  if (start >= p0) return;  // not a continuation
+  // segmented for long rows (internal.h, kFixSeg)
+  const int64_t first = start / K + 1;
   const int64_t last = (a.indptr[r + 1] - 1) / K;
+  const int64_t nseg = a.seg_cnt != nullptr ? (last - first + kFixSeg) / kFixSeg : 1;
+  if (nseg == 1 ? chunk != first : (chunk - first) % kFixSeg != 0) return;
+  const int64_t cend = nseg == 1 ? last : (chunk + kFixSeg - 1 < last ? chunk + kFixSeg - 1 : last);
   const int F4 = static_cast<int>(a.F / 4);
   const int H = a.H;
   const int64_t CW = with_vec ? a.F + H : H;
   const int64_t hoff = with_vec ? a.F : 0;
+  const float4 Z = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto add = [&](float4& accf, float& acce, int64_t c, int f4, int h, bool lead) {
+    const float* cr = a.carry + c * CW;
+    if (with_vec) {
+      const float4 t = ld4g(cr + 4 * f4);
+      accf = make_float4(accf.x + t.x, accf.y + t.y, accf.z + t.z, accf.w + t.w);
+    }
+    if (lead) acce += cr[hoff + h];
+  };
+  if (nseg > 1) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int f4 = lane + v * L;
+      if (f4 >= F4) continue;
+      const int h = (4 * f4) / a.D;
+      const bool lead = (4 * f4) % a.D == 0;
+      float4 accf = Z;
+      float acce = 0.0f;
+      for (int64_t c = chunk; c <= cend; ++c) add(accf, acce, c, f4, h, lead);
+      float* cr = a.carry + chunk * CW;
+      if (with_vec) st4g(cr + 4 * f4, accf);
+      if (lead) cr[hoff + h] = acce;
+    }
+    if (!seg_arrive_last(a.seg_cnt + first, nseg, L, lane)) return;
+  }
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int f4 = lane + v * L;
     if (f4 >= F4) continue;
     const int h = (4 * f4) / a.D;
     const bool lead = (4 * f4) % a.D == 0;
-    float4 accf = with_vec ? ld4g(vec_out + r * a.F + 4 * f4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 accf = with_vec ? ld4g(vec_out + r * a.F + 4 * f4) : Z;
     float acce = lead ? head_out[r * H + h] : 0.0f;
-    for (int64_t c = chunk; c <= last; ++c) {
-      const float* cr = a.carry + c * CW;
-      if (with_vec) {
-        const float4 t = ld4g(cr + 4 * f4);
-        accf = make_float4(accf.x + t.x, accf.y + t.y, accf.z + t.z, accf.w + t.w);
-      }
-      if (lead) acce += cr[hoff + h];
-    }
+    if (nseg > 1)
+      for (int64_t sg = 0; sg < nseg; ++sg) add(accf, acce, first + sg * kFixSeg, f4, h, lead);
+    else
+      for (int64_t c = first; c <= last; ++c) add(accf, acce, c, f4, h, lead);
     if (with_vec) st4g(vec_out + r * a.F + 4 * f4, accf);
     if (lead) head_out[r * H + h] = acce;
   }

@@ -306,10 +306,17 @@ int64_t fast_chunk_edges(int64_t nnz, int64_t F) {
   return k;
 }
 
+int64_t fast_carry_bytes(int64_t nnz, int64_t F) {
+  if (nnz == 0) return 0;
+  const int64_t k = fast_chunk_edges(nnz, F);
+  return (((nnz + k - 1) / k) * F * static_cast<int64_t>(sizeof(float)) + 15) & ~int64_t(15);
+}
+
+// carries + one segmented-fixup counter per chunk
 int64_t fast_workspace_bytes(int64_t nnz, int64_t F) {
   if (nnz == 0) return 0;
   const int64_t k = fast_chunk_edges(nnz, F);
-  return ((nnz + k - 1) / k) * F * static_cast<int64_t>(sizeof(float));
+  return fast_carry_bytes(nnz, F) + ((nnz + k - 1) / k) * static_cast<int64_t>(sizeof(int32_t));
 }
 
 bool fast_supported(int kind, int64_t F, int64_t head_dim) {

@@ -196,6 +196,7 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
   const int64_t p0 = chunk * K;
   if (p0 >= a.nnz) return;  // whole group exits together
   const int64_t p1 = p0 + K < a.nnz ? p0 + K : a.nnz;
+  if (a.seg_cnt != nullptr && lane == 0) a.seg_cnt[chunk] = 0;  // k_chunk_fixup's counters
   using V = typename VecT<VW>::T;
   const int F4 = static_cast<int>(a.F / VW);
   const V I = vident<VW, RED>();
@@ -302,8 +303,10 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
 }
 
 // Fold the carries of every row cut by chunk boundaries into its head, in
-// chunk order.  One group per chunk; only a row's first continuation chunk
-// does work.
+// chunk order.  One group per chunk; a row's first continuation chunk does the
+// work, or -- for rows of more than kFixSeg continuation chunks, when the
+// workspace has counters -- every kFixSeg-th one folds a segment and the last
+// to finish folds the head and the segment partials (internal.h).
 template <int RED, int L, int NV, bool EPI = false, int VW = 4>
 __global__ void __launch_bounds__(kBlock) k_chunk_fixup(FastArgs a, const int32_t* __restrict__ indptr) {
   constexpr int G = kBlock / L;
@@ -315,37 +318,57 @@ __global__ void __launch_bounds__(kBlock) k_chunk_fixup(FastArgs a, const int32_
   if (chunk == 0 || p0 >= a.nnz) return;
   const int64_t r = a.rows[p0];
   const int64_t start = indptr[r];
-  if (start >= p0 || start < p0 - K) return;  // not a continuation / not the first one
+  if (start >= p0) return;  // not a continuation
+  const int64_t first = start / K + 1;  // the row's first continuation chunk
   const int64_t last = (indptr[r + 1] - 1) / K;
+  const int64_t nseg = a.seg_cnt != nullptr ? (last - first + kFixSeg) / kFixSeg : 1;
+  if (nseg == 1 ? chunk != first : (chunk - first) % kFixSeg != 0) return;
+  const int64_t cend = nseg == 1 ? last : (chunk + kFixSeg - 1 < last ? chunk + kFixSeg - 1 : last);
   using V = typename VecT<VW>::T;
   const int F4 = static_cast<int>(a.F / VW);
+  auto fold = [&](V (&acc)[NV], int64_t c0, int64_t c1, int64_t step) {
+    int64_t c = c0;
+    for (; c + 3 * step <= c1; c += 4 * step) {
+      V t[4][NV];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          const int f4 = lane + v * L;
+          t[k][v] = f4 < F4 ? vld<VW>(a.carry + (c + k * step) * a.F + VW * f4) : vident<VW, RED>();
+        }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[v] = vred<RED>(acc[v], t[k][v]);
+    }
+    for (; c <= c1; c += step)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int f4 = lane + v * L;
+        if (f4 < F4) acc[v] = vred<RED>(acc[v], vld<VW>(a.carry + c * a.F + VW * f4));
+      }
+  };
   V acc[NV];
+  if (nseg > 1) {
+    // this segment's partial, into its own first carry record (already read)
+#pragma unroll
+    for (int v = 0; v < NV; ++v) acc[v] = vident<VW, RED>();
+    fold(acc, chunk, cend, 1);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int f4 = lane + v * L;
+      if (f4 < F4) vst(a.carry + chunk * a.F + VW * f4, acc[v]);
+    }
+    if (!seg_arrive_last(a.seg_cnt + first, nseg, L, lane)) return;
+  }
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int f4 = lane + v * L;
     acc[v] = f4 < F4 ? vld<VW>(a.out + r * a.F + VW * f4) : vident<VW, RED>();
   }
-  int64_t c = chunk;
-  for (; c + 3 <= last; c += 4) {
-    V t[4][NV];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        const int f4 = lane + v * L;
-        t[k][v] = f4 < F4 ? vld<VW>(a.carry + (c + k) * a.F + VW * f4) : vident<VW, RED>();
-      }
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int v = 0; v < NV; ++v) acc[v] = vred<RED>(acc[v], t[k][v]);
-  }
-  for (; c <= last; ++c)
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int f4 = lane + v * L;
-      if (f4 < F4) acc[v] = vred<RED>(acc[v], vld<VW>(a.carry + c * a.F + VW * f4));
-    }
+  if (nseg > 1) fold(acc, first, first + (nseg - 1) * kFixSeg, kFixSeg);
+  else fold(acc, first, last, 1);
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int f4 = lane + v * L;
