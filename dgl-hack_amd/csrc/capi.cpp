@@ -549,6 +549,7 @@ void forward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const D
     a.chunk = fast_chunk_edges(walk.nnz, D);
     Scratch carry(g, fast_workspace_bytes(walk.nnz, D), s);
     a.carry = static_cast<float*>(carry.ptr);
+    a.seg_cnt = reinterpret_cast<int32_t*>(static_cast<char*>(carry.ptr) + fast_carry_bytes(walk.nnz, D));
     launch_generic_lb(op, red, bc, false, a, s);
     check_hip(hipGetLastError(), "generic lb forward launch");
     if (epi) launch_epilogue(out->data, out_rows, D, epi->row_mul, epi->row_div, epi->bias, epi->addend, s);
@@ -712,6 +713,7 @@ void backward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const 
     a.chunk = fast_chunk_edges(walk.nnz, Dg);
     Scratch carry(g, fast_workspace_bytes(walk.nnz, Dg), s);
     a.carry = static_cast<float*>(carry.ptr);
+    a.seg_cnt = reinterpret_cast<int32_t*>(static_cast<char*>(carry.ptr) + fast_carry_bytes(walk.nnz, Dg));
     launch_generic_lb(op, red, bc, true, a, s);
     check_hip(hipGetLastError(), "generic lb backward launch");
     return;
@@ -1101,7 +1103,8 @@ int64_t DGLMIEdgeSoftmaxWorkspaceBytes(const DGLMICsr* in_csr, int64_t values_pe
   const int64_t chunks = (in_csr->nnz + softmax_chunk_edges(in_csr->nnz) - 1) /
                          softmax_chunk_edges(in_csr->nnz);
   const int64_t stats = ((2 * in_csr->num_rows * values_per_edge * 4) + 255) & ~int64_t(255);
-  return stats + chunks * 2 * values_per_edge * 4;
+  // carries, then one segmented-fixup counter per chunk
+  return stats + ((chunks * 2 * values_per_edge * 4 + 15) & ~int64_t(15)) + chunks * 4;
 }
 
 namespace {
@@ -1145,6 +1148,9 @@ int DGLMIEdgeSoftmaxForward(const DGLMIGraph* graph, const DGLMIArray* logits, D
   a.stat0 = static_cast<float*>(ws.ptr);
   a.stat1 = a.stat0 + a.num_rows * H;
   a.carry = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + stats);
+  a.seg_cnt = reinterpret_cast<int32_t*>(
+      reinterpret_cast<char*>(a.carry) +
+      ((((a.nnz + a.chunk - 1) / a.chunk) * 2 * H * 4 + 15) & ~int64_t(15)));
   a.s = logits->data;
   a.out = out->data;
   launch_edge_softmax(a, false, s);
@@ -1171,6 +1177,9 @@ int DGLMIEdgeSoftmaxBackward(const DGLMIGraph* graph, const DGLMIArray* out,
   const int64_t stats = ((2 * a.num_rows * H * 4) + 255) & ~int64_t(255);
   a.stat0 = static_cast<float*>(ws.ptr);
   a.carry = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + stats);
+  a.seg_cnt = reinterpret_cast<int32_t*>(
+      reinterpret_cast<char*>(a.carry) +
+      ((((a.nnz + a.chunk - 1) / a.chunk) * 2 * H * 4 + 15) & ~int64_t(15)));
   a.s = out->data;
   a.ga = grad_out->data;
   a.out = grad_logits->data;

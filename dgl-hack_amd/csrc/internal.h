@@ -63,6 +63,7 @@ struct EdgeArgs {
   // load-balanced reduce-to-row (launch_generic_lb)
   float* carry;            // workspace: num_chunks * out-row floats
   int64_t chunk;           // CSR positions per chunk
+  int32_t* seg_cnt;        // num_chunks counters after the carries (segmented fixup), or null
 };
 
 // ---- device helpers ---------------------------------------------------------
@@ -238,6 +239,7 @@ struct SoftmaxArgs {
   float* out;              // forward: softmax; backward: gradient wrt the logits
   float* carry;            // num_chunks x 2H
   int64_t chunk;
+  int32_t* seg_cnt;        // num_chunks counters after the carries (segmented fixup), or null
 };
 bool softmax_supported(int64_t H);
 int64_t softmax_chunk_edges(int64_t nnz);

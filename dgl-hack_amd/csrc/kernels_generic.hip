@@ -170,6 +170,7 @@ __global__ void __launch_bounds__(kBlock) k_lb_reduce(EdgeArgs a, int lane_bits)
   const int64_t p0 = chunk * K;
   if (p0 >= a.nnz) return;
   const int64_t p1 = p0 + K < a.nnz ? p0 + K : a.nnz;
+  if (a.seg_cnt != nullptr && lane == 0) a.seg_cnt[chunk] = 0;  // k_lb_fixup's counters
   const int64_t Do = BWD ? a.D * a.len : a.D;
   const int nv = static_cast<int>((Do + L - 1) / L);
   const float I = BWD ? 0.0f : red_identity<RED>();
@@ -244,16 +245,30 @@ __global__ void __launch_bounds__(kBlock) k_lb_fixup(EdgeArgs a, int lane_bits) 
   if (chunk == 0 || p0 >= a.nnz) return;
   const int64_t r = a.rows[p0];
   const int64_t start = a.indptr[r];
-  if (start >= p0 || start < p0 - K) return;  // not the first continuation of row r
+  if (start >= p0) return;  // not a continuation
+  // segmented for long rows (internal.h, kFixSeg)
+  const int64_t first = start / K + 1;
   const int64_t last = (a.indptr[r + 1] - 1) / K;
+  const int64_t nseg = a.seg_cnt != nullptr ? (last - first + kFixSeg) / kFixSeg : 1;
+  if (nseg == 1 ? chunk != first : (chunk - first) % kFixSeg != 0) return;
   const int64_t Do = BWD ? a.D * a.len : a.D;
+  auto red = [&](float acc, float t) { return BWD ? acc + t : red_apply<RED>(acc, t); };
+  if (nseg > 1) {
+    const int64_t cend = chunk + kFixSeg - 1 < last ? chunk + kFixSeg - 1 : last;
+    for (int64_t k = lane; k < Do; k += L) {
+      float acc = a.carry[chunk * Do + k];
+      for (int64_t c = chunk + 1; c <= cend; ++c) acc = red(acc, a.carry[c * Do + k]);
+      a.carry[chunk * Do + k] = acc;
+    }
+    if (!seg_arrive_last(a.seg_cnt + first, nseg, L, lane)) return;
+  }
   float* o = a.out + lb_out_row<BWD>(a, r) * Do;
   for (int64_t k = lane; k < Do; k += L) {
     float acc = o[k];
-    for (int64_t c = chunk; c <= last; ++c) {
-      const float t = a.carry[c * Do + k];
-      acc = BWD ? acc + t : red_apply<RED>(acc, t);
-    }
+    if (nseg > 1)
+      for (int64_t sg = 0; sg < nseg; ++sg) acc = red(acc, a.carry[(first + sg * kFixSeg) * Do + k]);
+    else
+      for (int64_t c = first; c <= last; ++c) acc = red(acc, a.carry[c * Do + k]);
     o[k] = acc;
   }
 }

@@ -72,6 +72,7 @@ __global__ void __launch_bounds__(kBlock) k_sm_rows(SoftmaxArgs a) {
   const int64_t p0 = chunk * K;
   if (p0 >= a.nnz) return;
   const int64_t p1 = p0 + K < a.nnz ? p0 + K : a.nnz;
+  if (a.seg_cnt != nullptr) a.seg_cnt[chunk] = 0;  // k_sm_fixup's counters
   int64_t cur = a.rows[p0];
   bool cont = p0 > 0 && a.rows[p0 - 1] == cur;
   float m[H], l[H];
@@ -139,12 +140,14 @@ __global__ void __launch_bounds__(kBlock) k_sm_fixup(SoftmaxArgs a) {
   if (chunk == 0 || p0 >= a.nnz) return;
   const int64_t r = a.rows[p0];
   const int64_t start = a.indptr[r];
-  if (start >= p0 || start < p0 - K) return;  // not the first continuation of row r
+  if (start >= p0) return;  // not a continuation
+  // segmented for long rows (internal.h, kFixSeg); one lane per chunk
+  const int64_t first = start / K + 1;
   const int64_t last = (a.indptr[r + 1] - 1) / K;
+  const int64_t nseg = a.seg_cnt != nullptr ? (last - first + kFixSeg) / kFixSeg : 1;
+  if (nseg == 1 ? chunk != first : (chunk - first) % kFixSeg != 0) return;
   float m[H], l[H];
-  ldrow<H>(a.stat0 + r * H, m);
-  if constexpr (MODE == SM_STATS) ldrow<H>(a.stat1 + r * H, l);
-  for (int64_t c = chunk; c <= last; ++c) {
+  auto add = [&](int64_t c) {
     float cm[H], cl[H];
     ldrow<H>(a.carry + c * 2 * H, cm);
     if constexpr (MODE == SM_STATS) {
@@ -155,7 +158,22 @@ __global__ void __launch_bounds__(kBlock) k_sm_fixup(SoftmaxArgs a) {
 #pragma unroll
       for (int h = 0; h < H; ++h) m[h] += cm[h];
     }
+  };
+  if (nseg > 1) {
+    const int64_t cend = chunk + kFixSeg - 1 < last ? chunk + kFixSeg - 1 : last;
+    ldrow<H>(a.carry + chunk * 2 * H, m);
+    if constexpr (MODE == SM_STATS) ldrow<H>(a.carry + chunk * 2 * H + H, l);
+    for (int64_t c = chunk + 1; c <= cend; ++c) add(c);
+    strow<H>(a.carry + chunk * 2 * H, m);
+    if constexpr (MODE == SM_STATS) strow<H>(a.carry + chunk * 2 * H + H, l);
+    if (!seg_arrive_last(a.seg_cnt + first, nseg, 1, 0)) return;
   }
+  ldrow<H>(a.stat0 + r * H, m);
+  if constexpr (MODE == SM_STATS) ldrow<H>(a.stat1 + r * H, l);
+  if (nseg > 1)
+    for (int64_t sg = 0; sg < nseg; ++sg) add(first + sg * kFixSeg);
+  else
+    for (int64_t c = first; c <= last; ++c) add(c);
   strow<H>(a.stat0 + r * H, m);
   if constexpr (MODE == SM_STATS) strow<H>(a.stat1 + r * H, l);
 }

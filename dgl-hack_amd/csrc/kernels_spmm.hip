@@ -126,6 +126,7 @@ __global__ void __launch_bounds__(kBlock) k_lane_reduce(FastArgs a) {
   const int64_t p0 = chunk * K;
   if (p0 >= a.nnz) return;
   const int64_t p1 = p0 + K < a.nnz ? p0 + K : a.nnz;
+  if (a.seg_cnt != nullptr) a.seg_cnt[chunk] = 0;  // k_lane_fixup's counters
   const float I = red_identity<RED>();
   float ident[F];
 #pragma unroll
@@ -203,16 +204,31 @@ __global__ void __launch_bounds__(kBlock) k_lane_fixup(FastArgs a) {
   if (chunk == 0 || p0 >= a.nnz) return;
   const int64_t r = a.rows[p0];
   const int64_t start = a.indptr[r];
-  if (start >= p0 || start < p0 - K) return;
+  if (start >= p0) return;  // not a continuation
+  // segmented for long rows (internal.h, kFixSeg); one lane per chunk
+  const int64_t first = start / K + 1;
   const int64_t last = (a.indptr[r + 1] - 1) / K;
+  const int64_t nseg = a.seg_cnt != nullptr ? (last - first + kFixSeg) / kFixSeg : 1;
+  if (nseg == 1 ? chunk != first : (chunk - first) % kFixSeg != 0) return;
   float acc[F];
-  load_row<F>(a.out + r * F, acc);
-  for (int64_t c = chunk; c <= last; ++c) {
+  auto add = [&](int64_t c) {
     float t[F];
     load_row<F>(a.carry + c * F, t);
 #pragma unroll
     for (int i = 0; i < F; ++i) acc[i] = red_apply<RED>(acc[i], t[i]);
+  };
+  if (nseg > 1) {
+    const int64_t cend = chunk + kFixSeg - 1 < last ? chunk + kFixSeg - 1 : last;
+    load_row<F>(a.carry + chunk * F, acc);
+    for (int64_t c = chunk + 1; c <= cend; ++c) add(c);
+    store_row<F>(a.carry + chunk * F, acc);
+    if (!seg_arrive_last(a.seg_cnt + first, nseg, 1, 0)) return;
   }
+  load_row<F>(a.out + r * F, acc);
+  if (nseg > 1)
+    for (int64_t sg = 0; sg < nseg; ++sg) add(first + sg * kFixSeg);
+  else
+    for (int64_t c = first; c <= last; ++c) add(c);
   epi_row<EPI, F>(a, r, acc);
   store_row<F>(a.out + r * F, acc);
 }

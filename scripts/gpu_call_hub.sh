@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_hub_rows_gpu.py tests/test_fused_gat_gpu.py -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread -rf > gpurun_out/pytest_hub.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_hub_rows_gpu.py tests/test_fused_gat_gpu.py tests/test_empty_rows_gpu.py -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread -rf > gpurun_out/pytest_hub.log 2>&1
 rc=$?; echo "hub tests rc=$rc"; tail -15 gpurun_out/pytest_hub.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 python scripts/hub_probe.py > gpurun_out/hub_probe.json 2> gpurun_out/hub_probe.err
 rc=$?; echo "probe rc=$rc"; cat gpurun_out/hub_probe.json; [ $rc -eq 0 ] || exit $rc

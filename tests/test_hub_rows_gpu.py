@@ -138,3 +138,43 @@ def test_fused_gat_star(reverse):
     for a, b, name in zip(gf, gr, ("ft", "el", "er")):
         err = (a.double() - b).abs().max().item()
         assert th.allclose(a.double(), b, rtol=1e-3, atol=1e-3), (name, err)
+
+
+def test_generic_binary_max_star():
+    """u_mul_v max reduces on the generic load-balanced kernel (k_lb_fixup)."""
+    n, m = 50_000, 1_000_000
+    src, dst = star(n, m, hub=99)
+    g = _graph(src, dst, n)
+    gen = th.Generator(device=DEV).manual_seed(5)
+    x = th.rand(n, 3, device=DEV, generator=gen) * 2 - 1
+    y = th.rand(n, 3, device=DEV, generator=gen) * 2 - 1
+    g.ndata["x"], g.ndata["y"] = x, y
+    g.update_all(fn.u_mul_v("x", "y", "m"), fn.max("m", "h"))
+    s, d, hubs, rest = _hub_split(src, dst, n)
+    ref = th.full((n, 3), float("-inf"), device=DEV).index_reduce_(0, d[rest], x[s[rest]] * y[d[rest]], "amax")
+    for hb in hubs:
+        ref[hb] = (x[s[d == hb]] * y[hb]).amax(0)
+    deg = th.bincount(d, minlength=n)
+    assert th.equal(g.ndata["h"][deg > 0], ref[deg > 0])
+
+
+def test_edge_softmax_star():
+    """edge_softmax over a 1 M-edge row: k_sm_fixup's segmented (m, l) merge."""
+    from dgl.nn.pytorch import edge_softmax
+    n, m = 50_000, 1_000_000
+    src, dst = star(n, m, hub=7)
+    g = _graph(src, dst, n)
+    gen = th.Generator(device=DEV).manual_seed(6)
+    e = (4 * th.randn(len(src), 4, 1, device=DEV, generator=gen)).requires_grad_()
+    a = edge_softmax(g, e)
+    go = th.randn(a.shape, device=DEV, generator=gen)
+    (ge,) = th.autograd.grad(a, e, go)
+    d = th.from_numpy(dst).to(DEV)
+    hub = d == 7
+    ed = e.detach().double()
+    ref = th.softmax(ed[hub], dim=0)
+    assert th.allclose(a[hub].double(), ref, rtol=1e-4, atol=1e-9)
+    gref = ref * (go[hub].double() - (ref * go[hub].double()).sum(0, keepdim=True))
+    assert th.allclose(ge[hub].double(), gref, rtol=1e-3, atol=1e-8)
+    assert th.allclose(a.sum().double(), th.tensor(float(len(th.unique(d))) * 4, dtype=th.float64,
+                                                    device=DEV), rtol=1e-5)
