@@ -189,7 +189,9 @@ int DGLMIKernelBackwardCopyReduce(const char* reducer, const DGLMIGraph* graph, 
  * The load-balanced path cuts the CSR positions into fixed-size edge chunks
  * (no reference counterpart: the reference relies on minigun's per-edge
  * binary search, binary_reduce_impl.cu:424-466); rows split across chunks
- * leave per-chunk partials here, combined afterwards in chunk order. */
+ * leave per-chunk partials here, combined afterwards in chunk order (rows of
+ * more than 32 continuation chunks in segments of 32, in segment order), plus
+ * one int32 counter per chunk for those segmented rows. */
 int64_t DGLMIKernelWorkspaceBytes(const DGLMICsr* csr, int64_t feat_len);
 
 /* Build DGLMIGraph.{in,out}_gather_cols (extension): out_cols[p] =
