@@ -12,7 +12,9 @@ dst-major CSR.  Generated on the GPU (seeded), CSRs built on the GPU.
 A step = one copy_u_sum pass (DGLGraph.update_all(copy_u, sum) lowers to
 exactly this call) over the resident graph: out[v] = sum_{u->v} X[u].
 
-Multi-GPU (torchrun, one process per GPU): weak scaling.  The global graph
+Multi-GPU (one process per GPU): `--gpus N` starts the N ranks itself when no
+launcher set WORLD_SIZE (launch_ranks), or runs as one rank of a
+torch.distributed.run job whose WORLD_SIZE must equal N.  Weak scaling.  The global graph
 has N x 100M edges (RMAT scale 23 + log2 N); every rank owns a contiguous
 block of destination rows with all their in-edges (1-D row partition, the
 halo-subgraph semantics of graph_op.cc:403-509 with num_hops = 1) and holds
@@ -491,13 +493,20 @@ def _timed(fn, steps, dist, cdev):
     return el
 
 
+# Exit status of a run whose headline line was printed but one of its side lines
+# (with-exchange, C4) failed: the line carries the errors under
+# `side_line_errors`, and the status tells the caller without parsing it.
+SIDE_LINE_RC = 3
+
+
 class SideLineGuard:
     """N > 1 only.  The side lines after the headline (with-exchange, C4) run
     collectives.  If one rank raises or stalls there, its peers wait inside RCCL,
-    and torchrun would end the job without the headline line.  So a failing rank
-    posts its error in the job's TCP store; rank 0's watchdog thread then prints
-    the line with the error recorded under the phase that failed, and every rank
-    leaves with status 0.  A phase that exceeds `budget_s` counts as failed."""
+    and the launcher would end the job without the headline line.  So a failing
+    rank posts its error in the job's TCP store; rank 0's watchdog thread then
+    prints the line with the error recorded under the phase that failed (and in
+    `side_line_errors`), and every rank leaves with status SIDE_LINE_RC.  A phase
+    that exceeds `budget_s` counts as failed."""
 
     KEY_ERR = "dglmi_bench_side_error"
     KEY_DONE = "dglmi_bench_line_printed"
@@ -520,13 +529,15 @@ class SideLineGuard:
         with self.lock:
             if not self.printed:
                 self.printed = True
-                self.res[self.phase or "side_line"] = {"error": err}
+                phase = self.phase or "side_line"
+                self.res[phase] = {"error": err}
+                self.res.setdefault("side_line_errors", []).append({"line": phase, "error": err})
                 print(json.dumps(self.res), flush=True)
             try:
                 self.store.set(self.KEY_DONE, "1")
             except Exception:  # noqa: BLE001
                 pass
-            os._exit(0)
+            os._exit(SIDE_LINE_RC)
 
     def _watch(self):
         seen = None
@@ -543,12 +554,12 @@ class SideLineGuard:
                 if seen is not None and self.rank == 0:
                     self._emit_and_exit(self.store.get(self.KEY_ERR).decode())
                 if seen is not None and self.store.check([self.KEY_DONE]):
-                    os._exit(0)
+                    os._exit(SIDE_LINE_RC)
             except Exception:  # noqa: BLE001  (store gone: rank 0 has printed and left)
                 if seen is not None or self.rank != 0:
-                    os._exit(0)
+                    os._exit(SIDE_LINE_RC)
             if seen is not None and time.time() - seen > 60:
-                os._exit(0)
+                os._exit(SIDE_LINE_RC)
 
     def fail(self, exc):
         err = "rank %d: %s" % (self.rank, exc if isinstance(exc, SystemExit) else repr(exc))
@@ -558,18 +569,164 @@ class SideLineGuard:
         try:
             self.store.set(self.KEY_ERR, err)
         except Exception:  # noqa: BLE001
-            os._exit(1)
+            os._exit(SIDE_LINE_RC)
         time.sleep(120)  # the watchdog leaves once rank 0 has printed
-        os._exit(1)
+        os._exit(SIDE_LINE_RC)
 
     def finish(self):
         """Normal end: rank 0 prints the line (the watchdog can no longer)."""
         with self.lock:
             if self.printed:
-                os._exit(0)  # pragma: no cover (the watchdog already printed and is exiting)
+                os._exit(SIDE_LINE_RC)  # pragma: no cover (the watchdog printed and is exiting)
             self.printed = True
             if self.rank == 0:
                 print(json.dumps(self.res), flush=True)
+
+
+class SideLines:
+    """Runs the side lines after the headline and prints the job's one JSON line.
+    A side line that fails is recorded under its key and in the top-level
+    `side_line_errors` list; `finish()` returns SIDE_LINE_RC then, else 0.  At
+    N > 1 the lines run under SideLineGuard (a raise or stall on one rank)."""
+
+    def __init__(self, dist, rank, res, budget_s=300.0):
+        self.rank, self.res = rank, res
+        self.guard = SideLineGuard(dist, rank, res, budget_s) if dist is not None else None
+
+    def run(self, key, fn):
+        if self.guard is not None:
+            self.guard.start(key)
+        try:
+            self.res[key] = fn()
+        except SystemExit as exc:
+            # parity checks agree across ranks (max over ranks) before exiting, so
+            # every rank lands here together
+            self._error(key, str(exc))
+        except Exception as exc:  # noqa: BLE001
+            if self.guard is not None:
+                self.guard.fail(exc)  # does not return
+            self._error(key, repr(exc))  # one process: keep the headline line
+        if self.guard is not None:
+            self.guard.phase = None
+        log("%s: %s" % (key, json.dumps(self.res[key])))
+
+    def _error(self, key, err):
+        self.res[key] = {"error": err}
+        self.res.setdefault("side_line_errors", []).append({"line": key, "error": err})
+
+    def finish(self):
+        if self.guard is not None:
+            self.guard.finish()
+        elif self.rank == 0:
+            print(json.dumps(self.res), flush=True)
+        return SIDE_LINE_RC if self.res.get("side_line_errors") else 0
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(nproc, argv, grace_s=60.0):
+    """`bench.py --gpus N` with N > 1 and no launcher around it: start one fresh
+    Python process per GPU running this script with the same arguments and the
+    environment torch.distributed.run would give it (RANK = LOCAL_RANK = i,
+    WORLD_SIZE = N, MASTER_ADDR 127.0.0.1, a free MASTER_PORT), as the reference's
+    multi-GPU example spawns one process per device itself
+    (examples/pytorch/graphsage/train_sampling_multi_gpu.py:193-200,336).  This
+    process never touches the GPU.  Rank 0 prints the JSON line straight to the
+    inherited stdout.  When a rank exits non-zero the others get `grace_s` to
+    finish (rank 0 may still be printing a line with side-line errors), then
+    their process groups are killed.  Returns the job's status: 0 when every rank
+    exited 0, else the status of the first rank that failed (128 + signal for a
+    rank killed by a signal)."""
+    import signal
+    import subprocess
+    port = _free_port()
+    procs = []
+
+    def kill_all(sig):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, sig)
+                except ProcessLookupError:
+                    pass
+
+    def on_term(signum, _frame):
+        kill_all(signal.SIGKILL)
+        os._exit(128 + signum)
+
+    signal.signal(signal.SIGTERM, on_term)
+    signal.signal(signal.SIGINT, on_term)
+    for r in range(nproc):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc),
+                   LOCAL_WORLD_SIZE=str(nproc), GROUP_RANK="0", ROLE_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DGLMI_BENCH_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv],
+                                      env=env, start_new_session=True))
+    print("launcher: %d ranks, pids %s, master 127.0.0.1:%d"
+          % (nproc, [p.pid for p in procs], port), file=sys.stderr, flush=True)
+    rcs = [None] * nproc
+    first = None  # (time, rank) of the first failure
+    killed = False
+    while any(rc is None for rc in rcs):
+        for r, p in enumerate(procs):
+            if rcs[r] is None and p.poll() is not None:
+                rcs[r] = p.returncode
+                if p.returncode != 0 and first is None:
+                    first = (time.time(), r)
+                    print("launcher: rank %d exited with status %d" % (r, p.returncode),
+                          file=sys.stderr, flush=True)
+        if first is not None and not killed and time.time() - first[0] > grace_s:
+            print("launcher: killing the ranks still running %.0f s after rank %d failed"
+                  % (grace_s, first[1]), file=sys.stderr, flush=True)
+            kill_all(signal.SIGKILL)
+            killed = True
+        time.sleep(0.1)
+    print("launcher: rank exit statuses %s" % rcs, file=sys.stderr, flush=True)
+    if first is None:
+        return 0
+    rc = rcs[first[1]]
+    return 128 - rc if rc < 0 else rc
+
+
+def launcher_stub(mode, world, rank):
+    """Worker body of the launcher's CPU test (``--launcher-stub MODE``): no GPU;
+    gloo collectives over the ranks the launcher started, then the same
+    side-line / print path as the real run.  MODE: ok | crash1 (rank 1 exits 7
+    before joining) | side1 (rank 1 raises inside a side line)."""
+    import torch.distributed as dist
+    if mode == "crash1" and rank == 1:
+        sys.exit(7)
+    if world > 1:
+        dist.init_process_group("gloo", timeout=__import__("datetime").timedelta(seconds=60))
+    ranks = [None] * world
+    info = (rank, int(os.environ.get("LOCAL_RANK", "0")), os.getpid())
+    if world > 1:
+        dist.all_gather_object(ranks, info)
+    else:
+        ranks = [info]
+    res = {"metric": "launcher-stub", "value": 1.0, "n_gpus": world, "ranks": ranks}
+    lines = SideLines(dist if world > 1 else None, rank, res, budget_s=60.0)
+
+    def c4():
+        if mode == "side1" and rank == 1:
+            raise RuntimeError("injected side-line failure")
+        t = th.ones(1)
+        if world > 1:
+            dist.all_reduce(t)
+        return {"value": float(t.item())}
+    lines.run("c4", c4)
+    rc = lines.finish()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return rc
 
 
 def measure_exchange(part, x, out_ref, args, dist, cdev, device, edges_total):
@@ -706,13 +863,32 @@ def main():
                     help="C4 hybrid exchange: push a partial sum when a part holds >= tau "
                          "sources of a destination")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--launch-grace", type=float, default=60.0,
+                    help="self-launched N > 1: seconds the other ranks get after one fails")
+    ap.add_argument("--launcher-stub", default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.pmc_child:
         pmc_child()
-        return
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+        return 0
+    if args.gpus < 1:
+        log("--gpus must be >= 1")
+        return 2
+    if args.same_device and args.gpus >= 3:
+        # three or more processes on one GPU crawl inside rocPRIM's
+        # decoupled-look-back sorts (partition_stats 180 s per rank at N = 3)
+        log("--same-device is refused for N >= 3 (concurrent look-back sorts stall)")
+        return 2
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no launcher around us: start the N ranks ourselves, before any GPU call
+        return launch_ranks(args.gpus, sys.argv[1:], args.launch_grace)
+    world = int(env_world or "1")
+    if world != args.gpus:
+        log("WORLD_SIZE=%d from the launcher but --gpus %d" % (world, args.gpus))
+        return 2
     rank = int(os.environ.get("RANK", "0"))
+    if args.launcher_stub:
+        return launcher_stub(args.launcher_stub, world, rank)
     m1 = world == 1 and args.edges_per_gpu == EDGES_PER_GPU and args.scale == SCALE
     pmc = None
     under_profiler = any(k.startswith("ROCPROF") for k in os.environ)
@@ -916,30 +1092,13 @@ def main():
         except Exception as exc:  # the baseline must never take the GPU line down
             res["cpu_baseline"] = {"value": None, "error": repr(exc)}
     # Side lines.  At N > 1 they run collectives under the guard, so a rank that
-    # fails or stalls in one cannot take the headline line down with it.
-    guard = SideLineGuard(dist, rank, res) if dist is not None else None
-
-    def side(key, fn):
-        if guard is not None:
-            guard.start(key)
-        try:
-            res[key] = fn()
-        except SystemExit as exc:
-            # parity checks agree across ranks (max over ranks) before exiting, so
-            # every rank lands here together
-            res[key] = {"error": str(exc)}
-        except Exception as exc:  # noqa: BLE001
-            if guard is not None:
-                guard.fail(exc)  # does not return
-            res[key] = {"error": repr(exc)}  # one process: keep the headline line
-        if guard is not None:
-            guard.phase = None
-        log("%s: %s" % (key, json.dumps(res[key])))
-
+    # fails or stalls in one cannot take the headline line down with it; a failed
+    # side line still makes the job's exit status SIDE_LINE_RC.
+    lines = SideLines(dist, rank, res)
     if part is not None:
         log("with-exchange line ...")
-        side("with_exchange",
-             lambda: measure_exchange(part, x, out, args, dist, cdev, device, edges_total))
+        lines.run("with_exchange",
+                  lambda: measure_exchange(part, x, out, args, dist, cdev, device, edges_total))
     if under_profiler and not args.no_c4:
         # under rocprofv3 the kernel statistics must describe the M1 launch alone
         # (C4 runs the same kernel on a 200 M-edge graph): skip the C4 line
@@ -949,15 +1108,13 @@ def main():
         if part is not None:
             del part
         th.cuda.empty_cache()
-        side("c4", lambda: measure_c4(world, rank, dist, cdev, device, args))
-    if guard is not None:
-        guard.finish()
-    elif rank == 0:
-        print(json.dumps(res), flush=True)
+        lines.run("c4", lambda: measure_c4(world, rank, dist, cdev, device, args))
+    rc = lines.finish()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    return rc
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

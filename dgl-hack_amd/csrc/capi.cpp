@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -380,7 +381,10 @@ void run_fast(const DGLMIGraph* g, const DGLMICsr& walk, int kind, int red, cons
 // (average in-degree 492) in-CSR order wins for wide node-only rows (u_dot_v
 // 8 x 8: 7.38 vs 8.10 ms) while narrow rows still prefer edge-id order (3.64 vs
 // 5.55 ms).  So: in-CSR order only for node-only operands, rows of >= 32
-// floats and average in-degree >= 64.  DGLMI_SDDMM_ORDER=coo|csr forces one.
+// floats and average in-degree >= 64.  DGLMISetSddmmOrder forces one (tests
+// of both walks, scripts/sddmm_order_probe.py).
+std::atomic<int> g_sddmm_order{DGLMI_SDDMM_ORDER_AUTO};
+
 SddmmArgs sddmm_items(const DGLMIGraph* g, const DGLMICsr& walk, bool edge_operand,
                       int64_t row_floats) {
   SddmmArgs e;
@@ -388,9 +392,9 @@ SddmmArgs sddmm_items(const DGLMIGraph* g, const DGLMICsr& walk, bool edge_opera
   e.nnz = walk.nnz;
   bool coo = g->coo_src != nullptr && g->coo_dst != nullptr;
   if (coo) {
-    const char* env = std::getenv("DGLMI_SDDMM_ORDER");
-    if (env && std::string(env) == "csr") coo = false;
-    else if (!(env && std::string(env) == "coo"))
+    const int forced = g_sddmm_order.load(std::memory_order_relaxed);
+    if (forced == DGLMI_SDDMM_ORDER_CSR) coo = false;
+    else if (forced != DGLMI_SDDMM_ORDER_COO)
       coo = edge_operand || row_floats < 32 || walk.nnz < 64 * std::max<int64_t>(walk.num_rows, 1);
   }
   if (coo) {
@@ -796,6 +800,15 @@ extern "C" {
 const char* DGLMIGetLastError(void) { return g_last_error.c_str(); }
 
 const char* DGLMIVersion(void) { return "0.4-mi355x"; }
+
+int DGLMISetSddmmOrder(int32_t order) {
+  API_BEGIN();
+  if (order != DGLMI_SDDMM_ORDER_AUTO && order != DGLMI_SDDMM_ORDER_COO &&
+      order != DGLMI_SDDMM_ORDER_CSR)
+    throw std::invalid_argument("DGLMISetSddmmOrder: order must be 0 (auto), 1 (coo) or 2 (csr)");
+  g_sddmm_order.store(order, std::memory_order_relaxed);
+  API_END();
+}
 
 int DGLMIKernelInferBinaryFeatureShape(const char* op, const DGLMIArray* lhs,
                                        const DGLMIArray* rhs, int64_t* out_shape,

@@ -305,11 +305,13 @@ void launch_mark_cold(const int32_t* cols, int64_t nnz, const int32_t* deg_indpt
 int64_t fast_chunk_edges(int64_t nnz, int64_t F) {
   // Enough chunks to give every CU several groups; long chunks otherwise so
   // that fewer rows are cut (each cut row costs one carry write + read).
+#if DGLMI_PROBES
   // DGLMI_CHUNK_EDGES overrides (tuning experiments; power of two >= 4).
   if (const char* env = std::getenv("DGLMI_CHUNK_EDGES")) {
     const long v = std::atol(env);
     if (v >= 4 && (v & (v - 1)) == 0) return v;
   }
+#endif
   // Measured on M1 (F = 16..256): 512 is best or within 1% (scripts/tune_spmm.py).
   // Narrow rows (F < 16) use one lane per chunk: shorter chunks, more lanes.
   // Small graphs go down to 8 edges per chunk: a launch-bound Cora-size copy_u

@@ -401,6 +401,12 @@ inline Cfg pick(int64_t slots, int vw) {
   return {64, 16};
 }
 
+#if DGLMI_PROBES
+// Probe build only (`make PROBES=1` -> libdglmi_probes.so): the cache-policy and
+// tuning variants of the headline kernel, picked per launch from the
+// environment by scripts/policy_probe.py and scripts/tune_spmm.py.  The shipped
+// library instantiates only the variants the dispatcher below picks and reads
+// no environment on the launch path.
 inline int spmm_policy() {
   const char* env = std::getenv("DGLMI_SPMM_POLICY");
   return env ? std::atoi(env) : 0;
@@ -410,6 +416,7 @@ inline int spmm_variant() {
   const char* env = std::getenv("DGLMI_SPMM_VARIANT");
   return env ? std::atoi(env) : 3;
 }
+#endif
 
 template <int KIND, int RED, int L, int NV, int VW>
 void run(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
@@ -418,6 +425,7 @@ void run(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
   const unsigned blocks = static_cast<unsigned>((chunks + G - 1) / G);
   if constexpr (KIND == FAST_COPY_COL && RED == RED_SUM && NV == 1 && L >= 16 && VW == 4) {
     if (a.marked) {  // cold-row hints present (capi.cpp run_fast decides)
+#if DGLMI_PROBES
       const int pol = spmm_policy();
       if (pol > 0 && !has_epi(a) && a.num_cols * a.F * 4 <= (int64_t)UINT32_MAX) {
         switch (pol) {
@@ -436,6 +444,7 @@ void run(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
           hipLaunchKernelGGL((k_chunk_fixup<RED, L, NV>), dim3(blocks), dim3(kBlock), 0, s, a, indptr);
         return;
       }
+#endif
       if (has_epi(a))
         hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 11, true>), dim3(blocks), dim3(kBlock),
                            0, s, a, indptr);
@@ -463,6 +472,7 @@ void run(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
       return;
     }
   }
+#if DGLMI_PROBES
   if constexpr (KIND == FAST_COPY_COL && RED == RED_SUM && L == 16 && NV == 1 && VW == 4) {
     // tuning variants of the headline kernel (scripts/tune_spmm.py)
     switch (spmm_variant()) {
@@ -474,7 +484,9 @@ void run(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
       case 27: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 27>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
       default: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
     }
-  } else {
+  } else
+#endif
+  {
     hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 3, false, VW>), dim3(blocks), dim3(kBlock),
                        0, s, a, indptr);
   }

@@ -67,18 +67,27 @@ class Array(ctypes.Structure):
     ]
 
 
+def _lib_name():
+    """libdglmi.so, or with DGLMI_PROBES=1 the probe build libdglmi_probes.so
+    (`make -C dgl-hack_amd PROBES=1`: the headline kernel's cache-policy and
+    tuning variants, selected by scripts/policy_probe.py / tune_spmm.py through
+    the environment; the shipped library has none of them)."""
+    return "libdglmi_probes.so" if os.environ.get("DGLMI_PROBES") == "1" else "libdglmi.so"
+
+
 def _lib_path():
     env = os.environ.get("DGL_LIBRARY_PATH")
+    name = _lib_name()
     cands = []
     if env:
-        cands.append(os.path.join(env, "libdglmi.so"))
-    cands.append(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libdglmi.so"))
+        cands.append(os.path.join(env, name))
+    cands.append(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", name))
     for c in cands:
         if os.path.exists(c):
             return c
     raise DGLError(
-        "libdglmi.so not found (looked in %s). Build it with `make -C dgl-hack_amd` or "
-        "__graft_entry__.build(); the engine has no CPU fallback." % ", ".join(cands))
+        "%s not found (looked in %s). Build it with `make -C dgl-hack_amd` or "
+        "__graft_entry__.build(); the engine has no CPU fallback." % (name, ", ".join(cands)))
 
 
 _LIB = None
@@ -86,6 +95,7 @@ _LIB = None
 _SIGS = {
     "DGLMIGetLastError": (ctypes.c_char_p, []),
     "DGLMIVersion": (ctypes.c_char_p, []),
+    "DGLMISetSddmmOrder": (ctypes.c_int, [ctypes.c_int32]),
     "DGLMIKernelInferBinaryFeatureShape": (ctypes.c_int, [
         ctypes.c_char_p, ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32)]),

@@ -236,6 +236,16 @@ def backward_copy_reduce(reducer, graph, target, in_data, out_data, grad_out_dat
     return grad_in_data
 
 
+_SDDMM_ORDERS = {"auto": 0, "coo": 1, "csr": 2}
+
+
+def set_sddmm_order(order):
+    """Item order of the per-edge (g-SDDMM) kernels, process-wide: "auto" (the
+    library picks per call), "coo" (edge-id order) or "csr"
+    (in-CSR order) -- DGLMISetSddmmOrder; tests and probes cover both walks."""
+    check_call(_ffi.lib().DGLMISetSddmmOrder(_SDDMM_ORDERS[order]))
+
+
 def _TARGET_CODE(t):
     if isinstance(t, str):
         return _TARGET[t]

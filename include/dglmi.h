@@ -131,6 +131,17 @@ const char* DGLMIGetLastError(void);
 /* Library version string ("0.4-mi355x"). */
 const char* DGLMIVersion(void);
 
+/* Item order of the per-edge (g-SDDMM) kernels, process-wide (extension, no
+ * reference counterpart).  AUTO (the default) picks edge-id order or in-CSR
+ * order per call from the operand shapes and the graph's average degree
+ * (DESIGN.md 4.2b); COO / CSR force one, so tests cover both walks. */
+enum DGLMISddmmOrder {
+  DGLMI_SDDMM_ORDER_AUTO = 0,
+  DGLMI_SDDMM_ORDER_COO = 1,
+  DGLMI_SDDMM_ORDER_CSR = 2
+};
+int DGLMISetSddmmOrder(int32_t order);
+
 /* _CAPI_DGLKernelInferBinaryFeatureShape (binary_reduce.cc:281-293).
  * Writes the broadcast feature shape into out_shape (capacity
  * DGLMI_MAX_NDIM + 1) and its rank into *out_ndim. Host-only. */

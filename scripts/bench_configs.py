@@ -223,13 +223,12 @@ def sd(dev, steps, warmup):
              ("u_add_v_H8", "add", el, er, 8 + 2 * 32 + 32)]
     for name, op, a, b, per_edge in cases:
         for order in ("auto", "coo", "csr"):
-            if order != "auto":
-                os.environ["DGLMI_SDDMM_ORDER"] = order
+            dgl.kernel.set_sddmm_order(order)
             try:
                 ms = timeit(lambda: dgl.backend.binary_reduce("none", op, gidx, 0, 1, a, b, m),
                             steps, warmup)
             finally:
-                os.environ.pop("DGLMI_SDDMM_ORDER", None)
+                dgl.kernel.set_sddmm_order("auto")
             res["%s_%s_ms" % (name, order)] = ms
             res["%s_%s_alg_GBps" % (name, order)] = per_edge * m / ms / 1e6
     return res

@@ -14,6 +14,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "dgl-hack_amd"))
 
+# the policy / tuning variants live in the probe build (make -C dgl-hack_amd PROBES=1)
+os.environ.setdefault("DGLMI_PROBES", "1")
+
 import numpy as np  # noqa: E402
 import torch as th  # noqa: E402
 

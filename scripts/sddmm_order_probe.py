@@ -25,8 +25,8 @@ for name, op, shape in (("u_dot_v_8x8", "dot", (8, 8)), ("u_add_v_8", "add", (8,
     a = th.rand((n,) + shape, device=dev)
     b = th.rand((n,) + shape, device=dev)
     for order in ("coo", "csr"):
-        os.environ["DGLMI_SDDMM_ORDER"] = order
+        dgl.kernel.set_sddmm_order(order)
         res["%s_%s_ms" % (name, order)] = timeit(
             lambda: dgl.backend.binary_reduce("none", op, gidx, 0, 1, a, b, m), 10, 3)
-    os.environ.pop("DGLMI_SDDMM_ORDER", None)
+    dgl.kernel.set_sddmm_order("auto")
 print(json.dumps(res))

@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--feats", default="64")
     ap.add_argument("--variants", default="0")
     args = ap.parse_args()
+    if args.mode != "single":
+        # chunk sizes and variants are picked in the probe build (make -C dgl-hack_amd PROBES=1)
+        os.environ.setdefault("DGLMI_PROBES", "1")
     dev = "cuda:0"
     th.cuda.set_device(0)
     from dgl import kernel as K

@@ -107,14 +107,14 @@ def test_sddmm(sk, lhs, rhs, op, shape):
     r_out, r_gl, r_gr = O.binary_reduce("none", op, ref, CODE[lhs], CODE[rhs], lv, rv, m,
                                         grad_out=go.reshape((m,) + (oshape or ())))
     for order in ("coo", "csr"):
-        os.environ["DGLMI_SDDMM_ORDER"] = order
+        dgl.kernel.set_sddmm_order(order)
         try:
             lt = th.from_numpy(lv).to(DEV).requires_grad_()
             rt = th.from_numpy(rv).to(DEV).requires_grad_()
             out = dgl.backend.binary_reduce("none", op, gidx, CODE[lhs], CODE[rhs], lt, rt, m)
             out.backward(th.from_numpy(go).to(DEV).reshape(out.shape))
         finally:
-            os.environ.pop("DGLMI_SDDMM_ORDER", None)
+            dgl.kernel.set_sddmm_order("auto")
         tag = "%s_%s_%s %s %s" % (lhs, op, rhs, shape, order)
         np.testing.assert_allclose(out.detach().cpu().numpy().reshape(r_out.shape), r_out,
                                    rtol=1e-4, atol=1e-4, err_msg=tag)
