@@ -744,6 +744,19 @@ int gat_blocks(const DGLMIGraph* g) {
   return nb;
 }
 
+// Chunk size of the backward walks: one halving beyond the forward's rule
+// (gat_chunk_edges) while a launch would have fewer than 2 x 16 K groups.  On C3's
+// column blocks (~14 M edges per launch) K = 512 leaves ~7000 waves per launch, and
+// the two backward walks wait on memory ~60 % of their wave cycles (SQ_WAIT_ANY /
+// SQ_WAVE_CYCLES, profiles/r03_gat_pmc_blocked.json); K = 256 hides more of it:
+// backward 8.92 -> 8.45 ms, while the forward stays best at 512
+// (profiles/r03_tune_gat_chunk.json).  Unblocked C3 (114 M edges) keeps 512.
+int64_t gat_bwd_chunk_edges(int64_t nnz) {
+  int64_t k = gat_chunk_edges(nnz);
+  if (k > 8 && nnz / k < 2 * 256 * 64) k >>= 1;
+  return k;
+}
+
 GatArgs gat_args(const DGLMIGraph* g, const DGLMIArray* ft, const DGLMIArray* el,
                  const DGLMIArray* er, float slope, DGLMIArray* out, DGLMIArray* mx,
                  DGLMIArray* sm) {
@@ -1002,6 +1015,7 @@ int DGLMIFusedGatBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src, c
   GatArgs a = gat_args(graph, feat_src, el, er, negative_slope, const_cast<DGLMIArray*>(out),
                        const_cast<DGLMIArray*>(max_in), const_cast<DGLMIArray*>(sum_in));
   hipStream_t s = static_cast<hipStream_t>(stream);
+  a.chunk = gat_bwd_chunk_edges(std::max<int64_t>(graph->in_csr.nnz, 1));
   check_array(grad_out, "grad_out");
   check_array(grad_feat_src, "grad_feat_src");
   check_array(grad_el, "grad_el");
@@ -1032,7 +1046,7 @@ int DGLMIFusedGatBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src, c
   int64_t chunks = (in.nnz + a.chunk - 1) / a.chunk;
   for (int b = 0; b < nb && nb > 1; ++b)
     for (const DGLMICsr* c : {&graph->in_col_blocks[b], &graph->out_col_blocks[b]}) {
-      const int64_t k = gat_chunk_edges(std::max<int64_t>(c->nnz, 1));
+      const int64_t k = gat_bwd_chunk_edges(std::max<int64_t>(c->nnz, 1));
       chunks = std::max(chunks, (c->nnz + k - 1) / k);
     }
   const int64_t stats_bytes = a.num_rows * a.H * 16;
@@ -1051,7 +1065,7 @@ int DGLMIFusedGatBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src, c
       g.indices = c.indices;
       g.nnz = c.nnz;
       g.num_rows = c.num_rows;
-      g.chunk = gat_chunk_edges(std::max<int64_t>(c.nnz, 1));
+      g.chunk = gat_bwd_chunk_edges(std::max<int64_t>(c.nnz, 1));
     };
     for (int b = 0; b < nb; ++b) {
       GatArgs ab = a;
@@ -1081,6 +1095,95 @@ int DGLMIFusedGatBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src, c
   b.num_rows = outc.num_rows;
   launch_gat_backward_src(b, s);
   check_hip(hipGetLastError(), "fused GAT backward (src) launch");
+  API_END();
+}
+
+// The reference's argument order (_CAPI_DGLFusedGatKernel /
+// _CAPI_DGLKernelBackwardFusedGat, binary_reduce.cc:380-396, 529-549) over the
+// kernels above.  The caller owns `sum` (N, H[, 1]) and `exp` (E, H[, 1]) and
+// hands both from the forward to the backward untouched (tensor.py:383-420); what
+// they hold is this library's softmax state, not the hack's per-edge exponentials:
+// when exp has room for N_dst * H floats it keeps the running max and sum the
+// sum of exp(s - max); otherwise sum keeps max + log(sum) and exp is unused.
+namespace {
+bool gat_exp_holds_max(const DGLMIGraph* g, const DGLMIArray* feat_src, const DGLMIArray* sum,
+                       const DGLMIArray* exp) {
+  check_array(sum, "sum");
+  check_array(exp, "exp");
+  DGLMI_CHECK(feat_src != nullptr && feat_src->ndim == 3, "feat_src must be (N, H, D)");
+  const int64_t H = feat_src->shape[1];
+  DGLMI_CHECK(exp->shape[0] == g->in_csr.nnz && feat_numel(exp) == H, "exp must be (E, H[, 1])");
+  DGLMI_CHECK(sum->shape[0] == g->in_csr.num_rows && feat_numel(sum) == H, "sum must be (N_dst, H[, 1])");
+  return g->in_csr.nnz >= g->in_csr.num_rows;
+}
+DGLMIArray gat_state_view(float* data, int64_t rows, int64_t H) {
+  DGLMIArray v;
+  std::memset(&v, 0, sizeof(v));
+  v.data = data;
+  v.ndim = 2;
+  v.shape[0] = rows;
+  v.shape[1] = H;
+  return v;
+}
+}  // namespace
+
+int DGLMIFusedGatKernel(const DGLMIGraph* graph, const DGLMIArray* feat_src, const DGLMIArray* el,
+                        const DGLMIArray* er, DGLMIArray* sum, DGLMIArray* exp, DGLMIArray* ret,
+                        float slope, void* stream) {
+  API_BEGIN();
+  check_graph(graph);
+  DeviceGuard guard(graph->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t N = graph->in_csr.num_rows, H = feat_src ? feat_src->shape[1] : 0;
+  DGLMIArray l = gat_state_view(sum->data, N, H);
+  if (gat_exp_holds_max(graph, feat_src, sum, exp)) {
+    DGLMIArray m = gat_state_view(exp->data, N, H);
+    if (DGLMIFusedGatForward(graph, feat_src, el, er, slope, ret, &m, &l, stream) != 0)
+      throw Error(g_last_error);
+  } else {
+    DGLMIGraph no_ws = *graph;  // the max must not alias the kernels' workspace
+    no_ws.workspace = nullptr;
+    no_ws.workspace_bytes = 0;
+    Scratch mx(&no_ws, N * H * static_cast<int64_t>(sizeof(float)), s);
+    DGLMIArray m = gat_state_view(static_cast<float*>(mx.ptr), N, H);
+    if (DGLMIFusedGatForward(graph, feat_src, el, er, slope, ret, &m, &l, stream) != 0)
+      throw Error(g_last_error);
+    launch_gat_fold_lse(m.data, l.data, N * H, s);
+    check_hip(hipGetLastError(), "fused GAT log-sum-exp");
+  }
+  API_END();
+}
+
+int DGLMIKernelBackwardFusedGat(const DGLMIGraph* graph, const DGLMIArray* feat_src,
+                                const DGLMIArray* el, const DGLMIArray* er, const DGLMIArray* sum,
+                                const DGLMIArray* exp, const DGLMIArray* ret,
+                                const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
+                                DGLMIArray* grad_el, DGLMIArray* grad_er, float slope,
+                                void* stream) {
+  API_BEGIN();
+  check_graph(graph);
+  DeviceGuard guard(graph->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t N = graph->in_csr.num_rows, H = feat_src ? feat_src->shape[1] : 0;
+  if (gat_exp_holds_max(graph, feat_src, sum, exp)) {
+    const DGLMIArray m = gat_state_view(exp->data, N, H);
+    const DGLMIArray l = gat_state_view(sum->data, N, H);
+    if (DGLMIFusedGatBackward(graph, feat_src, el, er, slope, ret, &m, &l, grad_out, grad_feat_src,
+                              grad_el, grad_er, stream) != 0)
+      throw Error(g_last_error);
+  } else {
+    // sum holds max + log(sum): attention = exp(s - lse) / 1
+    DGLMIGraph no_ws = *graph;
+    no_ws.workspace = nullptr;
+    no_ws.workspace_bytes = 0;
+    Scratch ones(&no_ws, N * H * static_cast<int64_t>(sizeof(float)), s);
+    launch_fill(static_cast<float*>(ones.ptr), N * H, 1.0f, s);
+    const DGLMIArray m = gat_state_view(sum->data, N, H);
+    const DGLMIArray l = gat_state_view(static_cast<float*>(ones.ptr), N, H);
+    if (DGLMIFusedGatBackward(graph, feat_src, el, er, slope, ret, &m, &l, grad_out, grad_feat_src,
+                              grad_el, grad_er, stream) != 0)
+      throw Error(g_last_error);
+  }
   API_END();
 }
 
@@ -1278,6 +1381,42 @@ void check_fast_width(int64_t F) {
               "unsupported feature width " + std::to_string(F));
 }
 
+// The prepared state an entry may use (dglmi.h DGLMIRgcnState): built from these
+// etypes, for this relation count and source count, with the layer's bit set.
+const DGLMIRgcnState* rgcn_state(const DGLMIGraph* g, const int32_t* etypes, int64_t R,
+                                 int64_t n_src, int layer) {
+  const DGLMIRgcnState* st = g->rgcn;
+  if (st == nullptr || st->etypes != etypes || st->num_rels != R || st->num_src != n_src ||
+      st->nnz != g->in_csr.nnz || !((st->layers >> layer) & 1))
+    return nullptr;
+  return st;
+}
+
+// A walk of the prepared in-CSR (relation-expanded columns of `layer`), with the
+// cached norm streamed in position order when it was built from this norm.
+DGLMICsr rgcn_in_walk(const DGLMIGraph* g, const DGLMIRgcnState* st, int layer, int64_t num_cols,
+                      const float* norm, const float** w) {
+  DGLMICsr walk = g->in_csr;
+  walk.indices = st->in_cols[layer];
+  walk.num_cols = num_cols;
+  *w = norm;
+  if (st->norm != nullptr && st->norm == norm && st->in_norm != nullptr) {
+    walk.data = st->positions;
+    *w = st->in_norm;
+  }
+  return walk;
+}
+
+DGLMICsr rgcn_out_walk(const DGLMIRgcnState* st, int layer, const float* norm, const float** w) {
+  DGLMICsr walk = st->out_typed[layer];
+  *w = norm;
+  if (st->norm != nullptr && st->norm == norm && st->out_norm[layer] != nullptr) {
+    walk.data = st->positions;
+    *w = st->out_norm[layer];
+  }
+  return walk;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1298,6 +1437,13 @@ int DGLMIRgcnLayer0(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIA
   DeviceGuard guard(graph->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   DGLMIGraph z = no_workspace(), pg = plain_graph(graph);
+  if (const DGLMIRgcnState* st = rgcn_state(graph, etypes, R, N, 0)) {
+    const float* w = nullptr;
+    const DGLMICsr walk = rgcn_in_walk(graph, st, 0, R * N, norm->data, &w);
+    run_fast(&pg, walk, FAST_COL_MUL_EDGE_BCAST, RED_SUM, weight->data, nullptr, w, nullptr,
+             ret->data, F, F, s);
+    return 0;
+  }
   Scratch cols(&z, in.nnz * 4, s);
   launch_typed_ids(in.indices, in.data, etypes, in.nnz, N, 0, static_cast<int32_t*>(cols.ptr), s);
   DGLMICsr walk = in;
@@ -1330,6 +1476,13 @@ int DGLMIRgcnLayer0Backward(const DGLMIGraph* graph, const int32_t* etypes,
     launch_fill(grad_weight->data, R * N * F, 0.0f, s);
     return 0;
   }
+  if (const DGLMIRgcnState* st = rgcn_state(graph, etypes, R, N, 0)) {
+    const float* w = nullptr;
+    const DGLMICsr walk = rgcn_out_walk(st, 0, norm->data, &w);
+    run_fast(&pg, walk, FAST_COL_MUL_EDGE_BCAST, RED_SUM, grad_out->data, nullptr, w, nullptr,
+             grad_weight->data, F, F, s);
+    return 0;
+  }
   TypedOutCsr typed(out, etypes, R * N, N, 0, s);
   run_fast(&pg, typed.csr, FAST_COL_MUL_EDGE_BCAST, RED_SUM, grad_out->data, nullptr, norm->data,
            nullptr, grad_weight->data, F, F, s);
@@ -1356,17 +1509,23 @@ int DGLMIRgcnLayer1(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIA
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t N = in.num_cols, M = R * X;
   DGLMIGraph z = no_workspace(), pg = plain_graph(graph);
-  Scratch wcat(&z, K * M * 4, s), y(&z, N * M * 4, s), cols(&z, in.nnz * 4, s);
+  const DGLMIRgcnState* st = rgcn_state(graph, etypes, R, N, 1);
+  Scratch wcat(&z, K * M * 4, s), y(&z, N * M * 4, s), cols(&z, st ? 0 : in.nnz * 4, s);
   launch_permute_rkx(weight->data, R, K, X, true, static_cast<float*>(wcat.ptr), s);
   // y[u, r * X + x] = sum_k hidden[u, k] w[r, k, x]; row u * R + r of the (N R, X) view
   launch_gemm(hidden->data, K, 1, static_cast<float*>(wcat.ptr), M, 1, static_cast<float*>(y.ptr), N,
               M, K, 1, nullptr, s);
-  launch_typed_ids(in.indices, in.data, etypes, in.nnz, R, 1, static_cast<int32_t*>(cols.ptr), s);
+  const float* w = norm->data;
   DGLMICsr walk = in;
-  walk.indices = static_cast<int32_t*>(cols.ptr);
-  walk.num_cols = N * R;
-  run_fast(&pg, walk, FAST_COL_MUL_EDGE_BCAST, RED_SUM, static_cast<float*>(y.ptr), nullptr,
-           norm->data, nullptr, ret->data, X, X, s);
+  if (st) {
+    walk = rgcn_in_walk(graph, st, 1, N * R, norm->data, &w);
+  } else {
+    launch_typed_ids(in.indices, in.data, etypes, in.nnz, R, 1, static_cast<int32_t*>(cols.ptr), s);
+    walk.indices = static_cast<int32_t*>(cols.ptr);
+    walk.num_cols = N * R;
+  }
+  run_fast(&pg, walk, FAST_COL_MUL_EDGE_BCAST, RED_SUM, static_cast<float*>(y.ptr), nullptr, w,
+           nullptr, ret->data, X, X, s);
   API_END();
 }
 
@@ -1400,7 +1559,12 @@ int DGLMIRgcnLayer1Backward(const DGLMIGraph* graph, const int32_t* etypes,
       parts(&z, splits > 1 ? splits * K * M * 4 : 0, s);
   launch_permute_rkx(weight->data, R, K, X, true, static_cast<float*>(wcat.ptr), s);
   // gy[u * R + t] = sum over out-edges of u with type t of norm_e * grad_out[v]
-  if (out.nnz > 0) {
+  if (const DGLMIRgcnState* st = out.nnz > 0 ? rgcn_state(graph, etypes, R, N, 1) : nullptr) {
+    const float* w = nullptr;
+    const DGLMICsr walk = rgcn_out_walk(st, 1, norm->data, &w);
+    run_fast(&pg, walk, FAST_COL_MUL_EDGE_BCAST, RED_SUM, grad_out->data, nullptr, w, nullptr,
+             static_cast<float*>(gy.ptr), X, X, s);
+  } else if (out.nnz > 0) {
     TypedOutCsr typed(out, etypes, N * R, R, 1, s);
     run_fast(&pg, typed.csr, FAST_COL_MUL_EDGE_BCAST, RED_SUM, grad_out->data, nullptr, norm->data,
              nullptr, static_cast<float*>(gy.ptr), X, X, s);
@@ -1414,6 +1578,95 @@ int DGLMIRgcnLayer1Backward(const DGLMIGraph* graph, const int32_t* etypes,
               M, N, splits, static_cast<float*>(parts.ptr), s);
   launch_permute_rkx(static_cast<float*>(gw.ptr), R, K, X, false, grad_weight->data, s);
   check_hip(hipGetLastError(), "rgcn layer1 backward launch");
+  API_END();
+}
+
+int DGLMIRgcnPrepare(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* norm,
+                     int32_t num_rels, int32_t layers, DGLMIRgcnState* state, void* stream) {
+  API_BEGIN();
+  DGLMI_CHECK(state != nullptr, "null state");
+  std::memset(state, 0, sizeof(*state));
+  DGLMI_CHECK(num_rels >= 1, "num_rels must be >= 1");
+  DGLMI_CHECK(layers >= 1 && layers <= 3, "layers must be 1 (layer 0), 2 (layer 1) or 3 (both)");
+  check_graph(graph);
+  const DGLMICsr& in = graph->in_csr;
+  const DGLMICsr& out = graph->out_csr;
+  const int64_t R = num_rels, N = in.num_cols, E = in.nnz;
+  rgcn_common(graph, etypes, R * N);
+  DGLMI_CHECK(out.num_rows == N, "out_csr rows != in_csr columns");
+  if (norm != nullptr) edge_values(norm, E, "norm");
+  DeviceGuard guard(graph->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // one allocation, carved into 256-byte aligned arrays
+  auto al = [](int64_t bytes) { return (bytes + 255) & ~int64_t(255); };
+  const int64_t e4 = al(E * 4), ptr4 = al((R * N + 1) * 4);
+  const int nl = (layers & 1) + ((layers >> 1) & 1);
+  const int64_t per_layer = e4 /*in cols*/ + ptr4 + 3 * e4 /*out idx, data, rows*/ +
+                            (norm ? e4 : 0) /*out norm*/;
+  const int64_t total = e4 /*positions*/ + (norm ? e4 : 0) /*in norm*/ + nl * per_layer;
+  struct Owner {
+    void* p = nullptr;
+    ~Owner() { if (p) (void)hipFree(p); }
+  } own;
+  check_hip(hipMalloc(&own.p, static_cast<size_t>(std::max<int64_t>(total, 256))), "hipMalloc");
+  char* cur = static_cast<char*>(own.p);
+  auto take = [&](int64_t bytes) { char* r = cur; cur += bytes; return r; };
+  int32_t* positions = reinterpret_cast<int32_t*>(take(e4));
+  float* in_norm = norm ? reinterpret_cast<float*>(take(e4)) : nullptr;
+  launch_iota_i32(positions, E, s);
+  if (norm) launch_gather_f32(norm->data, in.data, E, in_norm, s);
+  DGLMIGraph z = no_workspace();
+  for (int layer = 0; layer < 2; ++layer) {
+    if (!((layers >> layer) & 1)) continue;
+    const int64_t mul = layer == 0 ? N : R;
+    int32_t* cols = reinterpret_cast<int32_t*>(take(e4));
+    int32_t* ptr = reinterpret_cast<int32_t*>(take(ptr4));
+    int32_t* idx = reinterpret_cast<int32_t*>(take(e4));
+    int32_t* dat = reinterpret_cast<int32_t*>(take(e4));
+    int32_t* rows = reinterpret_cast<int32_t*>(take(e4));
+    float* onorm = norm ? reinterpret_cast<float*>(take(e4)) : nullptr;
+    launch_typed_ids(in.indices, in.data, etypes, E, mul, layer, cols, s);
+    // the out-CSR regrouped by the same key, stable (TypedOutCsr, kept)
+    const int64_t ws_bytes = DGLMICOOToCSRDeviceWorkspaceBytes(R * N, E);
+    Scratch keys(&z, E * 4, s), ws(&z, ws_bytes, s);
+    launch_typed_ids(out.rows, out.data, etypes, E, mul, layer, static_cast<int32_t*>(keys.ptr), s);
+    DGLMI_CHECK(DGLMICOOToCSRDevice(R * N, E, static_cast<int32_t*>(keys.ptr), out.indices, out.data,
+                                    ptr, idx, dat, ws.ptr, ws_bytes, s) == 0,
+                std::string("typed CSR build: ") + g_last_error);
+    DGLMI_CHECK(DGLMICSRExpandRows(ptr, R * N, E, rows, s) == 0,
+                std::string("typed CSR rows: ") + g_last_error);
+    if (norm) launch_gather_f32(norm->data, dat, E, onorm, s);
+    state->in_cols[layer] = cols;
+    DGLMICsr& c = state->out_typed[layer];
+    c.num_rows = R * N;
+    c.num_cols = out.num_cols;
+    c.nnz = E;
+    c.indptr = ptr;
+    c.indices = idx;
+    c.data = dat;
+    c.rows = rows;
+    state->out_norm[layer] = onorm;
+  }
+  check_hip(hipGetLastError(), "rgcn prepare launch");
+  state->etypes = etypes;
+  state->norm = norm ? norm->data : nullptr;
+  state->num_rels = num_rels;
+  state->layers = layers;
+  state->num_src = N;
+  state->nnz = E;
+  state->positions = positions;
+  state->in_norm = in_norm;
+  state->owner = own.p;
+  own.p = nullptr;  // the state owns it now
+  API_END();
+}
+
+int DGLMIRgcnRelease(DGLMIRgcnState* state) {
+  API_BEGIN();
+  if (state != nullptr) {
+    if (state->owner != nullptr) check_hip(hipFree(state->owner), "hipFree");
+    std::memset(state, 0, sizeof(*state));
+  }
   API_END();
 }
 
@@ -1435,22 +1688,27 @@ int DGLMINbAccess(const DGLMIGraph* graph, const DGLMIArray* feat, const int32_t
   hipStream_t s = static_cast<hipStream_t>(stream);
   DGLMIGraph z = no_workspace();
   Scratch sink(&z, in.num_rows * F * 4, s);
-  hipEvent_t a, b;
-  check_hip(hipEventCreate(&a), "hipEventCreate");
-  check_hip(hipEventCreate(&b), "hipEventCreate");
+  // destroyed on every path, a throwing check or launch included
+  struct Events {
+    hipEvent_t a = nullptr, b = nullptr;
+    ~Events() {
+      if (a) (void)hipEventDestroy(a);
+      if (b) (void)hipEventDestroy(b);
+    }
+  } ev;
+  check_hip(hipEventCreate(&ev.a), "hipEventCreate");
+  check_hip(hipEventCreate(&ev.b), "hipEventCreate");
   double total = 0.0;
   for (int i = 0; i < times; ++i) {
-    check_hip(hipEventRecord(a, s), "hipEventRecord");
+    check_hip(hipEventRecord(ev.a, s), "hipEventRecord");
     run_fast(graph, in, FAST_COPY_COL, RED_SUM, feat->data, nullptr, nullptr, nullptr,
              static_cast<float*>(sink.ptr), F, 1, s);
-    check_hip(hipEventRecord(b, s), "hipEventRecord");
-    check_hip(hipEventSynchronize(b), "hipEventSynchronize");
+    check_hip(hipEventRecord(ev.b, s), "hipEventRecord");
+    check_hip(hipEventSynchronize(ev.b), "hipEventSynchronize");
     float ms = 0.0f;
-    check_hip(hipEventElapsedTime(&ms, a, b), "hipEventElapsedTime");
+    check_hip(hipEventElapsedTime(&ms, ev.a, ev.b), "hipEventElapsedTime");
     if (i >= warm_up_times) total += ms * 1e3;
   }
-  (void)hipEventDestroy(a);
-  (void)hipEventDestroy(b);
   if (avg_us) *avg_us = total / (times - warm_up_times);
   API_END();
 }

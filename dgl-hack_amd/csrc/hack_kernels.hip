@@ -103,6 +103,210 @@ __global__ void __launch_bounds__(kBlock) k_gemm(const float* __restrict__ A, in
   }
 }
 
+// ---------------------------------------------------------------------------
+// Tall-skinny products of the R-GCN entries: one dimension is the node count (10^6 -
+// 10^7 rows), the other two are <= 256.  k_gemm above moves the same bytes 2-5x slower
+// on these shapes (C5, 5 M x 64 -> 256: 4.0 ms, 256 -> 64: 3.7 ms, the 5 M-row
+// reduction 6.95 ms; scripts/rgcn_capi_probe.py under rocprofv3), so each shape gets
+// its own kernel (v_mfma_f32_32x32x2_f32, exact f32 like k_gemm):
+//  * k_gemm_rows: C (M x N) = A (M x K) . B (K x N), A and C row-major.  All of B sits
+//    in LDS for the block's life; each of the 8 waves owns 32-row tiles of C (strided
+//    over the grid), stages its A tile through a private LDS slice 32 columns at a time
+//    (the next slice is loaded into registers while the MFMAs run on this one, so the
+//    waves need no block barrier) and writes C once, non-temporally.
+//  * k_gemm_tn: C (M x N) = A^T . B, A (R x M) and B (R x N) row-major, R = the node
+//    count: every block reduces a contiguous range of rows into its own M x N partial
+//    (32-row slices of A and B staged through two LDS buffers), k_sum_splits adds the
+//    partials in block order (deterministic).
+constexpr int kGemmThreads = 512;  // 8 waves, one block per CU (LDS)
+constexpr int kSlice = 32;
+// LDS row stride (floats) for rows of `cols` floats read as MFMA operands: lanes r and
+// r + 32 read rows kk and kk + 1, so a stride == 32 (mod 64) puts them in different
+// bank halves
+__host__ __device__ constexpr int mfma_lds_stride(int cols) {
+  return (cols % 64 == 0) ? cols + 32 : cols;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// NB = N / 32 (rounded up), KP = K rounded up to kSlice; needs K % 4 == 0, lda % 4 == 0
+// and a 16-byte aligned A (the host checks).
+template <int NB, int KP>
+__global__ void __launch_bounds__(kGemmThreads) k_gemm_rows(const float* __restrict__ A,
+                                                        int64_t lda, const float* __restrict__ B,
+                                                        int64_t b_rs, int64_t b_cs,
+                                                        float* __restrict__ C, int64_t M, int N,
+                                                        int K) {
+  constexpr int SB = mfma_lds_stride(NB * 32);
+  constexpr int SA = kSlice + 1;
+  constexpr int NSL = KP / kSlice;
+  __shared__ float Bs[KP * SB];
+  __shared__ float As[8][32 * SA];
+  for (int i = threadIdx.x; i < KP * NB * 32; i += kGemmThreads) {
+    const int k = i / (NB * 32), n = i % (NB * 32);
+    Bs[k * SB + n] = (k < K && n < N) ? B[k * b_rs + n * b_cs] : 0.0f;
+  }
+  __syncthreads();  // the only block barrier: the waves run independently after it
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  float* as = As[w];
+  const int64_t tiles = (M + 31) / 32;
+  const int64_t step = static_cast<int64_t>(gridDim.x) * 8;
+  int64_t tile = static_cast<int64_t>(blockIdx.x) * 8 + w;
+  if (tile >= tiles) return;
+  // staging map: lane -> rows (lane >> 3) + 8 j of the tile, float4 column lane & 7
+  const int srow = lane >> 3, sc4 = lane & 7;
+  float4 v[4];
+  auto load = [&](int64_t t, int sl) {
+    const int k = sl * kSlice + 4 * sc4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t m = t * 32 + srow + 8 * j;
+      v[j] = (m < M && k < K) ? *reinterpret_cast<const float4*>(A + m * lda + k)
+                              : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+  };
+  load(tile, 0);
+  while (true) {
+    f32x16 acc[NB];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x16{};
+#pragma unroll
+    for (int sl = 0; sl < NSL; ++sl) {
+      wave_lds_sync();  // every lane is done reading the previous slice
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float* d = as + (srow + 8 * j) * SA + 4 * sc4;
+        d[0] = v[j].x;
+        d[1] = v[j].y;
+        d[2] = v[j].z;
+        d[3] = v[j].w;
+      }
+      wave_lds_sync();
+      // the next slice (or the next tile's first) is in flight during the MFMAs
+      if (sl + 1 < NSL) load(tile, sl + 1);
+      else if (tile + step < tiles) load(tile + step, 0);
+#pragma unroll
+      for (int kk = 0; kk < kSlice; kk += 2) {
+        const float a = as[r * SA + kk + h];
+        const float* brow = Bs + (sl * kSlice + kk + h) * SB + r;
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+          acc[nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, brow[nb * 32], acc[nb], 0, 0, 0);
+      }
+    }
+    // C/D map: col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int64_t m = tile * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (m >= M) continue;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const int n = nb * 32 + r;
+        if (n < N) __builtin_nontemporal_store(acc[nb][reg], C + m * N + n);
+      }
+    }
+    tile += step;
+    if (tile >= tiles) break;
+  }
+}
+
+// C partial of block z (M x N) = sum over rows q in [z * rows_per_block, ...) of
+// A[q, m] * B[q, n].  MB = M / 32, NB = N / 32 (rounded up), MB * NB <= 16: wave w owns
+// the (m, n) 32 x 32 blocks w and w + 8.  Needs M, N, lda, ldb % 4 == 0 and 16-byte
+// aligned A, B.
+template <int MB, int NB>
+__global__ void __launch_bounds__(kGemmThreads) k_gemm_tn(const float* __restrict__ A, int64_t lda,
+                                                      const float* __restrict__ B, int64_t ldb,
+                                                      float* __restrict__ parts, int64_t R, int M,
+                                                      int N, int64_t rows_per_block) {
+  constexpr int SA = mfma_lds_stride(MB * 32), SB = mfma_lds_stride(NB * 32);
+  constexpr int A4 = MB * 8, B4 = NB * 8;                  // float4 per staged row
+  constexpr int AL = (kSlice * A4 + kGemmThreads - 1) / kGemmThreads;
+  constexpr int BL = (kSlice * B4 + kGemmThreads - 1) / kGemmThreads;
+  static_assert(MB * NB <= 16, "at most two 32 x 32 blocks per wave");
+  __shared__ float As[2][kSlice * SA];
+  __shared__ float Bs[2][kSlice * SB];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = r0 + rows_per_block < R ? r0 + rows_per_block : R;
+  const int nsl = r1 > r0 ? static_cast<int>((r1 - r0 + kSlice - 1) / kSlice) : 0;
+  float4 va[AL], vb[BL];
+  auto load = [&](int sl) {
+#pragma unroll
+    for (int j = 0; j < AL; ++j) {
+      const int idx = threadIdx.x + j * kGemmThreads;
+      const int row = idx / A4, c = 4 * (idx % A4);
+      const int64_t q = r0 + static_cast<int64_t>(sl) * kSlice + row;
+      va[j] = (idx < kSlice * A4 && q < r1 && c < M)
+                  ? *reinterpret_cast<const float4*>(A + q * lda + c)
+                  : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+#pragma unroll
+    for (int j = 0; j < BL; ++j) {
+      const int idx = threadIdx.x + j * kGemmThreads;
+      const int row = idx / B4, c = 4 * (idx % B4);
+      const int64_t q = r0 + static_cast<int64_t>(sl) * kSlice + row;
+      vb[j] = (idx < kSlice * B4 && q < r1 && c < N)
+                  ? *reinterpret_cast<const float4*>(B + q * ldb + c)
+                  : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < AL; ++j) {
+      const int idx = threadIdx.x + j * kGemmThreads;
+      if (idx < kSlice * A4)
+        *reinterpret_cast<float4*>(&As[buf][(idx / A4) * SA + 4 * (idx % A4)]) = va[j];
+    }
+#pragma unroll
+    for (int j = 0; j < BL; ++j) {
+      const int idx = threadIdx.x + j * kGemmThreads;
+      if (idx < kSlice * B4)
+        *reinterpret_cast<float4*>(&Bs[buf][(idx / B4) * SB + 4 * (idx % B4)]) = vb[j];
+    }
+  };
+  const int b0 = w, b1 = w + 8;
+  const bool has0 = b0 < MB * NB, has1 = b1 < MB * NB;
+  const int mb0 = b0 / NB, nb0 = b0 % NB, mb1 = b1 / NB, nb1 = b1 % NB;
+  f32x16 acc0 = {}, acc1 = {};
+  if (nsl > 0) load(0);
+  for (int sl = 0; sl < nsl; ++sl) {
+    store(sl & 1);
+    __syncthreads();
+    if (sl + 1 < nsl) load(sl + 1);
+    const float* as = As[sl & 1];
+    const float* bs = Bs[sl & 1];
+#pragma unroll
+    for (int kk = 0; kk < kSlice; kk += 2) {
+      if (has0)
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(as[(kk + h) * SA + mb0 * 32 + r],
+                                                    bs[(kk + h) * SB + nb0 * 32 + r], acc0, 0, 0, 0);
+      if (has1)
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(as[(kk + h) * SA + mb1 * 32 + r],
+                                                    bs[(kk + h) * SB + nb1 * 32 + r], acc1, 0, 0, 0);
+    }
+  }
+  float* P = parts + static_cast<int64_t>(blockIdx.x) * M * N;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+    if (has0) {
+      const int m = mb0 * 32 + row, n = nb0 * 32 + r;
+      if (m < M && n < N) P[m * N + n] = acc0[reg];
+    }
+    if (has1) {
+      const int m = mb1 * 32 + row, n = nb1 * 32 + r;
+      if (m < M && n < N) P[m * N + n] = acc1[reg];
+    }
+  }
+}
+
 // out[i] = sum over z (in order) of parts[z * n + i]
 __global__ void k_sum_splits(const float* __restrict__ parts, int splits, int64_t n,
                              float* __restrict__ out) {
@@ -119,7 +323,31 @@ unsigned grid1(int64_t n) {
   return static_cast<unsigned>(b < 1 ? 1 : (b > 65536 ? 65536 : b));
 }
 
+// out[p] = v[idx[p]] (a per-edge operand permuted into a walk's position order),
+// and out[p] = p
+__global__ void k_gather_f32(const float* __restrict__ v, const int32_t* __restrict__ idx, int64_t n,
+                             float* __restrict__ out) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t p = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; p < n; p += stride)
+    out[p] = v[idx[p]];
+}
+__global__ void k_iota_i32(int32_t* __restrict__ out, int64_t n) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t p = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; p < n; p += stride)
+    out[p] = static_cast<int32_t>(p);
+}
+
 }  // namespace
+
+void launch_gather_f32(const float* v, const int32_t* idx, int64_t n, float* out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_gather_f32, dim3(grid1(n)), dim3(kBlock), 0, s, v, idx, n, out);
+}
+
+void launch_iota_i32(int32_t* out, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_iota_i32, dim3(grid1(n)), dim3(kBlock), 0, s, out, n);
+}
 
 void launch_typed_ids(const int32_t* ids, const int32_t* eids, const int32_t* etypes, int64_t nnz,
                       int64_t mul, int mode, int32_t* out, hipStream_t s) {
@@ -143,6 +371,61 @@ int64_t gemm_splits(int64_t M, int64_t N, int64_t K) {
   return splits;
 }
 
+namespace {
+
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+template <int NB, int KP>
+void launch_rows(const float* A, int64_t lda, const float* B, int64_t b_rs, int64_t b_cs, float* C,
+                 int64_t M, int64_t N, int64_t K, hipStream_t s) {
+  const int64_t tiles = (M + 31) / 32;
+  const int64_t want = (tiles + 7) / 8;
+  const unsigned blocks = static_cast<unsigned>(want < 256 ? want : 256);  // one per CU
+  hipLaunchKernelGGL((k_gemm_rows<NB, KP>), dim3(blocks), dim3(kGemmThreads), 0, s, A, lda, B, b_rs,
+                     b_cs, C, M, static_cast<int>(N), static_cast<int>(K));
+}
+
+// k_gemm_rows when A is row-major with float4-loadable rows and B fits the LDS of one
+// of the instances; false = not taken
+bool try_rows(const float* A, int64_t a_rs, int64_t a_cs, const float* B, int64_t b_rs,
+              int64_t b_cs, float* C, int64_t M, int64_t N, int64_t K, hipStream_t s) {
+  if (a_cs != 1 || a_rs % 4 != 0 || K % 4 != 0 || !al16(A) || M < 4096) return false;
+  if (N <= 256 && K <= 64) launch_rows<8, 64>(A, a_rs, B, b_rs, b_cs, C, M, N, K, s);
+  else if (N <= 128 && K <= 128) launch_rows<4, 128>(A, a_rs, B, b_rs, b_cs, C, M, N, K, s);
+  else if (N <= 64 && K <= 256) launch_rows<2, 256>(A, a_rs, B, b_rs, b_cs, C, M, N, K, s);
+  else return false;
+  return true;
+}
+
+template <int MB, int NB>
+void launch_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t M,
+               int64_t N, int64_t R, int64_t max_blocks, float* partials, hipStream_t s) {
+  int64_t nb = max_blocks < 512 ? max_blocks : 512;
+  int64_t rpb = ((R + nb - 1) / nb + kSlice - 1) / kSlice * kSlice;
+  nb = (R + rpb - 1) / rpb;
+  hipLaunchKernelGGL((k_gemm_tn<MB, NB>), dim3(static_cast<unsigned>(nb)), dim3(kGemmThreads), 0, s,
+                     A, lda, B, ldb, partials, R, static_cast<int>(M), static_cast<int>(N), rpb);
+  hipLaunchKernelGGL(k_sum_splits, dim3(grid1(M * N)), dim3(kBlock), 0, s, partials,
+                     static_cast<int>(nb), M * N, C);
+}
+
+// k_gemm_tn for C = A^T B with A (K x M) and B (K x N) row-major (a_rs == 1, b_cs == 1),
+// K the long dimension, through the caller's `splits` partial buffers
+bool try_tn(const float* A, int64_t a_rs, int64_t a_cs, const float* B, int64_t b_rs,
+            int64_t b_cs, float* C, int64_t M, int64_t N, int64_t K, int64_t splits,
+            float* partials, hipStream_t s) {
+  if (a_rs != 1 || b_cs != 1 || splits < 2 || partials == nullptr || K < 4096) return false;
+  if (M % 4 != 0 || N % 4 != 0 || a_cs % 4 != 0 || b_rs % 4 != 0 || !al16(A) || !al16(B))
+    return false;
+  if (M <= 64 && N <= 256) launch_tn<2, 8>(A, a_cs, B, b_rs, C, M, N, K, splits, partials, s);
+  else if (M <= 128 && N <= 128) launch_tn<4, 4>(A, a_cs, B, b_rs, C, M, N, K, splits, partials, s);
+  else if (M <= 256 && N <= 64) launch_tn<8, 2>(A, a_cs, B, b_rs, C, M, N, K, splits, partials, s);
+  else return false;
+  return true;
+}
+
+}  // namespace
+
 void launch_gemm(const float* A, int64_t a_rs, int64_t a_cs, const float* B, int64_t b_rs,
                  int64_t b_cs, float* C, int64_t M, int64_t N, int64_t K, int64_t splits,
                  float* partials, hipStream_t s) {
@@ -151,6 +434,8 @@ void launch_gemm(const float* A, int64_t a_rs, int64_t a_cs, const float* B, int
     launch_fill(C, M * N, 0.0f, s);
     return;
   }
+  if (try_rows(A, a_rs, a_cs, B, b_rs, b_cs, C, M, N, K, s)) return;
+  if (try_tn(A, a_rs, a_cs, B, b_rs, b_cs, C, M, N, K, splits, partials, s)) return;
   const int64_t k_split = ((K + splits - 1) / splits + kTK - 1) / kTK * kTK;
   const int64_t used = (K + k_split - 1) / k_split;
   const dim3 grid(static_cast<unsigned>(((M + kTM - 1) / kTM) * ((N + kTN - 1) / kTN)), 1,

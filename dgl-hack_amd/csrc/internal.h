@@ -134,6 +134,10 @@ __device__ __forceinline__ void fill_empty_rows(const int32_t* __restrict__ indp
 // 39 K carries made a 20 M-edge star's copy_u sum 5.4 ms (0.8 ms spread over
 // 1 M rows; scripts/hub_probe.py).  Counters live after the carries in the
 // workspace, one per chunk, zeroed by the reduce kernel that precedes the fixup.
+// Like fill_empty_rows, seg_arrive_last needs the L lanes of a group inside ONE
+// wavefront (L <= 64: lane 0's counter value reaches the others by a shuffle);
+// the templated kernels static_assert it and the generic ones cap L at 64
+// (kernels_generic.hip kMaxLaneBits).
 constexpr int64_t kFixSeg = 32;
 __device__ __forceinline__ bool seg_arrive_last(int32_t* cnt, int64_t nseg, int L, int lane) {
   __threadfence();  // release: this group's partial, past its XCD's L2
@@ -337,6 +341,8 @@ void launch_gat_backward_src(const GatArgs& a, hipStream_t s);
 // l_part[b]), normalised; m / l of the merged softmax (blocks in order)
 void launch_gat_merge(const float* out_part, const float* m_part, const float* l_part, int nb,
                       int64_t num_rows, int H, int D, float* out, float* m, float* l, hipStream_t s);
+// l[i] = m[i] + log(l[i]) for i < n (one log-sum-exp per row and head)
+void launch_gat_fold_lse(const float* m, float* l, int64_t n, hipStream_t s);
 
 // R-GCN C entries (hack_kernels.hip): relation-expanded ids (mode 0: etypes[eid] *
 // mul + id, mode 1: id * mul + etypes[eid]; eids NULL = position), the relation
@@ -347,6 +353,9 @@ void launch_typed_ids(const int32_t* ids, const int32_t* eids, const int32_t* et
                       int64_t mul, int mode, int32_t* out, hipStream_t s);
 void launch_permute_rkx(const float* w, int64_t R, int64_t K, int64_t X, bool to_cat, float* out,
                         hipStream_t s);
+// out[p] = v[idx[p]]; out[p] = p
+void launch_gather_f32(const float* v, const int32_t* idx, int64_t n, float* out, hipStream_t s);
+void launch_iota_i32(int32_t* out, int64_t n, hipStream_t s);
 int64_t gemm_splits(int64_t M, int64_t N, int64_t K);
 void launch_gemm(const float* A, int64_t a_rs, int64_t a_cs, const float* B, int64_t b_rs,
                  int64_t b_cs, float* C, int64_t M, int64_t N, int64_t K, int64_t splits,

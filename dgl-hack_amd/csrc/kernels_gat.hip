@@ -45,8 +45,10 @@ __device__ __forceinline__ float dleaky(float x, float s) { return x > 0.0f ? 1.
 // e^x as one v_exp_f32 (2^(x log2 e)): the walks evaluate it once or twice per
 // edge and lane, where the accurate expf's range reduction cost ~12 VALU each.
 // Relative error ~|x| 2^-24 (< 2e-6 for the logits a softmax sees), far inside
-// the 1e-4 budget; forward and backward use the same function, so the
-// attention weights the backward recomputes are the forward's.
+// the 1e-4 budget.  The walks of the forward and the backward both use it; the
+// forward's rescales of stored (m, l) partials (the split-row fixup and the
+// column-block merge) use the accurate expf, so the attention weights the
+// backward recomputes match the forward's within that budget, not bit for bit.
 __device__ __forceinline__ float fexp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
 // Element offset of (row, off) in a table of rows `w` floats wide: 32-bit
 // arithmetic when every offset of the gathered tables fits (GatArgs::o32), one
@@ -82,6 +84,7 @@ __device__ __forceinline__ float head_sum(float x, int d4) {
 // ---------------------------------------------------------------------------
 template <int L, int NV, bool O32>
 __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
+  static_assert(L >= 1 && L <= 64, "a lane group must fit in one wavefront");
   constexpr int G = kBlock / L;
   constexpr int B = L > 16 ? L : 16;
   constexpr int U = NV == 1 ? 8 : 4;
@@ -224,6 +227,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
 
 template <int L, int NV>
 __global__ void __launch_bounds__(kBlock) k_gat_fwd_fixup(GatArgs a) {
+  static_assert(L >= 1 && L <= 64, "a lane group must fit in one wavefront");
   constexpr int G = kBlock / L;
   const int g = threadIdx.x / L;
   const int lane = threadIdx.x % L;
@@ -298,6 +302,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_fixup(GatArgs a) {
 // ---------------------------------------------------------------------------
 template <int L, int NV, bool O32>
 __global__ void __launch_bounds__(kBlock) k_gat_bwd_dst(GatArgs a) {
+  static_assert(L >= 1 && L <= 64, "a lane group must fit in one wavefront");
   constexpr int G = kBlock / L;
   constexpr int B = L > 16 ? L : 16;
   constexpr int U = NV == 1 ? 8 : 4;
@@ -426,6 +431,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_dst(GatArgs a) {
 // ---------------------------------------------------------------------------
 template <int L, int NV, bool O32>
 __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
+  static_assert(L >= 1 && L <= 64, "a lane group must fit in one wavefront");
   constexpr int G = kBlock / L;
   constexpr int B = L > 16 ? L : 16;
   constexpr int U = NV == 1 ? 8 : 4;
@@ -551,6 +557,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
 template <int L, int NV>
 __global__ void __launch_bounds__(kBlock) k_gat_bwd_fixup(GatArgs a, float* vec_out, float* head_out,
                                                           int with_vec) {
+  static_assert(L >= 1 && L <= 64, "a lane group must fit in one wavefront");
   constexpr int G = kBlock / L;
   const int g = threadIdx.x / L;
   const int lane = threadIdx.x % L;
@@ -743,6 +750,20 @@ void launch_gat_merge(const float* out_part, const float* m_part, const float* l
   const unsigned blocks = static_cast<unsigned>(want < 65536 ? want : 65536);
   hipLaunchKernelGGL(k_gat_merge, dim3(blocks), dim3(kBlock), 0, s, out_part, m_part, l_part, nb,
                      num_rows, H, D, out, m, l);
+}
+// l[i] = m[i] + log(l[i]): the softmax state of a row as one log-sum-exp, so the
+// backward's attention exp(s - m) / l becomes exp(s - lse) / 1 (the reference-order
+// entry point when its (E, H) exp buffer is too small to hold the running max).
+__global__ void k_gat_fold_lse(const float* __restrict__ m, float* __restrict__ l, int64_t n) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+    l[i] = m[i] + logf(l[i]);
+}
+void launch_gat_fold_lse(const float* m, float* l, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t want = (n + kBlock - 1) / kBlock;
+  const unsigned blocks = static_cast<unsigned>(want < 65536 ? want : 65536);
+  hipLaunchKernelGGL(k_gat_fold_lse, dim3(blocks), dim3(kBlock), 0, s, m, l, n);
 }
 void launch_gat_backward_dst(const GatArgs& a, hipStream_t s) { DGLMI_GAT_DISPATCH(bwd_dst_cfg, a, s); }
 void launch_gat_backward_src(const GatArgs& a, hipStream_t s) { DGLMI_GAT_DISPATCH(bwd_src_cfg, a, s); }

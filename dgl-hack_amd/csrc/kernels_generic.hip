@@ -297,9 +297,14 @@ __global__ void k_fill_i32(int32_t* __restrict__ out, int64_t n, int32_t v) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = v;
 }
 
+// Lanes per group as a power of two, at most 64: a group must fit in one
+// wavefront, because fill_empty_rows (a wave ballot) and seg_arrive_last (a
+// shuffle from lane 0) in k_lb_reduce / k_lb_fixup assume it (internal.h).
+constexpr int kMaxLaneBits = 6;
+static_assert((1 << kMaxLaneBits) <= 64, "a lane group must fit in one wavefront");
 int lane_bits_for(int64_t d) {
   int b = 0;
-  while ((1 << b) < d && b < 6) ++b;
+  while ((1 << b) < d && b < kMaxLaneBits) ++b;
   return b;
 }
 

@@ -309,12 +309,19 @@ extern "C" int DGLMIPartitionLabelProp(const DGLMIGraph* graph, int32_t num_part
     const int k = num_parts;
     // scratch: want (n), heavy list (n), two k x 256 histograms, loads / deltas /
     // cuts / rooms (k each), counters
-    char* ws = nullptr;
+    // released on every path out of here, the throwing ones included
+    struct AsyncBuf {
+      char* p = nullptr;
+      hipStream_t s = nullptr;
+      ~AsyncBuf() { if (p) (void)hipFreeAsync(p, s); }
+    } buf;
+    buf.s = s;
     const size_t want_b = ((n * sizeof(int32_t)) + 255) & ~size_t(255);
     const size_t hist_b = 2 * kMaxParts * 256 * sizeof(unsigned long long);
     const size_t small_b = 6 * kMaxParts * sizeof(long long) + 256;
-    ck(hipMallocAsync(reinterpret_cast<void**>(&ws), 2 * want_b + hist_b + small_b, s),
+    ck(hipMallocAsync(reinterpret_cast<void**>(&buf.p), 2 * want_b + hist_b + small_b, s),
        "hipMallocAsync");
+    char* ws = buf.p;
     int32_t* want = reinterpret_cast<int32_t*>(ws);
     int32_t* heavy = reinterpret_cast<int32_t*>(ws + want_b);
     unsigned long long* hist_a = reinterpret_cast<unsigned long long*>(ws + 2 * want_b);
@@ -337,10 +344,7 @@ extern "C" int DGLMIPartitionLabelProp(const DGLMIGraph* graph, int32_t num_part
     ck(hipMemcpyAsync(host_misc, misc, sizeof(host_misc), hipMemcpyDeviceToHost, s), "copy");
     ck(hipMemcpyAsync(host_load, load, k * sizeof(long long), hipMemcpyDeviceToHost, s), "copy");
     ck(hipStreamSynchronize(s), "sync");
-    if (host_misc[2]) {
-      (void)hipFreeAsync(ws, s);
-      throw Fail("initial assignment holds a part id outside [0, num_parts)");
-    }
+    if (host_misc[2]) throw Fail("initial assignment holds a part id outside [0, num_parts)");
     const int64_t num_heavy = static_cast<int64_t>(host_misc[0]);
     long long total = 0;
     for (int p = 0; p < k; ++p) total += host_load[p];
@@ -376,7 +380,8 @@ extern "C" int DGLMIPartitionLabelProp(const DGLMIGraph* graph, int32_t num_part
     }
     if (part_loads)
       ck(hipMemcpyAsync(host_load, load, k * sizeof(long long), hipMemcpyDeviceToHost, s), "copy");
-    (void)hipFreeAsync(ws, s);
+    (void)hipFreeAsync(buf.p, s);
+    buf.p = nullptr;
     ck(hipStreamSynchronize(s), "sync");
     if (cut_edges) *cut_edges = static_cast<int64_t>(host_misc[1]);
     if (part_loads)

@@ -181,6 +181,7 @@ __device__ __forceinline__ typename VecT<VW>::T epiv(const FastArgs& a, typename
 
 template <int KIND, int RED, int L, int NV, int VAR = 3, bool EPI = false, int VW = 4>
 __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32_t* __restrict__ indptr) {
+  static_assert(L >= 1 && L <= 64, "a lane group must fit in one wavefront (fill_empty_rows)");
   constexpr int G = kBlock / L;           // groups per block
   constexpr int B = (L > 16 ? L : 16) * ((VAR & 4) ? 2 : 1);  // positions staged per step
   constexpr int U = (NV == 1 ? 8 : (NV == 2 ? 4 : 2)) * ((VAR & 4) ? 2 : 1);
@@ -309,6 +310,7 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
 // to finish folds the head and the segment partials (internal.h).
 template <int RED, int L, int NV, bool EPI = false, int VW = 4>
 __global__ void __launch_bounds__(kBlock) k_chunk_fixup(FastArgs a, const int32_t* __restrict__ indptr) {
+  static_assert(L >= 1 && L <= 64, "a lane group must fit in one wavefront (seg_arrive_last)");
   constexpr int G = kBlock / L;
   const int g = threadIdx.x / L;
   const int lane = threadIdx.x % L;

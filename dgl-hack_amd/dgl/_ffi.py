@@ -47,6 +47,25 @@ class Graph(ctypes.Structure):
         ("num_col_blocks", ctypes.c_int32),
         ("in_col_blocks", ctypes.c_void_p),
         ("out_col_blocks", ctypes.c_void_p),
+        ("rgcn", ctypes.c_void_p),
+    ]
+
+
+class RgcnState(ctypes.Structure):
+    """DGLMIRgcnState (include/dglmi.h): per-graph R-GCN state, library-owned."""
+    _fields_ = [
+        ("etypes", ctypes.c_void_p),
+        ("norm", ctypes.c_void_p),
+        ("num_rels", ctypes.c_int32),
+        ("layers", ctypes.c_int32),
+        ("num_src", ctypes.c_int64),
+        ("nnz", ctypes.c_int64),
+        ("positions", ctypes.c_void_p),
+        ("in_cols", ctypes.c_void_p * 2),
+        ("in_norm", ctypes.c_void_p),
+        ("out_typed", CSR * 2),
+        ("out_norm", ctypes.c_void_p * 2),
+        ("owner", ctypes.c_void_p),
     ]
 
 
@@ -153,6 +172,15 @@ _SIGS = {
         ctypes.c_float, ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.c_void_p]),
+    "DGLMIFusedGatKernel": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.c_float,
+        ctypes.c_void_p]),
+    "DGLMIKernelBackwardFusedGat": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.c_float,
+        ctypes.c_void_p]),
     "DGLMIEdgeSoftmaxSupported": (ctypes.c_int, [ctypes.c_int64]),
     "DGLMIEdgeSoftmaxWorkspaceBytes": (ctypes.c_int64, [ctypes.POINTER(CSR), ctypes.c_int64]),
     "DGLMIEdgeSoftmaxForward": (ctypes.c_int, [
@@ -181,6 +209,10 @@ _SIGS = {
         ctypes.POINTER(Graph), ctypes.c_void_p, ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.c_void_p]),
+    "DGLMIRgcnPrepare": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.c_void_p, ctypes.POINTER(Array), ctypes.c_int32,
+        ctypes.c_int32, ctypes.POINTER(RgcnState), ctypes.c_void_p]),
+    "DGLMIRgcnRelease": (ctypes.c_int, [ctypes.POINTER(RgcnState)]),
     "DGLMINbAccess": (ctypes.c_int, [
         ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.c_void_p, ctypes.c_void_p,
         ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_double), ctypes.c_void_p]),

@@ -1,7 +1,12 @@
 """Graph files in the reference's binary format (``python/dgl/data/graph_serialize.py:63-160``,
 ``src/graph/graph_serialize.cc:130-301``).
 
-A file written here loads in the reference and the other way round.  Layout (little-endian,
+A file of int / uint / float tensors written here loads in the reference and the other
+way round.  bool and bfloat16 tensors are written with DLPack codes 6 and 4, which
+this library reads back; the reference's dlpack submodule is absent from its tree and
+older DLPack releases define only Int / UInt / Float, so whether the reference loads
+them is parity unpinned (convert to uint8 / float32 for a file the reference must
+read).  Layout (little-endian,
 dmlc-core stream encoding -- ``third_party/dmlc-core`` ``include/dmlc/serializer.h``, a
 submodule absent from the reference tree: a POD is its raw bytes, a ``std::string`` and a
 ``std::vector`` a ``uint64`` length followed by the elements, a ``std::pair`` its two halves):

@@ -321,6 +321,34 @@ def fused_gat_backward(graph, feat_src, el, er, slope, out, max_in, sum_in, grad
         _arr(grad_er, "grad_er"), _stream(grad_out)))
 
 
+def fused_gat_kernel(graph, feat_src, el, er, s, exp, ret, slope):
+    """The reference's ``kernel.fused_gat_kernel`` (kernel.py:150-151) in its own
+    argument order: _CAPI_DGLFusedGatKernel (binary_reduce.cc:380-396) ->
+    DGLMIFusedGatKernel.  ``s`` (N, H[, 1]) and ``exp`` (E, H[, 1]) are the
+    caller's buffers carrying the softmax state to :func:`backward_fused_gat`."""
+    _check_ctx(graph, [("feat_src", feat_src), ("el", el), ("er", er), ("s", s), ("exp", exp),
+                       ("ret", ret)])
+    g = graph.cstruct(None, col_blocks=gat_col_blocks(graph, feat_src))
+    check_call(_ffi.lib().DGLMIFusedGatKernel(
+        ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"), _arr(s, "s"),
+        _arr(exp, "exp"), _arr(ret, "ret"), float(slope), _stream(ret)))
+    return ret
+
+
+def backward_fused_gat(graph, feat_src, el, er, s, exp, ret, grad_out, grad_feat_src, grad_el,
+                       grad_er, slope):
+    """The reference's ``kernel.backward_fused_gat`` (kernel.py:153-154):
+    _CAPI_DGLKernelBackwardFusedGat (binary_reduce.cc:529-549) ->
+    DGLMIKernelBackwardFusedGat.  Overwrites the three gradients."""
+    _check_ctx(graph, [("feat_src", feat_src), ("grad_out", grad_out)])
+    g = graph.cstruct(None, col_blocks=gat_col_blocks(graph, feat_src, backward=True))
+    check_call(_ffi.lib().DGLMIKernelBackwardFusedGat(
+        ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"), _arr(s, "s"),
+        _arr(exp, "exp"), _arr(ret, "ret"), _arr(grad_out, "grad_out"),
+        _arr(grad_feat_src, "grad_feat_src"), _arr(grad_el, "grad_el"), _arr(grad_er, "grad_er"),
+        float(slope), _stream(grad_out)))
+
+
 def edge_softmax_supported(values_per_edge):
     return bool(_ffi.lib().DGLMIEdgeSoftmaxSupported(int(values_per_edge)))
 
@@ -372,11 +400,63 @@ def nb_access(graph, feat, node_map=None, deg_inc_node_map=None, times=15, warm_
     return avg.value
 
 
+class RgcnState:
+    """A prepared DGLMIRgcnState (DGLMIRgcnPrepare) of one graph for one etypes /
+    norm pair: the relation-expanded in-CSR columns, the out-CSR regrouped by
+    (relation, source) and norm in both walks' position orders, built once on the
+    device.  It holds the two tensors, so their memory cannot be reused by another
+    tensor while the state lives, and is released with the object."""
+
+    def __init__(self, graph, etypes, norm, num_rels, layers):
+        _etypes(graph, etypes)
+        if norm is not None:
+            _check_ctx(graph, [("norm", norm)])
+        self.etypes, self.norm = etypes, norm
+        self.versions = (etypes._version, None if norm is None else norm._version)
+        self.num_rels, self.layers = int(num_rels), int(layers)
+        self.c = _ffi.RgcnState()
+        check_call(_ffi.lib().DGLMIRgcnPrepare(
+            ctypes.byref(graph.cstruct()), ctypes.c_void_p(etypes.data_ptr()),
+            None if norm is None else _arr(norm, "norm"), self.num_rels, self.layers,
+            ctypes.byref(self.c), _stream(etypes)))
+        import weakref
+        self._fin = weakref.finalize(self, _ffi.lib().DGLMIRgcnRelease, ctypes.byref(self.c))
+
+    def matches(self, etypes, norm, num_rels, layer):
+        """True when a call with these tensors may use the state (the C entries also
+        check pointers; this also catches in-place writes through the version counters)."""
+        if etypes is not self.etypes or etypes._version != self.versions[0]:
+            return False
+        if self.norm is not None and norm is self.norm and norm._version != self.versions[1]:
+            return False
+        return int(num_rels) == self.num_rels and bool((self.layers >> layer) & 1)
+
+
+def rgcn_prepare(graph, etypes, norm, num_rels, layers=3):
+    """DGLMIRgcnPrepare: build the R-GCN state of ``graph`` for ``etypes`` (int32,
+    one per edge id) and ``norm`` (one float per edge id, or None) once; later
+    rgcn_layer* calls on this graph with these same tensors use it (layers bit 0:
+    Layer0 and its backward, bit 1: Layer1 and its backward).  Writing into etypes
+    or norm in place invalidates it (the next call derives everything per call)."""
+    st = RgcnState(graph, etypes, norm, num_rels, layers)
+    graph.__dict__["_rgcn_state"] = st
+    return st
+
+
+def _rgcn_cgraph(graph, etypes, norm, num_rels, layer):
+    g = graph.cstruct()
+    st = graph.__dict__.get("_rgcn_state")
+    if st is not None and st.matches(etypes, norm, num_rels, layer):
+        g.rgcn = ctypes.addressof(st.c)
+    return g
+
+
 def rgcn_layer0(graph, etypes, weight, norm, ret):
     """_CAPI_DGLRgcnLayer0: ret[v] = sum_e weight[etypes[e], u] * norm[e]."""
     _check_ctx(graph, [("weight", weight), ("norm", norm), ("ret", ret)])
     check_call(_ffi.lib().DGLMIRgcnLayer0(
-        ctypes.byref(graph.cstruct()), _etypes(graph, etypes), _arr(weight, "weight"),
+        ctypes.byref(_rgcn_cgraph(graph, etypes, norm, weight.shape[0], 0)),
+        _etypes(graph, etypes), _arr(weight, "weight"),
         _arr(norm, "norm"), _arr(ret, "ret"), _stream(ret)))
 
 
@@ -384,7 +464,8 @@ def rgcn_layer0_backward(graph, etypes, grad_out, norm, grad_weight):
     """_CAPI_DGLRgcnLayer0Backward (exact sums over repeated (source, relation) pairs)."""
     _check_ctx(graph, [("grad_out", grad_out), ("norm", norm), ("grad_weight", grad_weight)])
     check_call(_ffi.lib().DGLMIRgcnLayer0Backward(
-        ctypes.byref(graph.cstruct()), _etypes(graph, etypes), _arr(grad_out, "grad_out"),
+        ctypes.byref(_rgcn_cgraph(graph, etypes, norm, grad_weight.shape[0], 0)),
+        _etypes(graph, etypes), _arr(grad_out, "grad_out"),
         _arr(norm, "norm"), _arr(grad_weight, "grad_weight"), _stream(grad_out)))
 
 
@@ -392,7 +473,8 @@ def rgcn_layer1(graph, etypes, hidden, weight, norm, ret):
     """_CAPI_DGLRgcnLayer1: ret[v] = sum_e norm[e] * hidden[u] . weight[etypes[e]]."""
     _check_ctx(graph, [("hidden", hidden), ("weight", weight), ("norm", norm), ("ret", ret)])
     check_call(_ffi.lib().DGLMIRgcnLayer1(
-        ctypes.byref(graph.cstruct()), _etypes(graph, etypes), _arr(hidden, "hidden"),
+        ctypes.byref(_rgcn_cgraph(graph, etypes, norm, weight.shape[0], 1)),
+        _etypes(graph, etypes), _arr(hidden, "hidden"),
         _arr(weight, "weight"), _arr(norm, "norm"), _arr(ret, "ret"), _stream(ret)))
 
 
@@ -403,6 +485,7 @@ def rgcn_layer1_backward(graph, etypes, hidden, weight, norm, grad_out, grad_hid
                        ("grad_out", grad_out), ("grad_hidden", grad_hidden),
                        ("grad_weight", grad_weight)])
     check_call(_ffi.lib().DGLMIRgcnLayer1Backward(
-        ctypes.byref(graph.cstruct()), _etypes(graph, etypes), _arr(hidden, "hidden"),
+        ctypes.byref(_rgcn_cgraph(graph, etypes, norm, weight.shape[0], 1)),
+        _etypes(graph, etypes), _arr(hidden, "hidden"),
         _arr(weight, "weight"), _arr(norm, "norm"), _arr(grad_out, "grad_out"),
         _arr(grad_hidden, "grad_hidden"), _arr(grad_weight, "grad_weight"), _stream(grad_out)))

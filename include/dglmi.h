@@ -100,6 +100,10 @@ typedef struct {
   int32_t num_col_blocks;
   const DGLMICsr* in_col_blocks;
   const DGLMICsr* out_col_blocks;
+  /* Optional per-graph R-GCN state (extension): built once by DGLMIRgcnPrepare and
+   * read by the DGLMIRgcnLayer* entries when it matches the call's etypes (and norm)
+   * pointers.  NULL = every call derives what it needs from etypes / norm. */
+  const struct DGLMIRgcnState* rgcn;
 } DGLMIGraph;
 
 /* A contiguous row-major fp32 device array (NDArray / DLTensor subset). */
@@ -252,6 +256,27 @@ int DGLMIFusedGatBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src, c
                           const DGLMIArray* max_in, const DGLMIArray* sum_in,
                           const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
                           DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream);
+/* The same two kernels in the reference's argument order, for a binding of the hack's
+ * PackedFuncs that keeps its Python caller unchanged (tensor.py:383-420):
+ *   _CAPI_DGLFusedGatKernel(G, feat_src, el, er, sum, exp, ret, slope)
+ *   _CAPI_DGLKernelBackwardFusedGat(G, feat_src, el, er, sum, exp, ret, grad_out,
+ *                                   grad_feat_src, grad_el, grad_er, slope)
+ * (binary_reduce.cc:380-396, 529-549).  sum (N_dst, H[, 1]) and exp (E, H[, 1]) are
+ * caller-allocated state passed from the forward to the backward unchanged; their
+ * contents are this library's softmax state, not the hack's per-edge exponentials:
+ * when E >= N_dst, exp's first N_dst * H floats keep the running max and sum the sum
+ * of exp(s - max) (bit-identical to DGLMIFusedGatForward / Backward); otherwise sum
+ * keeps max + log(sum) and exp is not touched.  ret (N_dst, H, D) is overwritten, and
+ * the three gradients are overwritten (the hack's caller zero-fills them first). */
+int DGLMIFusedGatKernel(const DGLMIGraph* graph, const DGLMIArray* feat_src, const DGLMIArray* el,
+                        const DGLMIArray* er, DGLMIArray* sum, DGLMIArray* exp, DGLMIArray* ret,
+                        float slope, void* stream);
+int DGLMIKernelBackwardFusedGat(const DGLMIGraph* graph, const DGLMIArray* feat_src,
+                                const DGLMIArray* el, const DGLMIArray* er, const DGLMIArray* sum,
+                                const DGLMIArray* exp, const DGLMIArray* ret,
+                                const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
+                                DGLMIArray* grad_el, DGLMIArray* grad_er, float slope,
+                                void* stream);
 /* 1 if the fused GAT kernels support (heads, head_dim), else 0. */
 int DGLMIFusedGatSupported(int64_t heads, int64_t head_dim);
 
@@ -281,6 +306,44 @@ int DGLMIEdgeSoftmaxBackward(const DGLMIGraph* graph, const DGLMIArray* out,
  * hack's Layer0Backward overwrites repeated (source, relation) pairs
  * (binary_reduce_impl.cu:1004) and its Python wrapper drops Layer1's weight
  * gradient (tensor.py:493); these return the exact sums. */
+/* Per-graph state of the R-GCN entries (extension, no reference counterpart; the
+ * reference sorts its CSR by edge type once per graph inside the graph object,
+ * GetCsrSortedByEdgeType, graph.cc:690-746).  Without it every Layer* call
+ * gathers the relation of each edge by edge id, gathers norm by edge id and
+ * re-sorts the out-CSR by (source, relation).  DGLMIRgcnPrepare builds, on the
+ * device and once, for the relations `etypes` (one int32 per edge id, in
+ * [0, num_rels)) and the edge weights `norm` (one float per edge id; NULL = none
+ * cached):
+ *   layers bit 0 (Layer0 / Layer0Backward): the in-CSR columns etypes[e] * N_src + u
+ *     and the out-CSR regrouped by that key;
+ *   layers bit 1 (Layer1 / Layer1Backward): the in-CSR columns u * R + etypes[e]
+ *     and the out-CSR regrouped by that key;
+ * and norm permuted into each walk's position order, so the gathers stream it.
+ * Set DGLMIGraph.rgcn to the state; an entry uses it when graph->rgcn->etypes ==
+ * etypes, num_rels and the source count match and the layer's bit is set, and
+ * uses the cached norm copies only when norm->data == graph->rgcn->norm -- a caller
+ * that changes the VALUES behind those pointers must prepare again.  Results are
+ * bit-identical with and without the state.  The memory (about 6 int32/float per
+ * edge per layer) is the library's until DGLMIRgcnRelease.  Stream-ordered;
+ * DGLMIRgcnRelease synchronises the device. */
+typedef struct DGLMIRgcnState {
+  const int32_t* etypes;    /* the etypes pointer the state was built from */
+  const float* norm;        /* the norm pointer it was built from, or NULL */
+  int32_t num_rels;
+  int32_t layers;
+  int64_t num_src;
+  int64_t nnz;
+  const int32_t* positions; /* 0 .. nnz-1: the edge ids of position-ordered walks */
+  const int32_t* in_cols[2];   /* [0]: etypes[e] * num_src + u, [1]: u * num_rels + etypes[e] */
+  const float* in_norm;        /* norm[in_csr.data[p]] (NULL when no norm was cached) */
+  DGLMICsr out_typed[2];       /* out-CSR regrouped by the key of in_cols[i]; data = edge ids */
+  const float* out_norm[2];    /* norm per position of out_typed[i] */
+  void* owner;                 /* library-private */
+} DGLMIRgcnState;
+int DGLMIRgcnPrepare(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* norm,
+                     int32_t num_rels, int32_t layers, DGLMIRgcnState* state, void* stream);
+int DGLMIRgcnRelease(DGLMIRgcnState* state);
+
 /* _CAPI_DGLRgcnLayer0: ret[v, :] = sum_{e=(u->v)} weight[etypes[e], u, :] * norm[e];
  * weight (R, N_src, F), ret (N_dst, F). */
 int DGLMIRgcnLayer0(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* weight,

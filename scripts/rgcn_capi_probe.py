@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """C5 (5 M nodes, 80 M typed edges, 4 relations, 64 -> 64): the R-GCN C entries
-(DGLMIRgcnLayer1 / 1Backward: the library's tiled GEMM + relation-expanded gather,
-typed out-CSR re-sorted per call) against the Python path (RelGraphConv: hipBLASLt
-GEMM via torch + the cached typed gather).  HIP-event medians."""
+(DGLMIRgcnLayer1 / 1Backward: the library's tiled GEMM + relation-expanded gather)
+stateless (relations gathered by edge id and the typed out-CSR re-sorted per
+call) and with the per-graph state of DGLMIRgcnPrepare, against the Python path
+(RelGraphConv: hipBLASLt GEMM via torch + the cached typed gather).  HIP-event
+medians.  --capi-only [--prepared]: a few C-entry calls for rocprofv3."""
 import json
 import os
 import sys
@@ -49,6 +51,8 @@ def main():
     gh, gw = th.empty(n, F, device=dev), th.empty_like(W)
     res = {"config": "C5 R-GCN layer 64->64, 4 relations, 5M nodes / 80M edges"}
     if "--capi-only" in sys.argv:  # for rocprofv3 kernel statistics
+        if "--prepared" in sys.argv:
+            K.rgcn_prepare(gidx, et32, norm, R, layers=2)
         for _ in range(3):
             K.rgcn_layer1(gidx, et32, h, W, norm, ret)
             K.rgcn_layer1_backward(gidx, et32, h, W, norm, go, gh, gw)
@@ -66,7 +70,24 @@ def main():
         lambda: K.rgcn_layer1_backward(gidx, et32, h, W, norm, go, gh, gw))
     w0 = th.randn(R, n, 16, device=dev)
     r0 = th.empty(n, 16, device=dev)
+    gw0 = th.empty_like(w0)
     res["capi_layer0_F16_ms"] = ktime(lambda: K.rgcn_layer0(gidx, et32, w0, norm, r0))
+    res["capi_layer0_F16_backward_ms"] = ktime(lambda: K.rgcn_layer0_backward(gidx, et32, r0, norm, gw0))
+    ref = (ret.clone(), gh.clone(), gw.clone(), r0.clone(), gw0.clone())
+    th.cuda.synchronize()
+    t0 = __import__("time").time()
+    K.rgcn_prepare(gidx, et32, norm, R, layers=3)
+    th.cuda.synchronize()
+    res["prepare_s"] = __import__("time").time() - t0
+    res["prepared_layer1_ms"] = ktime(lambda: K.rgcn_layer1(gidx, et32, h, W, norm, ret))
+    res["prepared_layer1_backward_ms"] = ktime(
+        lambda: K.rgcn_layer1_backward(gidx, et32, h, W, norm, go, gh, gw))
+    res["prepared_layer1_fwd_bwd_ms"] = res["prepared_layer1_ms"] + res["prepared_layer1_backward_ms"]
+    res["prepared_layer0_F16_ms"] = ktime(lambda: K.rgcn_layer0(gidx, et32, w0, norm, r0))
+    res["prepared_layer0_F16_backward_ms"] = ktime(
+        lambda: K.rgcn_layer0_backward(gidx, et32, r0, norm, gw0))
+    res["prepared_bit_identical"] = all(bool(th.equal(a, b)) for a, b in
+                                        zip(ref, (ret, gh, gw, r0, gw0)))
     print(json.dumps(res), flush=True)
 
 

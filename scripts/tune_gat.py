@@ -47,13 +47,14 @@ sm = th.empty(n, H, device=dev)
 go = th.randn(n, H, D, device=dev)
 gft, gel, ger = th.empty_like(ft), th.empty_like(el), th.empty_like(er)
 res = {}
+# round 3: chunk size only (U = 8 is fixed in the kernels), with the automatic
+# column blocks (8 on C3: each launch walks ~14 M edges, ~7000 waves at K = 512)
+ks = sys.argv[1].split(",") if len(sys.argv) > 1 else ["128", "256", "512", "1024"]
 for rnd in range(2):
-    for u in ("0", "4", "16"):
-        for k in ("256", "512", "1024"):
-            os.environ["DGLMI_GAT_U"] = u
-            os.environ["DGLMI_CHUNK_EDGES"] = k
-            f = ev_time(lambda: K.fused_gat_forward(gidx, ft, el, er, 0.2, out, mx, sm))
-            b = ev_time(lambda: K.fused_gat_backward(gidx, ft, el, er, 0.2, out, mx, sm, go, gft, gel, ger))
-            res.setdefault("U%s_K%s" % (u, k), []).append((f, b))
+    for k in ks:
+        os.environ["DGLMI_CHUNK_EDGES"] = k
+        f = ev_time(lambda: K.fused_gat_forward(gidx, ft, el, er, 0.2, out, mx, sm))
+        b = ev_time(lambda: K.fused_gat_backward(gidx, ft, el, er, 0.2, out, mx, sm, go, gft, gel, ger))
+        res.setdefault("K%s" % k, []).append((f, b))
 summary = {key: {"fwd_ms": min(x[0] for x in v), "bwd_ms": min(x[1] for x in v)} for key, v in res.items()}
 print(json.dumps(summary, indent=1))

@@ -65,8 +65,20 @@ def test_rgcn_layer0_fwd_bwd(F, hub):
 
 @pytest.mark.parametrize("K_in,X,hub", [(16, 16, False), (32, 8, True), (20, 5, False)])
 def test_rgcn_layer1_fwd_bwd(K_in, X, hub):
+    _layer1_fwd_bwd(K_in, X, hub, 700, 9000)
+
+
+@pytest.mark.parametrize("K_in,X", [(64, 64), (20, 5), (128, 32)])
+def test_rgcn_layer1_tall_gemms(K_in, X):
+    """Node counts >= 4096 take the tall-skinny MFMA products (k_gemm_rows with B in
+    LDS for X . W and gY . W^T, k_gemm_tn for the row reduction X^T . gY), incl.
+    partial row tiles and widths that are not multiples of 32."""
+    _layer1_fwd_bwd(K_in, X, False, 40001, 200000)
+
+
+def _layer1_fwd_bwd(K_in, X, hub, n, m):
     from dgl import kernel as K
-    n, m, R = 700, 9000, 4
+    R = 4
     g, gidx, s, d, et, norm = _graph(n, m, R, seed=K_in + X, hub=hub)
     n = g.number_of_nodes()
     h = th.randn(n, K_in, device=DEV)
@@ -135,3 +147,71 @@ def test_nb_access_times_the_gather():
     x = th.randn(5000, 64, device=DEV)
     out, us = B.nb_access_bench(g, x, None, None, times=6, warm_up_times=2)
     assert out is x and us > 0
+
+
+def _layer_calls(K, gidx, et32, norm, n, R, layer, seed):
+    """forward + backward of one hack layer through the C entries (fixed inputs)."""
+    gen = th.Generator(device=DEV).manual_seed(seed)
+    if layer == 0:
+        F = 16
+        w = th.randn(R, n, F, device=DEV, generator=gen)
+        go = th.randn(n, F, device=DEV, generator=gen)
+        ret = th.empty(n, F, device=DEV)
+        gw = th.empty(R, n, F, device=DEV)
+        K.rgcn_layer0(gidx, et32, w, norm, ret)
+        K.rgcn_layer0_backward(gidx, et32, go, norm, gw)
+        return ret, gw
+    K_in, X = 32, 16
+    h = th.randn(n, K_in, device=DEV, generator=gen)
+    w = th.randn(R, K_in, X, device=DEV, generator=gen) / 4
+    go = th.randn(n, X, device=DEV, generator=gen)
+    ret = th.empty(n, X, device=DEV)
+    gh, gw = th.empty(n, K_in, device=DEV), th.empty(R, K_in, X, device=DEV)
+    K.rgcn_layer1(gidx, et32, h, w, norm, ret)
+    K.rgcn_layer1_backward(gidx, et32, h, w, norm, go, gh, gw)
+    return ret, gh, gw
+
+
+@pytest.mark.parametrize("layer", [0, 1])
+def test_rgcn_prepared_state_bit_identical(layer):
+    """DGLMIRgcnPrepare (relation-expanded columns, typed out-CSR and norm in
+    position order built once per graph): every entry returns the same bits as the
+    stateless call; a different norm tensor reuses the columns but gathers its own
+    norm; an in-place write into the cached norm stops the state from being used."""
+    from dgl import kernel as K
+    g, gidx, s, d, et, norm = _graph(700, 9000, 4, seed=21 + layer, hub=True)
+    n, R = g.number_of_nodes(), 4
+    et32 = et.int()
+    gidx.__dict__.pop("_rgcn_state", None)
+    plain = _layer_calls(K, gidx, et32, norm, n, R, layer, seed=5)
+    st = K.rgcn_prepare(gidx, et32, norm, R, layers=1 << layer)
+    assert st.c.owner and st.c.nnz == len(s)
+    prepared = _layer_calls(K, gidx, et32, norm, n, R, layer, seed=5)
+    for a, b in zip(plain, prepared):
+        assert th.equal(a, b)
+    norm2 = norm * 2 + 0.5
+    gidx.__dict__.pop("_rgcn_state")
+    plain2 = _layer_calls(K, gidx, et32, norm2, n, R, layer, seed=6)
+    gidx.__dict__["_rgcn_state"] = st
+    for a, b in zip(plain2, _layer_calls(K, gidx, et32, norm2, n, R, layer, seed=6)):
+        assert th.equal(a, b)
+    norm.mul_(3.0)  # in place: the cached copy is stale, the call must not use it
+    gidx.__dict__.pop("_rgcn_state")
+    plain3 = _layer_calls(K, gidx, et32, norm, n, R, layer, seed=7)
+    gidx.__dict__["_rgcn_state"] = st
+    assert not st.matches(et32, norm, R, layer)
+    for a, b in zip(plain3, _layer_calls(K, gidx, et32, norm, n, R, layer, seed=7)):
+        assert th.equal(a, b)
+    gidx.__dict__.pop("_rgcn_state")
+
+
+def test_rgcn_prepare_rejects_bad_arguments():
+    from dgl import kernel as K
+    from dgl._ffi import DGLError
+    g, gidx, s, d, et, norm = _graph(100, 500, 2, seed=1)
+    with pytest.raises(DGLError, match="layers"):
+        K.RgcnState(gidx, et.int(), norm, 2, 4)
+    with pytest.raises(DGLError, match="norm"):
+        K.RgcnState(gidx, et.int(), norm[:10], 2, 3)
+    with pytest.raises(DGLError, match="etypes"):
+        K.RgcnState(gidx, et.int()[:10], norm, 2, 3)

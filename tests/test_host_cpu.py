@@ -171,7 +171,8 @@ def test_ctypes_structs_match_header_layout(tmp_path):
     fields = {"DGLMICsr": (_ffi.CSR, [f[0] for f in _ffi.CSR._fields_]),
               "DGLMIGraph": (_ffi.Graph, [f[0] for f in _ffi.Graph._fields_]),
               "DGLMIArray": (_ffi.Array, [f[0] for f in _ffi.Array._fields_]),
-              "DGLMIEpilogue": (_ffi.Epilogue, [f[0] for f in _ffi.Epilogue._fields_])}
+              "DGLMIEpilogue": (_ffi.Epilogue, [f[0] for f in _ffi.Epilogue._fields_]),
+              "DGLMIRgcnState": (_ffi.RgcnState, [f[0] for f in _ffi.RgcnState._fields_])}
     lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "dglmi.h"', "int main(void) {"]
     for cname, (_, names) in fields.items():
         lines.append('printf("%%s %%zu\\n", "%s", sizeof(%s));' % (cname, cname))
