@@ -1392,6 +1392,19 @@ const DGLMIRgcnState* rgcn_state(const DGLMIGraph* g, const int32_t* etypes, int
   return st;
 }
 
+// The fused layer-1 walk (relation-major CSR `c` with its cached norm when the state
+// was built from this norm, else edge ids + the caller's norm).
+void rgcn_fused_walk(const DGLMIRgcnState* st, const DGLMICsr& c, const float* cached,
+                     const float* norm, const int32_t** eids, const float** w) {
+  if (st->norm != nullptr && st->norm == norm && cached != nullptr) {
+    *eids = nullptr;
+    *w = cached;
+  } else {
+    *eids = c.data;
+    *w = norm;
+  }
+}
+
 // A walk of the prepared in-CSR (relation-expanded columns of `layer`), with the
 // cached norm streamed in position order when it was built from this norm.
 DGLMICsr rgcn_in_walk(const DGLMIGraph* g, const DGLMIRgcnState* st, int layer, int64_t num_cols,
@@ -1509,6 +1522,18 @@ int DGLMIRgcnLayer1(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIA
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t N = in.num_cols, M = R * X;
   DGLMIGraph z = no_workspace(), pg = plain_graph(graph);
+  if (const DGLMIRgcnState* fs = rgcn_state(graph, etypes, R, N, 2)) {
+    if (rgcn_fused_ok(K, X, R) && aligned16(hidden->data) && in.nnz > 0) {
+      const int32_t* eids = nullptr;
+      const float* w = nullptr;
+      rgcn_fused_walk(fs, fs->in_rel, fs->in_rel_norm, norm->data, &eids, &w);
+      launch_rgcn_fused(false, fs->in_rel.indptr, fs->in_rel.indices, fs->in_rel.rows, eids, w,
+                        hidden->data, weight->data, K * X, X, 1, ret->data, nullptr, in.num_rows, R,
+                        X, s);
+      check_hip(hipGetLastError(), "rgcn fused layer1 launch");
+      return 0;
+    }
+  }
   const DGLMIRgcnState* st = rgcn_state(graph, etypes, R, N, 1);
   Scratch wcat(&z, K * M * 4, s), y(&z, N * M * 4, s), cols(&z, st ? 0 : in.nnz * 4, s);
   launch_permute_rkx(weight->data, R, K, X, true, static_cast<float*>(wcat.ptr), s);
@@ -1558,6 +1583,22 @@ int DGLMIRgcnLayer1Backward(const DGLMIGraph* graph, const int32_t* etypes,
   Scratch wcat(&z, K * M * 4, s), gy(&z, N * M * 4, s), gw(&z, K * M * 4, s),
       parts(&z, splits > 1 ? splits * K * M * 4 : 0, s);
   launch_permute_rkx(weight->data, R, K, X, true, static_cast<float*>(wcat.ptr), s);
+  const DGLMIRgcnState* fs = out.nnz > 0 ? rgcn_state(graph, etypes, R, N, 2) : nullptr;
+  if (fs && rgcn_fused_ok(X, K, R) && aligned16(grad_out->data) && fs->out_typed[0].indptr) {
+    // fused: gy rows and grad_hidden = sum_t G_t . W_t^T in one walk of the
+    // relation-major out-CSR; the weight gradient from gy below
+    const int32_t* eids = nullptr;
+    const float* w = nullptr;
+    rgcn_fused_walk(fs, fs->out_typed[0], fs->out_norm[0], norm->data, &eids, &w);
+    launch_rgcn_fused(true, fs->out_typed[0].indptr, fs->out_typed[0].indices, fs->out_typed[0].rows,
+                      eids, w, grad_out->data, weight->data, K * X, 1, X, grad_hidden->data,
+                      static_cast<float*>(gy.ptr), N, R, K, s);
+    launch_gemm(hidden->data, 1, K, static_cast<float*>(gy.ptr), M, 1, static_cast<float*>(gw.ptr), K,
+                M, N, splits, static_cast<float*>(parts.ptr), s);
+    launch_permute_rkx(static_cast<float*>(gw.ptr), R, K, X, false, grad_weight->data, s);
+    check_hip(hipGetLastError(), "rgcn fused layer1 backward launch");
+    return 0;
+  }
   // gy[u * R + t] = sum over out-edges of u with type t of norm_e * grad_out[v]
   if (const DGLMIRgcnState* st = out.nnz > 0 ? rgcn_state(graph, etypes, R, N, 1) : nullptr) {
     const float* w = nullptr;
@@ -1587,7 +1628,8 @@ int DGLMIRgcnPrepare(const DGLMIGraph* graph, const int32_t* etypes, const DGLMI
   DGLMI_CHECK(state != nullptr, "null state");
   std::memset(state, 0, sizeof(*state));
   DGLMI_CHECK(num_rels >= 1, "num_rels must be >= 1");
-  DGLMI_CHECK(layers >= 1 && layers <= 3, "layers must be 1 (layer 0), 2 (layer 1) or 3 (both)");
+  DGLMI_CHECK(layers >= 1 && layers <= 7,
+              "layers must be a mask of 1 (layer 0), 2 (layer 1) and 4 (fused layer 1)");
   check_graph(graph);
   const DGLMICsr& in = graph->in_csr;
   const DGLMICsr& out = graph->out_csr;
@@ -1600,10 +1642,16 @@ int DGLMIRgcnPrepare(const DGLMIGraph* graph, const int32_t* etypes, const DGLMI
   // one allocation, carved into 256-byte aligned arrays
   auto al = [](int64_t bytes) { return (bytes + 255) & ~int64_t(255); };
   const int64_t e4 = al(E * 4), ptr4 = al((R * N + 1) * 4);
-  const int nl = (layers & 1) + ((layers >> 1) & 1);
+  // bit 2 (fused layer 1) needs the relation-major out-CSR of layer 0 and the
+  // relation-major in-CSR
+  const bool want0 = (layers & 1) || (layers & 4), want1 = (layers & 2) != 0;
+  const bool want_rel = (layers & 4) != 0;
+  const int nl = (want0 ? 1 : 0) + (want1 ? 1 : 0);
   const int64_t per_layer = e4 /*in cols*/ + ptr4 + 3 * e4 /*out idx, data, rows*/ +
                             (norm ? e4 : 0) /*out norm*/;
-  const int64_t total = e4 /*positions*/ + (norm ? e4 : 0) /*in norm*/ + nl * per_layer;
+  const int64_t ptr_rel = al((R * in.num_rows + 1) * 4);
+  const int64_t rel_bytes = want_rel ? ptr_rel + 3 * e4 + (norm ? e4 : 0) : 0;
+  const int64_t total = e4 /*positions*/ + (norm ? e4 : 0) /*in norm*/ + nl * per_layer + rel_bytes;
   struct Owner {
     void* p = nullptr;
     ~Owner() { if (p) (void)hipFree(p); }
@@ -1617,7 +1665,7 @@ int DGLMIRgcnPrepare(const DGLMIGraph* graph, const int32_t* etypes, const DGLMI
   if (norm) launch_gather_f32(norm->data, in.data, E, in_norm, s);
   DGLMIGraph z = no_workspace();
   for (int layer = 0; layer < 2; ++layer) {
-    if (!((layers >> layer) & 1)) continue;
+    if (!(layer == 0 ? want0 : want1)) continue;
     const int64_t mul = layer == 0 ? N : R;
     int32_t* cols = reinterpret_cast<int32_t*>(take(e4));
     int32_t* ptr = reinterpret_cast<int32_t*>(take(ptr4));
@@ -1646,6 +1694,34 @@ int DGLMIRgcnPrepare(const DGLMIGraph* graph, const int32_t* etypes, const DGLMI
     c.data = dat;
     c.rows = rows;
     state->out_norm[layer] = onorm;
+  }
+  if (want_rel) {
+    // the in-CSR regrouped by etypes[e] * N_dst + v: one relation's rows of a tile of
+    // destinations are contiguous for the fused kernel
+    const int64_t nd = in.num_rows;
+    int32_t* ptr = reinterpret_cast<int32_t*>(take(ptr_rel));
+    int32_t* idx = reinterpret_cast<int32_t*>(take(e4));
+    int32_t* dat = reinterpret_cast<int32_t*>(take(e4));
+    int32_t* rows = reinterpret_cast<int32_t*>(take(e4));
+    float* rnorm = norm ? reinterpret_cast<float*>(take(e4)) : nullptr;
+    const int64_t ws_bytes = DGLMICOOToCSRDeviceWorkspaceBytes(R * nd, E);
+    Scratch keys(&z, E * 4, s), ws(&z, ws_bytes, s);
+    launch_typed_ids(in.rows, in.data, etypes, E, nd, 0, static_cast<int32_t*>(keys.ptr), s);
+    DGLMI_CHECK(DGLMICOOToCSRDevice(R * nd, E, static_cast<int32_t*>(keys.ptr), in.indices, in.data,
+                                    ptr, idx, dat, ws.ptr, ws_bytes, s) == 0,
+                std::string("relation-major CSR build: ") + g_last_error);
+    DGLMI_CHECK(DGLMICSRExpandRows(ptr, R * nd, E, rows, s) == 0,
+                std::string("relation-major CSR rows: ") + g_last_error);
+    if (norm) launch_gather_f32(norm->data, dat, E, rnorm, s);
+    DGLMICsr& c = state->in_rel;
+    c.num_rows = R * nd;
+    c.num_cols = in.num_cols;
+    c.nnz = E;
+    c.indptr = ptr;
+    c.indices = idx;
+    c.data = dat;
+    c.rows = rows;
+    state->in_rel_norm = rnorm;
   }
   check_hip(hipGetLastError(), "rgcn prepare launch");
   state->etypes = etypes;

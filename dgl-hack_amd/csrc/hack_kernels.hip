@@ -307,6 +307,145 @@ __global__ void __launch_bounds__(kGemmThreads) k_gemm_tn(const float* __restric
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fused R-GCN layer 1: aggregate each relation's rows first, transform after, in one
+// kernel.  out[v] = sum_t (sum_{e = (u -> v), type t} w_e T[u]) . W_t: every wave owns
+// 32-row tiles of out (strided over the grid); for each relation t it gathers the 32
+// rows' relation-t sums of T (64-float rows, 16 lanes per row, 8 rows per 16-lane
+// group, 8 gathers in flight per lane) into its private LDS slot, and one MFMA pass
+// (v_mfma_f32_32x32x2_f32) adds slot . W_t into the tile's accumulators; W (all
+// relations, <= 64 KB) sits in LDS for the block's life.  No Y = T . W_cat table
+// (5.1 GB on C5) is written or gathered: the gathers read T (1.3 GB) and the only HBM
+// write is the output.  Walks the relation-major CSR (rows t * num_rows + v, the
+// prepared state's in_rel / out_typed[0]), whose rows of one relation and tile are
+// contiguous.  Deterministic: each row's edges in position order, then relations
+// and k in order.  BWD: the same walk over the relation-major out-CSR gathers
+// grad_out rows into G_t (stored to gy for the weight gradient) and adds
+// G_t . W_t^T into grad_hidden.  The weights enter as W[t][k][n] =
+// W_src[t * ws_t + k * ws_k + n * ws_n] (k over the gathered width 64).
+constexpr int kFusedW = 64;  // gathered row width (floats)
+constexpr int kSlotStride = kFusedW + 1;
+
+template <bool BWD, int NB>
+__global__ void __launch_bounds__(kGemmThreads) k_rgcn_fused(
+    const int32_t* __restrict__ ptr, const int32_t* __restrict__ cols,
+    const int32_t* __restrict__ rows, const int32_t* __restrict__ eids, const float* __restrict__ w,
+    const float* __restrict__ T, const float* __restrict__ W, int64_t ws_t, int64_t ws_k,
+    int64_t ws_n, float* __restrict__ out, float* __restrict__ gy, int64_t num_rows, int R,
+    int out_w) {
+  constexpr int SW = NB * 32;
+  __shared__ float Ws[16384];
+  __shared__ float slots[8][32 * kSlotStride];
+  for (int i = threadIdx.x; i < R * kFusedW * SW; i += kGemmThreads) {
+    const int t = i / (kFusedW * SW), k = (i / SW) % kFusedW, n = i % SW;
+    Ws[i] = n < out_w ? W[t * ws_t + k * ws_k + n * ws_n] : 0.0f;
+  }
+  __syncthreads();  // the only block barrier
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r = lane & 31, hb = lane >> 5;
+  const int g = lane >> 4, q = lane & 15;  // 16-lane group, float4 column
+  float* slot = slots[wv];
+  const int64_t tiles = (num_rows + 31) / 32;
+  const int64_t step = static_cast<int64_t>(gridDim.x) * 8;
+  for (int64_t tile = static_cast<int64_t>(blockIdx.x) * 8 + wv; tile < tiles; tile += step) {
+    const int64_t v0 = tile * 32;
+    f32x16 acc[NB];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x16{};
+    for (int t = 0; t < R; ++t) {
+      // zero this group's 8 slot rows, then gather their relation-t sums
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float* d = slot + (8 * g + i) * kSlotStride + 4 * q;
+        d[0] = d[1] = d[2] = d[3] = 0.0f;
+      }
+      const int64_t vg = v0 + 8 * g;
+      const int cnt = vg < num_rows ? static_cast<int>(num_rows - vg < 8 ? num_rows - vg : 8) : 0;
+      const int64_t base = static_cast<int64_t>(t) * num_rows + vg;
+      const int64_t pb = cnt > 0 ? ptr[base] : 0, pe = cnt > 0 ? ptr[base + cnt] : 0;
+      float4 a4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      int cur = -1;
+      for (int64_t p = pb; p < pe; p += 16) {
+        const int n = pe - p < 16 ? static_cast<int>(pe - p) : 16;
+        int my_col = 0, my_row = -1;
+        float my_w = 0.0f;
+        if (q < n) {
+          my_col = cols[p + q];
+          my_row = static_cast<int>(rows[p + q] - base);
+          my_w = w[eids ? eids[p + q] : p + q];
+        }
+#pragma unroll
+        for (int j0 = 0; j0 < 16; j0 += 8) {
+          float4 x[8];
+          float wj[8];
+          int rj[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int c = __shfl(my_col, j0 + u, 16);
+            rj[u] = __shfl(my_row, j0 + u, 16);
+            wj[u] = __shfl(my_w, j0 + u, 16);
+            x[u] = *reinterpret_cast<const float4*>(T + static_cast<int64_t>(c) * kFusedW + 4 * q);
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            if (rj[u] < 0) break;  // past the batch (group-uniform)
+            if (rj[u] != cur) {
+              if (cur >= 0) {
+                float* d = slot + (8 * g + cur) * kSlotStride + 4 * q;
+                d[0] = a4.x; d[1] = a4.y; d[2] = a4.z; d[3] = a4.w;
+              }
+              a4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+              cur = rj[u];
+            }
+            a4.x += wj[u] * x[u].x;
+            a4.y += wj[u] * x[u].y;
+            a4.z += wj[u] * x[u].z;
+            a4.w += wj[u] * x[u].w;
+          }
+        }
+      }
+      if (cur >= 0) {
+        float* d = slot + (8 * g + cur) * kSlotStride + 4 * q;
+        d[0] = a4.x; d[1] = a4.y; d[2] = a4.z; d[3] = a4.w;
+      }
+      wave_lds_sync();
+      if constexpr (BWD) {
+        // G_t rows -> gy[v][t * 64 + c] (the weight gradient's operand)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (i >= cnt) break;
+          const float* s = slot + (8 * g + i) * kSlotStride + 4 * q;
+          float* d = gy + (vg + i) * (static_cast<int64_t>(R) * kFusedW) + t * kFusedW + 4 * q;
+          __builtin_nontemporal_store(s[0], d);
+          __builtin_nontemporal_store(s[1], d + 1);
+          __builtin_nontemporal_store(s[2], d + 2);
+          __builtin_nontemporal_store(s[3], d + 3);
+        }
+      }
+      const float* wt = Ws + t * kFusedW * SW;
+#pragma unroll
+      for (int kk = 0; kk < kFusedW; kk += 2) {
+        const float a = slot[r * kSlotStride + kk + hb];
+        const float* brow = wt + (kk + hb) * SW + r;
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+          acc[nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, brow[nb * 32], acc[nb], 0, 0, 0);
+      }
+      wave_lds_sync();  // the slot is read; the next relation may overwrite it
+    }
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int64_t m = v0 + (reg & 3) + 8 * (reg >> 2) + 4 * hb;
+      if (m >= num_rows) continue;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const int n = nb * 32 + r;
+        if (n < out_w) __builtin_nontemporal_store(acc[nb][reg], out + m * out_w + n);
+      }
+    }
+  }
+}
+
 // out[i] = sum over z (in order) of parts[z * n + i]
 __global__ void k_sum_splits(const float* __restrict__ parts, int splits, int64_t n,
                              float* __restrict__ out) {
@@ -425,6 +564,36 @@ bool try_tn(const float* A, int64_t a_rs, int64_t a_cs, const float* B, int64_t 
 }
 
 }  // namespace
+
+bool rgcn_fused_ok(int64_t gathered_w, int64_t out_w, int64_t R) {
+  if (gathered_w != kFusedW || out_w < 1 || out_w > 128 || R < 1) return false;
+  const int64_t nb = out_w <= 32 ? 1 : (out_w <= 64 ? 2 : 4);
+  return R * kFusedW * nb * 32 <= 16384;
+}
+
+void launch_rgcn_fused(bool bwd, const int32_t* ptr, const int32_t* cols, const int32_t* rows,
+                       const int32_t* eids, const float* w, const float* T, const float* W,
+                       int64_t ws_t, int64_t ws_k, int64_t ws_n, float* out, float* gy,
+                       int64_t num_rows, int64_t R, int64_t out_w, hipStream_t s) {
+  if (num_rows <= 0) return;
+  const int64_t tiles = (num_rows + 31) / 32;
+  const int64_t want = (tiles + 7) / 8;
+  const dim3 grid(static_cast<unsigned>(want < 256 ? want : 256)), block(kGemmThreads);
+  const int Ri = static_cast<int>(R), ow = static_cast<int>(out_w);
+#define DGLMI_RGCN_FUSED(B_, NB_)                                                               \
+  hipLaunchKernelGGL((k_rgcn_fused<B_, NB_>), grid, block, 0, s, ptr, cols, rows, eids, w, T, W, \
+                     ws_t, ws_k, ws_n, out, gy, num_rows, Ri, ow)
+  if (bwd) {
+    if (out_w <= 32) DGLMI_RGCN_FUSED(true, 1);
+    else if (out_w <= 64) DGLMI_RGCN_FUSED(true, 2);
+    else DGLMI_RGCN_FUSED(true, 4);
+  } else {
+    if (out_w <= 32) DGLMI_RGCN_FUSED(false, 1);
+    else if (out_w <= 64) DGLMI_RGCN_FUSED(false, 2);
+    else DGLMI_RGCN_FUSED(false, 4);
+  }
+#undef DGLMI_RGCN_FUSED
+}
 
 void launch_gemm(const float* A, int64_t a_rs, int64_t a_cs, const float* B, int64_t b_rs,
                  int64_t b_cs, float* C, int64_t M, int64_t N, int64_t K, int64_t splits,

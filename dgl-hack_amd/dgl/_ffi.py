@@ -65,6 +65,8 @@ class RgcnState(ctypes.Structure):
         ("in_norm", ctypes.c_void_p),
         ("out_typed", CSR * 2),
         ("out_norm", ctypes.c_void_p * 2),
+        ("in_rel", CSR),
+        ("in_rel_norm", ctypes.c_void_p),
         ("owner", ctypes.c_void_p),
     ]
 

@@ -429,15 +429,18 @@ class RgcnState:
             return False
         if self.norm is not None and norm is self.norm and norm._version != self.versions[1]:
             return False
-        return int(num_rels) == self.num_rels and bool((self.layers >> layer) & 1)
+        usable = (self.layers >> layer) & 1 or (layer == 1 and self.layers & 4)
+        return int(num_rels) == self.num_rels and bool(usable)
 
 
-def rgcn_prepare(graph, etypes, norm, num_rels, layers=3):
+def rgcn_prepare(graph, etypes, norm, num_rels, layers=7):
     """DGLMIRgcnPrepare: build the R-GCN state of ``graph`` for ``etypes`` (int32,
     one per edge id) and ``norm`` (one float per edge id, or None) once; later
     rgcn_layer* calls on this graph with these same tensors use it (layers bit 0:
-    Layer0 and its backward, bit 1: Layer1 and its backward).  Writing into etypes
-    or norm in place invalidates it (the next call derives everything per call)."""
+    Layer0 and its backward, bit 1: Layer1 and its backward, bit 2: the fused
+    Layer1 kernels for 64-wide gathered rows -- equal to the unfused path up to fp32
+    rounding).  Writing into etypes or norm in place invalidates it (the next call
+    derives everything per call)."""
     st = RgcnState(graph, etypes, norm, num_rels, layers)
     graph.__dict__["_rgcn_state"] = st
     return st

@@ -318,7 +318,12 @@ int DGLMIEdgeSoftmaxBackward(const DGLMIGraph* graph, const DGLMIArray* out,
  *     and the out-CSR regrouped by that key;
  *   layers bit 1 (Layer1 / Layer1Backward): the in-CSR columns u * R + etypes[e]
  *     and the out-CSR regrouped by that key;
- * and norm permuted into each walk's position order, so the gathers stream it.
+ * and norm permuted into each walk's position order, so the gathers stream it;
+ *   layers bit 2 (fused Layer1 / Layer1Backward): the in-CSR regrouped by
+ *     etypes[e] * N_dst + v (relation-major; the out-CSR regrouped by etypes[e] * N_src + u
+ *     is out_typed[0], built for bit 0 or bit 2): the fused kernels aggregate each
+ *     relation's rows and multiply by W_t in one pass (64-wide gathered rows, outputs
+ *     <= 128 wide); results then match the unfused path to fp32 rounding, not bit for bit.
  * Set DGLMIGraph.rgcn to the state; an entry uses it when graph->rgcn->etypes ==
  * etypes, num_rels and the source count match and the layer's bit is set, and
  * uses the cached norm copies only when norm->data == graph->rgcn->norm -- a caller
@@ -338,6 +343,8 @@ typedef struct DGLMIRgcnState {
   const float* in_norm;        /* norm[in_csr.data[p]] (NULL when no norm was cached) */
   DGLMICsr out_typed[2];       /* out-CSR regrouped by the key of in_cols[i]; data = edge ids */
   const float* out_norm[2];    /* norm per position of out_typed[i] */
+  DGLMICsr in_rel;             /* in-CSR regrouped by etypes[e] * N_dst + v; data = edge ids */
+  const float* in_rel_norm;    /* norm per position of in_rel */
   void* owner;                 /* library-private */
 } DGLMIRgcnState;
 int DGLMIRgcnPrepare(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* norm,

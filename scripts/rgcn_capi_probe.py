@@ -53,6 +53,8 @@ def main():
     if "--capi-only" in sys.argv:  # for rocprofv3 kernel statistics
         if "--prepared" in sys.argv:
             K.rgcn_prepare(gidx, et32, norm, R, layers=2)
+        if "--fused" in sys.argv:
+            K.rgcn_prepare(gidx, et32, norm, R, layers=4)
         for _ in range(3):
             K.rgcn_layer1(gidx, et32, h, W, norm, ret)
             K.rgcn_layer1_backward(gidx, et32, h, W, norm, go, gh, gw)
@@ -88,6 +90,14 @@ def main():
         lambda: K.rgcn_layer0_backward(gidx, et32, r0, norm, gw0))
     res["prepared_bit_identical"] = all(bool(th.equal(a, b)) for a, b in
                                         zip(ref, (ret, gh, gw, r0, gw0)))
+    # fused layer-1 kernels (state bit 2): aggregate per relation, then W_t, in one pass
+    K.rgcn_prepare(gidx, et32, norm, R, layers=7)
+    res["fused_layer1_ms"] = ktime(lambda: K.rgcn_layer1(gidx, et32, h, W, norm, ret))
+    res["fused_layer1_backward_ms"] = ktime(
+        lambda: K.rgcn_layer1_backward(gidx, et32, h, W, norm, go, gh, gw))
+    res["fused_layer1_fwd_bwd_ms"] = res["fused_layer1_ms"] + res["fused_layer1_backward_ms"]
+    rel = lambda a, b: float((a - b).abs().max() / b.abs().max().clamp(min=1e-30))
+    res["fused_max_rel_diff_vs_unfused"] = max(rel(ret, ref[0]), rel(gh, ref[1]), rel(gw, ref[2]))
     print(json.dumps(res), flush=True)
 
 

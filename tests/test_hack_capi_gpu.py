@@ -76,15 +76,29 @@ def test_rgcn_layer1_tall_gemms(K_in, X):
     _layer1_fwd_bwd(K_in, X, False, 40001, 200000)
 
 
-def _layer1_fwd_bwd(K_in, X, hub, n, m):
+@pytest.mark.parametrize("X,R,hub,cached_norm", [(64, 4, False, True), (64, 4, True, False),
+                                                 (32, 2, False, True), (100, 2, True, True)])
+def test_rgcn_layer1_fused(X, R, hub, cached_norm):
+    """The fused layer-1 kernels (prepared state bit 2: relation-major CSRs; each
+    relation's rows aggregated into LDS, then one MFMA pass by W_t -- no Y = X W_cat
+    table): forward and both gradients vs the fp64 restatement and the Python path,
+    with the norm streamed from the state or gathered by edge id."""
+    _layer1_fwd_bwd(64, X, hub, 40001, 200000, R=R, prepare=4, cached_norm=cached_norm)
+
+
+def _layer1_fwd_bwd(K_in, X, hub, n, m, R=4, prepare=0, cached_norm=True):
     from dgl import kernel as K
-    R = 4
     g, gidx, s, d, et, norm = _graph(n, m, R, seed=K_in + X, hub=hub)
     n = g.number_of_nodes()
+    gidx.__dict__.pop("_rgcn_state", None)
+    et32 = et.int()
+    if prepare:
+        K.rgcn_prepare(gidx, et32, norm if cached_norm else None, R, layers=prepare)
+        assert gidx._rgcn_state.matches(et32, norm, R, 1)
     h = th.randn(n, K_in, device=DEV)
     w = th.randn(R, K_in, X, device=DEV) / 4
     ret = th.full((n, X), float("nan"), device=DEV)
-    K.rgcn_layer1(gidx, et.int(), h, w, norm, ret)
+    K.rgcn_layer1(gidx, et32, h, w, norm, ret)
     msg = th.einsum("ek,ekx->ex", h.double()[s], w.double()[et]) * norm.double()
     ref = th.zeros(n, X, dtype=th.float64, device=DEV).index_add_(0, d, msg)
     mass = th.zeros(n, X, dtype=th.float64, device=DEV).index_add_(0, d, msg.abs())
@@ -92,22 +106,32 @@ def _layer1_fwd_bwd(K_in, X, hub, n, m):
     go = th.randn(n, X, device=DEV)
     gh = th.full((n, K_in), float("nan"), device=DEV)
     gw = th.full((R, K_in, X), float("nan"), device=DEV)
-    K.rgcn_layer1_backward(gidx, et.int(), h, w, norm, go, gh, gw)
+    K.rgcn_layer1_backward(gidx, et32, h, w, norm, go, gh, gw)
+    gidx.__dict__.pop("_rgcn_state", None)
     gmsg = go.double()[d] * norm.double()                        # (E, X)
     gh_ref = th.zeros(n, K_in, dtype=th.float64, device=DEV).index_add_(
         0, s, th.einsum("ex,ekx->ek", gmsg, w.double()[et]))
     gw_ref = th.zeros(R, K_in, X, dtype=th.float64, device=DEV).index_add_(
         0, et, th.einsum("ek,ex->ekx", h.double()[s], gmsg))
     th.testing.assert_close(gh.double(), gh_ref, rtol=1e-4, atol=1e-4)
-    th.testing.assert_close(gw.double(), gw_ref, rtol=1e-4, atol=2e-4)
+    # the weight gradient sums tens of thousands of terms per entry: the bound scales
+    # with their absolute mass, as for the other long fp32 sums
+    gw_mass = th.zeros(R, K_in, X, dtype=th.float64, device=DEV).index_add_(
+        0, et, th.einsum("ek,ex->ekx", h.double()[s].abs(), gmsg.abs()))
+    assert ((gw.double() - gw_ref).abs() <= 2e-4 + 1e-6 * gw_mass).all(), \
+        float(((gw.double() - gw_ref).abs() / (2e-4 + 1e-6 * gw_mass)).max())
     # the Python path (GEMM + typed gather, autograd) agrees
     from dgl import backend as B
     hr, wr = h.clone().requires_grad_(), w.clone().requires_grad_()
     out = B.rgcn_layer1(g, hr, wr, norm, et)
     out.backward(go)
-    th.testing.assert_close(out.detach(), ret, rtol=1e-4, atol=1e-4)
-    th.testing.assert_close(hr.grad, gh, rtol=1e-4, atol=1e-4)
-    th.testing.assert_close(wr.grad, gw, rtol=1e-4, atol=2e-4)
+    # (two fp32 summation orders, e.g. the fused path's aggregate-then-transform:
+    # bounds scaled by the absolute mass of the sums, as against fp64 above)
+    gh_mass = th.zeros(n, K_in, dtype=th.float64, device=DEV).index_add_(
+        0, s, th.einsum("ex,ekx->ek", gmsg.abs(), w.double()[et].abs()))
+    assert ((out.detach().double() - ret.double()).abs() <= 2e-4 + 2e-5 * mass).all()
+    assert ((hr.grad.double() - gh.double()).abs() <= 2e-4 + 2e-5 * gh_mass).all()
+    assert ((wr.grad.double() - gw.double()).abs() <= 4e-4 + 2e-6 * gw_mass).all()
 
 
 def test_rgcn_gemm_split_k_large_n():
@@ -210,7 +234,7 @@ def test_rgcn_prepare_rejects_bad_arguments():
     from dgl._ffi import DGLError
     g, gidx, s, d, et, norm = _graph(100, 500, 2, seed=1)
     with pytest.raises(DGLError, match="layers"):
-        K.RgcnState(gidx, et.int(), norm, 2, 4)
+        K.RgcnState(gidx, et.int(), norm, 2, 8)
     with pytest.raises(DGLError, match="norm"):
         K.RgcnState(gidx, et.int(), norm[:10], 2, 3)
     with pytest.raises(DGLError, match="etypes"):
