@@ -290,3 +290,111 @@ def edge_softmax(g, score):
     out_sum = copy_reduce("sum", g, EDGE, out, g.n)
     with np.errstate(invalid="ignore", divide="ignore"):
         return binary_op_reduce_raw("none", "div", g, EDGE, DST, out, out_sum, g.m)
+
+
+# --------------------------------------------------------------------------- #
+# The hack's GPU-only entry points (oracle/hack_ref.c)
+# --------------------------------------------------------------------------- #
+def _f32c(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def csr_sorted_by_edge_type(src, dst, etypes, num_nodes, num_types, transpose):
+    """``Graph::GetCsrSortedByEdgeType`` (``src/graph/graph.cc:690-746``): the
+    adjacency lists of a mutable graph (insertion = edge-id order per node) with every
+    row's entries ordered by edge type.  transpose=False: in-edges (rows = destinations,
+    ids = sources); True: out-edges (rows = sources, ids = destinations)."""
+    rows, ids = (_i64(src), _i64(dst)) if transpose else (_i64(dst), _i64(src))
+    indptr, cols, eids = coo_to_csr(num_nodes, rows, ids)
+    et = _i64(etypes)
+    o_ids, o_eids, o_types = (np.empty_like(cols) for _ in range(3))
+    rc = lib().hack_sort_rows_by_type(ctypes.c_int64(num_nodes), _p(indptr), _p(cols), _p(eids),
+                                      _p(et), ctypes.c_int64(num_types), _p(o_ids), _p(o_eids),
+                                      _p(o_types))
+    if rc != 0:
+        raise ValueError("edge type out of range")
+    return indptr, o_ids, o_eids, o_types
+
+
+def hack_fused_gat(src, dst, num_nodes, feat_src, el, er, slope):
+    """``FusedGatKernelImpl`` (``binary_reduce_impl.cu:47-112``) on the in-CSR of the
+    graph's immutable index (``CSRTranspose`` of the out-CSR, as ``get_immutable_gidx``
+    builds it).  Returns (exp (E,H), sum (N,H), ret (N,H,D))."""
+    g = RefGraph(src, dst, num_nodes)
+    fs, el, er = _f32c(feat_src), _f32c(el), _f32c(er)
+    n, H, D = fs.shape[0], el.reshape(el.shape[0], -1).shape[1], fs.shape[-1]
+    indptr, indices, data = g.in_csr
+    exp = np.empty((g.m, H), np.float32)
+    s = np.empty((n, H), np.float32)
+    ret = np.empty((n, H, D), np.float32)
+    lib().hack_fused_gat(ctypes.c_int64(n), _p(indptr), _p(indices), _p(data), ctypes.c_int64(H),
+                         ctypes.c_int64(D), _p(fs), _p(el), _p(er), ctypes.c_float(slope), _p(exp),
+                         _p(s), _p(ret))
+    return exp, s, ret
+
+
+def hack_fused_gat_backward(src, dst, num_nodes, feat_src, el, er, s, exp, ret, grad_out, slope):
+    """``BackwardFusedGatKernelImpl`` (``binary_reduce_impl.cu:1248-1308``) on the
+    out-CSR.  Returns (grad_feat_src, grad_el, grad_er)."""
+    g = RefGraph(src, dst, num_nodes)
+    fs, el, er = _f32c(feat_src), _f32c(el), _f32c(er)
+    s, exp, ret, go = _f32c(s), _f32c(exp), _f32c(ret), _f32c(grad_out)
+    n, H, D = fs.shape[0], s.shape[1], fs.shape[-1]
+    indptr, indices, data = g.out_csr
+    gfs = np.empty_like(fs)
+    gel = np.zeros((n, H), np.float32)
+    ger = np.zeros((n, H), np.float32)
+    lib().hack_fused_gat_backward(ctypes.c_int64(n), _p(indptr), _p(indices), _p(data),
+                                  ctypes.c_int64(H), ctypes.c_int64(D), _p(fs), _p(el), _p(er),
+                                  _p(s), _p(exp), _p(ret), _p(go), ctypes.c_float(slope), _p(gfs),
+                                  _p(gel), _p(ger))
+    return gfs, gel.reshape(el.shape), ger.reshape(er.shape)
+
+
+def hack_rgcn_layer0(src, dst, etypes, num_nodes, weight, norm):
+    """``RgcnLayer0Impl`` (``binary_reduce_impl.cu:913-980``): weight (R, N, F)."""
+    w, nm = _f32c(weight), _f32c(norm).reshape(-1)
+    R, F = w.shape[0], w.shape[2]
+    ranges, ids, eids, types = csr_sorted_by_edge_type(src, dst, etypes, num_nodes, R, False)
+    ret = np.empty((num_nodes, F), np.float32)
+    lib().hack_rgcn_layer0(ctypes.c_int64(num_nodes), _p(ranges), _p(ids), _p(eids), _p(types),
+                           _p(w), ctypes.c_int64(w.shape[1]), ctypes.c_int64(F), _p(nm), _p(ret))
+    return ret
+
+
+def hack_rgcn_layer0_backward(src, dst, etypes, num_nodes, grad_out, norm, num_rels,
+                              accumulate=True):
+    """``RgcnLayer0BackwardImpl`` (``:982-1047``); ``accumulate=False`` keeps the
+    reference's store (repeated (source, relation) pairs keep the last edge)."""
+    go, nm = _f32c(grad_out), _f32c(norm).reshape(-1)
+    F = go.shape[1]
+    ranges, ids, eids, types = csr_sorted_by_edge_type(src, dst, etypes, num_nodes, num_rels, True)
+    gw = np.zeros((num_rels, num_nodes, F), np.float32)
+    lib().hack_rgcn_layer0_backward(ctypes.c_int64(num_nodes), _p(ranges), _p(ids), _p(eids),
+                                    _p(types), _p(go), _p(nm), ctypes.c_int64(F),
+                                    ctypes.c_int(1 if accumulate else 0), _p(gw))
+    return gw
+
+
+def hack_rgcn_layer1(src, dst, etypes, num_nodes, hidden, weight, norm):
+    """``RgcnLayer1Impl`` (``:1082-1155``): hidden (N, Y), weight (R, Y, X)."""
+    h, w, nm = _f32c(hidden), _f32c(weight), _f32c(norm).reshape(-1)
+    R, Y, X = w.shape
+    ranges, ids, eids, types = csr_sorted_by_edge_type(src, dst, etypes, num_nodes, R, False)
+    ret = np.zeros((num_nodes, X), np.float32)
+    lib().hack_rgcn_layer1(ctypes.c_int64(num_nodes), _p(ranges), _p(ids), _p(eids), _p(types),
+                           _p(h), _p(w), ctypes.c_int64(Y), ctypes.c_int64(X), _p(nm), _p(ret))
+    return ret
+
+
+def hack_rgcn_layer1_backward(src, dst, etypes, num_nodes, hidden, weight, norm, grad_out):
+    """``RgcnLayer1BackwardImpl`` (``:1157-1245``).  Returns (grad_hidden, grad_weight)."""
+    h, w, nm, go = _f32c(hidden), _f32c(weight), _f32c(norm).reshape(-1), _f32c(grad_out)
+    R, Y, X = w.shape
+    ranges, ids, eids, types = csr_sorted_by_edge_type(src, dst, etypes, num_nodes, R, True)
+    gh = np.zeros((num_nodes, Y), np.float32)
+    gw = np.zeros((R, Y, X), np.float32)
+    lib().hack_rgcn_layer1_backward(ctypes.c_int64(num_nodes), _p(ranges), _p(ids), _p(eids),
+                                    _p(types), _p(h), _p(w), ctypes.c_int64(Y), ctypes.c_int64(X),
+                                    _p(nm), _p(go), _p(gh), _p(gw))
+    return gh, gw
