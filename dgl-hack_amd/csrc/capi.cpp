@@ -183,20 +183,45 @@ Bcast calc_bcast(int op, const DGLMIArray* lhs, const DGLMIArray* rhs, std::vect
   return b;
 }
 
+// 32: every index array int32 (the reference GPU envelope, common.h:62-69); 64: a
+// graph of 2^31 or more edges, whose indptr and data (edge ids) hold int64 -- the
+// width the reference's CPU kernels switch to (graph_index.py:941-952,
+// cpu/binary_reduce_sum.cc:15-23) -- while node ids (indices, rows, COO) stay int32.
 void check_graph(const DGLMIGraph* g) {
   DGLMI_CHECK(g != nullptr, "null graph");
-  if (g->num_bits != 32)
-    throw Error("Unsupported idx bits: " + std::to_string(g->num_bits));  // common.h:62-69
+  if (g->num_bits != 32 && g->num_bits != 64)
+    throw Error("Unsupported idx bits: " + std::to_string(g->num_bits));
 }
 
-void check_csr(const DGLMICsr& c, const char* which, bool need_rows) {
+// Entry points built for int32 graphs only (the hack's kernels are int32-only,
+// binary_reduce_impl.cu: typedef int32_t Idx).
+void check_graph32(const DGLMIGraph* g, const char* what) {
+  check_graph(g);
+  if (g->num_bits != 32)
+    throw Error(std::string(what) + " needs a graph of fewer than 2^31 edges (idx bits 32)");
+}
+
+bool wide(const DGLMIGraph* g) { return g->num_bits == 64; }
+
+IdxPtr idx(const DGLMIGraph* g, const int32_t* p) { return IdxPtr{p, wide(g) ? 1 : 0}; }
+
+void check_csr(const DGLMICsr& c, const char* which, bool need_rows, bool wide_ok = false) {
   if (c.num_rows < 0 || c.nnz < 0) throw Error(std::string("bad CSR sizes: ") + which);
   if (c.indptr == nullptr) throw Error(std::string("null indptr: ") + which);
   if (c.nnz > 0 && (c.indices == nullptr || c.data == nullptr))
     throw Error(std::string("null CSR arrays: ") + which);
   if (need_rows && c.nnz > 0 && c.rows == nullptr)
     throw Error(std::string("CSR row ids (rows) required: ") + which);
-  if (c.nnz > INT32_MAX || c.num_rows > INT32_MAX) throw Error("graph exceeds int32 indexing");
+  if (c.num_rows > INT32_MAX || c.num_cols > INT32_MAX)
+    throw Error("graph exceeds int32 node ids");
+  if (!wide_ok && c.nnz > INT32_MAX)
+    throw Error("graph exceeds int32 indexing (2^31 or more edges need idx bits 64)");
+}
+
+// Mappings index by edge id and name rows of int32 range: not for 64-bit graphs.
+void check_maps(const DGLMIGraph* g, const int32_t* a, const int32_t* b, const int32_t* c) {
+  if (wide(g) && (a || b || c))
+    throw Error("node / edge mappings need a graph of fewer than 2^31 edges (idx bits 32)");
 }
 
 int role_of(int target, bool walk_in) {
@@ -317,7 +342,7 @@ void run_fast(const DGLMIGraph* g, const DGLMICsr& walk, int kind, int red, cons
   // copy_u only: with an edge operand (u_mul_e) its per-edge gather by edge id
   // dominates and extra passes cost more than the smaller table saves (Reddit-size,
   // F = 64: copy_u_sum 3.88 -> 2.96 ms over 8 blocks, u_mul_e_sum 5.94 -> 7.23 ms)
-  if (g->num_col_blocks > 1 && red == RED_SUM && x_map == nullptr && walk.nnz > 0 &&
+  if (g->num_col_blocks > 1 && !wide(g) && red == RED_SUM && x_map == nullptr && walk.nnz > 0 &&
       kind == FAST_COPY_COL) {
     const DGLMICsr* blocks = &walk == &g->in_csr ? g->in_col_blocks
                              : (&walk == &g->out_csr ? g->out_col_blocks : nullptr);
@@ -333,10 +358,10 @@ void run_fast(const DGLMIGraph* g, const DGLMICsr& walk, int kind, int red, cons
   }
   FastArgs a;
   std::memset(&a, 0, sizeof(a));
-  a.indptr = walk.indptr;
+  a.indptr = idx(g, walk.indptr);
   a.rows = walk.rows;
   a.indices = walk.indices;
-  a.eids = walk.data;
+  a.eids = idx(g, walk.data);
   a.nnz = walk.nnz;
   a.num_rows = walk.num_rows;
   a.x = x;
@@ -400,21 +425,21 @@ SddmmArgs sddmm_items(const DGLMIGraph* g, const DGLMICsr& walk, bool edge_opera
   if (coo) {
     e.rows = g->coo_dst;
     e.cols = g->coo_src;
-    e.eids = nullptr;
+    e.eids = IdxPtr{nullptr, 0};
   } else {
     e.rows = walk.rows;
     e.cols = walk.indices;
-    e.eids = walk.data;
+    e.eids = idx(g, walk.data);
   }
   return e;
 }
 
-EdgeArgs base_args(const DGLMICsr& walk) {
+EdgeArgs base_args(const DGLMIGraph* g, const DGLMICsr& walk) {
   EdgeArgs a;
   std::memset(&a, 0, sizeof(a));
-  a.indptr = walk.indptr;
+  a.indptr = idx(g, walk.indptr);
   a.indices = walk.indices;
-  a.eids = walk.data;
+  a.eids = idx(g, walk.data);
   a.rows = walk.rows;
   a.num_rows = walk.num_rows;
   a.nnz = walk.nnz;
@@ -432,6 +457,7 @@ void forward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const D
   if (epi && !epi->row_mul && !epi->row_div && !epi->bias && !epi->addend) epi = nullptr;
   DGLMI_CHECK(epi == nullptr || red == RED_SUM, "a fused epilogue needs the sum reducer");
   check_graph(g);
+  check_maps(g, lhs_map, rhs_map, out_map);
   check_array(lhs, "lhs");
   check_array(out, "out");
   DGLMI_CHECK(lhs_t >= 0 && lhs_t <= 2, "bad lhs target");
@@ -446,7 +472,7 @@ void forward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const D
     }
   }
   const DGLMICsr& walk = g->in_csr;  // reductions go to dst; edges enumerated on the in-CSR
-  check_csr(walk, "in_csr", red == RED_NONE || true);
+  check_csr(walk, "in_csr", red == RED_NONE || true, wide(g));
 
   bool bc = false;
   Bcast binfo;
@@ -533,7 +559,7 @@ void forward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const D
   }
 
   // ---- generic path (load-balanced for reductions) ----
-  EdgeArgs a = base_args(walk);
+  EdgeArgs a = base_args(g, walk);
   a.lhs = Operand{lhs->data, lhs_map, role_of(lhs_t, true)};
   if (op == OP_USE_LHS) a.rhs = Operand{nullptr, nullptr, ROLE_NONE};
   else a.rhs = Operand{rhs->data, rhs_map, role_of(rhs_t, true)};
@@ -572,6 +598,7 @@ void backward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const 
               const DGLMIArray* rhs, const DGLMIArray* out, const DGLMIArray* grad_out,
               DGLMIArray* grad, int want, hipStream_t s) {
   check_graph(g);
+  check_maps(g, lhs_map, rhs_map, out_map);
   check_array(lhs, "lhs");
   check_array(out, "out");
   check_array(grad_out, "grad_out");
@@ -593,7 +620,7 @@ void backward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const 
   const int x_t = want == 0 ? lhs_t : rhs_t;
   const bool walk_in = x_t != DGLMI_TARGET_SRC;  // src grads are owned by out-CSR rows
   const DGLMICsr& walk = walk_in ? g->in_csr : g->out_csr;
-  check_csr(walk, walk_in ? "in_csr" : "out_csr", x_t == DGLMI_TARGET_EDGE);
+  check_csr(walk, walk_in ? "in_csr" : "out_csr", x_t == DGLMI_TARGET_EDGE, wide(g));
 
   bool bc = false;
   Bcast binfo;
@@ -693,7 +720,7 @@ void backward(int red, int op, const DGLMIGraph* g, int lhs_t, int rhs_t, const 
     return;
   }
 
-  EdgeArgs a = base_args(walk);
+  EdgeArgs a = base_args(g, walk);
   a.lhs = Operand{lhs->data, lhs_map, role_of(lhs_t, walk_in)};
   if (op == OP_USE_LHS) a.rhs = Operand{nullptr, nullptr, ROLE_NONE};
   else a.rhs = Operand{rhs->data, rhs_map, role_of(rhs_t, walk_in)};
@@ -844,6 +871,7 @@ int DGLMIKernelBinaryOpReduce(const char* reducer, const char* op, const DGLMIGr
   const int red = parse_reducer(reducer);
   const int o = parse_op(op);
   check_graph(graph);
+  check_maps(graph, lhs_mapping, rhs_mapping, out_mapping);
   DeviceGuard guard(graph->device);
   forward(red, o, graph, lhs_target, rhs_target, lhs, rhs, out, lhs_mapping, rhs_mapping,
           out_mapping, static_cast<hipStream_t>(stream));
@@ -860,6 +888,7 @@ int DGLMIKernelBinaryOpReduceEx(const char* reducer, const char* op, const DGLMI
   const int red = parse_reducer(reducer);
   const int o = parse_op(op);
   check_graph(graph);
+  check_maps(graph, lhs_mapping, rhs_mapping, out_mapping);
   DeviceGuard guard(graph->device);
   forward(red, o, graph, lhs_target, rhs_target, lhs, rhs, out, lhs_mapping, rhs_mapping,
           out_mapping, static_cast<hipStream_t>(stream), epilogue);
@@ -875,6 +904,7 @@ int DGLMIKernelBackwardLhsBinaryOpReduce(
   const int red = parse_reducer(reducer);
   const int o = parse_op(op);
   check_graph(graph);
+  check_maps(graph, lhs_mapping, rhs_mapping, out_mapping);
   DeviceGuard guard(graph->device);
   backward(red, o, graph, lhs_target, rhs_target, lhs_mapping, rhs_mapping, out_mapping, lhs, rhs,
            out, grad_out, grad_lhs, 0, static_cast<hipStream_t>(stream));
@@ -890,6 +920,7 @@ int DGLMIKernelBackwardRhsBinaryOpReduce(
   const int red = parse_reducer(reducer);
   const int o = parse_op(op);
   check_graph(graph);
+  check_maps(graph, lhs_mapping, rhs_mapping, out_mapping);
   DeviceGuard guard(graph->device);
   backward(red, o, graph, lhs_target, rhs_target, lhs_mapping, rhs_mapping, out_mapping, lhs, rhs,
            out, grad_out, grad_rhs, 1, static_cast<hipStream_t>(stream));
@@ -902,6 +933,7 @@ int DGLMIKernelCopyReduce(const char* reducer, const DGLMIGraph* graph, int32_t 
   API_BEGIN();
   const int red = parse_reducer(reducer);
   check_graph(graph);
+  check_maps(graph, in_mapping, out_mapping, nullptr);
   DeviceGuard guard(graph->device);
   forward(red, OP_USE_LHS, graph, target, DGLMI_TARGET_NONE, in, nullptr, out, in_mapping,
           nullptr, out_mapping, static_cast<hipStream_t>(stream));
@@ -915,6 +947,7 @@ int DGLMIKernelCopyReduceEx(const char* reducer, const DGLMIGraph* graph, int32_
   API_BEGIN();
   const int red = parse_reducer(reducer);
   check_graph(graph);
+  check_maps(graph, in_mapping, out_mapping, nullptr);
   DeviceGuard guard(graph->device);
   forward(red, OP_USE_LHS, graph, target, DGLMI_TARGET_NONE, in, nullptr, out, in_mapping,
           nullptr, out_mapping, static_cast<hipStream_t>(stream), epilogue);
@@ -929,6 +962,7 @@ int DGLMIKernelBackwardCopyReduce(const char* reducer, const DGLMIGraph* graph, 
   API_BEGIN();
   const int red = parse_reducer(reducer);
   check_graph(graph);
+  check_maps(graph, in_mapping, out_mapping, nullptr);
   DeviceGuard guard(graph->device);
   backward(red, OP_USE_LHS, graph, target, DGLMI_TARGET_NONE, in_mapping, nullptr, out_mapping, in,
            nullptr, out, grad_out, grad_in, 0, static_cast<hipStream_t>(stream));
@@ -943,7 +977,7 @@ int DGLMIFusedGatForward(const DGLMIGraph* graph, const DGLMIArray* feat_src, co
                          const DGLMIArray* er, float negative_slope, DGLMIArray* out,
                          DGLMIArray* max_out, DGLMIArray* sum_out, void* stream) {
   API_BEGIN();
-  check_graph(graph);
+  check_graph32(graph, "fused GAT");
   DeviceGuard guard(graph->device);
   GatArgs a = gat_args(graph, feat_src, el, er, negative_slope, out, max_out, sum_out);
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1010,7 +1044,7 @@ int DGLMIFusedGatBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src, c
                           const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
                           DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream) {
   API_BEGIN();
-  check_graph(graph);
+  check_graph32(graph, "fused GAT");
   DeviceGuard guard(graph->device);
   GatArgs a = gat_args(graph, feat_src, el, er, negative_slope, const_cast<DGLMIArray*>(out),
                        const_cast<DGLMIArray*>(max_in), const_cast<DGLMIArray*>(sum_in));
@@ -1131,7 +1165,7 @@ int DGLMIFusedGatKernel(const DGLMIGraph* graph, const DGLMIArray* feat_src, con
                         const DGLMIArray* er, DGLMIArray* sum, DGLMIArray* exp, DGLMIArray* ret,
                         float slope, void* stream) {
   API_BEGIN();
-  check_graph(graph);
+  check_graph32(graph, "fused GAT");
   DeviceGuard guard(graph->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t N = graph->in_csr.num_rows, H = feat_src ? feat_src->shape[1] : 0;
@@ -1161,7 +1195,7 @@ int DGLMIKernelBackwardFusedGat(const DGLMIGraph* graph, const DGLMIArray* feat_
                                 DGLMIArray* grad_el, DGLMIArray* grad_er, float slope,
                                 void* stream) {
   API_BEGIN();
-  check_graph(graph);
+  check_graph32(graph, "fused GAT");
   DeviceGuard guard(graph->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t N = graph->in_csr.num_rows, H = feat_src ? feat_src->shape[1] : 0;
@@ -1194,12 +1228,12 @@ int DGLMIKernelMarkColdColumns(const DGLMIGraph* graph, int32_t direction,
   DGLMI_CHECK(direction == 0 || direction == 1, "direction must be 0 (in-CSR) or 1 (out-CSR)");
   const DGLMICsr& c = direction == 0 ? graph->in_csr : graph->out_csr;
   const DGLMICsr& o = direction == 0 ? graph->out_csr : graph->in_csr;
-  check_csr(c, direction == 0 ? "in_csr" : "out_csr", false);
+  check_csr(c, direction == 0 ? "in_csr" : "out_csr", false, wide(graph));
   DGLMI_CHECK(o.indptr != nullptr && o.num_rows == c.num_cols,
               "the opposite CSR must have one row per column node");
   if (c.nnz > 0) DGLMI_CHECK(out_cols != nullptr, "null out_cols");
   DeviceGuard guard(graph->device);
-  launch_mark_cold(c.indices, c.nnz, o.indptr, min_hot_degree, out_cols,
+  launch_mark_cold(c.indices, c.nnz, idx(graph, o.indptr), min_hot_degree, out_cols,
                    static_cast<hipStream_t>(stream));
   check_hip(hipGetLastError(), "mark cold columns launch");
   API_END();
@@ -1230,15 +1264,15 @@ int64_t softmax_setup(const DGLMIGraph* g, const DGLMIArray* x, const char* name
   check_graph(g);
   check_array(x, name);
   const DGLMICsr& in = g->in_csr;
-  check_csr(in, "in_csr", true);
+  check_csr(in, "in_csr", true, wide(g));
   DGLMI_CHECK(x->shape[0] >= in.nnz, std::string(name) + " has fewer rows than edges");
   const int64_t H = feat_numel(x);
   DGLMI_CHECK(softmax_supported(H), "edge softmax supports 1, 2, 4, 8 or 16 values per edge");
   DGLMI_CHECK(aligned16(x->data), std::string(name) + " must be 16-byte aligned");
   std::memset(&a, 0, sizeof(a));
-  a.indptr = in.indptr;
+  a.indptr = idx(g, in.indptr);
   a.rows = in.rows;
-  a.eids = in.data;
+  a.eids = idx(g, in.data);
   a.coo_dst = (g->coo_src && g->coo_dst) ? g->coo_dst : nullptr;
   a.nnz = in.nnz;
   a.num_rows = in.num_rows;
@@ -1368,7 +1402,7 @@ struct TypedOutCsr {
 };
 
 void rgcn_common(const DGLMIGraph* g, const int32_t* etypes, int64_t rows_expanded) {
-  check_graph(g);
+  check_graph32(g, "R-GCN");
   check_csr(g->in_csr, "in_csr", true);
   check_csr(g->out_csr, "out_csr", true);
   DGLMI_CHECK(g->in_csr.nnz == g->out_csr.nnz, "in/out CSR edge counts differ");
@@ -1630,7 +1664,7 @@ int DGLMIRgcnPrepare(const DGLMIGraph* graph, const int32_t* etypes, const DGLMI
   DGLMI_CHECK(num_rels >= 1, "num_rels must be >= 1");
   DGLMI_CHECK(layers >= 1 && layers <= 7,
               "layers must be a mask of 1 (layer 0), 2 (layer 1) and 4 (fused layer 1)");
-  check_graph(graph);
+  check_graph32(graph, "R-GCN");
   const DGLMICsr& in = graph->in_csr;
   const DGLMICsr& out = graph->out_csr;
   const int64_t R = num_rels, N = in.num_cols, E = in.nnz;
@@ -1752,7 +1786,7 @@ int DGLMINbAccess(const DGLMIGraph* graph, const DGLMIArray* feat, const int32_t
   API_BEGIN();
   (void)node_map;          // the reference's sharding modes that read them are disabled
   (void)deg_inc_node_map;  // (binary_reduce_impl.cu:779-900); accepted and ignored
-  check_graph(graph);
+  check_graph32(graph, "NbAccess");
   check_array(feat, "feat");
   const DGLMICsr& in = graph->in_csr;
   check_csr(in, "in_csr", true);

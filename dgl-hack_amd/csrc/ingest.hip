@@ -141,6 +141,92 @@ size_t sort_temp_bytes(int64_t n, int64_t nnz) {
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
+// ---- 64-bit graphs (2^31 or more edges): int64 offsets and edge ids ----------
+// COO -> CSR as a stable counting sort by row done in batches of at most 2^30
+// positions, in position order.  Row counts (atomics) and their exclusive scan give
+// indptr; each batch is sorted by (row, position) with the same stable radix sort
+// as the int32 path (int item counts), and its run of row r is written after the
+// runs of the earlier batches (a per-row fill cursor), so every row keeps its
+// positions ascending: bit-identical to COOToCSR with int64 arrays.
+constexpr int64_t kBatch64 = int64_t(1) << 30;
+
+__global__ void k_count_rows64(const int32_t* __restrict__ row, int64_t nnz,
+                               unsigned long long* __restrict__ cnt) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nnz; i += stride)
+    atomicAdd(cnt + row[i], 1ull);
+}
+
+// rs[i] = i where a run of equal keys starts, else 0 (a max-scan then gives every
+// position its run's start)
+__global__ void k_run_starts(const int32_t* __restrict__ key, int64_t n, int32_t* __restrict__ rs) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    rs[i] = (i == 0 || key[i] != key[i - 1]) ? static_cast<int32_t>(i) : 0;
+}
+
+__global__ void k_scatter_batch64(const int32_t* __restrict__ key, const int32_t* __restrict__ perm,
+                                  const int32_t* __restrict__ rs, int64_t n, int64_t start,
+                                  const int32_t* __restrict__ col, const int64_t* __restrict__ data,
+                                  const int64_t* __restrict__ fill, int32_t* __restrict__ indices,
+                                  int64_t* __restrict__ out_data) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t p = start + perm[i];
+    const int64_t dest = fill[key[i]] + (i - rs[i]);
+    indices[dest] = col[p];
+    out_data[dest] = data ? data[p] : p;
+  }
+}
+
+// the last position of each run advances its row's cursor by the run's length
+__global__ void k_advance_fill(const int32_t* __restrict__ key, const int32_t* __restrict__ rs,
+                               int64_t n, int64_t* __restrict__ fill) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    if (i == n - 1 || key[i + 1] != key[i]) fill[key[i]] += i - rs[i] + 1;
+}
+
+__global__ void k_mark_row_starts64(const int64_t* __restrict__ indptr, int64_t n,
+                                    int32_t* __restrict__ rows) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += stride)
+    if (indptr[r + 1] > indptr[r]) rows[indptr[r]] = static_cast<int32_t>(r);
+}
+
+// carry of a batched max-scan: the batch's first element takes the previous
+// batch's final value into account
+__global__ void k_scan_carry(int32_t* __restrict__ v, int64_t start) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && v[start - 1] > v[start]) v[start] = v[start - 1];
+}
+
+struct Ws64 {
+  size_t fill, keys, perm_in, perm_out, rs, temp, total;
+};
+
+Ws64 ws64_layout(int64_t n, int64_t nnz) {
+  const int64_t b = nnz < kBatch64 ? nnz : kBatch64;
+  size_t sort_b = 0, scan_b = 0, max_b = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort_b, static_cast<const int32_t*>(nullptr),
+                                           static_cast<int32_t*>(nullptr),
+                                           static_cast<const int32_t*>(nullptr),
+                                           static_cast<int32_t*>(nullptr), static_cast<int>(b), 0,
+                                           bits_for(n));
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_b, static_cast<const int64_t*>(nullptr),
+                                         static_cast<int64_t*>(nullptr), static_cast<int>(n + 1));
+  (void)hipcub::DeviceScan::InclusiveScan(nullptr, max_b, static_cast<int32_t*>(nullptr),
+                                          static_cast<int32_t*>(nullptr), MaxOp(), static_cast<int>(b));
+  Ws64 w;
+  w.fill = 0;
+  w.keys = w.fill + align256((n + 1) * sizeof(int64_t));
+  w.perm_in = w.keys + align256(b * sizeof(int32_t));
+  w.perm_out = w.perm_in + align256(b * sizeof(int32_t));
+  w.rs = w.perm_out + align256(b * sizeof(int32_t));
+  w.temp = w.rs + align256(b * sizeof(int32_t));
+  w.total = w.temp + align256(std::max(sort_b, std::max(scan_b, max_b)));
+  return w;
+}
+
 thread_local std::string g_ingest_error;
 
 }  // namespace
@@ -198,6 +284,88 @@ int DGLMICOOToCSRDevice(int64_t num_rows, int64_t nnz, const int32_t* row, const
                      indices, out_data, nnz);
   hipLaunchKernelGGL(k_indptr_from_sorted, dim3(grid_of(nnz + 1)), dim3(256), 0, s, keys_out, nnz,
                      num_rows, indptr);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int64_t DGLMICOOToCSRDevice64WorkspaceBytes(int64_t num_rows, int64_t nnz) {
+  if (nnz <= 0 || num_rows < 0) return 256;
+  return static_cast<int64_t>(ws64_layout(num_rows, nnz).total);
+}
+
+int DGLMICOOToCSRDevice64(int64_t num_rows, int64_t nnz, const int32_t* row, const int32_t* col,
+                          const int64_t* data, int64_t* indptr, int32_t* indices, int64_t* out_data,
+                          void* workspace, int64_t workspace_bytes, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (num_rows < 0 || nnz < 0 || num_rows >= INT32_MAX || indptr == nullptr) return -1;
+  if (nnz == 0) {
+    if (hipMemsetAsync(indptr, 0, (num_rows + 1) * sizeof(int64_t), s) != hipSuccess) return -1;
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+  const Ws64 w = ws64_layout(num_rows, nnz);
+  if (workspace == nullptr || workspace_bytes < static_cast<int64_t>(w.total)) return -1;
+  char* ws = static_cast<char*>(workspace);
+  int64_t* fill = reinterpret_cast<int64_t*>(ws + w.fill);
+  int32_t* keys = reinterpret_cast<int32_t*>(ws + w.keys);
+  int32_t* perm_in = reinterpret_cast<int32_t*>(ws + w.perm_in);
+  int32_t* perm_out = reinterpret_cast<int32_t*>(ws + w.perm_out);
+  int32_t* rs = reinterpret_cast<int32_t*>(ws + w.rs);
+  void* temp = ws + w.temp;
+  const size_t temp_cap = w.total - w.temp;
+  // row counts -> indptr (exclusive scan over num_rows + 1 entries, the last zero)
+  if (hipMemsetAsync(fill, 0, (num_rows + 1) * sizeof(int64_t), s) != hipSuccess) return -1;
+  hipLaunchKernelGGL(k_count_rows64, dim3(grid_of(nnz)), dim3(256), 0, s, row, nnz,
+                     reinterpret_cast<unsigned long long*>(fill));
+  size_t tb = temp_cap;
+  if (hipcub::DeviceScan::ExclusiveSum(temp, tb, fill, indptr, static_cast<int>(num_rows + 1), s) !=
+      hipSuccess)
+    return -1;
+  if (hipMemcpyAsync(fill, indptr, num_rows * sizeof(int64_t), hipMemcpyDeviceToDevice, s) !=
+      hipSuccess)
+    return -1;
+  for (int64_t start = 0; start < nnz; start += kBatch64) {
+    const int64_t nb = std::min(kBatch64, nnz - start);
+    hipLaunchKernelGGL(k_iota, dim3(grid_of(nb)), dim3(256), 0, s, perm_in, nb);
+    tb = temp_cap;
+    if (hipcub::DeviceRadixSort::SortPairs(temp, tb, row + start, keys, perm_in, perm_out,
+                                           static_cast<int>(nb), 0, bits_for(num_rows), s) !=
+        hipSuccess)
+      return -1;
+    hipLaunchKernelGGL(k_run_starts, dim3(grid_of(nb)), dim3(256), 0, s, keys, nb, rs);
+    tb = temp_cap;
+    if (hipcub::DeviceScan::InclusiveScan(temp, tb, rs, rs, MaxOp(), static_cast<int>(nb), s) !=
+        hipSuccess)
+      return -1;
+    hipLaunchKernelGGL(k_scatter_batch64, dim3(grid_of(nb)), dim3(256), 0, s, keys, perm_out, rs, nb,
+                       start, col, data, fill, indices, out_data);
+    hipLaunchKernelGGL(k_advance_fill, dim3(grid_of(nb)), dim3(256), 0, s, keys, rs, nb, fill);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int DGLMICSRExpandRows64(const int64_t* indptr, int64_t num_rows, int64_t nnz, int32_t* rows,
+                         void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (nnz == 0) return 0;
+  if (num_rows >= INT32_MAX) return -1;
+  dglmi::launch_fill_i32(rows, nnz, 0, s);
+  hipLaunchKernelGGL(k_mark_row_starts64, dim3(grid_of(num_rows)), dim3(256), 0, s, indptr, num_rows,
+                     rows);
+  const int64_t b = std::min(kBatch64, nnz);
+  size_t temp_bytes = 0;
+  (void)hipcub::DeviceScan::InclusiveScan(nullptr, temp_bytes, rows, rows, MaxOp(), static_cast<int>(b),
+                                          s);
+  void* temp = nullptr;
+  if (hipMallocAsync(&temp, temp_bytes, s) != hipSuccess) return -1;
+  hipError_t e = hipSuccess;
+  for (int64_t start = 0; start < nnz && e == hipSuccess; start += kBatch64) {
+    const int64_t nb = std::min(kBatch64, nnz - start);
+    if (start > 0) hipLaunchKernelGGL(k_scan_carry, dim3(1), dim3(64), 0, s, rows, start);
+    size_t tb = temp_bytes;
+    e = hipcub::DeviceScan::InclusiveScan(temp, tb, rows + start, rows + start, MaxOp(),
+                                          static_cast<int>(nb), s);
+  }
+  (void)hipFreeAsync(temp, s);
+  if (e != hipSuccess) return -1;
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

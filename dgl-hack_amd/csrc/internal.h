@@ -23,6 +23,21 @@ enum Op : int { OP_ADD = 0, OP_SUB = 1, OP_MUL = 2, OP_DIV = 3, OP_DOT = 4, OP_U
 
 constexpr int kMaxDim = DGLMI_MAX_NDIM;
 
+// CSR offsets (indptr) and edge ids (csr.data) as the kernels read them: int32, or
+// int64 on a graph of 2^31 or more edges (DGLMIGraph.num_bits == 64; node ids stay
+// int32, so indices / rows / COO arrays keep their width).  A launch-uniform flag
+// picks the width on every read -- a scalar branch -- so no kernel is instantiated
+// twice per index width.
+struct IdxPtr {
+  const void* p;
+  int wide;
+  __host__ __device__ __forceinline__ int64_t operator[](int64_t i) const {
+    return wide ? static_cast<const int64_t*>(p)[i]
+                : static_cast<int64_t>(static_cast<const int32_t*>(p)[i]);
+  }
+  __host__ __device__ __forceinline__ explicit operator bool() const { return p != nullptr; }
+};
+
 // Flattened broadcast description (BcastInfo, binary_reduce.h / binary_reduce.cc:96-155).
 struct Bcast {
   int ndim;
@@ -40,9 +55,9 @@ struct Operand {
 
 // Everything a generic kernel needs; passed by value as the kernel argument.
 struct EdgeArgs {
-  const int32_t* indptr;   // CSR walked (rows = owners of the reduction)
+  IdxPtr indptr;           // CSR walked (rows = owners of the reduction)
   const int32_t* indices;  // column node per position
-  const int32_t* eids;     // edge id per position
+  IdxPtr eids;             // edge id per position
   const int32_t* rows;     // row per position (edge-wise kernels)
   int64_t num_rows;
   int64_t nnz;
@@ -99,8 +114,8 @@ __device__ __forceinline__ float red_backward(float val, float accum) {
 // One group filling a whole gap serialised contiguous empty rows: the ~3 M
 // trailing zero-in-degree rows of M1 renumbered by degree took one group 160 ms
 // (scripts/locality_probe.py).  Cost: one coalesced read of indptr per launch.
-template <typename Put>
-__device__ __forceinline__ void fill_empty_rows(const int32_t* __restrict__ indptr, int64_t num_rows,
+template <typename IP, typename Put>
+__device__ __forceinline__ void fill_empty_rows(IP indptr, int64_t num_rows,
                                                 int64_t chunk, int64_t num_chunks, int L, int lane,
                                                 Put&& put) {
   const int64_t R = (num_rows + num_chunks - 1) / num_chunks;
@@ -213,7 +228,7 @@ void launch_generic_lb(int op, int red, bool bcast, bool bwd, const EdgeArgs& a,
 struct SddmmArgs {
   const int32_t* rows;  // destination node per item
   const int32_t* cols;  // source node per item
-  const int32_t* eids;  // edge id per item; NULL: item index == edge id (COO order)
+  IdxPtr eids;          // edge id per item; NULL: item index == edge id (COO order)
   int64_t nnz;
   const float* lhs;
   const float* rhs;
@@ -229,9 +244,9 @@ void launch_sddmm(int op, bool bwd, const SddmmArgs& a, hipStream_t s);
 
 // Fused edge softmax (kernels_softmax.hip).
 struct SoftmaxArgs {
-  const int32_t* indptr;   // in-CSR
+  IdxPtr indptr;           // in-CSR
   const int32_t* rows;
-  const int32_t* eids;
+  IdxPtr eids;
   const int32_t* coo_dst;  // optional: edge-id order for the per-edge pass
   int64_t nnz;
   int64_t num_rows;
@@ -258,10 +273,10 @@ enum FastKind : int {
   FAST_COL_TIE = 4,     // v = XR[row] == W[col] ? X[col] : 0  (max / min gradient, tie mask)
 };
 struct FastArgs {
-  const int32_t* indptr;
+  IdxPtr indptr;
   const int32_t* rows;
   const int32_t* indices;
-  const int32_t* eids;
+  IdxPtr eids;
   int64_t nnz;
   int64_t num_rows;     // rows owned (out rows 0..num_rows-1 written)
   const float* x;       // column-node or edge features
@@ -292,7 +307,7 @@ int64_t fast_carry_bytes(int64_t nnz, int64_t F);      // offset of the counters
 bool fast_supported(int kind, int64_t F, int64_t head_dim);
 void launch_fast_reduce(int kind, int red, const FastArgs& a, hipStream_t s);  // needs a.indptr
 // out_cols[p] = cols[p] | (col_deg(cols[p]) < thresh ? 1 << 31 : 0), col_deg from deg_indptr
-void launch_mark_cold(const int32_t* cols, int64_t nnz, const int32_t* deg_indptr, int32_t thresh,
+void launch_mark_cold(const int32_t* cols, int64_t nnz, IdxPtr deg_indptr, int32_t thresh,
                       int32_t* out_cols, hipStream_t s);
 // row widths whose launch config has a marked variant (L >= 16 lanes, one float4 each)
 inline bool fast_marked_supported(int64_t F) { return F > 32 && F <= 256 && F % 4 == 0; }

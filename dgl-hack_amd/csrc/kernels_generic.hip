@@ -85,12 +85,12 @@ __global__ void __launch_bounds__(kBlock) k_node_fwd(EdgeArgs a, int lane_bits) 
   const int64_t row = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> lane_bits;
   const int lane = threadIdx.x & (L - 1);
   if (row >= a.num_rows) return;
-  const int32_t beg = a.indptr[row], end = a.indptr[row + 1];
+  const int64_t beg = a.indptr[row], end = a.indptr[row + 1];
   const int64_t orow = a.out_map ? a.out_map[row] : row;
   float* o = a.out + orow * a.D;
   for (int64_t tx = lane; tx < a.D; tx += L) {
     float acc = red_identity<RED>();
-    for (int32_t j = beg; j < end; ++j)
+    for (int64_t j = beg; j < end; ++j)
       acc = red_apply<RED>(acc, fwd_value<OP, BC>(a, row, a.indices[j], a.eids[j], tx));
     o[tx] = acc;
   }
@@ -117,11 +117,11 @@ __global__ void __launch_bounds__(kBlock) k_node_bwd(EdgeArgs a, int lane_bits) 
   const int64_t Dg = a.D * a.len;
   const int32_t* gmap = a.want == 0 ? a.lhs.map : a.rhs.map;
   const int64_t grow = gmap ? gmap[row] : row;
-  const int32_t beg = a.indptr[row], end = a.indptr[row + 1];
+  const int64_t beg = a.indptr[row], end = a.indptr[row + 1];
   float* g = a.out + grow * Dg;
   for (int64_t k = lane; k < Dg; k += L) {
     float acc = 0.0f;
-    for (int32_t j = beg; j < end; ++j)
+    for (int64_t j = beg; j < end; ++j)
       acc += bwd_value<OP, RED, BC>(a, row, a.indices[j], a.eids[j], k);
     g[k] = acc;
   }

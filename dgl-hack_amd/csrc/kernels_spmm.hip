@@ -69,7 +69,7 @@ __device__ __forceinline__ void store_row(float* __restrict__ p, const float (&v
 // `hidx` (bcast kind): edge value index of each of the F floats, i / head_dim, and
 // `wn` = F / head_dim values per edge, computed once per thread by the caller.
 template <int KIND, int F>
-__device__ __forceinline__ void lane_value(const FastArgs& a, int32_t col, int32_t eid, float (&v)[F],
+__device__ __forceinline__ void lane_value(const FastArgs& a, int32_t col, int64_t eid, float (&v)[F],
                                            const int (&hidx)[F], int wn, int32_t row) {
   if constexpr (KIND == FAST_COL_TIE) {
     float o[F], xr[F];
@@ -149,7 +149,8 @@ __global__ void __launch_bounds__(kBlock) k_lane_reduce(FastArgs a) {
 #pragma unroll
   for (int i = 0; i < F; ++i) acc[i] = I;
   for (int64_t base = p0; base < p1; base += U) {
-    int32_t r[U], c[U], e[U];
+    int32_t r[U], c[U];
+    int64_t e[U];
     if (base + U <= p1) {
       const int4 r0 = *reinterpret_cast<const int4*>(a.rows + base);
       const int4 r1 = *reinterpret_cast<const int4*>(a.rows + base + 4);
@@ -158,9 +159,15 @@ __global__ void __launch_bounds__(kBlock) k_lane_reduce(FastArgs a) {
       r[0] = r0.x; r[1] = r0.y; r[2] = r0.z; r[3] = r0.w; r[4] = r1.x; r[5] = r1.y; r[6] = r1.z; r[7] = r1.w;
       c[0] = c0.x; c[1] = c0.y; c[2] = c0.z; c[3] = c0.w; c[4] = c1.x; c[5] = c1.y; c[6] = c1.z; c[7] = c1.w;
       if constexpr (needs_eid<KIND>()) {
-        const int4 e0 = *reinterpret_cast<const int4*>(a.eids + base);
-        const int4 e1 = *reinterpret_cast<const int4*>(a.eids + base + 4);
-        e[0] = e0.x; e[1] = e0.y; e[2] = e0.z; e[3] = e0.w; e[4] = e1.x; e[5] = e1.y; e[6] = e1.z; e[7] = e1.w;
+        if (a.eids.wide) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) e[u] = a.eids[base + u];
+        } else {
+          const int32_t* ep = static_cast<const int32_t*>(a.eids.p) + base;
+          const int4 e0 = *reinterpret_cast<const int4*>(ep);
+          const int4 e1 = *reinterpret_cast<const int4*>(ep + 4);
+          e[0] = e0.x; e[1] = e0.y; e[2] = e0.z; e[3] = e0.w; e[4] = e1.x; e[5] = e1.y; e[6] = e1.z; e[7] = e1.w;
+        }
       }
     } else {
 #pragma unroll
@@ -268,7 +275,7 @@ void run_lane_f(const FastArgs& a, hipStream_t s) {
 
 
 template <int KIND, int RED>
-void run_cfg(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
+void run_cfg(const FastArgs& a, IdxPtr indptr, hipStream_t s) {
   if (a.F < 16 && lane_kernel_width(a.F)) {
     run_lane_f<KIND, RED>(a, s);
     return;
@@ -280,20 +287,19 @@ void run_cfg(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
   }
 }
 
-__global__ void k_mark_cold(const int32_t* __restrict__ cols, int64_t nnz,
-                            const int32_t* __restrict__ deg_indptr, int32_t thresh,
-                            int32_t* __restrict__ out) {
+__global__ void k_mark_cold(const int32_t* __restrict__ cols, int64_t nnz, IdxPtr deg_indptr,
+                            int32_t thresh, int32_t* __restrict__ out) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   for (int64_t p = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; p < nnz; p += stride) {
     const int32_t c = cols[p];
-    const int32_t d = deg_indptr[c + 1] - deg_indptr[c];
+    const int64_t d = deg_indptr[c + 1] - deg_indptr[c];
     out[p] = d < thresh ? static_cast<int32_t>(static_cast<uint32_t>(c) | 0x80000000u) : c;
   }
 }
 
 }  // namespace
 
-void launch_mark_cold(const int32_t* cols, int64_t nnz, const int32_t* deg_indptr, int32_t thresh,
+void launch_mark_cold(const int32_t* cols, int64_t nnz, IdxPtr deg_indptr, int32_t thresh,
                       int32_t* out_cols, hipStream_t s) {
   if (nnz <= 0) return;
   const int64_t want = (nnz + kBlock - 1) / kBlock;
@@ -347,7 +353,7 @@ bool fast_supported(int kind, int64_t F, int64_t head_dim) {
 }
 
 void launch_fast_reduce(int kind, int red, const FastArgs& a, hipStream_t s) {
-  const int32_t* indptr = a.indptr;
+  const IdxPtr indptr = a.indptr;
   switch (kind) {
     case FAST_COPY_COL:
       if (red == RED_MAX) run_cfg<FAST_COPY_COL, RED_MAX>(a, indptr, s);

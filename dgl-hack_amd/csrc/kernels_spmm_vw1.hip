@@ -5,7 +5,7 @@
 namespace dglmi {
 
 void launch_fast_chunk_vw1(int kind, int red, const FastArgs& a, hipStream_t s) {
-  const int32_t* indptr = a.indptr;
+  const IdxPtr indptr = a.indptr;
   switch (kind) {
     case FAST_COPY_COL:
       if (red == RED_MAX) run_vw<FAST_COPY_COL, RED_MAX, 1>(a, indptr, s);

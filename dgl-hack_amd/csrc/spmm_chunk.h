@@ -121,7 +121,7 @@ constexpr bool needs_eid() {
 // values per edge, F / head_dim -- both hoisted out of the edge loop by the
 // caller (64-bit divisions per edge cost 1.7 ms on the C5 typed gather).
 template <int KIND, int VW>
-__device__ __forceinline__ typename VecT<VW>::T edge_value(const FastArgs& a, int32_t col, int32_t eid,
+__device__ __forceinline__ typename VecT<VW>::T edge_value(const FastArgs& a, int32_t col, int64_t eid,
                                                           int fv, int hs = 0, int64_t wn = 1,
                                                           int32_t row = 0) {
   if constexpr (KIND == FAST_COL_TIE) {
@@ -152,6 +152,15 @@ __device__ __forceinline__ int32_t ld_stream(const int32_t* p) {
   if constexpr (VAR & 1) return __builtin_nontemporal_load(p);
   else return *p;
 }
+template <int VAR>
+__device__ __forceinline__ int64_t ld_stream(IdxPtr q, int64_t p) {
+  if (q.wide) {
+    const int64_t* x = static_cast<const int64_t*>(q.p) + p;
+    if constexpr (VAR & 1) return __builtin_nontemporal_load(x);
+    else return *x;
+  }
+  return ld_stream<VAR>(static_cast<const int32_t*>(q.p) + p);
+}
 template <int VAR, typename V>
 __device__ __forceinline__ void st_out(float* p, V v) {
   if constexpr (VAR & 2) vst_nt(p, v);
@@ -180,7 +189,7 @@ __device__ __forceinline__ typename VecT<VW>::T epiv(const FastArgs& a, typename
 }
 
 template <int KIND, int RED, int L, int NV, int VAR = 3, bool EPI = false, int VW = 4>
-__global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32_t* __restrict__ indptr) {
+__global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, IdxPtr indptr) {
   static_assert(L >= 1 && L <= 64, "a lane group must fit in one wavefront (fill_empty_rows)");
   constexpr int G = kBlock / L;           // groups per block
   constexpr int B = (L > 16 ? L : 16) * ((VAR & 4) ? 2 : 1);  // positions staged per step
@@ -188,7 +197,7 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
   static_assert(B % U == 0, "B must be a multiple of U");
   __shared__ int32_t s_row[G][B];
   __shared__ int32_t s_col[G][B];
-  __shared__ int32_t s_eid[needs_eid<KIND>() ? G : 1][needs_eid<KIND>() ? B : 1];
+  __shared__ int64_t s_eid[needs_eid<KIND>() ? G : 1][needs_eid<KIND>() ? B : 1];
 
   const int g = threadIdx.x / L;
   const int lane = threadIdx.x % L;
@@ -222,7 +231,7 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
       const bool ok = p < p1;
       s_row[g][q] = ok ? ld_stream<VAR>(a.rows + p) : INT_MAX;
       s_col[g][q] = ok ? ld_stream<VAR>(a.indices + p) : 0;
-      if constexpr (needs_eid<KIND>()) s_eid[needs_eid<KIND>() ? g : 0][q] = ok ? ld_stream<VAR>(a.eids + p) : 0;
+      if constexpr (needs_eid<KIND>()) s_eid[needs_eid<KIND>() ? g : 0][q] = ok ? ld_stream<VAR>(a.eids, p) : 0;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -233,7 +242,7 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int32_t col = s_col[g][ub + u];
-        const int32_t eid = needs_eid<KIND>() ? s_eid[needs_eid<KIND>() ? g : 0][ub + u] : 0;
+        const int64_t eid = needs_eid<KIND>() ? s_eid[needs_eid<KIND>() ? g : 0][ub + u] : 0;
         const bool ok = s_row[g][ub + u] != INT_MAX;
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
@@ -309,7 +318,7 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, const int32
 // workspace has counters -- every kFixSeg-th one folds a segment and the last
 // to finish folds the head and the segment partials (internal.h).
 template <int RED, int L, int NV, bool EPI = false, int VW = 4>
-__global__ void __launch_bounds__(kBlock) k_chunk_fixup(FastArgs a, const int32_t* __restrict__ indptr) {
+__global__ void __launch_bounds__(kBlock) k_chunk_fixup(FastArgs a, IdxPtr indptr) {
   static_assert(L >= 1 && L <= 64, "a lane group must fit in one wavefront (seg_arrive_last)");
   constexpr int G = kBlock / L;
   const int g = threadIdx.x / L;
@@ -421,7 +430,7 @@ inline int spmm_variant() {
 #endif
 
 template <int KIND, int RED, int L, int NV, int VW>
-void run(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
+void run(const FastArgs& a, IdxPtr indptr, hipStream_t s) {
   constexpr int G = kBlock / L;
   const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
   const unsigned blocks = static_cast<unsigned>((chunks + G - 1) / G);
@@ -508,7 +517,7 @@ inline int fast_vw(int64_t F, int kind, int64_t head_dim) {
 inline bool lane_kernel_width(int64_t F) { return F >= 1 && (F <= 8 || F == 12); }
 
 template <int KIND, int RED, int VW>
-void run_vw(const FastArgs& a, const int32_t* indptr, hipStream_t s) {
+void run_vw(const FastArgs& a, IdxPtr indptr, hipStream_t s) {
   const Cfg c = pick(a.F / VW, VW);
   switch (c.L * 10 + c.NV) {
     case 41: if constexpr (VW == 4) run<KIND, RED, 4, 1, VW>(a, indptr, s); break;

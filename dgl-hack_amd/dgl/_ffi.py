@@ -195,6 +195,13 @@ _SIGS = {
         ctypes.c_void_p]),
     "DGLMICSRExpandRows": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "DGLMICSRExpandRows64": (ctypes.c_int, [
+        ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "DGLMICOOToCSRDevice64WorkspaceBytes": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int64]),
+    "DGLMICOOToCSRDevice64": (ctypes.c_int, [
+        ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+        ctypes.c_void_p]),
     "DGLMIPartitionLabelProp": (ctypes.c_int, [
         ctypes.POINTER(Graph), ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_void_p,
         ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),

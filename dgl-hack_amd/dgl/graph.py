@@ -862,7 +862,7 @@ class DGLGraph(object):
         mfuncs, rfuncs = self._as_list(message_func), self._as_list(reduce_func)
         self._check_builtin(mfuncs, rfuncs)
         dev = self._device(self._node_frame, self._edge_frame)
-        sub = _PartialIndex(self.number_of_nodes(), src, dst, eid)
+        sub = _PartialIndex(self.number_of_nodes(), src, dst, eid, bits=self._graph._bits)
         gidx = sub.get_immutable_gidx(dev)
         res = self._reduce(gidx, mfuncs, rfuncs,
                            lambda: (th.as_tensor(src, device=dev), th.as_tensor(dst, device=dev),
@@ -925,7 +925,8 @@ class DGLGraph(object):
                 e = th.arange(m, device=dev)
             else:
                 src, dst, eid = self._resolve_edges(edges)
-                gidx = _PartialIndex(self.number_of_nodes(), src, dst, eid).get_immutable_gidx(dev)
+                gidx = _PartialIndex(self.number_of_nodes(), src, dst, eid,
+                                     bits=self._graph._bits).get_immutable_gidx(dev)
                 e = th.as_tensor(eid, device=dev)
             msgs = self._messages(gidx, mfuncs, None, None, e, dev)
         if not hasattr(self, "_msg_frame") or self._msg_frame is None:
@@ -964,7 +965,7 @@ class DGLGraph(object):
             return
         dev = self._device(self._node_frame, self._edge_frame)
         gidx = _PartialIndex(self.number_of_nodes(), src[mask], dst[mask],
-                             eid[mask]).get_immutable_gidx(dev)
+                             eid[mask], bits=self._graph._bits).get_immutable_gidx(dev)
         res = self._reduce(gidx, [], rfuncs,
                            lambda: (th.as_tensor(src[mask], device=dev),
                                     th.as_tensor(dst[mask], device=dev),
@@ -1016,7 +1017,7 @@ class DGLGraph(object):
                                    reducer="none")
             else:
                 src, dst, eid = self._resolve_edges(edges)
-                sub = _PartialIndex(self.number_of_nodes(), src, dst, eid)
+                sub = _PartialIndex(self.number_of_nodes(), src, dst, eid, bits=self._graph._bits)
                 gidx = sub.get_immutable_gidx(dev)
                 res = func._invoke(gidx, self._node_frame, self._node_frame, self._edge_frame, m,
                                    reducer="none")
@@ -1094,10 +1095,17 @@ class _PartialIndex(GraphIndex):
     relabel maps for the same purpose, spmv.py:146-180)."""
     _eid_is_perm = False
 
-    def __init__(self, n, src, dst, parent_eid):
+    def __init__(self, n, src, dst, parent_eid, bits=None):
         super().__init__(n)
         self.add_edges(src, dst)
         self._parent = np.asarray(parent_eid, np.int64)
+        self._bits = bits  # the parent's forced width (GraphIndex.asbits)
+
+    def bits_needed(self):
+        # the CSR data holds parent edge ids: 64-bit once they reach 2^31
+        if self._parent.size and int(self._parent.max()) >= 0x7FFFFFFF:
+            return 64
+        return super().bits_needed()
 
     def host_csr(self):
         if self._host_csr is None:

@@ -13,9 +13,15 @@ and ``src/graph/{graph,immutable_graph}.cc``):
 
 MI355X specifics: device CSRs are int32 (the reference GPU path is int32
 only, ``kernel/common.h:62-69``) and carry the row id of every position
-(``rows``), which the edge-wise and load-balanced kernels read.  Large
-graphs can be built directly on the GPU (:meth:`GraphIndex.from_device_coo`):
-two stable radix sorts give arrays bit-identical to the host path.
+(``rows``), which the edge-wise and load-balanced kernels read.  A graph of 2^31
+or more edges -- where the reference switches to int64 (``bits_needed``,
+``graph_index.py:941-952``) and only its CPU kernels run -- gets 64-bit offsets:
+int64 ``indptr`` and ``data`` (edge ids), int32 ``indices`` / ``rows`` (node ids
+stay below 2^31; 288 GB of HBM holds such a graph, about 16 B per edge and
+direction).  ``GraphIndex.asbits(64)`` forces that layout on any graph (parity
+tests).  Large graphs can be built directly on the GPU
+(:meth:`GraphIndex.from_device_coo`): stable radix sorts give arrays
+bit-identical to the host path.
 """
 from __future__ import annotations
 
@@ -34,9 +40,11 @@ def _ptr(t):
 
 
 class DeviceCSR:
-    """One direction of the adjacency on a device (int32 arrays)."""
+    """One direction of the adjacency on a device: int32 arrays, or int64
+    ``indptr`` / ``data`` for a 64-bit graph."""
 
     def __init__(self, indptr, indices, data, rows, num_cols):
+        self.bits = 64 if indptr.dtype == th.int64 else 32
         self.indptr = indptr
         self.indices = indices
         self.data = data
@@ -63,7 +71,7 @@ class DeviceCSR:
         return c
 
     def degrees(self):
-        """Row degrees on the device (int32), computed once and cached."""
+        """Row degrees on the device (the indptr's dtype), computed once and cached."""
         if getattr(self, "_deg", None) is None:
             self._deg = self.indptr[1:] - self.indptr[:-1]
         return self._deg
@@ -87,6 +95,11 @@ class ImmutableGraphIndex:
 
     def number_of_edges(self):
         return self.in_csr.nnz
+
+    @property
+    def num_bits(self):
+        """32, or 64 when indptr / edge ids are int64 (DGLMIGraph.num_bits)."""
+        return self.in_csr.bits
 
     def coo(self):
         """(src, dst) by edge id, int32 on the device, scattered from the in-CSR
@@ -124,7 +137,7 @@ class ImmutableGraphIndex:
         if self._gather_cols is None:
             self._gather_cols = (None, None)
             hot = int(os.environ.get("DGLMI_HOT_DEGREE", self.HOT_DEGREE))
-            if hot > 0 and self.in_csr.nnz >= self.MIN_HINT_EDGES and self.in_csr.nnz < 2 ** 31:
+            if hot > 0 and self.in_csr.nnz >= self.MIN_HINT_EDGES:
                 cols = []
                 g = self._cstruct_base()
                 for direction, csr in ((0, self.in_csr), (1, self.out_csr)):
@@ -195,7 +208,7 @@ class ImmutableGraphIndex:
             self._pos_views, self._pos_operands = {}, {}
         if direction not in self._pos_views:
             dev = ic.indices.device
-            pos = th.arange(ic.nnz, device=dev, dtype=th.int32)
+            pos = th.arange(ic.nnz, device=dev, dtype=ic.data.dtype)
             walk, other = (ic, oc) if direction == "in" else (oc, ic)
             inv = th.empty_like(pos)
             inv[walk.data.long()] = pos
@@ -242,7 +255,7 @@ class ImmutableGraphIndex:
         g = _ffi.Graph()
         g.in_csr = self.in_csr.cstruct()
         g.out_csr = self.out_csr.cstruct()
-        g.num_bits = 32
+        g.num_bits = self.num_bits
         g.device = self.device.index if self.device.index is not None else th.cuda.current_device()
         g.workspace = None
         g.workspace_bytes = 0
@@ -252,6 +265,8 @@ class ImmutableGraphIndex:
         """The DGLMIGraph of a call: a cached template per (coo, col_blocks) -- every
         pointer in it is fixed for the graph's life -- copied, plus the call's
         workspace (cuts the host cost of a launch-bound call, C1-size graphs)."""
+        if self.num_bits == 64:
+            col_blocks = 0  # the blocked kernels are int32-only
         key = (bool(coo), int(col_blocks))
         tmpls = self.__dict__.setdefault("_ctmpl", {})
         if key not in tmpls:
@@ -280,7 +295,7 @@ class ImmutableGraphIndex:
         ic, oc = self.gather_cols()
         g.in_gather_cols = ic.data_ptr() if ic is not None else None
         g.out_gather_cols = oc.data_ptr() if oc is not None else None
-        g.num_bits = 32
+        g.num_bits = self.num_bits
         g.device = self.device.index if self.device.index is not None else th.cuda.current_device()
         g.workspace = None
         g.workspace_bytes = 0
@@ -353,14 +368,37 @@ def device_coo_to_csr(num_rows, row, col, data=None):
 def device_expand_rows(indptr, nnz):
     rows = th.empty(nnz, dtype=th.int32, device=indptr.device)
     if nnz:
-        rc = _ffi.lib().DGLMICSRExpandRows(_ptr(indptr), indptr.shape[0] - 1, nnz, _ptr(rows),
-                                           _stream_ptr(indptr.device))
+        fn = (_ffi.lib().DGLMICSRExpandRows64 if indptr.dtype == th.int64
+              else _ffi.lib().DGLMICSRExpandRows)
+        rc = fn(_ptr(indptr), indptr.shape[0] - 1, nnz, _ptr(rows), _stream_ptr(indptr.device))
         if rc != 0:
             raise DGLError("CSR row expansion failed")
     return rows
 
 
-def device_block_gidx(num_src, num_dst, src, dst):
+def device_coo_to_csr64(num_rows, row, col, data=None):
+    """COO -> CSR on the GPU for 64-bit graphs: int32 row / col, optional int64 data;
+    returns int64 indptr, int32 indices, int64 data (edge ids), bit-identical to
+    host_coo_to_csr."""
+    dev = row.device
+    nnz = int(row.shape[0])
+    L = _ffi.lib()
+    indptr = th.empty(num_rows + 1, dtype=th.int64, device=dev)
+    indices = th.empty(nnz, dtype=th.int32, device=dev)
+    out = th.empty(nnz, dtype=th.int64, device=dev)
+    ws = th.empty(int(L.DGLMICOOToCSRDevice64WorkspaceBytes(num_rows, nnz)), dtype=th.uint8,
+                  device=dev)
+    rc = L.DGLMICOOToCSRDevice64(num_rows, nnz, _ptr(row), _ptr(col), _ptr(data), _ptr(indptr),
+                                 _ptr(indices), _ptr(out), _ptr(ws), ws.numel(), _stream_ptr(dev))
+    if rc != 0:
+        raise DGLError("device COOToCSR (64-bit) failed")
+    return indptr, indices, out
+
+
+MAX_NODES = 0x7FFFFFFF  # node ids are int32 on the device, in both layouts
+
+
+def device_block_gidx(num_src, num_dst, src, dst, bits=None):
     """In/out CSRs of a (num_src -> num_dst) block from device int32 COO, on the GPU.
 
     out-CSR = stable sort of the eid-ordered COO by src; in-CSR = stable re-sort
@@ -369,14 +407,16 @@ def device_block_gidx(num_src, num_dst, src, dst):
     """
     dev = src.device
     m = int(src.shape[0])
-    if max(int(num_src), int(num_dst), m) >= 0x7FFFFFFF:
-        # the reference's GPU kernels are int32-only too (common.h:61-68)
-        raise DGLError("Unsupported idx bits: 64 (graphs need < 2^31 nodes and edges)")
+    if max(int(num_src), int(num_dst)) >= MAX_NODES:
+        raise DGLError("Unsupported graph: 2^31 or more nodes (device node ids are int32)")
+    if bits is None:
+        bits = 64 if m >= 0x7FFFFFFF else 32
     src = src.to(th.int32).contiguous()
     dst = dst.to(th.int32).contiguous()
-    o_ptr, o_idx, o_dat = device_coo_to_csr(num_src, src, dst)
+    build = device_coo_to_csr64 if bits == 64 else device_coo_to_csr
+    o_ptr, o_idx, o_dat = build(num_src, src, dst)
     o_rows = device_expand_rows(o_ptr, m)
-    i_ptr, i_idx, i_dat = device_coo_to_csr(num_dst, o_idx, o_rows, o_dat)
+    i_ptr, i_idx, i_dat = build(num_dst, o_idx, o_rows, o_dat)
     i_rows = device_expand_rows(i_ptr, m)
     return ImmutableGraphIndex(DeviceCSR(i_ptr, i_idx, i_dat, i_rows, num_src),
                                DeviceCSR(o_ptr, o_idx, o_dat, o_rows, num_dst),
@@ -397,6 +437,7 @@ class GraphIndex:
         self._etype = None        # per-edge relation ids (add_edges_with_type), numpy int64
         self._typed = {}
         self._device_only = None  # (src, dst) device tensors when built on the GPU
+        self._bits = None         # forced device index width (asbits)
 
     # ---- construction -----------------------------------------------------
     @classmethod
@@ -505,6 +546,23 @@ class GraphIndex:
         # graph_index.py:941-952
         return 32 if max(self._n, self.number_of_edges()) < 0x7FFFFFFF else 64
 
+    def device_bits(self):
+        """Index width of the device CSRs: bits_needed(), or 64 when forced by asbits."""
+        return 64 if self._bits == 64 else self.bits_needed()
+
+    def asbits(self, bits):
+        """graph_index.py:954-967: the same graph with the given index width.  Here
+        the device CSRs of the returned index use int64 offsets and edge ids when
+        ``bits`` is 64 (any graph, so small graphs exercise the 64-bit kernels);
+        32 keeps the width bits_needed() asks for."""
+        if bits not in (32, 64):
+            raise DGLError("Invalid bit width: %s (32 or 64)" % bits)
+        g = self.__class__.__new__(self.__class__)
+        g.__dict__.update(self.__dict__)
+        g._cache, g._typed = {}, {}
+        g._bits = bits if bits == 64 else None
+        return g
+
     def edges(self):
         """(src, dst, eid) in edge-id order (numpy int64)."""
         if self._device_only is not None:
@@ -549,8 +607,8 @@ class GraphIndex:
             device = th.device("cuda", th.cuda.current_device())
         key = str(device)
         if key not in self._cache:
-            if self.bits_needed() != 32:
-                raise DGLError("Unsupported idx bits: 64 (graphs need < 2^31 nodes and edges)")
+            if self._n >= MAX_NODES:
+                raise DGLError("Unsupported graph: 2^31 or more nodes (device node ids are int32)")
             if self._device_only is not None:
                 self._cache[key] = self._build_on_device(device)
             else:
@@ -561,16 +619,18 @@ class GraphIndex:
     def _upload(self, device):
         (op, oi, od), (ip, ii, idd) = self.host_csr()
         n = self._n
+        off = np.int64 if self.device_bits() == 64 else np.int32
 
         def mk(indptr, indices, data):
             rows = np.repeat(np.arange(n, dtype=np.int32), np.diff(indptr).astype(np.int64))
-            t = lambda a: th.from_numpy(np.ascontiguousarray(a, dtype=np.int32)).to(device)
-            return DeviceCSR(t(indptr), t(indices), t(data), t(rows), n)
+            t = lambda a, dt=np.int32: th.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(device)
+            return DeviceCSR(t(indptr, off), t(indices), t(data, off), t(rows), n)
 
         return ImmutableGraphIndex(mk(ip, ii, idd), mk(op, oi, od), n, n, device)
 
     def _build_on_device(self, device):
         src, dst = self._device_only
-        g = device_block_gidx(self._n, self._n, src.to(device), dst.to(device))
+        g = device_block_gidx(self._n, self._n, src.to(device), dst.to(device),
+                              bits=self.device_bits())
         g.device = th.device(device)
         return g

@@ -101,7 +101,9 @@ class GATConv(nn.Module):
             feat_src = feat_dst = B.project(h_src, self.fc.weight.t()).view(-1, self._num_heads, self._out_feats)
         el = (feat_src * self.attn_l).sum(dim=-1).unsqueeze(-1)
         er = (feat_dst * self.attn_r).sum(dim=-1).unsqueeze(-1)
-        if self._fused_ok():
+        # the fused kernels are int32-only: a 64-bit graph (2^31+ edges) takes the
+        # composition, whose kernels have 64-bit offsets
+        if self._fused_ok() and getattr(graph._graph, "device_bits", lambda: 32)() == 32:
             rst = self._fused(graph, feat_src, el, er)
         else:
             graph.srcdata.update({"ft": feat_src, "el": el})

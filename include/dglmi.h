@@ -24,7 +24,10 @@
  *
  * Deliberate differences (documented in DESIGN.md):
  *   - device work only (gfx950); fp32 features; int32 indices -- the same
- *     envelope as the reference GPU path (common.h:49-69);
+ *     envelope as the reference GPU path (common.h:49-69) -- or, for graphs of
+ *     2^31 or more edges (num_bits == 64), int64 offsets and edge ids with int32
+ *     node ids, where the reference falls back to its int64 CPU kernels
+ *     (graph_index.py:941-952, cpu/binary_reduce_sum.cc:15-23);
  *   - an edge-target mapping is indexed by edge id (the value of csr.data),
  *     not by CSR position, so one mapping serves every traversal direction;
  *   - node mappings (src/dst targets) must be injective (they are relabel
@@ -49,14 +52,16 @@ enum DGLMITarget {
   DGLMI_TARGET_NONE = 3
 };
 
-/* One direction of the adjacency (aten::CSRMatrix, include/dgl/array.h). */
+/* One direction of the adjacency (aten::CSRMatrix, include/dgl/array.h).
+ * When the graph's num_bits is 64, `indptr` and `data` point at int64_t arrays
+ * (cast the pointers); indices and rows are int32 in both layouts. */
 typedef struct {
   int64_t num_rows;
   int64_t num_cols;
   int64_t nnz;
-  const int32_t* indptr;  /* num_rows + 1 */
+  const int32_t* indptr;  /* num_rows + 1 (int64 values when num_bits == 64) */
   const int32_t* indices; /* nnz, column node ids */
-  const int32_t* data;    /* nnz, edge ids */
+  const int32_t* data;    /* nnz, edge ids (int64 values when num_bits == 64) */
   const int32_t* rows;    /* nnz, row id of every position (COO rows, ascending);
                              required: the edge-wise kernels and the load-balanced
                              reduce path read the row of a position from it */
@@ -66,7 +71,11 @@ typedef struct {
 typedef struct {
   DGLMICsr in_csr;        /* rows = destination nodes, cols = source nodes */
   DGLMICsr out_csr;       /* rows = source nodes, cols = destination nodes */
-  int32_t num_bits;       /* index width; must be 32 */
+  int32_t num_bits;       /* 32, or 64: int64 indptr / data (graphs of >= 2^31 edges;
+                             node ids < 2^31).  64-bit graphs take every builtin
+                             message / reduce / SDDMM / edge-softmax entry without
+                             mappings; the fused GAT, R-GCN, NbAccess, partitioning
+                             and column-block entries need 32. */
   int32_t device;         /* HIP device ordinal the arrays live on */
   void* workspace;        /* caller-owned scratch for this call (may be NULL) */
   int64_t workspace_bytes;
@@ -239,6 +248,18 @@ int DGLMICOOToCSRDevice(int64_t num_rows, int64_t nnz, const int32_t* row, const
 /* Row id of every CSR position (CSRToCOO rows, spmat_op_impl.cc:375-387), device. */
 int DGLMICSRExpandRows(const int32_t* indptr, int64_t num_rows, int64_t nnz, int32_t* rows,
                        void* stream);
+/* 64-bit graphs (num_bits == 64): device COO -> CSR with int64 offsets and edge ids
+ * (row / col int32 node ids, optional int64 data; indptr int64, indices int32,
+ * out_data int64), bit-identical to DGLMICOOToCSR; a stable counting sort in
+ * batches of 2^30 positions.  Workspace: DGLMICOOToCSRDevice64WorkspaceBytes. */
+int64_t DGLMICOOToCSRDevice64WorkspaceBytes(int64_t num_rows, int64_t nnz);
+int DGLMICOOToCSRDevice64(int64_t num_rows, int64_t nnz, const int32_t* row, const int32_t* col,
+                          const int64_t* data, int64_t* indptr, int32_t* indices,
+                          int64_t* out_data, void* workspace, int64_t workspace_bytes,
+                          void* stream);
+/* DGLMICSRExpandRows for an int64 indptr. */
+int DGLMICSRExpandRows64(const int64_t* indptr, int64_t num_rows, int64_t nnz, int32_t* rows,
+                         void* stream);
 
 /* ---- fused GAT (hack kernels _CAPI_DGLFusedGatKernel / _CAPI_DGLKernelBackwardFusedGat,
  * binary_reduce.cc:380-396, 529-549) ------------------------------------------

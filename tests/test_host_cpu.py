@@ -141,10 +141,22 @@ def test_capi_errors_without_device():
     rc = L.DGLMIKernelBinaryOpReduce(b"sum", b"pow", ctypes.byref(g), 0, 2, ctypes.byref(a),
                                      ctypes.byref(a), ctypes.byref(a), None, None, None, None)
     assert rc == -1 and "Unsupported binary op" in _ffi.last_error()
-    g.num_bits = 64
+    g.num_bits = 16
     rc = L.DGLMIKernelCopyReduce(b"sum", ctypes.byref(g), 0, ctypes.byref(a), ctypes.byref(a),
                                  None, None, None)
     assert rc == -1 and "idx bits" in _ffi.last_error()
+    # 64-bit graphs: mappings, and the int32-only entries, are refused before any device work
+    g.num_bits = 64
+    m = (ctypes.c_int32 * 2)()
+    rc = L.DGLMIKernelCopyReduce(b"sum", ctypes.byref(g), 0, ctypes.byref(a), ctypes.byref(a),
+                                 m, None, None)
+    assert rc == -1 and "mappings need a graph of fewer than 2^31 edges" in _ffi.last_error()
+    rc = L.DGLMIFusedGatForward(ctypes.byref(g), ctypes.byref(a), ctypes.byref(a), ctypes.byref(a),
+                                0.2, ctypes.byref(a), ctypes.byref(a), ctypes.byref(a), None)
+    assert rc == -1 and "fused GAT needs a graph of fewer than 2^31 edges" in _ffi.last_error()
+    st = _ffi.RgcnState()
+    rc = L.DGLMIRgcnPrepare(ctypes.byref(g), None, None, 2, 1, ctypes.byref(st), None)
+    assert rc == -1 and "R-GCN needs a graph of fewer than 2^31 edges" in _ffi.last_error()
 
 
 def test_builtin_names():
@@ -190,16 +202,28 @@ def test_ctypes_structs_match_header_layout(tmp_path):
             assert int(got["%s.%s" % (cname, f)]) == getattr(cls, f).offset, (cname, f)
 
 
-def test_64bit_graphs_rejected_loudly():
-    """graph_index.py:941-952 switches to int64 ids at 2^31 nodes or edges; the
-    reference's GPU kernels are int32-only (common.h:61-68), and so are these:
-    such graphs raise DGLError instead of wrapping indices."""
+def test_64bit_graph_selection():
+    """graph_index.py:941-952 switches to int64 ids at 2^31 nodes or edges.  Device
+    node ids stay int32, so 2^31 nodes raise DGLError; 2^31 edges (or asbits(64))
+    select the 64-bit layout: int64 offsets and edge ids (checked on the GPU in
+    tests/test_int64_gpu.py)."""
     from dgl.graph_index import device_block_gidx
     g = GraphIndex(2 ** 31)
     assert g.bits_needed() == 64
-    with pytest.raises(dgl.DGLError, match="idx bits: 64"):
+    with pytest.raises(dgl.DGLError, match="2\\^31 or more nodes"):
         g.get_immutable_gidx("cuda:0")
     tiny = th.zeros(1, dtype=th.int32)
-    with pytest.raises(dgl.DGLError, match="idx bits: 64"):
+    with pytest.raises(dgl.DGLError, match="2\\^31 or more nodes"):
         device_block_gidx(2 ** 31, 4, tiny, tiny)
     assert GraphIndex(2 ** 31 - 2).bits_needed() == 32
+    small = GraphIndex(3)
+    small.add_edges([0, 1], [1, 2])
+    assert small.device_bits() == 32
+    wide = small.asbits(64)
+    assert wide.device_bits() == 64 and small.device_bits() == 32
+    assert wide.number_of_edges() == 2 and wide.asbits(32).device_bits() == 32
+    with pytest.raises(dgl.DGLError, match="Invalid bit width"):
+        small.asbits(16)
+    from dgl.graph import _PartialIndex
+    assert _PartialIndex(4, [0], [1], [2 ** 31]).bits_needed() == 64
+    assert _PartialIndex(4, [0], [1], [5]).bits_needed() == 32
