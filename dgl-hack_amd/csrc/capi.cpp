@@ -1077,6 +1077,18 @@ int DGLMIFusedGatBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src, c
   a.g_el = grad_el->data;
   a.g_ft = grad_feat_src->data;
   const int nb = gat_blocks(graph);
+  // Edge-position backward (DGLMIGraph.gat_edge_pos): no destination-side walk.  The
+  // stats come from a dense pass, the source-side walk stores every edge's grad_er
+  // term in out-CSR order, and grad_er is one copy_e-style gather-sum over the in-CSR
+  // through the position map -- a 32-B term per edge instead of a 256-B feature row
+  // and a logit (C3 unblocked, H = 8: backward 11.98 -> 9.57 ms; M1-size RMAT
+  // 11.48 -> 10.89 ms).  Unblocked walks only: with column blocks the destination
+  // walk's gathers hit L2 and the term writes plus their random re-reads cost more
+  // (C3, 8 blocks: 8.52 -> 9.15 ms; profiles/r03_gat_edge_pos.json).
+  const bool blocks_given = graph->num_col_blocks > 1 && graph->in_col_blocks != nullptr &&
+                            graph->out_col_blocks != nullptr;
+  const bool pos_path = graph->gat_edge_pos != nullptr && nb == 1 && !blocks_given &&
+                        fast_supported(FAST_COPY_EDGE, a.H, 1) && aligned16(grad_er->data);
   int64_t chunks = (in.nnz + a.chunk - 1) / a.chunk;
   for (int b = 0; b < nb && nb > 1; ++b)
     for (const DGLMICsr* c : {&graph->in_col_blocks[b], &graph->out_col_blocks[b]}) {
@@ -1089,6 +1101,30 @@ int DGLMIFusedGatBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src, c
   a.stats = static_cast<float4*>(ws.ptr);
   a.carry = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + ((stats_bytes + 255) & ~int64_t(255)));
   a.seg_cnt = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(a.carry) + carry_bytes);
+  if (pos_path) {
+    DGLMIGraph nows;  // t must not alias the caller's workspace (the reduce's carries)
+    std::memset(&nows, 0, sizeof(nows));
+    Scratch tbuf(&nows, in.nnz * a.H * static_cast<int64_t>(sizeof(float)), s);
+    a.t = static_cast<float*>(tbuf.ptr);
+    launch_gat_stats(a, s);
+    GatArgs b = a;
+    b.indptr = outc.indptr;
+    b.rows = outc.rows;
+    b.indices = outc.indices;
+    b.nnz = outc.nnz;
+    b.num_rows = outc.num_rows;
+    launch_gat_backward_src(b, s);
+    check_hip(hipGetLastError(), "fused GAT backward (src) launch");
+    DGLMIGraph gp = *graph;  // no blocks / hints for the gather-sum
+    gp.num_col_blocks = 0;
+    gp.in_col_blocks = gp.out_col_blocks = nullptr;
+    gp.in_gather_cols = gp.out_gather_cols = nullptr;
+    DGLMICsr walk = in;
+    walk.data = graph->gat_edge_pos;
+    run_fast(&gp, walk, FAST_COPY_EDGE, RED_SUM, a.t, nullptr, nullptr, nullptr, grad_er->data, a.H,
+             1, s);
+    return 0;
+  }
   if (nb > 1) {
     // column-blocked: block 0 writes every row's stats and the first gradient
     // terms, later blocks add theirs (block order), first the destination side

@@ -346,12 +346,19 @@ struct GatArgs {
   int accumulate;   // backward: add into g_er / g_ft / g_el instead of overwriting
   int skip_stats;   // backward (dst side): stats already written by an earlier block
   int o32;          // every gathered row offset (ft, el, grad_out, stats) < 2^31 elements
+  // edge-position backward (DGLMIGraph.gat_edge_pos): the source-side walk stores every
+  // edge's grad_er term at t[(t_off + position) * H + h]; NULL = not stored
+  float* t;
+  int64_t t_off;
 };
 bool gat_supported(int64_t H, int64_t D);
 int64_t gat_chunk_edges(int64_t nnz);
 void launch_gat_forward(const GatArgs& a, hipStream_t s);
 void launch_gat_backward_dst(const GatArgs& a, hipStream_t s);
 void launch_gat_backward_src(const GatArgs& a, hipStream_t s);
+// stats[v, h] = {er, m, 1/l, <grad_out[v,h,:], out[v,h,:]>} for every destination row
+// (dense; replaces the destination-side walk's stats when gat_edge_pos is given)
+void launch_gat_stats(const GatArgs& a, hipStream_t s);
 // out[r] = merge over blocks b of the unnormalised partials (out_part[b], m_part[b],
 // l_part[b]), normalised; m / l of the merged softmax (blocks in order)
 void launch_gat_merge(const float* out_part, const float* m_part, const float* l_part, int nb,

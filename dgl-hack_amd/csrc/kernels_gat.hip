@@ -540,7 +540,11 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
           const float att = fexp(leaky(pre, a.slope) - sv.y) * sv.z;
           const float4 gv = gov[u][v];
           const float ge = head_sum(dot4(gv, ftv[v]), D4);
-          acce[v] += att * (ge - sv.w) * dleaky(pre, a.slope);
+          const float te = att * (ge - sv.w) * dleaky(pre, a.slope);
+          acce[v] += te;
+          // the edge's grad_er term, in this walk's position order (edge-position
+          // backward: grad_er is then one gather-sum over the in-CSR)
+          if (a.t != nullptr && lead[v]) a.t[(a.t_off + base + ub + u) * H + hd[v]] = te;
           accf[v] = make_float4(accf[v].x + att * gv.x, accf[v].y + att * gv.y,
                                 accf[v].z + att * gv.z, accf[v].w + att * gv.w);
         }
@@ -660,6 +664,32 @@ __global__ void __launch_bounds__(kBlock) k_gat_merge(const float* __restrict__ 
   }
 }
 
+// Destination stats without a destination-side walk (edge-position backward): one
+// thread per float4 slot of a row, the head's D4 slots adjacent and aligned in the
+// wavefront, so delta is reduced by the same head_sum as the destination walk's
+// (bit-identical stats).  Every lane reaches the shuffles (no early exit).
+__global__ void k_gat_stats(GatArgs a) {
+  const int F4 = static_cast<int>(a.F / 4), D4 = a.D / 4;
+  const int64_t n = a.num_rows * F4;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  const int64_t start = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t span = (n + stride - 1) / stride * stride;  // wave-uniform trip count
+  for (int64_t i = start; i < span; i += stride) {
+    const bool ok = i < n;
+    const int64_t r = ok ? i / F4 : 0;
+    const int f4 = ok ? static_cast<int>(i - r * F4) : 0;
+    const float4 Z = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 g = ok ? ld4g(a.go + r * a.F + 4 * f4) : Z;
+    const float4 o = ok ? ld4g(a.fo + r * a.F + 4 * f4) : Z;
+    const float d = head_sum(dot4(g, o), D4);
+    if (ok && f4 % D4 == 0) {
+      const int64_t j = r * a.H + f4 / D4;
+      const float l = a.l_in[j];
+      a.stats[j] = make_float4(a.er[j], a.m_in[j], l > 0.0f ? 1.0f / l : 0.0f, d);
+    }
+  }
+}
+
 struct Cfg {
   int L, NV;
 };
@@ -767,5 +797,12 @@ void launch_gat_fold_lse(const float* m, float* l, int64_t n, hipStream_t s) {
 }
 void launch_gat_backward_dst(const GatArgs& a, hipStream_t s) { DGLMI_GAT_DISPATCH(bwd_dst_cfg, a, s); }
 void launch_gat_backward_src(const GatArgs& a, hipStream_t s) { DGLMI_GAT_DISPATCH(bwd_src_cfg, a, s); }
+void launch_gat_stats(const GatArgs& a, hipStream_t s) {
+  const int64_t n = a.num_rows * (a.F / 4);
+  if (n <= 0) return;
+  const int64_t want = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_gat_stats, dim3(static_cast<unsigned>(want < 65536 ? want : 65536)),
+                     dim3(kBlock), 0, s, a);
+}
 
 }  // namespace dglmi

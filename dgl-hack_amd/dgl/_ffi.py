@@ -48,6 +48,7 @@ class Graph(ctypes.Structure):
         ("in_col_blocks", ctypes.c_void_p),
         ("out_col_blocks", ctypes.c_void_p),
         ("rgcn", ctypes.c_void_p),
+        ("gat_edge_pos", ctypes.c_void_p),
     ]
 
 

@@ -261,16 +261,30 @@ class ImmutableGraphIndex:
         g.workspace_bytes = 0
         return g
 
-    def cstruct(self, workspace=None, coo=False, col_blocks=0):
-        """The DGLMIGraph of a call: a cached template per (coo, col_blocks) -- every
-        pointer in it is fixed for the graph's life -- copied, plus the call's
+    def gat_edge_pos(self):
+        """DGLMIGraph.gat_edge_pos: for every in-CSR position, the out-CSR position of
+        the same edge, built once on the device (int32, 4 B per edge)."""
+        if getattr(self, "_gat_pos", None) is None:
+            ic, oc = self.in_csr, self.out_csr
+            dev = ic.indices.device
+            inv = th.empty(ic.nnz, dtype=th.int32, device=dev)
+            inv[oc.data.long()] = th.arange(oc.nnz, dtype=th.int32, device=dev)
+            self._gat_pos = inv[ic.data.long()].contiguous()
+        return self._gat_pos
+
+    def cstruct(self, workspace=None, coo=False, col_blocks=0, edge_pos=False):
+        """The DGLMIGraph of a call: a cached template per (coo, col_blocks, edge_pos)
+        -- every pointer in it is fixed for the graph's life -- copied, plus the call's
         workspace (cuts the host cost of a launch-bound call, C1-size graphs)."""
         if self.num_bits == 64:
-            col_blocks = 0  # the blocked kernels are int32-only
-        key = (bool(coo), int(col_blocks))
+            col_blocks, edge_pos = 0, False  # the blocked and GAT kernels are int32-only
+        edge_pos = bool(edge_pos) and self.eid_perm and self.in_csr.nnz > 0 and col_blocks <= 1
+        key = (bool(coo), int(col_blocks), edge_pos)
         tmpls = self.__dict__.setdefault("_ctmpl", {})
         if key not in tmpls:
             tmpls[key] = self._make_cstruct(coo, col_blocks)
+            if edge_pos:
+                tmpls[key].gat_edge_pos = self.gat_edge_pos().data_ptr()
         g = _ffi.Graph.from_buffer_copy(tmpls[key])
         if workspace is not None:
             g.workspace = workspace.data_ptr()

@@ -298,6 +298,22 @@ def gat_col_blocks(graph, feat_src, backward=False):
     return nb
 
 
+def gat_edge_pos(graph, col_blocks):
+    """Whether the fused GAT backward takes the edge-position path (DGLMIGraph
+    .gat_edge_pos: no destination-side walk; grad_er from the source-side walk's
+    per-edge terms): unblocked whole graphs (edge ids a permutation).  C3 unblocked
+    11.98 -> 9.57 ms, M1-size RMAT 11.48 -> 10.89 ms; with column blocks the
+    destination walk stays faster (8.52 vs 9.15 ms; profiles/r03_gat_edge_pos.json).
+    DGLMI_GAT_EDGE_POS=0 keeps the destination-side walk."""
+    return (os.environ.get("DGLMI_GAT_EDGE_POS", "1") != "0" and graph.eid_perm
+            and col_blocks <= 1)
+
+
+def _gat_bwd_cgraph(graph, feat_src):
+    nb = gat_col_blocks(graph, feat_src, backward=True)
+    return graph.cstruct(None, col_blocks=nb, edge_pos=gat_edge_pos(graph, nb))
+
+
 def fused_gat_forward(graph, feat_src, el, er, slope, out, max_out, sum_out):
     """_CAPI_DGLFusedGatKernel (binary_reduce.cc:380-396) -> DGLMIFusedGatForward."""
     _check_ctx(graph, [("feat_src", feat_src), ("el", el), ("er", er), ("out", out)])
@@ -313,7 +329,7 @@ def fused_gat_backward(graph, feat_src, el, er, slope, out, max_in, sum_in, grad
                        grad_feat_src, grad_el, grad_er):
     """_CAPI_DGLKernelBackwardFusedGat (binary_reduce.cc:529-549) -> DGLMIFusedGatBackward."""
     _check_ctx(graph, [("feat_src", feat_src), ("grad_out", grad_out)])
-    g = graph.cstruct(None, col_blocks=gat_col_blocks(graph, feat_src, backward=True))
+    g = _gat_bwd_cgraph(graph, feat_src)
     check_call(_ffi.lib().DGLMIFusedGatBackward(
         ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"), float(slope),
         _arr(out, "out"), _arr(max_in, "max_in"), _arr(sum_in, "sum_in"),
@@ -341,7 +357,7 @@ def backward_fused_gat(graph, feat_src, el, er, s, exp, ret, grad_out, grad_feat
     _CAPI_DGLKernelBackwardFusedGat (binary_reduce.cc:529-549) ->
     DGLMIKernelBackwardFusedGat.  Overwrites the three gradients."""
     _check_ctx(graph, [("feat_src", feat_src), ("grad_out", grad_out)])
-    g = graph.cstruct(None, col_blocks=gat_col_blocks(graph, feat_src, backward=True))
+    g = _gat_bwd_cgraph(graph, feat_src)
     check_call(_ffi.lib().DGLMIKernelBackwardFusedGat(
         ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"), _arr(s, "s"),
         _arr(exp, "exp"), _arr(ret, "ret"), _arr(grad_out, "grad_out"),

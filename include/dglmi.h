@@ -113,6 +113,13 @@ typedef struct {
    * read by the DGLMIRgcnLayer* entries when it matches the call's etypes (and norm)
    * pointers.  NULL = every call derives what it needs from etypes / norm. */
   const struct DGLMIRgcnState* rgcn;
+  /* Optional (extension): for every in-CSR position p, the out-CSR position of the
+   * same edge.  When present and the fused GAT backward runs unblocked (no column
+   * blocks), it drops its destination-side walk: the source-side walk stores each
+   * edge's grad_er term in out-CSR order and grad_er is one gather-sum over the
+   * in-CSR (a 256-B feature row and a logit gathered per edge become one H-float
+   * term; C3 unblocked 11.98 -> 9.57 ms).  NULL = the destination-side walk. */
+  const int32_t* gat_edge_pos;
 } DGLMIGraph;
 
 /* A contiguous row-major fp32 device array (NDArray / DLTensor subset). */

@@ -33,8 +33,15 @@ def run(args):
     from dgl import kernel as K
     from bench_configs import chung_lu
     dev = "cuda:0"
-    n, m, H, D = 232965, 114615892, 8, 8
-    g = chung_lu(n, m, 0.4, 3, dev)
+    H, D = 8, 8
+    if args.graph == "m1":  # the bench's M1 graph (RMAT scale 23, 100 M edges)
+        import dgl
+        from bench import build_workload
+        n, _, src, dst, _ = build_workload(1, 0, th.device(dev))
+        g = dgl.DGLGraph.from_device_coo(src, dst, n)
+    else:
+        n, m = 232965, 114615892
+        g = chung_lu(n, m, 0.4, 3, dev)
     gidx = g._graph.get_immutable_gidx(dev)
     gen = th.Generator(device=dev)
     gen.manual_seed(3)
@@ -53,15 +60,23 @@ def run(args):
     for blocks in (os.environ.get("GAT_AB_BLOCKS", "auto 1")).split():
         if blocks != "auto":
             os.environ["DGLMI_GAT_BLOCKS"] = blocks
-        fwd = lambda: K.fused_gat_forward(gidx, ft, el, er, 0.2, out, mx, sm)
-        bwd = lambda: K.fused_gat_backward(gidx, ft, el, er, 0.2, out, mx, sm, go, gft, gel, ger)
-        res["fwd_ms_" + blocks] = ev_time(fwd)
-        res["bwd_ms_" + blocks] = ev_time(bwd)
-        fwd()
-        bwd()
-        th.cuda.synchronize()
-        saved[blocks] = [t.cpu().clone() for t in (out, mx, sm, gft, gel, ger)]
+        # GAT_AB_POS: the backward's edge-position path (1) and destination-side walk (0)
+        for pos in (os.environ.get("GAT_AB_POS", "1")).split():
+            os.environ["DGLMI_GAT_EDGE_POS"] = pos
+            key = blocks if pos == "1" else blocks + "_dstwalk"
+            fwd = lambda: K.fused_gat_forward(gidx, ft, el, er, 0.2, out, mx, sm)
+            bwd = lambda: K.fused_gat_backward(gidx, ft, el, er, 0.2, out, mx, sm, go, gft, gel, ger)
+            res["fwd_ms_" + key] = ev_time(fwd)
+            res["bwd_ms_" + key] = ev_time(bwd)
+            fwd()
+            bwd()
+            th.cuda.synchronize()
+            saved[key] = [t.cpu().clone() for t in (out, mx, sm, gft, gel, ger)]
+            if key.endswith("_dstwalk") and blocks in saved:
+                d = (saved[key][5].double() - saved[blocks][5].double()).abs()
+                res["g_er_maxabs_pos_vs_dstwalk_" + blocks] = float(d.max())
     os.environ.pop("DGLMI_GAT_BLOCKS", None)
+    os.environ.pop("DGLMI_GAT_EDGE_POS", None)
     if args.save:
         th.save(saved, args.save)
     print(json.dumps(res), flush=True)
@@ -82,6 +97,7 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--save", default=None)
     ap.add_argument("--compare", nargs=2, default=None)
+    ap.add_argument("--graph", default="c3", choices=["c3", "m1"])
     args = ap.parse_args()
     if args.compare:
         compare(*args.compare)

@@ -206,3 +206,38 @@ def test_gatconv_padded_head_width_matches_unfused(heads, out):
     yb.pow(2).sum().backward()
     for pa, pb in zip(a.parameters(), b.parameters()):
         assert th.allclose(pa.grad, pb.grad, rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("H,D", [(8, 8), (3, 16), (16, 4)])
+def test_fused_gat_edge_position_backward(H, D, monkeypatch):
+    """The unblocked backward without its destination-side walk (DGLMIGraph
+    .gat_edge_pos): dense stats, grad_er terms stored in out-CSR order by the
+    source-side walk, one gather-sum over the in-CSR.  The feature and el gradients
+    equal the destination-walk backward bit for bit (the same source-side walk);
+    grad_er differs only in summation order; all three match the fp64
+    restatement, hub rows included."""
+    src, dst, n = powerlaw(20000, 300000, seed=29)
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    gen = th.Generator(device=DEV).manual_seed(9)
+    ft = th.randn(n, H, D, device=DEV, generator=gen).requires_grad_()
+    el = (3 * th.randn(n, H, 1, device=DEV, generator=gen)).requires_grad_()
+    er = (3 * th.randn(n, H, 1, device=DEV, generator=gen)).requires_grad_()
+    go = None
+    grads = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("DGLMI_GAT_EDGE_POS", mode)
+        out = B.fused_gat(g, ft, el, er, 0.2)
+        if go is None:
+            go = th.randn(out.shape, device=DEV, generator=gen)
+        grads[mode] = th.autograd.grad(out, (ft, el, er), go)
+    gidx = g._graph.get_immutable_gidx(th.device(DEV))
+    assert getattr(gidx, "_gat_pos", None) is not None  # the edge-position path ran
+    assert th.equal(grads["1"][0], grads["0"][0]) and th.equal(grads["1"][1], grads["0"][1])
+    assert th.allclose(grads["1"][2], grads["0"][2], rtol=1e-5, atol=1e-5)
+    fd, eld, erd = (t.detach().double().requires_grad_() for t in (ft, el, er))
+    ref = dense_gat(src, dst, n, fd, eld, erd, 0.2)
+    gr = th.autograd.grad(ref, (fd, eld, erd), go.double())
+    for a, b, name in zip(grads["1"], gr, ("ft", "el", "er")):
+        assert th.allclose(a.double(), b, rtol=1e-3, atol=1e-3), name
