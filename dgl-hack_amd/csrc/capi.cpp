@@ -1572,9 +1572,10 @@ int DGLMIRgcnLayer0Backward(const DGLMIGraph* graph, const int32_t* etypes,
   API_END();
 }
 
-int DGLMIRgcnLayer1(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* hidden,
-                    const DGLMIArray* weight, const DGLMIArray* norm, DGLMIArray* ret,
-                    void* stream) {
+namespace {
+int rgcn_layer1_impl(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* hidden,
+                     const DGLMIArray* weight, const DGLMIArray* norm, const DGLMIEpilogue* epi,
+                     DGLMIArray* ret, void* stream) {
   API_BEGIN();
   check_array(hidden, "hidden");
   check_array(weight, "weight");
@@ -1588,6 +1589,12 @@ int DGLMIRgcnLayer1(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIA
   DGLMI_CHECK(ret->shape[0] == in.num_rows && feat_numel(ret) == X, "ret must be (num_dst, F_out)");
   edge_values(norm, in.nnz, "norm");
   check_fast_width(X);
+  const float* bias = epi ? epi->bias : nullptr;
+  const float* addend = epi ? epi->addend : nullptr;
+  DGLMI_CHECK(!epi || (!epi->row_mul && !epi->row_div),
+              "the R-GCN epilogue takes bias and addend only");
+  DGLMI_CHECK(!addend || (addend != ret->data && aligned16(addend)),
+              "addend must not alias ret and must be 16-byte aligned");
   DeviceGuard guard(graph->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t N = in.num_cols, M = R * X;
@@ -1599,7 +1606,7 @@ int DGLMIRgcnLayer1(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIA
       rgcn_fused_walk(fs, fs->in_rel, fs->in_rel_norm, norm->data, &eids, &w);
       launch_rgcn_fused(false, fs->in_rel.indptr, fs->in_rel.indices, fs->in_rel.rows, eids, w,
                         hidden->data, weight->data, K * X, X, 1, ret->data, nullptr, in.num_rows, R,
-                        X, s);
+                        X, s, bias, addend);
       check_hip(hipGetLastError(), "rgcn fused layer1 launch");
       return 0;
     }
@@ -1619,9 +1626,23 @@ int DGLMIRgcnLayer1(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIA
     walk.indices = static_cast<int32_t*>(cols.ptr);
     walk.num_cols = N * R;
   }
+  const DGLMIEpilogue e2{nullptr, nullptr, bias, addend};
   run_fast(&pg, walk, FAST_COL_MUL_EDGE_BCAST, RED_SUM, static_cast<float*>(y.ptr), nullptr, w,
-           nullptr, ret->data, X, X, s);
+           nullptr, ret->data, X, X, s, (bias || addend) ? &e2 : nullptr);
   API_END();
+}
+}  // namespace
+
+int DGLMIRgcnLayer1(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* hidden,
+                    const DGLMIArray* weight, const DGLMIArray* norm, DGLMIArray* ret,
+                    void* stream) {
+  return rgcn_layer1_impl(graph, etypes, hidden, weight, norm, nullptr, ret, stream);
+}
+
+int DGLMIRgcnLayer1Ex(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* hidden,
+                      const DGLMIArray* weight, const DGLMIArray* norm,
+                      const DGLMIEpilogue* epilogue, DGLMIArray* ret, void* stream) {
+  return rgcn_layer1_impl(graph, etypes, hidden, weight, norm, epilogue, ret, stream);
 }
 
 int DGLMIRgcnLayer1Backward(const DGLMIGraph* graph, const int32_t* etypes,

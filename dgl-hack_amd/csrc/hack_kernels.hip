@@ -11,6 +11,8 @@
 // the C entries keep the library free of a second BLAS runtime in the caller's
 // process and use the kernel below -- these shapes (K, F <= a few hundred) are
 // bound by reading X and writing Y, not by the FMAs.
+#include <stdexcept>
+
 #include "internal.h"
 
 namespace dglmi {
@@ -310,16 +312,18 @@ __global__ void __launch_bounds__(kGemmThreads) k_gemm_tn(const float* __restric
 // ---------------------------------------------------------------------------
 // Fused R-GCN layer 1: aggregate each relation's rows first, transform after, in one
 // kernel.  out[v] = sum_t (sum_{e = (u -> v), type t} w_e T[u]) . W_t: every wave owns
-// 32-row tiles of out (strided over the grid); for each relation t it gathers the 32
-// rows' relation-t sums of T (64-float rows, 16 lanes per row, 8 rows per 16-lane
-// group, 8 gathers in flight per lane) into its private LDS slot, and one MFMA pass
+// 32-row tiles of out (drawn from a queue); for each relation t it gathers the 32
+// rows' relation-t sums of T (64-float rows, 16 lanes per row; the tile's edges cut
+// into four equal shares, one per 16-lane group, rows cut by a share boundary
+// finished through per-group carries in group order; 8 gathers in flight per lane)
+// into its private LDS slot, and one MFMA pass
 // (v_mfma_f32_32x32x2_f32) adds slot . W_t into the tile's accumulators; W (all
 // relations, <= 64 KB) sits in LDS for the block's life.  No Y = T . W_cat table
 // (5.1 GB on C5) is written or gathered: the gathers read T (1.3 GB) and the only HBM
 // write is the output.  Walks the relation-major CSR (rows t * num_rows + v, the
 // prepared state's in_rel / out_typed[0]), whose rows of one relation and tile are
-// contiguous.  Deterministic: each row's edges in position order, then relations
-// and k in order.  BWD: the same walk over the relation-major out-CSR gathers
+// contiguous.  Deterministic: each row's edges in position order (a cut row's
+// share sums added in share order), then relations and k in order.  BWD: the same walk over the relation-major out-CSR gathers
 // grad_out rows into G_t (stored to gy for the weight gradient) and adds
 // G_t . W_t^T into grad_hidden.  The weights enter as W[t][k][n] =
 // W_src[t * ws_t + k * ws_k + n * ws_n] (k over the gathered width 64).
@@ -332,10 +336,12 @@ __global__ void __launch_bounds__(kGemmThreads) k_rgcn_fused(
     const int32_t* __restrict__ rows, const int32_t* __restrict__ eids, const float* __restrict__ w,
     const float* __restrict__ T, const float* __restrict__ W, int64_t ws_t, int64_t ws_k,
     int64_t ws_n, float* __restrict__ out, float* __restrict__ gy, int64_t num_rows, int R,
-    int out_w) {
+    int out_w, const float* __restrict__ bias, const float* __restrict__ addend,
+    unsigned* __restrict__ tile_ctr) {
   constexpr int SW = NB * 32;
   __shared__ float Ws[16384];
   __shared__ float slots[8][32 * kSlotStride];
+  __shared__ float carries[8][4][kFusedW];
   for (int i = threadIdx.x; i < R * kFusedW * SW; i += kGemmThreads) {
     const int t = i / (kFusedW * SW), k = (i / SW) % kFusedW, n = i % SW;
     Ws[i] = n < out_w ? W[t * ws_t + k * ws_k + n * ws_n] : 0.0f;
@@ -345,28 +351,52 @@ __global__ void __launch_bounds__(kGemmThreads) k_rgcn_fused(
   const int r = lane & 31, hb = lane >> 5;
   const int g = lane >> 4, q = lane & 15;  // 16-lane group, float4 column
   float* slot = slots[wv];
+  float* carry = carries[wv][0];
   const int64_t tiles = (num_rows + 31) / 32;
-  const int64_t step = static_cast<int64_t>(gridDim.x) * 8;
-  for (int64_t tile = static_cast<int64_t>(blockIdx.x) * 8 + wv; tile < tiles; tile += step) {
+  for (;;) {
+    // tiles from a queue (one vector atomic per tile): a wave that drew a hub row's
+    // tile does not hold the others back; each tile's result does not depend on
+    // which wave computed it
+    unsigned tv = 0;
+    if (lane == 0) tv = atomicAdd(tile_ctr, 1u);
+    const int64_t tile = static_cast<unsigned>(__shfl(static_cast<int>(tv), 0));
+    if (tile >= tiles) break;
     const int64_t v0 = tile * 32;
+    const int tile_rows = num_rows - v0 < 32 ? static_cast<int>(num_rows - v0) : 32;
     f32x16 acc[NB];
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x16{};
     for (int t = 0; t < R; ++t) {
-      // zero this group's 8 slot rows, then gather their relation-t sums
+      const int64_t base = static_cast<int64_t>(t) * num_rows + v0;
+      const int64_t pb = ptr[base], pe = ptr[base + tile_rows];
+      if (!BWD && pb == pe) continue;  // no relation-t edge into the tile
+      // zero the 32 slot rows (8 per group; the stores below come later in this
+      // wave's program order)
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         float* d = slot + (8 * g + i) * kSlotStride + 4 * q;
         d[0] = d[1] = d[2] = d[3] = 0.0f;
       }
-      const int64_t vg = v0 + 8 * g;
-      const int cnt = vg < num_rows ? static_cast<int>(num_rows - vg < 8 ? num_rows - vg : 8) : 0;
-      const int64_t base = static_cast<int64_t>(t) * num_rows + vg;
-      const int64_t pb = cnt > 0 ? ptr[base] : 0, pe = cnt > 0 ? ptr[base + cnt] : 0;
+      // the tile's relation-t edges (contiguous) in four equal shares, one per
+      // 16-lane group; a row cut by a share boundary is stored by the group holding
+      // its first edge and continued in the next groups' carries
+      const int64_t share = (pe - pb + 3) / 4;
+      const int64_t gb = pb + g * share < pe ? pb + g * share : pe;
+      const int64_t ge = gb + share < pe ? gb + share : pe;
+      const bool cont = gb < ge && gb > pb && rows[gb - 1] == rows[gb];
+      bool first = true;
+      int crow = -1;  // the row this group's carry continues (-1: none)
       float4 a4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
       int cur = -1;
-      for (int64_t p = pb; p < pe; p += 16) {
-        const int n = pe - p < 16 ? static_cast<int>(pe - p) : 16;
+      auto flush = [&]() {
+        float* d = (first && cont) ? carry + g * kFusedW + 4 * q
+                                   : slot + cur * kSlotStride + 4 * q;
+        if (first && cont) crow = cur;
+        d[0] = a4.x; d[1] = a4.y; d[2] = a4.z; d[3] = a4.w;
+        first = false;
+      };
+      for (int64_t p = gb; p < ge; p += 16) {
+        const int n = ge - p < 16 ? static_cast<int>(ge - p) : 16;
         int my_col = 0, my_row = -1;
         float my_w = 0.0f;
         if (q < n) {
@@ -390,10 +420,7 @@ __global__ void __launch_bounds__(kGemmThreads) k_rgcn_fused(
           for (int u = 0; u < 8; ++u) {
             if (rj[u] < 0) break;  // past the batch (group-uniform)
             if (rj[u] != cur) {
-              if (cur >= 0) {
-                float* d = slot + (8 * g + cur) * kSlotStride + 4 * q;
-                d[0] = a4.x; d[1] = a4.y; d[2] = a4.z; d[3] = a4.w;
-              }
+              if (cur >= 0) flush();
               a4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
               cur = rj[u];
             }
@@ -404,16 +431,21 @@ __global__ void __launch_bounds__(kGemmThreads) k_rgcn_fused(
           }
         }
       }
-      if (cur >= 0) {
-        float* d = slot + (8 * g + cur) * kSlotStride + 4 * q;
-        d[0] = a4.x; d[1] = a4.y; d[2] = a4.z; d[3] = a4.w;
+      if (cur >= 0) flush();
+      wave_lds_sync();
+      // carries into their rows, in group order (deterministic)
+#pragma unroll
+      for (int gg = 1; gg < 4; ++gg) {
+        const int cr = __shfl(crow, gg * 16);
+        if (cr >= 0) slot[cr * kSlotStride + lane] += carry[gg * kFusedW + lane];
       }
       wave_lds_sync();
       if constexpr (BWD) {
         // G_t rows -> gy[v][t * 64 + c] (the weight gradient's operand)
+        const int64_t vg = v0 + 8 * g;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          if (i >= cnt) break;
+          if (8 * g + i >= tile_rows) break;
           const float* s = slot + (8 * g + i) * kSlotStride + 4 * q;
           float* d = gy + (vg + i) * (static_cast<int64_t>(R) * kFusedW) + t * kFusedW + 4 * q;
           __builtin_nontemporal_store(s[0], d);
@@ -440,7 +472,13 @@ __global__ void __launch_bounds__(kGemmThreads) k_rgcn_fused(
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) {
         const int n = nb * 32 + r;
-        if (n < out_w) __builtin_nontemporal_store(acc[nb][reg], out + m * out_w + n);
+        if (n >= out_w) continue;
+        // forward epilogue (RelGraphConv, relgraphconv.py:186-190): + h_bias, then
+        // + the self-loop message, in the reference's order
+        float v = acc[nb][reg];
+        if (bias) v += bias[n];
+        if (addend) v += addend[m * out_w + n];
+        __builtin_nontemporal_store(v, out + m * out_w + n);
       }
     }
   }
@@ -574,15 +612,21 @@ bool rgcn_fused_ok(int64_t gathered_w, int64_t out_w, int64_t R) {
 void launch_rgcn_fused(bool bwd, const int32_t* ptr, const int32_t* cols, const int32_t* rows,
                        const int32_t* eids, const float* w, const float* T, const float* W,
                        int64_t ws_t, int64_t ws_k, int64_t ws_n, float* out, float* gy,
-                       int64_t num_rows, int64_t R, int64_t out_w, hipStream_t s) {
+                       int64_t num_rows, int64_t R, int64_t out_w, hipStream_t s,
+                       const float* bias, const float* addend) {
   if (num_rows <= 0) return;
   const int64_t tiles = (num_rows + 31) / 32;
   const int64_t want = (tiles + 7) / 8;
   const dim3 grid(static_cast<unsigned>(want < 256 ? want : 256)), block(kGemmThreads);
   const int Ri = static_cast<int>(R), ow = static_cast<int>(out_w);
+  // the tile queue's counter: stream-ordered, zeroed before and released after
+  unsigned* ctr = nullptr;
+  if (hipMallocAsync(reinterpret_cast<void**>(&ctr), sizeof(unsigned), s) != hipSuccess ||
+      hipMemsetAsync(ctr, 0, sizeof(unsigned), s) != hipSuccess)
+    throw std::runtime_error("rgcn fused: tile counter allocation failed");
 #define DGLMI_RGCN_FUSED(B_, NB_)                                                               \
   hipLaunchKernelGGL((k_rgcn_fused<B_, NB_>), grid, block, 0, s, ptr, cols, rows, eids, w, T, W, \
-                     ws_t, ws_k, ws_n, out, gy, num_rows, Ri, ow)
+                     ws_t, ws_k, ws_n, out, gy, num_rows, Ri, ow, bias, addend, ctr)
   if (bwd) {
     if (out_w <= 32) DGLMI_RGCN_FUSED(true, 1);
     else if (out_w <= 64) DGLMI_RGCN_FUSED(true, 2);
@@ -593,6 +637,7 @@ void launch_rgcn_fused(bool bwd, const int32_t* ptr, const int32_t* cols, const 
     else DGLMI_RGCN_FUSED(false, 4);
   }
 #undef DGLMI_RGCN_FUSED
+  (void)hipFreeAsync(ctr, s);
 }
 
 void launch_gemm(const float* A, int64_t a_rs, int64_t a_cs, const float* B, int64_t b_rs,

@@ -383,7 +383,8 @@ bool rgcn_fused_ok(int64_t gathered_w, int64_t out_w, int64_t R);
 void launch_rgcn_fused(bool bwd, const int32_t* ptr, const int32_t* cols, const int32_t* rows,
                        const int32_t* eids, const float* w, const float* T, const float* W,
                        int64_t ws_t, int64_t ws_k, int64_t ws_n, float* out, float* gy,
-                       int64_t num_rows, int64_t R, int64_t out_w, hipStream_t s);
+                       int64_t num_rows, int64_t R, int64_t out_w, hipStream_t s,
+                       const float* bias = nullptr, const float* addend = nullptr);
 // out[p] = v[idx[p]]; out[p] = p
 void launch_gather_f32(const float* v, const int32_t* idx, int64_t n, float* out, hipStream_t s);
 void launch_iota_i32(int32_t* out, int64_t n, hipStream_t s);

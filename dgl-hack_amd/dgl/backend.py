@@ -468,6 +468,80 @@ def _typed_aggregate(graph, num_rels, y, norm, etypes, node_major=False, bias=No
     return out
 
 
+class _FusedRgcnLayer1(th.autograd.Function):
+    """RelGraphConv's layer on the hack's layer-1 C entries with the prepared state
+    (``DGLMIRgcnLayer1Ex`` / ``DGLMIRgcnLayer1Backward``, fused aggregate-then-transform
+    kernels): no (N, R * F_out) table Y = X [W_0 | ... | W_{R-1}] is
+    written or gathered, bias and self-loop ride in the output pass.  Gradients for
+    x, the relation weights, bias and the self-loop term; the norm is constant."""
+
+    @staticmethod
+    def forward(ctx, gidx, et32, norm, x, w, bias, addend):
+        ret = x.new_empty((gidx.num_dst, w.shape[2]))
+        K.rgcn_layer1_ex(gidx, et32, x, w, norm, ret, bias, addend)
+        ctx.gidx, ctx.et32, ctx.norm = gidx, et32, norm
+        ctx.has_bias, ctx.has_addend = bias is not None, addend is not None
+        ctx.save_for_backward(x, w)
+        return ret
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        x, w = ctx.saved_tensors
+        g = grad_out.contiguous()
+        gx = gw = gb = ga = None
+        if ctx.needs_input_grad[3] or ctx.needs_input_grad[4]:
+            gx, gw = th.empty_like(x), th.empty_like(w)
+            K.rgcn_layer1_backward(ctx.gidx, ctx.et32, x, w, ctx.norm, g, gx, gw)
+        if ctx.has_bias and ctx.needs_input_grad[5]:
+            gb = g.sum(0)
+        if ctx.has_addend and ctx.needs_input_grad[6]:
+            ga = g
+        return None, None, None, gx, gw, gb, ga
+
+
+def rgcn_fused_route(graph, x, weight_shape, norm, etypes):
+    """(gidx, etypes int32, norm flat) when a RelGraphConv layer can run on the
+    fused layer-1 C entries both ways (64-float rows gathered forward and backward,
+    DGLMIRgcnLayer1 / Backward with a prepared state), else None.  The state
+    (``kernel.rgcn_prepare``, ~6 values per edge) is built once per graph, device,
+    etypes and norm, and rebuilt when either tensor is written in place."""
+    R, fi, fo = weight_shape
+    if not (x.is_cuda and x.dtype == th.float32 and x.dim() == 2 and x.shape[1] == fi
+            and K.rgcn_fused_ok(fi, fo, R) and K.rgcn_fused_ok(fo, fi, R)):
+        return None
+    if norm is None or norm.requires_grad or not norm.is_cuda or norm.dtype != th.float32:
+        return None
+    if etypes is None or not isinstance(etypes, th.Tensor) or etypes.device != x.device:
+        return None
+    gi = graph._graph
+    if x.shape[0] != graph.number_of_nodes() or gi.device_bits() != 32:
+        return None
+    if norm.numel() != graph.number_of_edges() or etypes.numel() != graph.number_of_edges():
+        return None
+    key = (str(x.device), int(R), etypes.data_ptr(), etypes._version, norm.data_ptr(),
+           norm._version, int(etypes.numel()))
+    hit = gi.__dict__.get("_rgcn_fused")
+    if hit is None or hit[0] != key:
+        gidx = gi.get_immutable_gidx(x.device)
+        et = etypes.reshape(-1)
+        if et.numel() and (int(et.min()) < 0 or int(et.max()) >= R):
+            raise DGLError("edge type out of range [0, %d)" % R)
+        et32 = et.to(th.int32).contiguous()
+        nf = norm.reshape(-1).contiguous()
+        gi.__dict__["_rgcn_fused"] = None  # release the old state first (~2 GB on C5)
+        K.rgcn_prepare(gidx, et32, nf, R, layers=6)
+        # the cache holds the caller's tensors, so their addresses stay theirs
+        hit = (key, gidx, et32, nf, etypes, norm)
+        gi.__dict__["_rgcn_fused"] = hit
+    return hit[1], hit[2], hit[3]
+
+
+def rgcn_fused_layer1(route, x, weight, bias=None, addend=None):
+    gidx, et32, nf = route
+    return _FusedRgcnLayer1.apply(gidx, et32, nf, x.contiguous(), weight.contiguous(), bias,
+                                  None if addend is None else addend.contiguous())
+
+
 def rgcn_layer0(graph, weight, norm, etypes=None):
     """Layer with one-hot (node id) input: ret[v] = sum_e W[type_e, u] * norm_e.
 

@@ -497,6 +497,29 @@ def rgcn_layer1(graph, etypes, hidden, weight, norm, ret):
         _arr(weight, "weight"), _arr(norm, "norm"), _arr(ret, "ret"), _stream(ret)))
 
 
+def rgcn_layer1_ex(graph, etypes, hidden, weight, norm, ret, bias=None, addend=None):
+    """DGLMIRgcnLayer1Ex: rgcn_layer1 with RelGraphConv's bias (F_out) and self-loop
+    message (ret's shape) added in the output pass (relgraphconv.py:186-190 order)."""
+    _check_ctx(graph, [("hidden", hidden), ("weight", weight), ("norm", norm), ("ret", ret)])
+    epi = _epilogue((None, None, bias, addend), ret)
+    if epi is not None and epi.addend and epi.addend % 16:
+        raise DGLError("epilogue addend must be 16-byte aligned")
+    check_call(_ffi.lib().DGLMIRgcnLayer1Ex(
+        ctypes.byref(_rgcn_cgraph(graph, etypes, norm, weight.shape[0], 1)),
+        _etypes(graph, etypes), _arr(hidden, "hidden"),
+        _arr(weight, "weight"), _arr(norm, "norm"),
+        None if epi is None else ctypes.byref(epi), _arr(ret, "ret"), _stream(ret)))
+
+
+def rgcn_fused_ok(gathered_w, out_w, num_rels):
+    """The shapes the fused layer-1 kernels take (hack_kernels.hip rgcn_fused_ok):
+    64-float gathered rows, 1..128 outputs, all relations' weights in 64 KB of LDS."""
+    if gathered_w != 64 or not 1 <= out_w <= 128 or num_rels < 1:
+        return False
+    nb = 1 if out_w <= 32 else (2 if out_w <= 64 else 4)
+    return num_rels * 64 * nb * 32 <= 16384
+
+
 def rgcn_layer1_backward(graph, etypes, hidden, weight, norm, grad_out, grad_hidden, grad_weight):
     """_CAPI_DGLRgcnLayer1Backward: both gradients (the hack's wrapper drops the
     weight gradient, tensor.py:493; it is returned here)."""

@@ -6,7 +6,10 @@ function is a per-edge batched matmul UDF (``bmm_maybe_select``).  Here the
 relation transforms are dense GEMMs over the node features (one per relation,
 on MFMA) and all relations are aggregated by one typed gather kernel
 (``dgl.backend.rgcn_layer1``): per edge the bytes of one output row instead of
-an F_in x F_out product.
+an F_in x F_out product.  Layers whose gathered rows are 64 floats both ways
+(64 -> 64, up to 4 relations) with a constant norm instead run the hack's fused
+layer-1 C entries (aggregate per relation, then transform, in one kernel; DESIGN.md
+4.4).
 """
 import torch as th
 from torch import nn
@@ -53,6 +56,10 @@ class RelGraphConv(nn.Module):
             self.loop_weight = nn.Parameter(th.Tensor(in_feat, out_feat))
             nn.init.xavier_uniform_(self.loop_weight, gain=nn.init.calculate_gain("relu"))
         self.dropout = nn.Dropout(dropout)
+        # extension: layers of 64-float rows (both ways) with a constant norm run on the
+        # fused layer-1 kernels (dgl.backend.rgcn_fused_route); False keeps the
+        # GEMM + typed-gather path below
+        self.use_fused = True
 
     def _relation_weights(self):
         if self.num_bases < self.num_rels:
@@ -80,6 +87,18 @@ class RelGraphConv(nn.Module):
         return th.einsum("nbi,rbio->nrbo", xb, w), True
 
     def forward(self, g, x, etypes, norm=None):
+        if self.use_fused and self.regularizer == "basis":
+            route = B.rgcn_fused_route(g, x, (self.num_rels, self.in_feat, self.out_feat), norm,
+                                       etypes)
+            if route is not None:
+                # aggregate-then-transform on the fused layer-1 C entries, bias and
+                # self-loop message in the output pass (B.rgcn_fused_layer1)
+                loop = B.project(x, self.loop_weight) if self.self_loop else None
+                node_repr = B.rgcn_fused_layer1(route, x, self._relation_weights(),
+                                                self.h_bias if self.bias else None, loop)
+                if self.activation:
+                    node_repr = self.activation(node_repr)
+                return self.dropout(node_repr)
         y, node_major = self._transform(x)
         y = y.contiguous()
         n = g.number_of_nodes()

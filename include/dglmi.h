@@ -393,6 +393,15 @@ int DGLMIRgcnLayer0Backward(const DGLMIGraph* graph, const int32_t* etypes,
 int DGLMIRgcnLayer1(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* hidden,
                     const DGLMIArray* weight, const DGLMIArray* norm, DGLMIArray* ret,
                     void* stream);
+/* Extension (no reference counterpart): DGLMIRgcnLayer1 with RelGraphConv's bias and
+ * self-loop message in the output pass, ret[v] = agg[v] + bias + addend[v] in the order
+ * of relgraphconv.py:186-190 (python/dgl/nn/pytorch/conv/relgraphconv.py), so the
+ * module needs no extra passes over the output.  epilogue->bias has F_out floats,
+ * epilogue->addend the shape of ret (not aliasing it); row_mul / row_div must be NULL.
+ * A NULL epilogue is DGLMIRgcnLayer1. */
+int DGLMIRgcnLayer1Ex(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* hidden,
+                      const DGLMIArray* weight, const DGLMIArray* norm,
+                      const DGLMIEpilogue* epilogue, DGLMIArray* ret, void* stream);
 /* _CAPI_DGLRgcnLayer1Backward: grad_hidden[u] = sum_{e out of u} norm[e] * grad_out[v]
  * . weight[t]^T; grad_weight[t] = sum_{e of relation t} norm[e] hidden[u]^T grad_out[v]. */
 int DGLMIRgcnLayer1Backward(const DGLMIGraph* graph, const int32_t* etypes,

@@ -194,6 +194,11 @@ def c5(dev, steps, warmup):
             conv(g, x, et, norm)
     ms_fb = timeit(fwd_bwd, steps, warmup)
     ms_f = timeit(fwd, steps, warmup)
+    fused = g._graph.__dict__.get("_rgcn_fused") is not None
+    conv.use_fused = False  # the GEMM + typed-gather path, for comparison
+    ms_fb_u = timeit(fwd_bwd, steps, warmup)
+    ms_f_u = timeit(fwd, steps, warmup)
+    conv.use_fused = True
     from dgl import backend as B
     y = th.randn(R * n, f, device=dev)
     ms_g = timeit(lambda: B._typed_aggregate(g, R, y, norm, et), steps, warmup)
@@ -201,7 +206,9 @@ def c5(dev, steps, warmup):
     # edge, indptr + output row per node
     alg = 4 * (n + 1) + m * (4 + 4 + 4 * f + 4) + 4 * f * n
     return {"config": "C5 R-GCN RelGraphConv 4 rel basis 64->64", "nodes": n, "edges": m,
-            "layer_fwd_ms": ms_f, "layer_fwd_bwd_ms": ms_fb, "typed_gather_ms": ms_g,
+            "layer_fwd_ms": ms_f, "layer_fwd_bwd_ms": ms_fb, "fused_route": fused,
+            "gemm_gather_fwd_ms": ms_f_u, "gemm_gather_fwd_bwd_ms": ms_fb_u,
+            "typed_gather_ms": ms_g,
             "typed_gather_alg_GBps": alg / ms_g / 1e6, "typed_gather_Gedges_s": m / ms_g / 1e6}
 
 

@@ -36,8 +36,14 @@ def main():
     n, m, R, F = 5_000_000, 80_000_000, 4, 64
     g0 = th.Generator(device=dev)
     g0.manual_seed(8)
-    src = th.randint(0, n, (m,), device=dev, generator=g0, dtype=th.int32)
-    dst = th.randint(0, n, (m,), device=dev, generator=g0, dtype=th.int32)
+    if "--chung-lu" in sys.argv:  # the C5 config's power-law graph (bench_configs.c5)
+        w = th.arange(1, n + 1, device=dev, dtype=th.float64).pow(-0.5)
+        w = w[th.randperm(n, generator=g0, device=dev)].float()
+        src = th.multinomial(w, m, replacement=True, generator=g0).to(th.int32)
+        dst = th.multinomial(w, m, replacement=True, generator=g0).to(th.int32)
+    else:
+        src = th.randint(0, n, (m,), device=dev, generator=g0, dtype=th.int32)
+        dst = th.randint(0, n, (m,), device=dev, generator=g0, dtype=th.int32)
     et = th.randint(0, R, (m,), device=dev, generator=g0)
     g = dgl.DGLGraph.from_device_coo(src, dst, n)
     gidx = g._graph.get_immutable_gidx(dev)
@@ -49,7 +55,8 @@ def main():
     ret = th.empty(n, F, device=dev)
     go = th.randn(n, F, device=dev)
     gh, gw = th.empty(n, F, device=dev), th.empty_like(W)
-    res = {"config": "C5 R-GCN layer 64->64, 4 relations, 5M nodes / 80M edges"}
+    res = {"config": "C5 R-GCN layer 64->64, 4 relations, 5M nodes / 80M edges",
+           "graph": "chung-lu alpha 0.5" if "--chung-lu" in sys.argv else "uniform random"}
     if "--capi-only" in sys.argv:  # for rocprofv3 kernel statistics
         if "--prepared" in sys.argv:
             K.rgcn_prepare(gidx, et32, norm, R, layers=2)

@@ -13,16 +13,22 @@ def free_port():
     return port
 
 
-def _entry(rank, world, port, fn, args):
+def _entry(rank, world, port, fn, args, backend="gloo"):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":  # RCCL: one rank per GPU (cuda:rank)
+        import torch
+        torch.cuda.set_device(rank)
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", rank))
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
     try:
         fn(rank, world, *args)
     finally:
         dist.destroy_process_group()
 
 
-def run_world(fn, world=2, args=()):
-    mp.spawn(_entry, args=(world, free_port(), fn, args), nprocs=world, join=True)
+def run_world(fn, world=2, args=(), backend="gloo"):
+    mp.spawn(_entry, args=(world, free_port(), fn, args, backend), nprocs=world, join=True)

@@ -181,6 +181,7 @@ def test_c5_rgcn_python_path_vs_c_entry():
     g = dgl.DGLGraph.from_device_coo(src, dst, n)
     norm = (1.0 / th.bincount(dst.long(), minlength=n).clamp(min=1).float())[dst.long()].view(-1, 1)
     conv = RelGraphConv(64, 64, R, "basis", num_bases=R, bias=False).to(DEV)
+    conv.use_fused = False  # the GEMM + typed-gather path, against the C entries
     h = th.randn(n, 64, device=DEV, requires_grad=True)
     out = conv(g, h, et, norm)
     go = th.randn_like(out)

@@ -201,3 +201,32 @@ def test_dist_gat_and_rgcn_match_single_gpu(planner):
     q = ctx.Queue()
     run_world(_gat_rgcn_worker, 2, (src, dst, et, n, q, planner))
     assert q.get(timeout=5) == "ok"
+
+
+def _rccl_world1_worker(rank, world, src, dst, et, n, q):
+    """Every collective of the distributed path on RCCL (backend "nccl", device
+    tensors, async all-to-all-v on the collective stream) at world size 1: the GCN
+    with all three planners, the overlapped aggregation and DistGAT / DistRelGraphConv."""
+    import torch.distributed as dist
+    assert dist.get_backend() == "nccl"
+    for planner in ("host_ldg", "device_contiguous", "device_lp_hybrid"):
+        _worker(rank, world, src, dst, n, q, planner)
+    _overlap_worker(rank, world, src, dst, n, q)
+    for planner in ("host_ldg", "device_contiguous", "device_lp"):
+        _gat_rgcn_worker(rank, world, src, dst, et, n, q, planner)
+
+
+def test_rccl_world1_collectives():
+    """The N>1 runs use RCCL, which refuses two ranks on one GPU; a world of one
+    rank still drives every RCCL call of the path (halo all-to-all-v with zero
+    splits, gradient all-reduce, all_gather_object) on the device."""
+    import torch.multiprocessing as mp
+    from dist_util import run_world
+    from graphs import powerlaw
+    src, dst, n = powerlaw(3000, 40000, seed=6)
+    et = np.random.default_rng(6).integers(0, 3, len(src))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    run_world(_rccl_world1_worker, 1, (src, dst, et, n, q), backend="nccl")
+    got = [q.get(timeout=5) for _ in range(7)]
+    assert got == ["ok"] * 7, got

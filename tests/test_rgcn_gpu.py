@@ -136,3 +136,82 @@ def test_constant_norm_position_cache_follows_the_tensor():
     assert th.equal(d, b)
     (gn,) = th.autograd.grad(d.sum(), (ng,))
     assert gn.shape == ng.shape
+
+
+@pytest.mark.parametrize("R,bases,loop,act", [(4, None, True, False), (4, 2, False, True),
+                                              (2, None, True, True), (3, 2, False, False)])
+def test_relgraphconv_fused_route(R, bases, loop, act):
+    """64 -> 64 layers with a constant norm run on the fused layer-1 C entries
+    (dgl.backend.rgcn_fused_route, bias and self-loop in the output pass): equal to
+    the fp64 per-edge bmm restatement and to the GEMM + typed-gather path, forward
+    and every parameter / input gradient."""
+    g, src, dst, et, n = typed_graph(seed=5, R=R)
+    th.manual_seed(1)
+    conv = RelGraphConv(64, 64, R, "basis", num_bases=bases, self_loop=loop,
+                        activation=th.tanh if act else None).to(DEV)
+    x = th.randn(n, 64, device=DEV, requires_grad=True)
+    etypes = th.from_numpy(et).to(DEV)
+    norm = th.rand(len(src), 1, device=DEV)
+    out = conv(g, x, etypes, norm)
+    assert g._graph.__dict__.get("_rgcn_fused") is not None  # the fused route ran
+    ref = ref_relgraphconv(conv, src, dst, x.detach(), et, norm, n)
+    if act:
+        ref = th.tanh(ref)
+    assert th.allclose(out.double(), ref, rtol=1e-4, atol=1e-4)
+    go = th.randn_like(out)
+    params = [x] + list(conv.parameters())
+    grads = th.autograd.grad(out, params, go)
+    conv.use_fused = False
+    out2 = conv(g, x, etypes, norm)
+    grads2 = th.autograd.grad(out2, params, go)
+    assert th.allclose(out, out2, rtol=1e-4, atol=1e-4)  # fp32, other summation order
+    for a, b in zip(grads, grads2):  # long fp32 sums in other orders: scaled bound
+        assert (a - b).abs().max().item() <= 1e-3 + 1e-4 * b.abs().max().item()
+    # the fp64 gradients
+    xd = x.detach().double().requires_grad_()
+    conv64 = RelGraphConv(64, 64, R, "basis", num_bases=bases, self_loop=loop,
+                          activation=th.tanh if act else None).to(DEV).double()
+    conv64.load_state_dict({k: v.double() for k, v in conv.state_dict().items()})
+    ref = ref_relgraphconv(conv64, src, dst, xd, et, norm, n)
+    if act:
+        ref = th.tanh(ref)
+    rgrads = th.autograd.grad(ref, [xd] + list(conv64.parameters()), go.double())
+    for a, b in zip(grads, rgrads):
+        mass = b.abs().max().item()
+        assert (a.double() - b).abs().max().item() <= 1e-3 + 1e-4 * mass
+
+
+def test_relgraphconv_fused_state_follows_the_tensors():
+    """The fused route's prepared state is keyed on etypes / norm and their version
+    counters: an in-place update, a new norm per call and new etypes rebuild it;
+    a norm that needs a gradient and 32-wide layers keep the typed-gather path."""
+    g, src, dst, et, n = typed_graph(seed=6)
+    R = 4
+    th.manual_seed(2)
+    conv = RelGraphConv(64, 64, R, "basis", bias=False).to(DEV)
+    x = th.randn(n, 64, device=DEV)
+    etypes = th.from_numpy(et).to(DEV)
+    norm = th.rand(len(src), 1, device=DEV)
+    with th.no_grad():
+        a = conv(g, x, etypes, norm)
+        norm.mul_(2.0)
+        b = conv(g, x, etypes, norm)
+        assert th.allclose(b, 2 * a, rtol=1e-5, atol=1e-5)
+        outs = [conv(g, x, etypes, th.full((len(src), 1), float(k), device=DEV)) for k in (1, 2, 3)]
+        assert th.allclose(outs[1], 2 * outs[0], rtol=1e-5, atol=1e-5)
+        assert th.allclose(outs[2], 3 * outs[0], rtol=1e-4, atol=1e-4)
+        et2 = (etypes + 1) % R
+        c = conv(g, x, et2, norm)
+        conv.use_fused = False
+        c2 = conv(g, x, et2, norm)
+        assert th.allclose(c, c2, rtol=1e-4, atol=1e-4)
+        conv.use_fused = True
+    ng = norm.clone().requires_grad_()
+    g._graph.__dict__["_rgcn_fused"] = None
+    d = conv(g, x, etypes, ng)
+    assert g._graph.__dict__.get("_rgcn_fused") is None
+    (gn,) = th.autograd.grad(d.sum(), (ng,))
+    assert gn.shape == ng.shape
+    narrow = RelGraphConv(32, 64, R, "basis").to(DEV)
+    narrow(g, th.randn(n, 32, device=DEV), etypes, norm)
+    assert g._graph.__dict__.get("_rgcn_fused") is None
