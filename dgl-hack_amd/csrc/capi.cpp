@@ -1573,9 +1573,17 @@ int DGLMIRgcnLayer0Backward(const DGLMIGraph* graph, const int32_t* etypes,
 }
 
 namespace {
+// RelGraphConv's self-loop weight (F_in x F_out) on a square graph
+void check_loop_weight(const DGLMIArray* loop, int64_t K, int64_t X, const DGLMICsr& in) {
+  check_array(loop, "loop_weight");
+  DGLMI_CHECK(loop->ndim == 2 && loop->shape[0] == K && loop->shape[1] == X,
+              "loop_weight must be (F_in, F_out)");
+  DGLMI_CHECK(in.num_rows == in.num_cols, "a self-loop weight needs num_src == num_dst");
+}
+
 int rgcn_layer1_impl(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* hidden,
-                     const DGLMIArray* weight, const DGLMIArray* norm, const DGLMIEpilogue* epi,
-                     DGLMIArray* ret, void* stream) {
+                     const DGLMIArray* weight, const DGLMIArray* norm, const DGLMIArray* loop,
+                     const DGLMIEpilogue* epi, DGLMIArray* ret, void* stream) {
   API_BEGIN();
   check_array(hidden, "hidden");
   check_array(weight, "weight");
@@ -1595,18 +1603,19 @@ int rgcn_layer1_impl(const DGLMIGraph* graph, const int32_t* etypes, const DGLMI
               "the R-GCN epilogue takes bias and addend only");
   DGLMI_CHECK(!addend || (addend != ret->data && aligned16(addend)),
               "addend must not alias ret and must be 16-byte aligned");
+  if (loop) check_loop_weight(loop, K, X, in);
   DeviceGuard guard(graph->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t N = in.num_cols, M = R * X;
   DGLMIGraph z = no_workspace(), pg = plain_graph(graph);
   if (const DGLMIRgcnState* fs = rgcn_state(graph, etypes, R, N, 2)) {
-    if (rgcn_fused_ok(K, X, R) && aligned16(hidden->data) && in.nnz > 0) {
+    if (rgcn_fused_ok(K, X, R + (loop != nullptr)) && aligned16(hidden->data) && in.nnz > 0) {
       const int32_t* eids = nullptr;
       const float* w = nullptr;
       rgcn_fused_walk(fs, fs->in_rel, fs->in_rel_norm, norm->data, &eids, &w);
       launch_rgcn_fused(false, fs->in_rel.indptr, fs->in_rel.indices, fs->in_rel.rows, eids, w,
                         hidden->data, weight->data, K * X, X, 1, ret->data, nullptr, in.num_rows, R,
-                        X, s, bias, addend);
+                        X, s, bias, addend, loop ? loop->data : nullptr);
       check_hip(hipGetLastError(), "rgcn fused layer1 launch");
       return 0;
     }
@@ -1626,6 +1635,14 @@ int rgcn_layer1_impl(const DGLMIGraph* graph, const int32_t* etypes, const DGLMI
     walk.indices = static_cast<int32_t*>(cols.ptr);
     walk.num_cols = N * R;
   }
+  // the self-loop message hidden . loop (+ the caller's addend) enters as the addend
+  Scratch lt(&z, loop ? N * X * 4 : 0, s);
+  if (loop) {
+    launch_gemm(hidden->data, K, 1, loop->data, X, 1, static_cast<float*>(lt.ptr), N, X, K, 1,
+                nullptr, s);
+    if (addend) launch_add_into(static_cast<float*>(lt.ptr), addend, N * X, s);
+    addend = static_cast<const float*>(lt.ptr);
+  }
   const DGLMIEpilogue e2{nullptr, nullptr, bias, addend};
   run_fast(&pg, walk, FAST_COL_MUL_EDGE_BCAST, RED_SUM, static_cast<float*>(y.ptr), nullptr, w,
            nullptr, ret->data, X, X, s, (bias || addend) ? &e2 : nullptr);
@@ -1636,19 +1653,22 @@ int rgcn_layer1_impl(const DGLMIGraph* graph, const int32_t* etypes, const DGLMI
 int DGLMIRgcnLayer1(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* hidden,
                     const DGLMIArray* weight, const DGLMIArray* norm, DGLMIArray* ret,
                     void* stream) {
-  return rgcn_layer1_impl(graph, etypes, hidden, weight, norm, nullptr, ret, stream);
+  return rgcn_layer1_impl(graph, etypes, hidden, weight, norm, nullptr, nullptr, ret, stream);
 }
 
 int DGLMIRgcnLayer1Ex(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* hidden,
                       const DGLMIArray* weight, const DGLMIArray* norm,
-                      const DGLMIEpilogue* epilogue, DGLMIArray* ret, void* stream) {
-  return rgcn_layer1_impl(graph, etypes, hidden, weight, norm, epilogue, ret, stream);
+                      const DGLMIArray* loop_weight, const DGLMIEpilogue* epilogue,
+                      DGLMIArray* ret, void* stream) {
+  return rgcn_layer1_impl(graph, etypes, hidden, weight, norm, loop_weight, epilogue, ret, stream);
 }
 
-int DGLMIRgcnLayer1Backward(const DGLMIGraph* graph, const int32_t* etypes,
-                            const DGLMIArray* hidden, const DGLMIArray* weight,
-                            const DGLMIArray* norm, const DGLMIArray* grad_out,
-                            DGLMIArray* grad_hidden, DGLMIArray* grad_weight, void* stream) {
+namespace {
+int rgcn_layer1_backward_impl(const DGLMIGraph* graph, const int32_t* etypes,
+                              const DGLMIArray* hidden, const DGLMIArray* weight,
+                              const DGLMIArray* norm, const DGLMIArray* loop,
+                              const DGLMIArray* grad_out, DGLMIArray* grad_hidden,
+                              DGLMIArray* grad_weight, DGLMIArray* grad_loop, void* stream) {
   API_BEGIN();
   check_array(hidden, "hidden");
   check_array(weight, "weight");
@@ -1667,15 +1687,32 @@ int DGLMIRgcnLayer1Backward(const DGLMIGraph* graph, const int32_t* etypes,
               "grad_out must be (num_dst, F_out)");
   edge_values(norm, out.nnz, "norm");
   check_fast_width(X);
+  if (loop) check_loop_weight(loop, K, X, graph->in_csr);
+  if (grad_loop) {
+    DGLMI_CHECK(loop != nullptr, "grad_loop_weight needs loop_weight");
+    check_loop_weight(grad_loop, K, X, graph->in_csr);
+  }
   DeviceGuard guard(graph->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   DGLMIGraph z = no_workspace(), pg = plain_graph(graph);
-  const int64_t splits = gemm_splits(K, M, N);
-  Scratch wcat(&z, K * M * 4, s), gy(&z, N * M * 4, s), gw(&z, K * M * 4, s),
-      parts(&z, splits > 1 ? splits * K * M * 4 : 0, s);
-  launch_permute_rkx(weight->data, R, K, X, true, static_cast<float*>(wcat.ptr), s);
   const DGLMIRgcnState* fs = out.nnz > 0 ? rgcn_state(graph, etypes, R, N, 2) : nullptr;
-  if (fs && rgcn_fused_ok(X, K, R) && aligned16(grad_out->data) && fs->out_typed[0].indptr) {
+  const bool fused = fs && rgcn_fused_ok(X, K, R + (loop != nullptr)) &&
+                     aligned16(grad_out->data) && fs->out_typed[0].indptr;
+  // the fused walk also stores grad_out as gy's last block when there is a self-loop:
+  // one GEMM hidden^T . gy gives both weight gradients
+  const int64_t MG = fused && loop ? M + X : M;
+  const int64_t splits = gemm_splits(K, MG, N);
+  const int64_t lsplits = grad_loop && !fused ? gemm_splits(K, X, N) : 1;
+  Scratch gy(&z, N * MG * 4, s), gw(&z, K * MG * 4, s),
+      parts(&z, std::max(splits > 1 ? splits * K * MG * 4 : 0, lsplits > 1 ? lsplits * K * X * 4 : 0),
+            s);
+  // grad_loop = hidden^T (K x N) . grad_out (N x X), split over N
+  auto loop_weight_grad = [&]() {
+    if (grad_loop)
+      launch_gemm(hidden->data, 1, K, grad_out->data, X, 1, grad_loop->data, K, X, N, lsplits,
+                  static_cast<float*>(parts.ptr), s);
+  };
+  if (fused) {
     // fused: gy rows and grad_hidden = sum_t G_t . W_t^T in one walk of the
     // relation-major out-CSR; the weight gradient from gy below
     const int32_t* eids = nullptr;
@@ -1683,13 +1720,28 @@ int DGLMIRgcnLayer1Backward(const DGLMIGraph* graph, const int32_t* etypes,
     rgcn_fused_walk(fs, fs->out_typed[0], fs->out_norm[0], norm->data, &eids, &w);
     launch_rgcn_fused(true, fs->out_typed[0].indptr, fs->out_typed[0].indices, fs->out_typed[0].rows,
                       eids, w, grad_out->data, weight->data, K * X, 1, X, grad_hidden->data,
-                      static_cast<float*>(gy.ptr), N, R, K, s);
-    launch_gemm(hidden->data, 1, K, static_cast<float*>(gy.ptr), M, 1, static_cast<float*>(gw.ptr), K,
-                M, N, splits, static_cast<float*>(parts.ptr), s);
-    launch_permute_rkx(static_cast<float*>(gw.ptr), R, K, X, false, grad_weight->data, s);
+                      static_cast<float*>(gy.ptr), N, R, K, s, nullptr, nullptr,
+                      loop ? loop->data : nullptr);
+    launch_gemm(hidden->data, 1, K, static_cast<float*>(gy.ptr), MG, 1, static_cast<float*>(gw.ptr),
+                K, MG, N, splits, static_cast<float*>(parts.ptr), s);
+    if (!loop) {
+      launch_permute_rkx(static_cast<float*>(gw.ptr), R, K, X, false, grad_weight->data, s);
+    } else {
+      // gw (K x (R + 1) X) -> [R + 1][K][X]: the relation blocks, then the self-loop one
+      Scratch gp(&z, (R + 1) * K * X * 4, s);
+      float* p = static_cast<float*>(gp.ptr);
+      launch_permute_rkx(static_cast<float*>(gw.ptr), R + 1, K, X, false, p, s);
+      check_hip(hipMemcpyAsync(grad_weight->data, p, R * K * X * 4, hipMemcpyDeviceToDevice, s),
+                "copy grad_weight");
+      if (grad_loop)
+        check_hip(hipMemcpyAsync(grad_loop->data, p + R * K * X, K * X * 4,
+                                 hipMemcpyDeviceToDevice, s), "copy grad_loop_weight");
+    }
     check_hip(hipGetLastError(), "rgcn fused layer1 backward launch");
     return 0;
   }
+  Scratch wcat(&z, K * M * 4, s);
+  launch_permute_rkx(weight->data, R, K, X, true, static_cast<float*>(wcat.ptr), s);
   // gy[u * R + t] = sum over out-edges of u with type t of norm_e * grad_out[v]
   if (const DGLMIRgcnState* st = out.nnz > 0 ? rgcn_state(graph, etypes, R, N, 1) : nullptr) {
     const float* w = nullptr;
@@ -1709,8 +1761,34 @@ int DGLMIRgcnLayer1Backward(const DGLMIGraph* graph, const int32_t* etypes,
   launch_gemm(hidden->data, 1, K, static_cast<float*>(gy.ptr), M, 1, static_cast<float*>(gw.ptr), K,
               M, N, splits, static_cast<float*>(parts.ptr), s);
   launch_permute_rkx(static_cast<float*>(gw.ptr), R, K, X, false, grad_weight->data, s);
+  if (loop) {  // grad_hidden += grad_out . loop^T
+    Scratch lt(&z, N * K * 4, s);
+    launch_gemm(grad_out->data, X, 1, loop->data, 1, X, static_cast<float*>(lt.ptr), N, K, X, 1,
+                nullptr, s);
+    launch_add_into(grad_hidden->data, static_cast<float*>(lt.ptr), N * K, s);
+  }
+  loop_weight_grad();
   check_hip(hipGetLastError(), "rgcn layer1 backward launch");
   API_END();
+}
+}  // namespace
+
+int DGLMIRgcnLayer1Backward(const DGLMIGraph* graph, const int32_t* etypes,
+                            const DGLMIArray* hidden, const DGLMIArray* weight,
+                            const DGLMIArray* norm, const DGLMIArray* grad_out,
+                            DGLMIArray* grad_hidden, DGLMIArray* grad_weight, void* stream) {
+  return rgcn_layer1_backward_impl(graph, etypes, hidden, weight, norm, nullptr, grad_out,
+                                   grad_hidden, grad_weight, nullptr, stream);
+}
+
+int DGLMIRgcnLayer1BackwardEx(const DGLMIGraph* graph, const int32_t* etypes,
+                              const DGLMIArray* hidden, const DGLMIArray* weight,
+                              const DGLMIArray* norm, const DGLMIArray* loop_weight,
+                              const DGLMIArray* grad_out, DGLMIArray* grad_hidden,
+                              DGLMIArray* grad_weight, DGLMIArray* grad_loop_weight,
+                              void* stream) {
+  return rgcn_layer1_backward_impl(graph, etypes, hidden, weight, norm, loop_weight, grad_out,
+                                   grad_hidden, grad_weight, grad_loop_weight, stream);
 }
 
 int DGLMIRgcnPrepare(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* norm,

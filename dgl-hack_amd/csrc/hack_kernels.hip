@@ -230,7 +230,8 @@ __global__ void __launch_bounds__(kGemmThreads) k_gemm_tn(const float* __restric
   constexpr int A4 = MB * 8, B4 = NB * 8;                  // float4 per staged row
   constexpr int AL = (kSlice * A4 + kGemmThreads - 1) / kGemmThreads;
   constexpr int BL = (kSlice * B4 + kGemmThreads - 1) / kGemmThreads;
-  static_assert(MB * NB <= 16, "at most two 32 x 32 blocks per wave");
+  constexpr int BPW = (MB * NB + 7) / 8;  // 32 x 32 output blocks per wave
+  static_assert(BPW <= 3, "at most three 32 x 32 blocks per wave");
   __shared__ float As[2][kSlice * SA];
   __shared__ float Bs[2][kSlice * SB];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -273,10 +274,9 @@ __global__ void __launch_bounds__(kGemmThreads) k_gemm_tn(const float* __restric
         *reinterpret_cast<float4*>(&Bs[buf][(idx / B4) * SB + 4 * (idx % B4)]) = vb[j];
     }
   };
-  const int b0 = w, b1 = w + 8;
-  const bool has0 = b0 < MB * NB, has1 = b1 < MB * NB;
-  const int mb0 = b0 / NB, nb0 = b0 % NB, mb1 = b1 / NB, nb1 = b1 % NB;
-  f32x16 acc0 = {}, acc1 = {};
+  f32x16 acc[BPW];
+#pragma unroll
+  for (int i = 0; i < BPW; ++i) acc[i] = f32x16{};
   if (nsl > 0) load(0);
   for (int sl = 0; sl < nsl; ++sl) {
     store(sl & 1);
@@ -286,25 +286,25 @@ __global__ void __launch_bounds__(kGemmThreads) k_gemm_tn(const float* __restric
     const float* bs = Bs[sl & 1];
 #pragma unroll
     for (int kk = 0; kk < kSlice; kk += 2) {
-      if (has0)
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(as[(kk + h) * SA + mb0 * 32 + r],
-                                                    bs[(kk + h) * SB + nb0 * 32 + r], acc0, 0, 0, 0);
-      if (has1)
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(as[(kk + h) * SA + mb1 * 32 + r],
-                                                    bs[(kk + h) * SB + nb1 * 32 + r], acc1, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < BPW; ++i) {
+        const int b = w + 8 * i;  // wave-uniform
+        if (b < MB * NB)
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(as[(kk + h) * SA + (b / NB) * 32 + r],
+                                                        bs[(kk + h) * SB + (b % NB) * 32 + r], acc[i],
+                                                        0, 0, 0);
+      }
     }
   }
   float* P = parts + static_cast<int64_t>(blockIdx.x) * M * N;
 #pragma unroll
-  for (int reg = 0; reg < 16; ++reg) {
-    const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-    if (has0) {
-      const int m = mb0 * 32 + row, n = nb0 * 32 + r;
-      if (m < M && n < N) P[m * N + n] = acc0[reg];
-    }
-    if (has1) {
-      const int m = mb1 * 32 + row, n = nb1 * 32 + r;
-      if (m < M && n < N) P[m * N + n] = acc1[reg];
+  for (int i = 0; i < BPW; ++i) {
+    const int b = w + 8 * i;
+    if (b >= MB * NB) continue;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int m = (b / NB) * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h, n = (b % NB) * 32 + r;
+      if (m < M && n < N) P[m * N + n] = acc[i][reg];
     }
   }
 }
@@ -322,13 +322,48 @@ __global__ void __launch_bounds__(kGemmThreads) k_gemm_tn(const float* __restric
 // (5.1 GB on C5) is written or gathered: the gathers read T (1.3 GB) and the only HBM
 // write is the output.  Walks the relation-major CSR (rows t * num_rows + v, the
 // prepared state's in_rel / out_typed[0]), whose rows of one relation and tile are
-// contiguous.  Deterministic: each row's edges in position order (a cut row's
+// contiguous.  With Lw (RelGraphConv's self-loop) one more pass multiplies the tile's
+// own rows of T by Lw; BWD also stores those rows as gy's last block, so one GEMM gives
+// the relation and self-loop weight gradients.  Deterministic: each row's edges in position order (a cut row's
 // share sums added in share order), then relations and k in order.  BWD: the same walk over the relation-major out-CSR gathers
 // grad_out rows into G_t (stored to gy for the weight gradient) and adds
 // G_t . W_t^T into grad_hidden.  The weights enter as W[t][k][n] =
 // W_src[t * ws_t + k * ws_k + n * ws_n] (k over the gathered width 64).
 constexpr int kFusedW = 64;  // gathered row width (floats)
 constexpr int kSlotStride = kFusedW + 1;
+// LDS for the weights: (relations + self-loop) x 64 x (out width rounded to 32)
+constexpr int kFusedWsFloats = 20480;
+
+// the slot's rows -> gy[v][t * 64 + c], gy rows `mats` blocks of 64 wide (the weight
+// gradients' operand: G_t per relation, then the tile's own rows for the self-loop)
+__device__ __forceinline__ void store_gy(const float* slot, float* gy, int64_t v0, int g, int q,
+                                         int tile_rows, int mats, int t) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (8 * g + i >= tile_rows) break;
+    const float* s = slot + (8 * g + i) * kSlotStride + 4 * q;
+    float* d = gy + (v0 + 8 * g + i) * (static_cast<int64_t>(mats) * kFusedW) + t * kFusedW + 4 * q;
+    __builtin_nontemporal_store(s[0], d);
+    __builtin_nontemporal_store(s[1], d + 1);
+    __builtin_nontemporal_store(s[2], d + 2);
+    __builtin_nontemporal_store(s[3], d + 3);
+  }
+}
+
+// acc[nb] += slot (32 x 64) . wt (64 x SW): one v_mfma_f32_32x32x2_f32 per 2 k and
+// 32 output columns
+template <int NB, int SW>
+__device__ __forceinline__ void mfma_slot(const float* slot, const float* wt, int r, int hb,
+                                          f32x16 (&acc)[NB]) {
+#pragma unroll
+  for (int kk = 0; kk < kFusedW; kk += 2) {
+    const float a = slot[r * kSlotStride + kk + hb];
+    const float* brow = wt + (kk + hb) * SW + r;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+      acc[nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, brow[nb * 32], acc[nb], 0, 0, 0);
+  }
+}
 
 template <bool BWD, int NB>
 __global__ void __launch_bounds__(kGemmThreads) k_rgcn_fused(
@@ -337,14 +372,16 @@ __global__ void __launch_bounds__(kGemmThreads) k_rgcn_fused(
     const float* __restrict__ T, const float* __restrict__ W, int64_t ws_t, int64_t ws_k,
     int64_t ws_n, float* __restrict__ out, float* __restrict__ gy, int64_t num_rows, int R,
     int out_w, const float* __restrict__ bias, const float* __restrict__ addend,
-    unsigned* __restrict__ tile_ctr) {
+    const float* __restrict__ Lw, unsigned* __restrict__ tile_ctr) {
   constexpr int SW = NB * 32;
-  __shared__ float Ws[16384];
+  __shared__ float Ws[kFusedWsFloats];
   __shared__ float slots[8][32 * kSlotStride];
   __shared__ float carries[8][4][kFusedW];
-  for (int i = threadIdx.x; i < R * kFusedW * SW; i += kGemmThreads) {
+  const int RL = R + (Lw != nullptr);  // the self-loop weight is one more matrix
+  for (int i = threadIdx.x; i < RL * kFusedW * SW; i += kGemmThreads) {
     const int t = i / (kFusedW * SW), k = (i / SW) % kFusedW, n = i % SW;
-    Ws[i] = n < out_w ? W[t * ws_t + k * ws_k + n * ws_n] : 0.0f;
+    Ws[i] = n >= out_w ? 0.0f
+                       : (t < R ? W[t * ws_t + k * ws_k + n * ws_n] : Lw[k * ws_k + n * ws_n]);
   }
   __syncthreads();  // the only block barrier
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -366,7 +403,24 @@ __global__ void __launch_bounds__(kGemmThreads) k_rgcn_fused(
     f32x16 acc[NB];
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x16{};
-    for (int t = 0; t < R; ++t) {
+    for (int t = 0; t < RL; ++t) {
+      if (t == R) {
+        // self-loop: the tile's own rows of T (coalesced, no gather) through Lw
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int64_t v = v0 + 8 * g + i;
+          const float4 a = v < num_rows
+                               ? *reinterpret_cast<const float4*>(T + v * kFusedW + 4 * q)
+                               : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+          float* d = slot + (8 * g + i) * kSlotStride + 4 * q;
+          d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w;
+        }
+        wave_lds_sync();
+        if constexpr (BWD) store_gy(slot, gy, v0, g, q, tile_rows, RL, t);
+        mfma_slot<NB, SW>(slot, Ws + t * kFusedW * SW, r, hb, acc);
+        wave_lds_sync();
+        continue;
+      }
       const int64_t base = static_cast<int64_t>(t) * num_rows + v0;
       const int64_t pb = ptr[base], pe = ptr[base + tile_rows];
       if (!BWD && pb == pe) continue;  // no relation-t edge into the tile
@@ -440,29 +494,8 @@ __global__ void __launch_bounds__(kGemmThreads) k_rgcn_fused(
         if (cr >= 0) slot[cr * kSlotStride + lane] += carry[gg * kFusedW + lane];
       }
       wave_lds_sync();
-      if constexpr (BWD) {
-        // G_t rows -> gy[v][t * 64 + c] (the weight gradient's operand)
-        const int64_t vg = v0 + 8 * g;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          if (8 * g + i >= tile_rows) break;
-          const float* s = slot + (8 * g + i) * kSlotStride + 4 * q;
-          float* d = gy + (vg + i) * (static_cast<int64_t>(R) * kFusedW) + t * kFusedW + 4 * q;
-          __builtin_nontemporal_store(s[0], d);
-          __builtin_nontemporal_store(s[1], d + 1);
-          __builtin_nontemporal_store(s[2], d + 2);
-          __builtin_nontemporal_store(s[3], d + 3);
-        }
-      }
-      const float* wt = Ws + t * kFusedW * SW;
-#pragma unroll
-      for (int kk = 0; kk < kFusedW; kk += 2) {
-        const float a = slot[r * kSlotStride + kk + hb];
-        const float* brow = wt + (kk + hb) * SW + r;
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
-          acc[nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, brow[nb * 32], acc[nb], 0, 0, 0);
-      }
+      if constexpr (BWD) store_gy(slot, gy, v0, g, q, tile_rows, RL, t);
+      mfma_slot<NB, SW>(slot, Ws + t * kFusedW * SW, r, hb, acc);
       wave_lds_sync();  // the slot is read; the next relation may overwrite it
     }
 #pragma unroll
@@ -493,6 +526,13 @@ __global__ void k_sum_splits(const float* __restrict__ parts, int splits, int64_
     for (int z = 0; z < splits; ++z) s += parts[z * n + i];
     out[i] = s;
   }
+}
+
+// out[i] += a[i]
+__global__ void k_add_into(float* __restrict__ out, const float* __restrict__ a, int64_t n) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+    out[i] += a[i];
 }
 
 unsigned grid1(int64_t n) {
@@ -531,6 +571,11 @@ void launch_typed_ids(const int32_t* ids, const int32_t* eids, const int32_t* et
   if (nnz <= 0) return;
   hipLaunchKernelGGL(k_typed_ids, dim3(grid1(nnz)), dim3(kBlock), 0, s, ids, eids, etypes, nnz, mul,
                      mode, out);
+}
+
+void launch_add_into(float* out, const float* a, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_add_into, dim3(grid1(n)), dim3(kBlock), 0, s, out, a, n);
 }
 
 void launch_permute_rkx(const float* w, int64_t R, int64_t K, int64_t X, bool to_cat, float* out,
@@ -595,6 +640,7 @@ bool try_tn(const float* A, int64_t a_rs, int64_t a_cs, const float* B, int64_t 
   if (M % 4 != 0 || N % 4 != 0 || a_cs % 4 != 0 || b_rs % 4 != 0 || !al16(A) || !al16(B))
     return false;
   if (M <= 64 && N <= 256) launch_tn<2, 8>(A, a_cs, B, b_rs, C, M, N, K, splits, partials, s);
+  else if (M <= 64 && N <= 320) launch_tn<2, 10>(A, a_cs, B, b_rs, C, M, N, K, splits, partials, s);
   else if (M <= 128 && N <= 128) launch_tn<4, 4>(A, a_cs, B, b_rs, C, M, N, K, splits, partials, s);
   else if (M <= 256 && N <= 64) launch_tn<8, 2>(A, a_cs, B, b_rs, C, M, N, K, splits, partials, s);
   else return false;
@@ -606,14 +652,14 @@ bool try_tn(const float* A, int64_t a_rs, int64_t a_cs, const float* B, int64_t 
 bool rgcn_fused_ok(int64_t gathered_w, int64_t out_w, int64_t R) {
   if (gathered_w != kFusedW || out_w < 1 || out_w > 128 || R < 1) return false;
   const int64_t nb = out_w <= 32 ? 1 : (out_w <= 64 ? 2 : 4);
-  return R * kFusedW * nb * 32 <= 16384;
+  return R * kFusedW * nb * 32 <= kFusedWsFloats;
 }
 
 void launch_rgcn_fused(bool bwd, const int32_t* ptr, const int32_t* cols, const int32_t* rows,
                        const int32_t* eids, const float* w, const float* T, const float* W,
                        int64_t ws_t, int64_t ws_k, int64_t ws_n, float* out, float* gy,
                        int64_t num_rows, int64_t R, int64_t out_w, hipStream_t s,
-                       const float* bias, const float* addend) {
+                       const float* bias, const float* addend, const float* loop_w) {
   if (num_rows <= 0) return;
   const int64_t tiles = (num_rows + 31) / 32;
   const int64_t want = (tiles + 7) / 8;
@@ -626,7 +672,7 @@ void launch_rgcn_fused(bool bwd, const int32_t* ptr, const int32_t* cols, const 
     throw std::runtime_error("rgcn fused: tile counter allocation failed");
 #define DGLMI_RGCN_FUSED(B_, NB_)                                                               \
   hipLaunchKernelGGL((k_rgcn_fused<B_, NB_>), grid, block, 0, s, ptr, cols, rows, eids, w, T, W, \
-                     ws_t, ws_k, ws_n, out, gy, num_rows, Ri, ow, bias, addend, ctr)
+                     ws_t, ws_k, ws_n, out, gy, num_rows, Ri, ow, bias, addend, loop_w, ctr)
   if (bwd) {
     if (out_w <= 32) DGLMI_RGCN_FUSED(true, 1);
     else if (out_w <= 64) DGLMI_RGCN_FUSED(true, 2);

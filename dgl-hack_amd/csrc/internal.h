@@ -378,13 +378,18 @@ void launch_permute_rkx(const float* w, int64_t R, int64_t K, int64_t X, bool to
 // Fused R-GCN layer 1 (hack_kernels.hip k_rgcn_fused): the relation-major CSR (rows
 // t * num_rows + v, `rows` = its COO rows, eids NULL = w by position), gathered table T
 // of 64-float rows, weights W[t][k][n] by strides; out (num_rows x out_w); bwd also
-// writes gy (num_rows x R * 64).  rgcn_fused_ok: the shapes it takes.
+// writes gy (num_rows x R * 64).  loop_w (same k / n strides): one more matrix applied
+// to the tile's own rows of T (RelGraphConv's self-loop; square graphs).
+// rgcn_fused_ok: the shapes it takes (R counts the self-loop matrix too).
 bool rgcn_fused_ok(int64_t gathered_w, int64_t out_w, int64_t R);
 void launch_rgcn_fused(bool bwd, const int32_t* ptr, const int32_t* cols, const int32_t* rows,
                        const int32_t* eids, const float* w, const float* T, const float* W,
                        int64_t ws_t, int64_t ws_k, int64_t ws_n, float* out, float* gy,
                        int64_t num_rows, int64_t R, int64_t out_w, hipStream_t s,
-                       const float* bias = nullptr, const float* addend = nullptr);
+                       const float* bias = nullptr, const float* addend = nullptr,
+                       const float* loop_w = nullptr);
+// out[i] += a[i], i < n
+void launch_add_into(float* out, const float* a, int64_t n, hipStream_t s);
 // out[p] = v[idx[p]]; out[p] = p
 void launch_gather_f32(const float* v, const int32_t* idx, int64_t n, float* out, hipStream_t s);
 void launch_iota_i32(int32_t* out, int64_t n, hipStream_t s);

@@ -217,7 +217,12 @@ _SIGS = {
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.c_void_p]),
     "DGLMIRgcnLayer1Ex": (ctypes.c_int, [
         ctypes.POINTER(Graph), ctypes.c_void_p, ctypes.POINTER(Array), ctypes.POINTER(Array),
-        ctypes.POINTER(Array), ctypes.POINTER(Epilogue), ctypes.POINTER(Array), ctypes.c_void_p]),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Epilogue),
+        ctypes.POINTER(Array), ctypes.c_void_p]),
+    "DGLMIRgcnLayer1BackwardEx": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.c_void_p, ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.c_void_p]),
     "DGLMIRgcnLayer1Backward": (ctypes.c_int, [
         ctypes.POINTER(Graph), ctypes.c_void_p, ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),

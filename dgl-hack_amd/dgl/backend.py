@@ -470,44 +470,46 @@ def _typed_aggregate(graph, num_rels, y, norm, etypes, node_major=False, bias=No
 
 class _FusedRgcnLayer1(th.autograd.Function):
     """RelGraphConv's layer on the hack's layer-1 C entries with the prepared state
-    (``DGLMIRgcnLayer1Ex`` / ``DGLMIRgcnLayer1Backward``, fused aggregate-then-transform
+    (``DGLMIRgcnLayer1Ex`` / ``DGLMIRgcnLayer1BackwardEx``, fused aggregate-then-transform
     kernels): no (N, R * F_out) table Y = X [W_0 | ... | W_{R-1}] is
-    written or gathered, bias and self-loop ride in the output pass.  Gradients for
-    x, the relation weights, bias and the self-loop term; the norm is constant."""
+    written or gathered, and the self-loop message is one more MFMA pass over each
+    tile's own rows, the bias added in the same output pass.  Gradients for x, the
+    relation weights, the self-loop weight and the bias; the norm is constant."""
 
     @staticmethod
-    def forward(ctx, gidx, et32, norm, x, w, bias, addend):
+    def forward(ctx, gidx, et32, norm, x, w, loop_w, bias):
         ret = x.new_empty((gidx.num_dst, w.shape[2]))
-        K.rgcn_layer1_ex(gidx, et32, x, w, norm, ret, bias, addend)
+        K.rgcn_layer1_ex(gidx, et32, x, w, norm, ret, loop_weight=loop_w, bias=bias)
         ctx.gidx, ctx.et32, ctx.norm = gidx, et32, norm
-        ctx.has_bias, ctx.has_addend = bias is not None, addend is not None
-        ctx.save_for_backward(x, w)
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x, w, loop_w)
         return ret
 
     @staticmethod
     def backward(ctx, grad_out):
-        x, w = ctx.saved_tensors
+        x, w, loop_w = ctx.saved_tensors
         g = grad_out.contiguous()
-        gx = gw = gb = ga = None
-        if ctx.needs_input_grad[3] or ctx.needs_input_grad[4]:
+        gx = gw = gl = gb = None
+        if any(ctx.needs_input_grad[3:6]):
             gx, gw = th.empty_like(x), th.empty_like(w)
-            K.rgcn_layer1_backward(ctx.gidx, ctx.et32, x, w, ctx.norm, g, gx, gw)
-        if ctx.has_bias and ctx.needs_input_grad[5]:
+            gl = th.empty_like(loop_w) if loop_w is not None and ctx.needs_input_grad[5] else None
+            K.rgcn_layer1_backward_ex(ctx.gidx, ctx.et32, x, w, ctx.norm, loop_w, g, gx, gw, gl)
+        if ctx.has_bias and ctx.needs_input_grad[6]:
             gb = g.sum(0)
-        if ctx.has_addend and ctx.needs_input_grad[6]:
-            ga = g
-        return None, None, None, gx, gw, gb, ga
+        return None, None, None, gx, gw, gl, gb
 
 
-def rgcn_fused_route(graph, x, weight_shape, norm, etypes):
+def rgcn_fused_route(graph, x, weight_shape, norm, etypes, self_loop=False):
     """(gidx, etypes int32, norm flat) when a RelGraphConv layer can run on the
     fused layer-1 C entries both ways (64-float rows gathered forward and backward,
-    DGLMIRgcnLayer1 / Backward with a prepared state), else None.  The state
-    (``kernel.rgcn_prepare``, ~6 values per edge) is built once per graph, device,
-    etypes and norm, and rebuilt when either tensor is written in place."""
+    the relation and self-loop weights in LDS; DGLMIRgcnLayer1Ex / BackwardEx with a
+    prepared state), else None.  The state (``kernel.rgcn_prepare``, ~6 values per
+    edge) is built once per graph, device, etypes and norm, and rebuilt when either
+    tensor is written in place."""
     R, fi, fo = weight_shape
+    mats = R + int(bool(self_loop))
     if not (x.is_cuda and x.dtype == th.float32 and x.dim() == 2 and x.shape[1] == fi
-            and K.rgcn_fused_ok(fi, fo, R) and K.rgcn_fused_ok(fo, fi, R)):
+            and K.rgcn_fused_ok(fi, fo, mats) and K.rgcn_fused_ok(fo, fi, mats)):
         return None
     if norm is None or norm.requires_grad or not norm.is_cuda or norm.dtype != th.float32:
         return None
@@ -536,10 +538,10 @@ def rgcn_fused_route(graph, x, weight_shape, norm, etypes):
     return hit[1], hit[2], hit[3]
 
 
-def rgcn_fused_layer1(route, x, weight, bias=None, addend=None):
+def rgcn_fused_layer1(route, x, weight, loop_weight=None, bias=None):
     gidx, et32, nf = route
-    return _FusedRgcnLayer1.apply(gidx, et32, nf, x.contiguous(), weight.contiguous(), bias,
-                                  None if addend is None else addend.contiguous())
+    return _FusedRgcnLayer1.apply(gidx, et32, nf, x.contiguous(), weight.contiguous(),
+                                  None if loop_weight is None else loop_weight.contiguous(), bias)
 
 
 def rgcn_layer0(graph, weight, norm, etypes=None):

@@ -497,27 +497,47 @@ def rgcn_layer1(graph, etypes, hidden, weight, norm, ret):
         _arr(weight, "weight"), _arr(norm, "norm"), _arr(ret, "ret"), _stream(ret)))
 
 
-def rgcn_layer1_ex(graph, etypes, hidden, weight, norm, ret, bias=None, addend=None):
-    """DGLMIRgcnLayer1Ex: rgcn_layer1 with RelGraphConv's bias (F_out) and self-loop
-    message (ret's shape) added in the output pass (relgraphconv.py:186-190 order)."""
-    _check_ctx(graph, [("hidden", hidden), ("weight", weight), ("norm", norm), ("ret", ret)])
+def rgcn_layer1_ex(graph, etypes, hidden, weight, norm, ret, loop_weight=None, bias=None,
+                   addend=None):
+    """DGLMIRgcnLayer1Ex: rgcn_layer1 + hidden . loop_weight + bias (+ addend), RelGraphConv's
+    self-loop and bias in the same pass (relgraphconv.py:186-190 order)."""
+    _check_ctx(graph, [("hidden", hidden), ("weight", weight), ("norm", norm), ("ret", ret),
+                       ("loop_weight", loop_weight)])
     epi = _epilogue((None, None, bias, addend), ret)
     if epi is not None and epi.addend and epi.addend % 16:
         raise DGLError("epilogue addend must be 16-byte aligned")
     check_call(_ffi.lib().DGLMIRgcnLayer1Ex(
         ctypes.byref(_rgcn_cgraph(graph, etypes, norm, weight.shape[0], 1)),
         _etypes(graph, etypes), _arr(hidden, "hidden"),
-        _arr(weight, "weight"), _arr(norm, "norm"),
+        _arr(weight, "weight"), _arr(norm, "norm"), _arr(loop_weight, "loop_weight"),
         None if epi is None else ctypes.byref(epi), _arr(ret, "ret"), _stream(ret)))
+
+
+def rgcn_layer1_backward_ex(graph, etypes, hidden, weight, norm, loop_weight, grad_out,
+                            grad_hidden, grad_weight, grad_loop_weight=None):
+    """DGLMIRgcnLayer1BackwardEx: rgcn_layer1_backward with the self-loop term in
+    grad_hidden, and hidden^T . grad_out into grad_loop_weight (if given)."""
+    _check_ctx(graph, [("hidden", hidden), ("weight", weight), ("norm", norm),
+                       ("loop_weight", loop_weight), ("grad_out", grad_out),
+                       ("grad_hidden", grad_hidden), ("grad_weight", grad_weight),
+                       ("grad_loop_weight", grad_loop_weight)])
+    check_call(_ffi.lib().DGLMIRgcnLayer1BackwardEx(
+        ctypes.byref(_rgcn_cgraph(graph, etypes, norm, weight.shape[0], 1)),
+        _etypes(graph, etypes), _arr(hidden, "hidden"),
+        _arr(weight, "weight"), _arr(norm, "norm"), _arr(loop_weight, "loop_weight"),
+        _arr(grad_out, "grad_out"), _arr(grad_hidden, "grad_hidden"),
+        _arr(grad_weight, "grad_weight"), _arr(grad_loop_weight, "grad_loop_weight"),
+        _stream(grad_out)))
 
 
 def rgcn_fused_ok(gathered_w, out_w, num_rels):
     """The shapes the fused layer-1 kernels take (hack_kernels.hip rgcn_fused_ok):
-    64-float gathered rows, 1..128 outputs, all relations' weights in 64 KB of LDS."""
+    64-float gathered rows, 1..128 outputs, all weight matrices (``num_rels`` counts the
+    self-loop one too) in 80 KB of LDS."""
     if gathered_w != 64 or not 1 <= out_w <= 128 or num_rels < 1:
         return False
     nb = 1 if out_w <= 32 else (2 if out_w <= 64 else 4)
-    return num_rels * 64 * nb * 32 <= 16384
+    return num_rels * 64 * nb * 32 <= 20480
 
 
 def rgcn_layer1_backward(graph, etypes, hidden, weight, norm, grad_out, grad_hidden, grad_weight):

@@ -89,13 +89,13 @@ class RelGraphConv(nn.Module):
     def forward(self, g, x, etypes, norm=None):
         if self.use_fused and self.regularizer == "basis":
             route = B.rgcn_fused_route(g, x, (self.num_rels, self.in_feat, self.out_feat), norm,
-                                       etypes)
+                                       etypes, self.self_loop)
             if route is not None:
-                # aggregate-then-transform on the fused layer-1 C entries, bias and
-                # self-loop message in the output pass (B.rgcn_fused_layer1)
-                loop = B.project(x, self.loop_weight) if self.self_loop else None
+                # aggregate-then-transform on the fused layer-1 C entries, the self-loop
+                # message and the bias in the same kernel (B.rgcn_fused_layer1)
                 node_repr = B.rgcn_fused_layer1(route, x, self._relation_weights(),
-                                                self.h_bias if self.bias else None, loop)
+                                                self.loop_weight if self.self_loop else None,
+                                                self.h_bias if self.bias else None)
                 if self.activation:
                     node_repr = self.activation(node_repr)
                 return self.dropout(node_repr)

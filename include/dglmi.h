@@ -393,21 +393,33 @@ int DGLMIRgcnLayer0Backward(const DGLMIGraph* graph, const int32_t* etypes,
 int DGLMIRgcnLayer1(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* hidden,
                     const DGLMIArray* weight, const DGLMIArray* norm, DGLMIArray* ret,
                     void* stream);
-/* Extension (no reference counterpart): DGLMIRgcnLayer1 with RelGraphConv's bias and
- * self-loop message in the output pass, ret[v] = agg[v] + bias + addend[v] in the order
- * of relgraphconv.py:186-190 (python/dgl/nn/pytorch/conv/relgraphconv.py), so the
- * module needs no extra passes over the output.  epilogue->bias has F_out floats,
- * epilogue->addend the shape of ret (not aliasing it); row_mul / row_div must be NULL.
- * A NULL epilogue is DGLMIRgcnLayer1. */
+/* Extension (no reference counterpart): DGLMIRgcnLayer1 with RelGraphConv's self-loop
+ * and bias, ret[v] = agg[v] + bias + hidden[v] . loop_weight (+ epilogue->addend[v]),
+ * in the order of relgraphconv.py:186-190 (python/dgl/nn/pytorch/conv/relgraphconv.py),
+ * so the module needs no extra GEMM or passes over the output: on the fused kernels the
+ * self-loop is one more MFMA pass over the tile's own rows.  loop_weight (F_in, F_out)
+ * or NULL, square graphs only; epilogue->bias has F_out floats, epilogue->addend the
+ * shape of ret (not aliasing it); row_mul / row_div must be NULL.  NULL loop_weight and
+ * epilogue give DGLMIRgcnLayer1. */
 int DGLMIRgcnLayer1Ex(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* hidden,
                       const DGLMIArray* weight, const DGLMIArray* norm,
-                      const DGLMIEpilogue* epilogue, DGLMIArray* ret, void* stream);
+                      const DGLMIArray* loop_weight, const DGLMIEpilogue* epilogue,
+                      DGLMIArray* ret, void* stream);
 /* _CAPI_DGLRgcnLayer1Backward: grad_hidden[u] = sum_{e out of u} norm[e] * grad_out[v]
  * . weight[t]^T; grad_weight[t] = sum_{e of relation t} norm[e] hidden[u]^T grad_out[v]. */
 int DGLMIRgcnLayer1Backward(const DGLMIGraph* graph, const int32_t* etypes,
                             const DGLMIArray* hidden, const DGLMIArray* weight,
                             const DGLMIArray* norm, const DGLMIArray* grad_out,
                             DGLMIArray* grad_hidden, DGLMIArray* grad_weight, void* stream);
+/* Extension: DGLMIRgcnLayer1Backward of DGLMIRgcnLayer1Ex's self-loop as well:
+ * grad_hidden also gets grad_out . loop_weight^T, and grad_loop_weight (F_in, F_out; may
+ * be NULL) = hidden^T . grad_out.  NULL loop_weight gives DGLMIRgcnLayer1Backward. */
+int DGLMIRgcnLayer1BackwardEx(const DGLMIGraph* graph, const int32_t* etypes,
+                              const DGLMIArray* hidden, const DGLMIArray* weight,
+                              const DGLMIArray* norm, const DGLMIArray* loop_weight,
+                              const DGLMIArray* grad_out, DGLMIArray* grad_hidden,
+                              DGLMIArray* grad_weight, DGLMIArray* grad_loop_weight,
+                              void* stream);
 /* _CAPI_DGLNbAccess: the in-neighbour gather benchmark.  Runs `times` in-neighbour
  * row gathers of feat over the in-CSR (the load-balanced copy_u sum, into scratch;
  * the reference's timed kernels read rows without using them) and writes the mean

@@ -239,3 +239,76 @@ def test_rgcn_prepare_rejects_bad_arguments():
         K.RgcnState(gidx, et.int(), norm[:10], 2, 3)
     with pytest.raises(DGLError, match="etypes"):
         K.RgcnState(gidx, et.int()[:10], norm, 2, 3)
+
+
+@pytest.mark.parametrize("K_in,X,R,prepare,hub", [(64, 64, 4, 6, True), (64, 32, 3, 6, False),
+                                                  (64, 64, 4, 0, False), (24, 16, 2, 2, True)])
+def test_rgcn_layer1_ex_self_loop(K_in, X, R, prepare, hub):
+    """DGLMIRgcnLayer1Ex / BackwardEx: the relation sum + hidden . loop_weight + bias
+    (+ addend) forward, and grad_hidden with the self-loop term plus grad_loop_weight,
+    vs fp64 -- on the fused kernels (64-wide rows, prepared state: the self-loop is one
+    more MFMA pass over the tile's own rows) and on the GEMM + gather path."""
+    from dgl import kernel as K
+    g, gidx, s, d, et, norm = _graph(20001, 150000, R, seed=K_in + X + R, hub=hub)
+    n = g.number_of_nodes()
+    gidx.__dict__.pop("_rgcn_state", None)
+    et32 = et.int()
+    if prepare:
+        K.rgcn_prepare(gidx, et32, norm, R, layers=prepare)
+    h = th.randn(n, K_in, device=DEV)
+    w = th.randn(R, K_in, X, device=DEV) / 4
+    lw = th.randn(K_in, X, device=DEV) / 4
+    bias = th.randn(X, device=DEV)
+    add = th.randn(n, X, device=DEV)
+    msg = th.einsum("ek,ekx->ex", h.double()[s], w.double()[et]) * norm.double()
+    agg = th.zeros(n, X, dtype=th.float64, device=DEV).index_add_(0, d, msg)
+    mass = th.zeros(n, X, dtype=th.float64, device=DEV).index_add_(0, d, msg.abs())
+    loop = h.double() @ lw.double()
+    lmass = h.double().abs() @ lw.double().abs()
+    for addend in (None, add):
+        ret = th.full((n, X), float("nan"), device=DEV)
+        K.rgcn_layer1_ex(gidx, et32, h, w, norm, ret, loop_weight=lw, bias=bias, addend=addend)
+        ref = agg + bias.double() + loop + (0 if addend is None else addend.double())
+        assert ((ret.double() - ref).abs() <= 1e-4 + 1e-5 * (mass + lmass)).all()
+    go = th.randn(n, X, device=DEV)
+    gh = th.full((n, K_in), float("nan"), device=DEV)
+    gw = th.full((R, K_in, X), float("nan"), device=DEV)
+    gl = th.full((K_in, X), float("nan"), device=DEV)
+    K.rgcn_layer1_backward_ex(gidx, et32, h, w, norm, lw, go, gh, gw, gl)
+    gmsg = go.double()[d] * norm.double()
+    gh_ref = th.zeros(n, K_in, dtype=th.float64, device=DEV).index_add_(
+        0, s, th.einsum("ex,ekx->ek", gmsg, w.double()[et])) + go.double() @ lw.double().t()
+    gh_mass = th.zeros(n, K_in, dtype=th.float64, device=DEV).index_add_(
+        0, s, th.einsum("ex,ekx->ek", gmsg.abs(), w.double()[et].abs())) + \
+        go.double().abs() @ lw.double().abs().t()
+    assert ((gh.double() - gh_ref).abs() <= 1e-4 + 1e-5 * gh_mass).all()
+    gw_ref = th.zeros(R, K_in, X, dtype=th.float64, device=DEV).index_add_(
+        0, et, th.einsum("ek,ex->ekx", h.double()[s], gmsg))
+    gw_mass = th.zeros(R, K_in, X, dtype=th.float64, device=DEV).index_add_(
+        0, et, th.einsum("ek,ex->ekx", h.double()[s].abs(), gmsg.abs()))
+    assert ((gw.double() - gw_ref).abs() <= 2e-4 + 1e-6 * gw_mass).all()
+    gl_ref = h.double().t() @ go.double()
+    gl_mass = h.double().abs().t() @ go.double().abs()
+    assert ((gl.double() - gl_ref).abs() <= 2e-4 + 1e-6 * gl_mass).all()
+    # no loop weight: the plain entries' results
+    ret0, ret1 = th.empty(n, X, device=DEV), th.empty(n, X, device=DEV)
+    K.rgcn_layer1(gidx, et32, h, w, norm, ret0)
+    K.rgcn_layer1_ex(gidx, et32, h, w, norm, ret1)
+    assert th.equal(ret0, ret1)
+    gidx.__dict__.pop("_rgcn_state", None)
+
+
+def test_rgcn_layer1_ex_rejects_bad_arguments():
+    from dgl import kernel as K
+    from dgl._ffi import DGLError
+    g, gidx, s, d, et, norm = _graph(3000, 20000, 2, seed=3)
+    n = g.number_of_nodes()
+    et32 = et.int()
+    h, w = th.randn(n, 16, device=DEV), th.randn(2, 16, 8, device=DEV)
+    ret = th.empty(n, 8, device=DEV)
+    with pytest.raises(DGLError, match="loop_weight"):
+        K.rgcn_layer1_ex(gidx, et32, h, w, norm, ret, loop_weight=th.randn(8, 16, device=DEV))
+    with pytest.raises(DGLError, match="grad_loop_weight needs loop_weight"):
+        K.rgcn_layer1_backward_ex(gidx, et32, h, w, norm, None, th.randn(n, 8, device=DEV),
+                                  th.empty(n, 16, device=DEV), th.empty_like(w),
+                                  th.empty(16, 8, device=DEV))

@@ -227,3 +227,13 @@ def test_64bit_graph_selection():
     from dgl.graph import _PartialIndex
     assert _PartialIndex(4, [0], [1], [2 ** 31]).bits_needed() == 64
     assert _PartialIndex(4, [0], [1], [5]).bits_needed() == 32
+
+
+def test_rgcn_fused_ok_matches_the_kernel_rule():
+    """dgl.kernel.rgcn_fused_ok restates hack_kernels.hip rgcn_fused_ok (20480 LDS floats
+    of weights): C5's 4 relations + self-loop at 64 -> 64 fit, a sixth matrix does not."""
+    from dgl import kernel as K
+    assert K.rgcn_fused_ok(64, 64, 5) and not K.rgcn_fused_ok(64, 64, 6)
+    assert K.rgcn_fused_ok(64, 128, 2) and not K.rgcn_fused_ok(64, 128, 3)
+    assert K.rgcn_fused_ok(64, 32, 10) and not K.rgcn_fused_ok(64, 32, 11)
+    assert not K.rgcn_fused_ok(32, 64, 1) and not K.rgcn_fused_ok(64, 129, 1)
