@@ -346,6 +346,10 @@ constexpr int kFusedW = 64;  // gathered row width (floats)
 constexpr int kSlotStride = kFusedW + 1;
 // LDS for the weights: (relations + self-loop) x 64 x (out width rounded to 32)
 constexpr int kFusedWsFloats = 20480;
+// tile queues of the fused kernels: tiles per atomic, and the spacing of the eight
+// counters (unsigned; one 128-B line each)
+constexpr int kTileGrab = 2;
+constexpr int kCtrStride = 32;
 
 // the slot's rows -> gy[v][t * 64 + c], gy rows `mats` blocks of 64 wide (the weight
 // gradients' operand: G_t per relation, then the tile's own rows for the self-loop)
@@ -403,14 +407,27 @@ __global__ void __launch_bounds__(kGemmThreads) k_rgcn_fused(
   float* slot = slots[wv];
   float* carry = carries[wv][0];
   const int64_t tiles = (num_rows + 31) / 32;
-  for (;;) {
-    // tiles from a queue (one vector atomic per tile): a wave that drew a hub row's
-    // tile does not hold the others back; each tile's result does not depend on
-    // which wave computed it
-    unsigned tv = 0;
-    if (lane == 0) tv = atomicAdd(tile_ctr, 1u);
-    const int64_t tile = static_cast<unsigned>(__shfl(static_cast<int>(tv), 0));
-    if (tile >= tiles) break;
+  // tiles from queues (one vector atomic per kTileGrab tiles): a wave that drew a hub
+  // row's tile does not hold the others back, and a tile's result does not depend on
+  // which wave computed it.  Eight queues (fewer on a grid of fewer blocks), tiles q,
+  // q + 8, ... in queue q, served by the blocks b with b % 8 == q (one XCD each under
+  // round-robin dispatch; correctness does not depend on the placement): the atomics
+  // of one counter serialise, and a single counter for every wave cost ~10 ns per
+  // tile, 1.6 ms of a C5 launch.
+  // (fewer queues than blocks on a small grid: every queue must have a server)
+  const int nq = gridDim.x < 8 ? static_cast<int>(gridDim.x) : 8;
+  const int64_t qid = blockIdx.x % nq;
+  unsigned* ctr = tile_ctr + qid * kCtrStride;
+  const int64_t qtiles = tiles > qid ? (tiles - qid + nq - 1) / nq : 0;
+  for (int64_t k0 = 0;;) {
+    if ((k0 & (kTileGrab - 1)) == 0) {
+      unsigned tv = 0;
+      if (lane == 0) tv = atomicAdd(ctr, static_cast<unsigned>(kTileGrab));
+      k0 = static_cast<unsigned>(__shfl(static_cast<int>(tv), 0));
+    }
+    if (k0 >= qtiles) break;
+    const int64_t tile = qid + nq * k0;
+    ++k0;
     const int64_t v0 = tile * 32;
     const int tile_rows = num_rows - v0 < 32 ? static_cast<int>(num_rows - v0) : 32;
     f32x16 acc[NB];
@@ -680,8 +697,9 @@ void launch_rgcn_fused(bool bwd, const int32_t* ptr, const int32_t* cols, const 
   const int Ri = static_cast<int>(R), ow = static_cast<int>(out_w);
   // the tile queue's counter: stream-ordered, zeroed before and released after
   unsigned* ctr = nullptr;
-  if (hipMallocAsync(reinterpret_cast<void**>(&ctr), sizeof(unsigned), s) != hipSuccess ||
-      hipMemsetAsync(ctr, 0, sizeof(unsigned), s) != hipSuccess)
+  const size_t ctr_bytes = 8 * kCtrStride * sizeof(unsigned);
+  if (hipMallocAsync(reinterpret_cast<void**>(&ctr), ctr_bytes, s) != hipSuccess ||
+      hipMemsetAsync(ctr, 0, ctr_bytes, s) != hipSuccess)
     throw std::runtime_error("rgcn fused: tile counter allocation failed");
 #define DGLMI_RGCN_FUSED(B_, NB_)                                                               \
   hipLaunchKernelGGL((k_rgcn_fused<B_, NB_>), grid, block, 0, s, ptr, cols, rows, eids, w, T, W, \

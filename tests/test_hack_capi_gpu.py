@@ -312,3 +312,10 @@ def test_rgcn_layer1_ex_rejects_bad_arguments():
         K.rgcn_layer1_backward_ex(gidx, et32, h, w, norm, None, th.randn(n, 8, device=DEV),
                                   th.empty(n, 16, device=DEV), th.empty_like(w),
                                   th.empty(16, 8, device=DEV))
+
+
+@pytest.mark.parametrize("n,m", [(500, 4000), (1700, 20000), (33, 300)])
+def test_rgcn_layer1_fused_small_grids(n, m):
+    """Graphs of fewer than 57 row tiles launch the fused kernels on fewer than eight
+    blocks: the tile queues shrink to the grid (every queue has a server)."""
+    _layer1_fwd_bwd(64, 64, False, n, m, R=4, prepare=4)
