@@ -832,6 +832,29 @@ def measure_update_all(g, x, out_ref, args):
             "path": "DGLGraph.update_all(fn.copy_u, fn.sum) incl. output allocation"}
 
 
+def measure_configs(device, steps=5, warmup=2):
+    """The other single-GPU BASELINE configs at N = 1, timed on this box beside the
+    headline (scripts/bench_configs.py): C2 arxiv-size copy_u_sum and GraphConv layer,
+    C3 Reddit-size fused GATConv forward / forward + backward, C5 RelGraphConv on the
+    fused R-GCN entries.  Informational: a config that fails is recorded under its key
+    and does not change the job's status (the headline contract is the M1 line)."""
+    import gc
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import bench_configs as bc
+    out = {"steps": steps, "warmup": warmup, "source": "scripts/bench_configs.py"}
+    for name in ("c2", "c3", "c5"):
+        t0 = time.time()
+        try:
+            out[name] = getattr(bc, name)(device, steps, warmup)
+        except Exception as exc:  # noqa: BLE001 -- informational only
+            out[name] = {"error": repr(exc)[:300]}
+        out[name]["wall_s"] = time.time() - t0
+        gc.collect()
+        th.cuda.empty_cache()
+        log("configs %s: %s" % (name, json.dumps(out[name])))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -852,6 +875,8 @@ def main():
                     help="N=1: skip the rocprofv3 PMC passes (roofline traffic)")
     ap.add_argument("--no-c4", action="store_true",
                     help="skip the fixed-size C4 (10M / 200M, partitioned, with exchange) line")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="N=1: skip the informational C2 / C3 / C5 config timings")
     ap.add_argument("--c4-nodes", type=int, default=C4_NODES, help=argparse.SUPPRESS)
     ap.add_argument("--c4-edges", type=int, default=C4_EDGES, help=argparse.SUPPRESS)
     ap.add_argument("--c4-rounds", type=int, default=24,
@@ -1109,6 +1134,8 @@ def main():
             del part
         th.cuda.empty_cache()
         lines.run("c4", lambda: measure_c4(world, rank, dist, cdev, device, args))
+    if world == 1 and not under_profiler and not args.no_configs:
+        res["configs"] = measure_configs(device)
     rc = lines.finish()
     if dist is not None:
         dist.barrier()
