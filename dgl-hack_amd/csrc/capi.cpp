@@ -1673,7 +1673,7 @@ int rgcn_layer1_backward_impl(const DGLMIGraph* graph, const int32_t* etypes,
   check_array(hidden, "hidden");
   check_array(weight, "weight");
   check_array(grad_out, "grad_out");
-  check_array(grad_hidden, "grad_hidden");
+  if (grad_hidden) check_array(grad_hidden, "grad_hidden");  // NULL (Ex only): not wanted
   check_array(grad_weight, "grad_weight");
   DGLMI_CHECK(weight->ndim == 3 && grad_weight->ndim == 3, "weights must be (num_rels, F_in, F_out)");
   const int64_t R = weight->shape[0], K = weight->shape[1], X = weight->shape[2];
@@ -1682,7 +1682,8 @@ int rgcn_layer1_backward_impl(const DGLMIGraph* graph, const int32_t* etypes,
   rgcn_common(graph, etypes, R * out.num_rows);
   const int64_t N = out.num_rows, M = R * X;
   DGLMI_CHECK(hidden->shape[0] == N && feat_numel(hidden) == K, "hidden must be (num_src, F_in)");
-  DGLMI_CHECK(grad_hidden->shape[0] == N && feat_numel(grad_hidden) == K, "grad_hidden shape");
+  DGLMI_CHECK(!grad_hidden || (grad_hidden->shape[0] == N && feat_numel(grad_hidden) == K),
+              "grad_hidden shape");
   DGLMI_CHECK(grad_out->shape[0] == graph->in_csr.num_rows && feat_numel(grad_out) == X,
               "grad_out must be (num_dst, F_out)");
   edge_values(norm, out.nnz, "norm");
@@ -1719,9 +1720,9 @@ int rgcn_layer1_backward_impl(const DGLMIGraph* graph, const int32_t* etypes,
     const float* w = nullptr;
     rgcn_fused_walk(fs, fs->out_typed[0], fs->out_norm[0], norm->data, &eids, &w);
     launch_rgcn_fused(true, fs->out_typed[0].indptr, fs->out_typed[0].indices, fs->out_typed[0].rows,
-                      eids, w, grad_out->data, weight->data, K * X, 1, X, grad_hidden->data,
-                      static_cast<float*>(gy.ptr), N, R, K, s, nullptr, nullptr,
-                      loop ? loop->data : nullptr);
+                      eids, w, grad_out->data, weight->data, K * X, 1, X,
+                      grad_hidden ? grad_hidden->data : nullptr, static_cast<float*>(gy.ptr), N, R,
+                      K, s, nullptr, nullptr, loop ? loop->data : nullptr);
     launch_gemm(hidden->data, 1, K, static_cast<float*>(gy.ptr), MG, 1, static_cast<float*>(gw.ptr),
                 K, MG, N, splits, static_cast<float*>(parts.ptr), s);
     if (!loop) {
@@ -1756,12 +1757,13 @@ int rgcn_layer1_backward_impl(const DGLMIGraph* graph, const int32_t* etypes,
     launch_fill(static_cast<float*>(gy.ptr), N * M, 0.0f, s);
   }
   // grad_hidden = gy (N x RX) . wcat^T ; grad_wcat = hidden^T (K x N) . gy (split over N)
-  launch_gemm(static_cast<float*>(gy.ptr), M, 1, static_cast<float*>(wcat.ptr), 1, M,
-              grad_hidden->data, N, K, M, 1, nullptr, s);
+  if (grad_hidden)
+    launch_gemm(static_cast<float*>(gy.ptr), M, 1, static_cast<float*>(wcat.ptr), 1, M,
+                grad_hidden->data, N, K, M, 1, nullptr, s);
   launch_gemm(hidden->data, 1, K, static_cast<float*>(gy.ptr), M, 1, static_cast<float*>(gw.ptr), K,
               M, N, splits, static_cast<float*>(parts.ptr), s);
   launch_permute_rkx(static_cast<float*>(gw.ptr), R, K, X, false, grad_weight->data, s);
-  if (loop) {  // grad_hidden += grad_out . loop^T
+  if (loop && grad_hidden) {  // grad_hidden += grad_out . loop^T
     Scratch lt(&z, N * K * 4, s);
     launch_gemm(grad_out->data, X, 1, loop->data, 1, X, static_cast<float*>(lt.ptr), N, K, X, 1,
                 nullptr, s);
@@ -1777,6 +1779,10 @@ int DGLMIRgcnLayer1Backward(const DGLMIGraph* graph, const int32_t* etypes,
                             const DGLMIArray* hidden, const DGLMIArray* weight,
                             const DGLMIArray* norm, const DGLMIArray* grad_out,
                             DGLMIArray* grad_hidden, DGLMIArray* grad_weight, void* stream) {
+  if (grad_hidden == nullptr) {  // the reference entry always returns both gradients
+    g_last_error = "grad_hidden is NULL";
+    return -1;
+  }
   return rgcn_layer1_backward_impl(graph, etypes, hidden, weight, norm, nullptr, grad_out,
                                    grad_hidden, grad_weight, nullptr, stream);
 }

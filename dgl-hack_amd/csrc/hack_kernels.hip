@@ -337,7 +337,8 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda,
 // prepared state's in_rel / out_typed[0]), whose rows of one relation and tile are
 // contiguous.  With Lw (RelGraphConv's self-loop) one more pass multiplies the tile's
 // own rows of T by Lw; BWD also stores those rows as gy's last block, so one GEMM gives
-// the relation and self-loop weight gradients.  Deterministic: each row's edges in position order (a cut row's
+// the relation and self-loop weight gradients.  BWD with out == nullptr (no input
+// gradient wanted) skips the MFMA passes and stores only gy.  Deterministic: each row's edges in position order (a cut row's
 // share sums added in share order), then relations and k in order.  BWD: the same walk over the relation-major out-CSR gathers
 // grad_out rows into G_t (stored to gy for the weight gradient) and adds
 // G_t . W_t^T into grad_hidden.  The weights enter as W[t][k][n] =
@@ -447,7 +448,7 @@ __global__ void __launch_bounds__(kGemmThreads) k_rgcn_fused(
         }
         wave_lds_sync();
         if constexpr (BWD) store_gy(slot, gy, v0, g, q, tile_rows, RL, t);
-        mfma_slot<NB, SW>(slot, Ws + t * kFusedW * SW, r, hb, acc);
+        if (out != nullptr) mfma_slot<NB, SW>(slot, Ws + t * kFusedW * SW, r, hb, acc);
         wave_lds_sync();
         continue;
       }
@@ -525,9 +526,10 @@ __global__ void __launch_bounds__(kGemmThreads) k_rgcn_fused(
       }
       wave_lds_sync();
       if constexpr (BWD) store_gy(slot, gy, v0, g, q, tile_rows, RL, t);
-      mfma_slot<NB, SW>(slot, Ws + t * kFusedW * SW, r, hb, acc);
+      if (out != nullptr) mfma_slot<NB, SW>(slot, Ws + t * kFusedW * SW, r, hb, acc);
       wave_lds_sync();  // the slot is read; the next relation may overwrite it
     }
+    if (out == nullptr) continue;  // BWD without grad_hidden: only gy was wanted
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
       const int64_t m = v0 + (reg & 3) + 8 * (reg >> 2) + 4 * hb;

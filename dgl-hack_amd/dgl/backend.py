@@ -491,7 +491,10 @@ class _FusedRgcnLayer1(th.autograd.Function):
         g = grad_out.contiguous()
         gx = gw = gl = gb = None
         if any(ctx.needs_input_grad[3:6]):
-            gx, gw = th.empty_like(x), th.empty_like(w)
+            # no input gradient wanted (a first layer over data): the walk skips its
+            # MFMA passes and stores only the weight gradients' operand
+            gx = th.empty_like(x) if ctx.needs_input_grad[3] else None
+            gw = th.empty_like(w)
             gl = th.empty_like(loop_w) if loop_w is not None and ctx.needs_input_grad[5] else None
             K.rgcn_layer1_backward_ex(ctx.gidx, ctx.et32, x, w, ctx.norm, loop_w, g, gx, gw, gl)
         if ctx.has_bias and ctx.needs_input_grad[6]:

@@ -961,7 +961,9 @@ class DistRelGraphConv(th.nn.Module):
     the halo sources arrive with one all-to-all-v (the narrower of x and the
     relation transforms is exchanged: x, then the (N, R * out) GEMM over owned +
     halo rows), and the typed gather runs on the local block; the self-loop and
-    bias use the owned rows.  ``etypes`` / ``norm`` are per LOCAL edge
+    bias use the owned rows.  Layers the fused R-GCN kernels take (64-float rows
+    both ways, constant norm; ``RelGraphConv.use_fused``) run them on the local block
+    instead, halo rows included and dropped after.  ``etypes`` / ``norm`` are per LOCAL edge
     (:meth:`Partition.local_edge_data` slices global ones)."""
 
     def __init__(self, in_feat, out_feat, num_rels, regularizer="basis", num_bases=None,
@@ -976,6 +978,11 @@ class DistRelGraphConv(th.nn.Module):
         c = self.conv
         g = part.local_graph(feat.device)
         x_full = halo_exchange(feat, part, group)
+        if c.use_fused and c.regularizer == "basis" and B.rgcn_fused_route(
+                g, x_full, (c.num_rels, c.in_feat, c.out_feat), norm, etypes, c.self_loop):
+            # the local block is square over owned + halo rows (owned first, only they
+            # have in-edges): the module's fused R-GCN route on it, owned rows kept
+            return c(g, x_full, etypes, norm)[:part.n_inner]
         y, node_major = c._transform(x_full)
         n = g.number_of_nodes()
         rst = B._typed_aggregate(g, c.num_rels, y.contiguous().view(c.num_rels * n, c.out_feat),

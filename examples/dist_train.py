@@ -64,6 +64,8 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0, help="fraction of the config's size")
     ap.add_argument("--dist-backend", default="nccl")
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (rehearsal)")
+    ap.add_argument("--no-fused", action="store_true",
+                    help="rgcn: the GEMM + typed-gather path instead of the fused R-GCN kernels")
     args = ap.parse_args()
     cfg = CONFIGS[args.model]
 
@@ -128,6 +130,8 @@ def main():
                                 num_bases=cfg["rels"], self_loop=True, activation=th.relu)
         l2 = D.DistRelGraphConv(cfg["hidden"], cfg["classes"], cfg["rels"], "basis",
                                 num_bases=cfg["rels"], self_loop=True)
+        if args.no_fused:
+            l1.conv.use_fused = l2.conv.use_fused = False
 
         def forward():
             return l2(part, l1(part, x, et_l, norm_l), et_l, norm_l)

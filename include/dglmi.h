@@ -413,7 +413,9 @@ int DGLMIRgcnLayer1Backward(const DGLMIGraph* graph, const int32_t* etypes,
                             DGLMIArray* grad_hidden, DGLMIArray* grad_weight, void* stream);
 /* Extension: DGLMIRgcnLayer1Backward of DGLMIRgcnLayer1Ex's self-loop as well:
  * grad_hidden also gets grad_out . loop_weight^T, and grad_loop_weight (F_in, F_out; may
- * be NULL) = hidden^T . grad_out.  NULL loop_weight gives DGLMIRgcnLayer1Backward. */
+ * be NULL) = hidden^T . grad_out.  grad_hidden may be NULL when the input gradient is
+ * not wanted (the fused walk then skips its MFMA passes).  NULL loop_weight gives
+ * DGLMIRgcnLayer1Backward. */
 int DGLMIRgcnLayer1BackwardEx(const DGLMIGraph* graph, const int32_t* etypes,
                               const DGLMIArray* hidden, const DGLMIArray* weight,
                               const DGLMIArray* norm, const DGLMIArray* loop_weight,

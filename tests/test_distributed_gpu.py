@@ -120,17 +120,17 @@ def test_aggregate_with_halo_overlapped():
     assert q.get(timeout=5) == "ok"
 
 
-def _gat_rgcn_worker(rank, world, src, dst, et, n, q, planner):
+def _gat_rgcn_worker(rank, world, src, dst, et, n, q, planner, fin=16, fout=8):
     import dgl
     from dgl import distributed as D
     from dgl.nn.pytorch import GATConv, RelGraphConv
     dev = "cuda:0"
     R = 3
     th.manual_seed(0)
-    gat = GATConv(16, 8, 4).to(dev)
-    rel = RelGraphConv(16, 8, R, "basis", num_bases=2, self_loop=True).to(dev)
-    dg = D.DistGATConv(16, 8, 4).to(dev)
-    dr = D.DistRelGraphConv(16, 8, R, "basis", num_bases=2, self_loop=True).to(dev)
+    gat = GATConv(fin, 8, 4).to(dev)
+    rel = RelGraphConv(fin, fout, R, "basis", num_bases=2, self_loop=True).to(dev)
+    dg = D.DistGATConv(fin, 8, 4).to(dev)
+    dr = D.DistRelGraphConv(fin, fout, R, "basis", num_bases=2, self_loop=True).to(dev)
     dg.conv.load_state_dict(gat.state_dict())
     dr.conv.load_state_dict(rel.state_dict())
     et_t = th.from_numpy(et).to(dev)
@@ -154,11 +154,13 @@ def _gat_rgcn_worker(rank, world, src, dst, et, n, q, planner):
                                         th.from_numpy(dst[sel] - lo).to(dev).int(), bounds, rank)
         idx = th.from_numpy(np.nonzero(sel)[0]).to(dev)
         et_l, norm_l = et_t[idx], norm[idx]
-    x = th.from_numpy(np.random.RandomState(2).randn(n, 16).astype(np.float32)).to(dev)
+    x = th.from_numpy(np.random.RandomState(2).randn(n, fin).astype(np.float32)).to(dev)
     inner = th.from_numpy(part.inner).to(dev)
     xi = x[inner]
     og = dg(part, xi)
     orl = dr(part, xi, et_l, norm_l)
+    fused = part.local_graph(dev)._graph.__dict__.get("_rgcn_fused") is not None
+    assert fused == (fin == 64 and fout == 64)  # the fused R-GCN route on the local block
     (og.pow(2).sum() + orl.pow(2).sum()).backward()
     params = list(dg.parameters()) + list(dr.parameters())
     D.allreduce_gradients(params, average=False)
@@ -183,8 +185,25 @@ def _gat_rgcn_worker(rank, world, src, dst, et, n, q, planner):
         np.testing.assert_allclose(full_g, rg.detach().cpu().numpy(), rtol=1e-4, atol=1e-4)
         np.testing.assert_allclose(full_r, rr.detach().cpu().numpy(), rtol=1e-4, atol=1e-4)
         for a, b in zip(objs[0]["grads"], ref_grads):
-            np.testing.assert_allclose(a, b, rtol=1e-3, atol=1e-3)
+            # long fp32 sums (tens of thousands of terms) in other orders: scaled bound
+            assert np.abs(a - b).max() <= 1e-3 + 1e-4 * np.abs(b).max()
         q.put("ok")
+
+
+@pytest.mark.parametrize("planner", ["host_ldg", "device_contiguous"])
+def test_dist_rgcn_fused_route_matches_single_gpu(planner):
+    """DistRelGraphConv 64 -> 64 runs the fused R-GCN kernels on each rank's local
+    block (owned + halo rows): outputs and all-reduced gradients equal the
+    whole-graph module's, 2 ranks on one GPU."""
+    import torch.multiprocessing as mp
+    from dist_util import run_world
+    from graphs import powerlaw
+    src, dst, n = powerlaw(3000, 40000, seed=7)
+    et = np.random.default_rng(7).integers(0, 3, len(src))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    run_world(_gat_rgcn_worker, 2, (src, dst, et, n, q, planner, 64, 64))
+    assert q.get(timeout=5) == "ok"
 
 
 @pytest.mark.parametrize("planner", ["host_ldg", "device_contiguous", "device_lp"])

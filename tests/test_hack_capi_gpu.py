@@ -319,3 +319,24 @@ def test_rgcn_layer1_fused_small_grids(n, m):
     """Graphs of fewer than 57 row tiles launch the fused kernels on fewer than eight
     blocks: the tile queues shrink to the grid (every queue has a server)."""
     _layer1_fwd_bwd(64, 64, False, n, m, R=4, prepare=4)
+
+
+@pytest.mark.parametrize("prepare", [6, 0])
+def test_rgcn_layer1_backward_ex_without_grad_hidden(prepare):
+    """BackwardEx with grad_hidden NULL (a first layer over data): the weight and
+    self-loop gradients are the ones the full call returns, bit for bit."""
+    from dgl import kernel as K
+    g, gidx, s, d, et, norm = _graph(20001, 150000, 4, seed=9)
+    n = g.number_of_nodes()
+    gidx.__dict__.pop("_rgcn_state", None)
+    et32 = et.int()
+    if prepare:
+        K.rgcn_prepare(gidx, et32, norm, 4, layers=prepare)
+    h, w = th.randn(n, 64, device=DEV), th.randn(4, 64, 64, device=DEV) / 4
+    lw, go = th.randn(64, 64, device=DEV) / 4, th.randn(n, 64, device=DEV)
+    gh, gw, gl = th.empty(n, 64, device=DEV), th.empty_like(w), th.empty_like(lw)
+    K.rgcn_layer1_backward_ex(gidx, et32, h, w, norm, lw, go, gh, gw, gl)
+    gw2, gl2 = th.full_like(w, float("nan")), th.full_like(lw, float("nan"))
+    K.rgcn_layer1_backward_ex(gidx, et32, h, w, norm, lw, go, None, gw2, gl2)
+    assert th.equal(gw, gw2) and th.equal(gl, gl2)
+    gidx.__dict__.pop("_rgcn_state", None)
