@@ -1437,12 +1437,14 @@ struct TypedOutCsr {
   }
 };
 
-void rgcn_common(const DGLMIGraph* g, const int32_t* etypes, int64_t rows_expanded) {
+// the graph's relation ids (DGLMIGraph.etypes) are what the entries group edges by
+void rgcn_common(const DGLMIGraph* g, int64_t rows_expanded) {
   check_graph32(g, "R-GCN");
   check_csr(g->in_csr, "in_csr", true);
   check_csr(g->out_csr, "out_csr", true);
   DGLMI_CHECK(g->in_csr.nnz == g->out_csr.nnz, "in/out CSR edge counts differ");
-  DGLMI_CHECK(g->in_csr.nnz == 0 || etypes != nullptr, "null etypes");
+  DGLMI_CHECK(g->in_csr.nnz == 0 || g->etypes != nullptr,
+              "the graph has no edge types (DGLMIGraph.etypes is NULL)");
   DGLMI_CHECK(rows_expanded < INT32_MAX, "relations x nodes exceeds int32 indexing");
 }
 
@@ -1451,12 +1453,11 @@ void check_fast_width(int64_t F) {
               "unsupported feature width " + std::to_string(F));
 }
 
-// The prepared state an entry may use (dglmi.h DGLMIRgcnState): built from these
-// etypes, for this relation count and source count, with the layer's bit set.
-const DGLMIRgcnState* rgcn_state(const DGLMIGraph* g, const int32_t* etypes, int64_t R,
-                                 int64_t n_src, int layer) {
+// The prepared state an entry may use (dglmi.h DGLMIRgcnState): built from the
+// graph's etypes, for this relation count and source count, with the layer's bit set.
+const DGLMIRgcnState* rgcn_state(const DGLMIGraph* g, int64_t R, int64_t n_src, int layer) {
   const DGLMIRgcnState* st = g->rgcn;
-  if (st == nullptr || st->etypes != etypes || st->num_rels != R || st->num_src != n_src ||
+  if (st == nullptr || st->etypes != g->etypes || st->num_rels != R || st->num_src != n_src ||
       st->nnz != g->in_csr.nnz || !((st->layers >> layer) & 1))
     return nullptr;
   return st;
@@ -1504,14 +1505,15 @@ DGLMICsr rgcn_out_walk(const DGLMIRgcnState* st, int layer, const float* norm, c
 
 extern "C" {
 
-int DGLMIRgcnLayer0(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* weight,
+int DGLMIRgcnLayer0(const DGLMIGraph* graph, const DGLMIArray* weight,
                     const DGLMIArray* norm, DGLMIArray* ret, void* stream) {
   API_BEGIN();
   check_array(weight, "weight");
   check_array(ret, "ret");
   DGLMI_CHECK(weight->ndim == 3, "weight must be (num_rels, num_src, F)");
   const int64_t R = weight->shape[0], N = weight->shape[1], F = weight->shape[2];
-  rgcn_common(graph, etypes, R * N);
+  rgcn_common(graph, R * N);
+  const int32_t* etypes = graph->etypes;
   const DGLMICsr& in = graph->in_csr;
   DGLMI_CHECK(in.num_cols == N, "weight rows must equal the number of source nodes");
   DGLMI_CHECK(ret->shape[0] == in.num_rows && feat_numel(ret) == F, "ret must be (num_dst, F)");
@@ -1520,7 +1522,7 @@ int DGLMIRgcnLayer0(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIA
   DeviceGuard guard(graph->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   DGLMIGraph z = no_workspace(), pg = plain_graph(graph);
-  if (const DGLMIRgcnState* st = rgcn_state(graph, etypes, R, N, 0)) {
+  if (const DGLMIRgcnState* st = rgcn_state(graph, R, N, 0)) {
     const float* w = nullptr;
     const DGLMICsr walk = rgcn_in_walk(graph, st, 0, R * N, norm->data, &w);
     run_fast(&pg, walk, FAST_COL_MUL_EDGE_BCAST, RED_SUM, weight->data, nullptr, w, nullptr,
@@ -1537,7 +1539,7 @@ int DGLMIRgcnLayer0(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIA
   API_END();
 }
 
-int DGLMIRgcnLayer0Backward(const DGLMIGraph* graph, const int32_t* etypes,
+int DGLMIRgcnLayer0Backward(const DGLMIGraph* graph,
                             const DGLMIArray* grad_out, const DGLMIArray* norm,
                             DGLMIArray* grad_weight, void* stream) {
   API_BEGIN();
@@ -1545,7 +1547,8 @@ int DGLMIRgcnLayer0Backward(const DGLMIGraph* graph, const int32_t* etypes,
   check_array(grad_weight, "grad_weight");
   DGLMI_CHECK(grad_weight->ndim == 3, "grad_weight must be (num_rels, num_src, F)");
   const int64_t R = grad_weight->shape[0], N = grad_weight->shape[1], F = grad_weight->shape[2];
-  rgcn_common(graph, etypes, R * N);
+  rgcn_common(graph, R * N);
+  const int32_t* etypes = graph->etypes;
   const DGLMICsr& out = graph->out_csr;
   DGLMI_CHECK(out.num_rows == N, "grad_weight rows must equal the number of source nodes");
   DGLMI_CHECK(grad_out->shape[0] == graph->in_csr.num_rows && feat_numel(grad_out) == F,
@@ -1559,7 +1562,7 @@ int DGLMIRgcnLayer0Backward(const DGLMIGraph* graph, const int32_t* etypes,
     launch_fill(grad_weight->data, R * N * F, 0.0f, s);
     return 0;
   }
-  if (const DGLMIRgcnState* st = rgcn_state(graph, etypes, R, N, 0)) {
+  if (const DGLMIRgcnState* st = rgcn_state(graph, R, N, 0)) {
     const float* w = nullptr;
     const DGLMICsr walk = rgcn_out_walk(st, 0, norm->data, &w);
     run_fast(&pg, walk, FAST_COL_MUL_EDGE_BCAST, RED_SUM, grad_out->data, nullptr, w, nullptr,
@@ -1581,7 +1584,7 @@ void check_loop_weight(const DGLMIArray* loop, int64_t K, int64_t X, const DGLMI
   DGLMI_CHECK(in.num_rows == in.num_cols, "a self-loop weight needs num_src == num_dst");
 }
 
-int rgcn_layer1_impl(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* hidden,
+int rgcn_layer1_impl(const DGLMIGraph* graph, const DGLMIArray* hidden,
                      const DGLMIArray* weight, const DGLMIArray* norm, const DGLMIArray* loop,
                      const DGLMIEpilogue* epi, DGLMIArray* ret, void* stream) {
   API_BEGIN();
@@ -1591,7 +1594,8 @@ int rgcn_layer1_impl(const DGLMIGraph* graph, const int32_t* etypes, const DGLMI
   DGLMI_CHECK(weight->ndim == 3, "weight must be (num_rels, F_in, F_out)");
   const int64_t R = weight->shape[0], K = weight->shape[1], X = weight->shape[2];
   const DGLMICsr& in = graph ? graph->in_csr : DGLMICsr{};
-  rgcn_common(graph, etypes, R * in.num_cols);
+  rgcn_common(graph, R * in.num_cols);
+  const int32_t* etypes = graph->etypes;
   DGLMI_CHECK(hidden->shape[0] == in.num_cols && feat_numel(hidden) == K,
               "hidden must be (num_src, F_in)");
   DGLMI_CHECK(ret->shape[0] == in.num_rows && feat_numel(ret) == X, "ret must be (num_dst, F_out)");
@@ -1608,7 +1612,7 @@ int rgcn_layer1_impl(const DGLMIGraph* graph, const int32_t* etypes, const DGLMI
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t N = in.num_cols, M = R * X;
   DGLMIGraph z = no_workspace(), pg = plain_graph(graph);
-  if (const DGLMIRgcnState* fs = rgcn_state(graph, etypes, R, N, 2)) {
+  if (const DGLMIRgcnState* fs = rgcn_state(graph, R, N, 2)) {
     if (rgcn_fused_ok(K, X, R + (loop != nullptr)) && aligned16(hidden->data) && in.nnz > 0) {
       const int32_t* eids = nullptr;
       const float* w = nullptr;
@@ -1620,7 +1624,7 @@ int rgcn_layer1_impl(const DGLMIGraph* graph, const int32_t* etypes, const DGLMI
       return 0;
     }
   }
-  const DGLMIRgcnState* st = rgcn_state(graph, etypes, R, N, 1);
+  const DGLMIRgcnState* st = rgcn_state(graph, R, N, 1);
   Scratch wcat(&z, K * M * 4, s), y(&z, N * M * 4, s), cols(&z, st ? 0 : in.nnz * 4, s);
   launch_permute_rkx(weight->data, R, K, X, true, static_cast<float*>(wcat.ptr), s);
   // y[u, r * X + x] = sum_k hidden[u, k] w[r, k, x]; row u * R + r of the (N R, X) view
@@ -1650,21 +1654,21 @@ int rgcn_layer1_impl(const DGLMIGraph* graph, const int32_t* etypes, const DGLMI
 }
 }  // namespace
 
-int DGLMIRgcnLayer1(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* hidden,
+int DGLMIRgcnLayer1(const DGLMIGraph* graph, const DGLMIArray* hidden,
                     const DGLMIArray* weight, const DGLMIArray* norm, DGLMIArray* ret,
                     void* stream) {
-  return rgcn_layer1_impl(graph, etypes, hidden, weight, norm, nullptr, nullptr, ret, stream);
+  return rgcn_layer1_impl(graph, hidden, weight, norm, nullptr, nullptr, ret, stream);
 }
 
-int DGLMIRgcnLayer1Ex(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* hidden,
+int DGLMIRgcnLayer1Ex(const DGLMIGraph* graph, const DGLMIArray* hidden,
                       const DGLMIArray* weight, const DGLMIArray* norm,
                       const DGLMIArray* loop_weight, const DGLMIEpilogue* epilogue,
                       DGLMIArray* ret, void* stream) {
-  return rgcn_layer1_impl(graph, etypes, hidden, weight, norm, loop_weight, epilogue, ret, stream);
+  return rgcn_layer1_impl(graph, hidden, weight, norm, loop_weight, epilogue, ret, stream);
 }
 
 namespace {
-int rgcn_layer1_backward_impl(const DGLMIGraph* graph, const int32_t* etypes,
+int rgcn_layer1_backward_impl(const DGLMIGraph* graph,
                               const DGLMIArray* hidden, const DGLMIArray* weight,
                               const DGLMIArray* norm, const DGLMIArray* loop,
                               const DGLMIArray* grad_out, DGLMIArray* grad_hidden,
@@ -1679,7 +1683,8 @@ int rgcn_layer1_backward_impl(const DGLMIGraph* graph, const int32_t* etypes,
   const int64_t R = weight->shape[0], K = weight->shape[1], X = weight->shape[2];
   for (int i = 0; i < 3; ++i) DGLMI_CHECK(grad_weight->shape[i] == weight->shape[i], "grad_weight shape");
   const DGLMICsr& out = graph ? graph->out_csr : DGLMICsr{};
-  rgcn_common(graph, etypes, R * out.num_rows);
+  rgcn_common(graph, R * out.num_rows);
+  const int32_t* etypes = graph->etypes;
   const int64_t N = out.num_rows, M = R * X;
   DGLMI_CHECK(hidden->shape[0] == N && feat_numel(hidden) == K, "hidden must be (num_src, F_in)");
   DGLMI_CHECK(!grad_hidden || (grad_hidden->shape[0] == N && feat_numel(grad_hidden) == K),
@@ -1696,7 +1701,7 @@ int rgcn_layer1_backward_impl(const DGLMIGraph* graph, const int32_t* etypes,
   DeviceGuard guard(graph->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   DGLMIGraph z = no_workspace(), pg = plain_graph(graph);
-  const DGLMIRgcnState* fs = out.nnz > 0 ? rgcn_state(graph, etypes, R, N, 2) : nullptr;
+  const DGLMIRgcnState* fs = out.nnz > 0 ? rgcn_state(graph, R, N, 2) : nullptr;
   const bool fused = fs && rgcn_fused_ok(X, K, R + (loop != nullptr)) &&
                      aligned16(grad_out->data) && fs->out_typed[0].indptr;
   // the fused walk also stores grad_out as gy's last block when there is a self-loop:
@@ -1744,7 +1749,7 @@ int rgcn_layer1_backward_impl(const DGLMIGraph* graph, const int32_t* etypes,
   Scratch wcat(&z, K * M * 4, s);
   launch_permute_rkx(weight->data, R, K, X, true, static_cast<float*>(wcat.ptr), s);
   // gy[u * R + t] = sum over out-edges of u with type t of norm_e * grad_out[v]
-  if (const DGLMIRgcnState* st = out.nnz > 0 ? rgcn_state(graph, etypes, R, N, 1) : nullptr) {
+  if (const DGLMIRgcnState* st = out.nnz > 0 ? rgcn_state(graph, R, N, 1) : nullptr) {
     const float* w = nullptr;
     const DGLMICsr walk = rgcn_out_walk(st, 1, norm->data, &w);
     run_fast(&pg, walk, FAST_COL_MUL_EDGE_BCAST, RED_SUM, grad_out->data, nullptr, w, nullptr,
@@ -1775,7 +1780,7 @@ int rgcn_layer1_backward_impl(const DGLMIGraph* graph, const int32_t* etypes,
 }
 }  // namespace
 
-int DGLMIRgcnLayer1Backward(const DGLMIGraph* graph, const int32_t* etypes,
+int DGLMIRgcnLayer1Backward(const DGLMIGraph* graph,
                             const DGLMIArray* hidden, const DGLMIArray* weight,
                             const DGLMIArray* norm, const DGLMIArray* grad_out,
                             DGLMIArray* grad_hidden, DGLMIArray* grad_weight, void* stream) {
@@ -1783,21 +1788,21 @@ int DGLMIRgcnLayer1Backward(const DGLMIGraph* graph, const int32_t* etypes,
     g_last_error = "grad_hidden is NULL";
     return -1;
   }
-  return rgcn_layer1_backward_impl(graph, etypes, hidden, weight, norm, nullptr, grad_out,
+  return rgcn_layer1_backward_impl(graph, hidden, weight, norm, nullptr, grad_out,
                                    grad_hidden, grad_weight, nullptr, stream);
 }
 
-int DGLMIRgcnLayer1BackwardEx(const DGLMIGraph* graph, const int32_t* etypes,
+int DGLMIRgcnLayer1BackwardEx(const DGLMIGraph* graph,
                               const DGLMIArray* hidden, const DGLMIArray* weight,
                               const DGLMIArray* norm, const DGLMIArray* loop_weight,
                               const DGLMIArray* grad_out, DGLMIArray* grad_hidden,
                               DGLMIArray* grad_weight, DGLMIArray* grad_loop_weight,
                               void* stream) {
-  return rgcn_layer1_backward_impl(graph, etypes, hidden, weight, norm, loop_weight, grad_out,
+  return rgcn_layer1_backward_impl(graph, hidden, weight, norm, loop_weight, grad_out,
                                    grad_hidden, grad_weight, grad_loop_weight, stream);
 }
 
-int DGLMIRgcnPrepare(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* norm,
+int DGLMIRgcnPrepare(const DGLMIGraph* graph, const DGLMIArray* norm,
                      int32_t num_rels, int32_t layers, DGLMIRgcnState* state, void* stream) {
   API_BEGIN();
   DGLMI_CHECK(state != nullptr, "null state");
@@ -1809,7 +1814,8 @@ int DGLMIRgcnPrepare(const DGLMIGraph* graph, const int32_t* etypes, const DGLMI
   const DGLMICsr& in = graph->in_csr;
   const DGLMICsr& out = graph->out_csr;
   const int64_t R = num_rels, N = in.num_cols, E = in.nnz;
-  rgcn_common(graph, etypes, R * N);
+  rgcn_common(graph, R * N);
+  const int32_t* etypes = graph->etypes;
   DGLMI_CHECK(out.num_rows == N, "out_csr rows != in_csr columns");
   if (norm != nullptr) edge_values(norm, E, "norm");
   DeviceGuard guard(graph->device);
@@ -1821,6 +1827,9 @@ int DGLMIRgcnPrepare(const DGLMIGraph* graph, const int32_t* etypes, const DGLMI
   // relation-major in-CSR
   const bool want0 = (layers & 1) || (layers & 4), want1 = (layers & 2) != 0;
   const bool want_rel = (layers & 4) != 0;
+  // the relation-major in-CSR keys etypes[e] * N_dst + v in int32
+  DGLMI_CHECK(!want_rel || R * in.num_rows < INT32_MAX,
+              "relations x destination nodes exceeds int32 indexing");
   const int nl = (want0 ? 1 : 0) + (want1 ? 1 : 0);
   const int64_t per_layer = e4 /*in cols*/ + ptr4 + 3 * e4 /*out idx, data, rows*/ +
                             (norm ? e4 : 0) /*out norm*/;
@@ -1909,6 +1918,30 @@ int DGLMIRgcnPrepare(const DGLMIGraph* graph, const int32_t* etypes, const DGLMI
   state->in_norm = in_norm;
   state->owner = own.p;
   own.p = nullptr;  // the state owns it now
+  API_END();
+}
+
+int DGLMIRgcnRefreshNorm(const DGLMIGraph* graph, const DGLMIArray* norm, DGLMIRgcnState* state,
+                         void* stream) {
+  API_BEGIN();
+  DGLMI_CHECK(state != nullptr && state->owner != nullptr, "state is not prepared");
+  DGLMI_CHECK(state->in_norm != nullptr, "the state was prepared without a norm");
+  check_graph32(graph, "R-GCN");
+  DGLMI_CHECK(graph->in_csr.nnz == state->nnz, "the graph is not the state's");
+  const int64_t E = state->nnz;
+  edge_values(norm, E, "norm");
+  DeviceGuard guard(graph->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // every cached copy is norm permuted into a walk's position order (edge ids = data)
+  launch_gather_f32(norm->data, graph->in_csr.data, E, const_cast<float*>(state->in_norm), s);
+  for (int layer = 0; layer < 2; ++layer)
+    if (state->out_norm[layer] != nullptr)
+      launch_gather_f32(norm->data, state->out_typed[layer].data, E,
+                        const_cast<float*>(state->out_norm[layer]), s);
+  if (state->in_rel_norm != nullptr)
+    launch_gather_f32(norm->data, state->in_rel.data, E, const_cast<float*>(state->in_rel_norm), s);
+  check_hip(hipGetLastError(), "rgcn refresh norm launch");
+  state->norm = norm->data;
   API_END();
 }
 

@@ -49,6 +49,7 @@ class Graph(ctypes.Structure):
         ("out_col_blocks", ctypes.c_void_p),
         ("rgcn", ctypes.c_void_p),
         ("gat_edge_pos", ctypes.c_void_p),
+        ("etypes", ctypes.c_void_p),
     ]
 
 
@@ -207,29 +208,31 @@ _SIGS = {
         ctypes.POINTER(Graph), ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_void_p,
         ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "DGLMIRgcnLayer0": (ctypes.c_int, [
-        ctypes.POINTER(Graph), ctypes.c_void_p, ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.c_void_p]),
     "DGLMIRgcnLayer0Backward": (ctypes.c_int, [
-        ctypes.POINTER(Graph), ctypes.c_void_p, ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.c_void_p]),
     "DGLMIRgcnLayer1": (ctypes.c_int, [
-        ctypes.POINTER(Graph), ctypes.c_void_p, ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.c_void_p]),
     "DGLMIRgcnLayer1Ex": (ctypes.c_int, [
-        ctypes.POINTER(Graph), ctypes.c_void_p, ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Epilogue),
         ctypes.POINTER(Array), ctypes.c_void_p]),
     "DGLMIRgcnLayer1BackwardEx": (ctypes.c_int, [
-        ctypes.POINTER(Graph), ctypes.c_void_p, ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.c_void_p]),
     "DGLMIRgcnLayer1Backward": (ctypes.c_int, [
-        ctypes.POINTER(Graph), ctypes.c_void_p, ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.c_void_p]),
     "DGLMIRgcnPrepare": (ctypes.c_int, [
-        ctypes.POINTER(Graph), ctypes.c_void_p, ctypes.POINTER(Array), ctypes.c_int32,
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.c_int32,
         ctypes.c_int32, ctypes.POINTER(RgcnState), ctypes.c_void_p]),
+    "DGLMIRgcnRefreshNorm": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(RgcnState), ctypes.c_void_p]),
     "DGLMIRgcnRelease": (ctypes.c_int, [ctypes.POINTER(RgcnState)]),
     "DGLMINbAccess": (ctypes.c_int, [
         ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.c_void_p, ctypes.c_void_p,

@@ -479,7 +479,7 @@ class _FusedRgcnLayer1(th.autograd.Function):
     @staticmethod
     def forward(ctx, gidx, et32, norm, x, w, loop_w, bias):
         ret = x.new_empty((gidx.num_dst, w.shape[2]))
-        K.rgcn_layer1_ex(gidx, et32, x, w, norm, ret, loop_weight=loop_w, bias=bias)
+        K.rgcn_layer1_ex(gidx, x, w, norm, ret, loop_weight=loop_w, bias=bias, etypes=et32)
         ctx.gidx, ctx.et32, ctx.norm = gidx, et32, norm
         ctx.has_bias = bias is not None
         ctx.save_for_backward(x, w, loop_w)
@@ -496,7 +496,8 @@ class _FusedRgcnLayer1(th.autograd.Function):
             gx = th.empty_like(x) if ctx.needs_input_grad[3] else None
             gw = th.empty_like(w)
             gl = th.empty_like(loop_w) if loop_w is not None and ctx.needs_input_grad[5] else None
-            K.rgcn_layer1_backward_ex(ctx.gidx, ctx.et32, x, w, ctx.norm, loop_w, g, gx, gw, gl)
+            K.rgcn_layer1_backward_ex(ctx.gidx, x, w, ctx.norm, loop_w, g, gx, gw, gl,
+                                      etypes=ctx.et32)
         if ctx.has_bias and ctx.needs_input_grad[6]:
             gb = g.sum(0)
         return None, None, None, gx, gw, gl, gb
@@ -507,8 +508,8 @@ def rgcn_fused_route(graph, x, weight_shape, norm, etypes, self_loop=False):
     fused layer-1 C entries both ways (64-float rows gathered forward and backward,
     the relation and self-loop weights in LDS; DGLMIRgcnLayer1Ex / BackwardEx with a
     prepared state), else None.  The state (``kernel.rgcn_prepare``, ~6 values per
-    edge) is built once per graph, device, etypes and norm, and rebuilt when either
-    tensor is written in place."""
+    edge) is built once per graph, device and etypes, and rebuilt when etypes is
+    written in place; a different or rewritten norm only re-gathers its cached copies."""
     R, fi, fo = weight_shape
     mats = R + int(bool(self_loop))
     if not (x.is_cuda and x.dtype == th.float32 and x.dim() == 2 and x.shape[1] == fi
@@ -523,8 +524,9 @@ def rgcn_fused_route(graph, x, weight_shape, norm, etypes, self_loop=False):
         return None
     if norm.numel() != graph.number_of_edges() or etypes.numel() != graph.number_of_edges():
         return None
-    key = (str(x.device), int(R), etypes.data_ptr(), etypes._version, norm.data_ptr(),
-           norm._version, int(etypes.numel()))
+    # the state depends on the relation ids only; a new or rewritten norm re-gathers
+    # its cached copies (kernel.RgcnState.sync_norm) instead of rebuilding
+    key = (str(x.device), int(R), etypes.data_ptr(), etypes._version, int(etypes.numel()))
     hit = gi.__dict__.get("_rgcn_fused")
     if hit is None or hit[0] != key:
         gidx = gi.get_immutable_gidx(x.device)
@@ -532,13 +534,13 @@ def rgcn_fused_route(graph, x, weight_shape, norm, etypes, self_loop=False):
         if et.numel() and (int(et.min()) < 0 or int(et.max()) >= R):
             raise DGLError("edge type out of range [0, %d)" % R)
         et32 = et.to(th.int32).contiguous()
-        nf = norm.reshape(-1).contiguous()
-        gi.__dict__["_rgcn_fused"] = None  # release the old state first (~2 GB on C5)
-        K.rgcn_prepare(gidx, et32, nf, R, layers=6)
-        # the cache holds the caller's tensors, so their addresses stay theirs
-        hit = (key, gidx, et32, nf, etypes, norm)
+        gi.__dict__.pop("_rgcn_fused", None)
+        # rgcn_prepare releases the graph's previous state before allocating (~2 GB on C5)
+        K.rgcn_prepare(gidx, norm.reshape(-1).contiguous(), R, layers=6, etypes=et32)
+        # the cache holds the caller's etypes, so its address stays theirs
+        hit = (key, gidx, et32, etypes)
         gi.__dict__["_rgcn_fused"] = hit
-    return hit[1], hit[2], hit[3]
+    return hit[1], hit[2], norm.reshape(-1).contiguous()
 
 
 def rgcn_fused_layer1(route, x, weight, loop_weight=None, bias=None):

@@ -92,6 +92,23 @@ class ImmutableGraphIndex:
         self._coo = None
         self._gather_cols = None
         self._col_blocks = {}
+        # relation id per edge id (int32 on the device) for the R-GCN entries, which
+        # read it from the graph like the reference (DGLMIGraph.etypes); None = untyped
+        self.etypes = None
+
+    def set_edge_types(self, etypes):
+        """Attach the relation id of every edge (int32-convertible, one per edge id)."""
+        if etypes is None:
+            self.etypes = None
+            return self
+        t = th.as_tensor(etypes).reshape(-1)
+        if t.numel() != self.in_csr.nnz:
+            raise DGLError("etypes needs one entry per edge (%d, got %d)"
+                           % (self.in_csr.nnz, t.numel()))
+        if t.numel() and int(t.min()) < 0:
+            raise DGLError("negative edge type")
+        self.etypes = t.to(device=self.in_csr.indices.device, dtype=th.int32).contiguous()
+        return self
 
     def number_of_edges(self):
         return self.in_csr.nnz
@@ -628,6 +645,9 @@ class GraphIndex:
             else:
                 self._cache[key] = self._upload(device)
             self._cache[key].eid_perm = self._eid_is_perm
+            et = self.edge_types() if self._eid_is_perm else None
+            if et is not None:  # add_edges_with_type: the graph carries its relations
+                self._cache[key].set_edge_types(th.from_numpy(et))
         return self._cache[key]
 
     def _upload(self, device):

@@ -396,12 +396,21 @@ def edge_softmax_backward(graph, out, grad_out, grad_logits):
 # --------------------------------------------------------------------------- #
 # the hack's extra kernels (kernel.py:156-169 of the reference)
 # --------------------------------------------------------------------------- #
-def _etypes(graph, etypes):
+def _etypes(graph, etypes=None):
+    """The relation ids a call uses: ``etypes`` when given, else the graph's own
+    (``graph.etypes``, from ``add_edges_with_type``), like the reference's kernels read
+    them from the graph object (``graph.cc:690-746``).  int32 on the graph device, one
+    entry per edge id."""
+    if etypes is None:
+        etypes = getattr(graph, "etypes", None)
+        if etypes is None:
+            raise DGLError("the graph has no edge types (add_edges_with_type) and no etypes "
+                           "were given")
     if not isinstance(etypes, th.Tensor) or etypes.dtype != th.int32 or etypes.device != graph.device:
         raise DGLError("etypes must be an int32 tensor on the graph device (one entry per edge id)")
     if etypes.numel() != graph.in_csr.nnz:
         raise DGLError("etypes needs one entry per edge")
-    return ctypes.c_void_p(etypes.contiguous().data_ptr())
+    return etypes if etypes.is_contiguous() else etypes.contiguous()
 
 
 def nb_access(graph, feat, node_map=None, deg_inc_node_map=None, times=15, warm_up_times=5):
@@ -417,88 +426,133 @@ def nb_access(graph, feat, node_map=None, deg_inc_node_map=None, times=15, warm_
 
 
 class RgcnState:
-    """A prepared DGLMIRgcnState (DGLMIRgcnPrepare) of one graph for one etypes /
-    norm pair: the relation-expanded in-CSR columns, the out-CSR regrouped by
-    (relation, source) and norm in both walks' position orders, built once on the
-    device.  It holds the two tensors, so their memory cannot be reused by another
-    tensor while the state lives, and is released with the object."""
+    """A prepared DGLMIRgcnState (DGLMIRgcnPrepare) of one graph for one set of edge
+    types: the relation-expanded in-CSR columns, the out-CSR regrouped by (relation,
+    source) and the edge weights in both walks' position orders, built once on the
+    device.  It holds the etypes and norm tensors, so their memory cannot be reused by
+    another tensor while the state lives.  A different or rewritten norm re-gathers
+    the cached copies (DGLMIRgcnRefreshNorm: three E-float gathers, no re-sort).
+    Released by ``release()`` or with the object."""
 
-    def __init__(self, graph, etypes, norm, num_rels, layers):
-        _etypes(graph, etypes)
+    live = 0  # states holding device memory (tests check a rebuild keeps one)
+
+    def __init__(self, graph, norm, num_rels, layers, etypes=None):
+        et = _etypes(graph, etypes)
         if norm is not None:
             _check_ctx(graph, [("norm", norm)])
-        self.etypes, self.norm = etypes, norm
-        self.versions = (etypes._version, None if norm is None else norm._version)
+        self.etypes, self.norm = et, norm
+        self.versions = (et._version, None if norm is None else norm._version)
         self.num_rels, self.layers = int(num_rels), int(layers)
         self.c = _ffi.RgcnState()
+        g = graph.cstruct()
+        g.etypes = et.data_ptr()
         check_call(_ffi.lib().DGLMIRgcnPrepare(
-            ctypes.byref(graph.cstruct()), ctypes.c_void_p(etypes.data_ptr()),
-            None if norm is None else _arr(norm, "norm"), self.num_rels, self.layers,
-            ctypes.byref(self.c), _stream(etypes)))
+            ctypes.byref(g), None if norm is None else _arr(norm, "norm"), self.num_rels,
+            self.layers, ctypes.byref(self.c), _stream(et)))
+        self._graph_struct = g  # for DGLMIRgcnRefreshNorm (pointers fixed for the graph's life)
         import weakref
-        self._fin = weakref.finalize(self, _ffi.lib().DGLMIRgcnRelease, ctypes.byref(self.c))
+        RgcnState.live += 1
+        self._fin = weakref.finalize(self, RgcnState._free, self.c)
 
-    def matches(self, etypes, norm, num_rels, layer):
-        """True when a call with these tensors may use the state (the C entries also
-        check pointers; this also catches in-place writes through the version counters)."""
-        if etypes is not self.etypes or etypes._version != self.versions[0]:
-            return False
-        if self.norm is not None and norm is self.norm and norm._version != self.versions[1]:
+    @staticmethod
+    def _free(c):
+        _ffi.lib().DGLMIRgcnRelease(ctypes.byref(c))
+        RgcnState.live -= 1
+
+    def release(self):
+        """Free the device memory now (DGLMIRgcnRelease)."""
+        self._fin()
+
+    def matches(self, etypes, num_rels, layer):
+        """True when a call over these relation ids may use the state (the C entries
+        compare pointers; the version counter also catches in-place writes, and views
+        of the same storage share it)."""
+        if not self._fin.alive or etypes.data_ptr() != self.etypes.data_ptr() \
+                or etypes.numel() != self.etypes.numel() or etypes._version != self.versions[0]:
             return False
         usable = (self.layers >> layer) & 1 or (layer == 1 and self.layers & 4)
         return int(num_rels) == self.num_rels and bool(usable)
 
+    def sync_norm(self, norm):
+        """Before a call with ``norm``: the C side streams the cached copies whenever the
+        pointer equals the cached one, so a rewritten (version changed) or new norm is
+        re-gathered first."""
+        if self.norm is None or norm is None:
+            return
+        if norm.data_ptr() == self.norm.data_ptr() and norm._version == self.versions[1]:
+            return
+        flat = norm.reshape(-1)
+        if not flat.is_contiguous() or flat.numel() != self.c.nnz:
+            return  # read by edge id (the pointer differs from the cached one)
+        g = self._graph_struct
+        check_call(_ffi.lib().DGLMIRgcnRefreshNorm(ctypes.byref(g), _arr(norm, "norm"),
+                                                   ctypes.byref(self.c), _stream(norm)))
+        self.norm = norm
+        self.versions = (self.versions[0], norm._version)
 
-def rgcn_prepare(graph, etypes, norm, num_rels, layers=7):
-    """DGLMIRgcnPrepare: build the R-GCN state of ``graph`` for ``etypes`` (int32,
-    one per edge id) and ``norm`` (one float per edge id, or None) once; later
-    rgcn_layer* calls on this graph with these same tensors use it (layers bit 0:
-    Layer0 and its backward, bit 1: Layer1 and its backward, bit 2: the fused
-    Layer1 kernels for 64-wide gathered rows -- equal to the unfused path up to fp32
-    rounding).  Writing into etypes or norm in place invalidates it (the next call
-    derives everything per call)."""
-    st = RgcnState(graph, etypes, norm, num_rels, layers)
+
+def rgcn_prepare(graph, norm, num_rels, layers=7, etypes=None):
+    """DGLMIRgcnPrepare: build the R-GCN state of ``graph`` for its edge types (or
+    ``etypes``: int32, one per edge id) and ``norm`` (one float per edge id, or None)
+    once; later rgcn_layer* calls on this graph over the same relation ids use it
+    (layers bit 0: Layer0 and its backward, bit 1: Layer1 and its backward, bit 2: the
+    fused Layer1 kernels for 64-wide gathered rows -- equal to the unfused path up to
+    fp32 rounding).  The graph's previous state is released first, so a rebuild never
+    holds two.  Writing into etypes in place invalidates the state (the next call
+    derives everything per call); a new or rewritten norm is re-gathered."""
+    old = graph.__dict__.pop("_rgcn_state", None)
+    if old is not None:
+        old.release()
+    st = RgcnState(graph, norm, num_rels, layers, etypes)
     graph.__dict__["_rgcn_state"] = st
     return st
 
 
 def _rgcn_cgraph(graph, etypes, norm, num_rels, layer):
+    """The DGLMIGraph of an R-GCN call: the graph's relation ids in ``etypes`` (the
+    reference's graph object carries them) and its prepared state when it applies."""
+    et = _etypes(graph, etypes)
     g = graph.cstruct()
+    g.etypes = et.data_ptr()
     st = graph.__dict__.get("_rgcn_state")
-    if st is not None and st.matches(etypes, norm, num_rels, layer):
+    if st is not None and st.matches(et, num_rels, layer):
+        st.sync_norm(norm)
         g.rgcn = ctypes.addressof(st.c)
-    return g
+    return g, et
 
 
-def rgcn_layer0(graph, etypes, weight, norm, ret):
-    """_CAPI_DGLRgcnLayer0: ret[v] = sum_e weight[etypes[e], u] * norm[e]."""
+def rgcn_layer0(graph, weight, norm, ret, etypes=None):
+    """_CAPI_DGLRgcnLayer0(G, weight, norm, ret) (kernel.py:159-160 of the reference):
+    ret[v] = sum_e weight[etypes[e], u] * norm[e], the relation ids from the graph."""
     _check_ctx(graph, [("weight", weight), ("norm", norm), ("ret", ret)])
+    g, et = _rgcn_cgraph(graph, etypes, norm, weight.shape[0], 0)
     check_call(_ffi.lib().DGLMIRgcnLayer0(
-        ctypes.byref(_rgcn_cgraph(graph, etypes, norm, weight.shape[0], 0)),
-        _etypes(graph, etypes), _arr(weight, "weight"),
-        _arr(norm, "norm"), _arr(ret, "ret"), _stream(ret)))
+        ctypes.byref(g), _arr(weight, "weight"), _arr(norm, "norm"), _arr(ret, "ret"),
+        _stream(ret)))
 
 
-def rgcn_layer0_backward(graph, etypes, grad_out, norm, grad_weight):
-    """_CAPI_DGLRgcnLayer0Backward (exact sums over repeated (source, relation) pairs)."""
+def rgcn_layer0_backward(graph, grad_out, norm, grad_weight, etypes=None):
+    """_CAPI_DGLRgcnLayer0Backward(G, grad_out, norm, grad_weight) (exact sums over
+    repeated (source, relation) pairs)."""
     _check_ctx(graph, [("grad_out", grad_out), ("norm", norm), ("grad_weight", grad_weight)])
+    g, et = _rgcn_cgraph(graph, etypes, norm, grad_weight.shape[0], 0)
     check_call(_ffi.lib().DGLMIRgcnLayer0Backward(
-        ctypes.byref(_rgcn_cgraph(graph, etypes, norm, grad_weight.shape[0], 0)),
-        _etypes(graph, etypes), _arr(grad_out, "grad_out"),
-        _arr(norm, "norm"), _arr(grad_weight, "grad_weight"), _stream(grad_out)))
+        ctypes.byref(g), _arr(grad_out, "grad_out"), _arr(norm, "norm"),
+        _arr(grad_weight, "grad_weight"), _stream(grad_out)))
 
 
-def rgcn_layer1(graph, etypes, hidden, weight, norm, ret):
-    """_CAPI_DGLRgcnLayer1: ret[v] = sum_e norm[e] * hidden[u] . weight[etypes[e]]."""
-    _check_ctx(graph, [("hidden", hidden), ("weight", weight), ("norm", norm), ("ret", ret)])
+def rgcn_layer1(graph, x, weight, norm, ret, etypes=None):
+    """_CAPI_DGLRgcnLayer1(G, hidden, weight, norm, ret):
+    ret[v] = sum_e norm[e] * x[u] . weight[etypes[e]]."""
+    _check_ctx(graph, [("hidden", x), ("weight", weight), ("norm", norm), ("ret", ret)])
+    g, et = _rgcn_cgraph(graph, etypes, norm, weight.shape[0], 1)
     check_call(_ffi.lib().DGLMIRgcnLayer1(
-        ctypes.byref(_rgcn_cgraph(graph, etypes, norm, weight.shape[0], 1)),
-        _etypes(graph, etypes), _arr(hidden, "hidden"),
-        _arr(weight, "weight"), _arr(norm, "norm"), _arr(ret, "ret"), _stream(ret)))
+        ctypes.byref(g), _arr(x, "hidden"), _arr(weight, "weight"), _arr(norm, "norm"),
+        _arr(ret, "ret"), _stream(ret)))
 
 
-def rgcn_layer1_ex(graph, etypes, hidden, weight, norm, ret, loop_weight=None, bias=None,
-                   addend=None):
+def rgcn_layer1_ex(graph, hidden, weight, norm, ret, loop_weight=None, bias=None,
+                   addend=None, etypes=None):
     """DGLMIRgcnLayer1Ex: rgcn_layer1 + hidden . loop_weight + bias (+ addend), RelGraphConv's
     self-loop and bias in the same pass (relgraphconv.py:186-190 order)."""
     _check_ctx(graph, [("hidden", hidden), ("weight", weight), ("norm", norm), ("ret", ret),
@@ -506,28 +560,27 @@ def rgcn_layer1_ex(graph, etypes, hidden, weight, norm, ret, loop_weight=None, b
     epi = _epilogue((None, None, bias, addend), ret)
     if epi is not None and epi.addend and epi.addend % 16:
         raise DGLError("epilogue addend must be 16-byte aligned")
+    g, et = _rgcn_cgraph(graph, etypes, norm, weight.shape[0], 1)
     check_call(_ffi.lib().DGLMIRgcnLayer1Ex(
-        ctypes.byref(_rgcn_cgraph(graph, etypes, norm, weight.shape[0], 1)),
-        _etypes(graph, etypes), _arr(hidden, "hidden"),
-        _arr(weight, "weight"), _arr(norm, "norm"), _arr(loop_weight, "loop_weight"),
-        None if epi is None else ctypes.byref(epi), _arr(ret, "ret"), _stream(ret)))
+        ctypes.byref(g), _arr(hidden, "hidden"), _arr(weight, "weight"), _arr(norm, "norm"),
+        _arr(loop_weight, "loop_weight"), None if epi is None else ctypes.byref(epi),
+        _arr(ret, "ret"), _stream(ret)))
 
 
-def rgcn_layer1_backward_ex(graph, etypes, hidden, weight, norm, loop_weight, grad_out,
-                            grad_hidden, grad_weight, grad_loop_weight=None):
+def rgcn_layer1_backward_ex(graph, hidden, weight, norm, loop_weight, grad_out,
+                            grad_hidden, grad_weight, grad_loop_weight=None, etypes=None):
     """DGLMIRgcnLayer1BackwardEx: rgcn_layer1_backward with the self-loop term in
     grad_hidden, and hidden^T . grad_out into grad_loop_weight (if given)."""
     _check_ctx(graph, [("hidden", hidden), ("weight", weight), ("norm", norm),
                        ("loop_weight", loop_weight), ("grad_out", grad_out),
                        ("grad_hidden", grad_hidden), ("grad_weight", grad_weight),
                        ("grad_loop_weight", grad_loop_weight)])
+    g, et = _rgcn_cgraph(graph, etypes, norm, weight.shape[0], 1)
     check_call(_ffi.lib().DGLMIRgcnLayer1BackwardEx(
-        ctypes.byref(_rgcn_cgraph(graph, etypes, norm, weight.shape[0], 1)),
-        _etypes(graph, etypes), _arr(hidden, "hidden"),
-        _arr(weight, "weight"), _arr(norm, "norm"), _arr(loop_weight, "loop_weight"),
-        _arr(grad_out, "grad_out"), _arr(grad_hidden, "grad_hidden"),
-        _arr(grad_weight, "grad_weight"), _arr(grad_loop_weight, "grad_loop_weight"),
-        _stream(grad_out)))
+        ctypes.byref(g), _arr(hidden, "hidden"), _arr(weight, "weight"), _arr(norm, "norm"),
+        _arr(loop_weight, "loop_weight"), _arr(grad_out, "grad_out"),
+        _arr(grad_hidden, "grad_hidden"), _arr(grad_weight, "grad_weight"),
+        _arr(grad_loop_weight, "grad_loop_weight"), _stream(grad_out)))
 
 
 def rgcn_fused_ok(gathered_w, out_w, num_rels):
@@ -540,14 +593,16 @@ def rgcn_fused_ok(gathered_w, out_w, num_rels):
     return num_rels * 64 * nb * 32 <= 20480
 
 
-def rgcn_layer1_backward(graph, etypes, hidden, weight, norm, grad_out, grad_hidden, grad_weight):
-    """_CAPI_DGLRgcnLayer1Backward: both gradients (the hack's wrapper drops the
-    weight gradient, tensor.py:493; it is returned here)."""
+def rgcn_layer1_backward(graph, hidden, weight, norm, grad_out, grad_hidden, grad_weight,
+                         etypes=None):
+    """_CAPI_DGLRgcnLayer1Backward(G, hidden, weight, norm, grad_out, grad_hidden,
+    grad_weight): both gradients (the hack's wrapper drops the weight gradient,
+    tensor.py:493; it is returned here)."""
     _check_ctx(graph, [("hidden", hidden), ("weight", weight), ("norm", norm),
                        ("grad_out", grad_out), ("grad_hidden", grad_hidden),
                        ("grad_weight", grad_weight)])
+    g, et = _rgcn_cgraph(graph, etypes, norm, weight.shape[0], 1)
     check_call(_ffi.lib().DGLMIRgcnLayer1Backward(
-        ctypes.byref(_rgcn_cgraph(graph, etypes, norm, weight.shape[0], 1)),
-        _etypes(graph, etypes), _arr(hidden, "hidden"),
-        _arr(weight, "weight"), _arr(norm, "norm"), _arr(grad_out, "grad_out"),
-        _arr(grad_hidden, "grad_hidden"), _arr(grad_weight, "grad_weight"), _stream(grad_out)))
+        ctypes.byref(g), _arr(hidden, "hidden"), _arr(weight, "weight"), _arr(norm, "norm"),
+        _arr(grad_out, "grad_out"), _arr(grad_hidden, "grad_hidden"),
+        _arr(grad_weight, "grad_weight"), _stream(grad_out)))

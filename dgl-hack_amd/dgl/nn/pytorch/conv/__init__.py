@@ -11,8 +11,5 @@ from .tagconv import TAGConv  # noqa: F401
 from .chebconv import ChebConv  # noqa: F401
 from .agnnconv import AGNNConv  # noqa: F401
 from .edgeconv import EdgeConv  # noqa: F401
-from .gmmconv import GMMConv  # noqa: F401
-from .nnconv import NNConv  # noqa: F401
 from .gatedgraphconv import GatedGraphConv  # noqa: F401
-from .cfconv import CFConv  # noqa: F401
 from .dense import DenseGraphConv, DenseSAGEConv, DenseChebConv  # noqa: F401

@@ -110,8 +110,8 @@ typedef struct {
   const DGLMICsr* in_col_blocks;
   const DGLMICsr* out_col_blocks;
   /* Optional per-graph R-GCN state (extension): built once by DGLMIRgcnPrepare and
-   * read by the DGLMIRgcnLayer* entries when it matches the call's etypes (and norm)
-   * pointers.  NULL = every call derives what it needs from etypes / norm. */
+   * read by the DGLMIRgcnLayer* entries when it matches the graph's etypes (and the
+   * call's norm) pointers.  NULL = every call derives what it needs from etypes / norm. */
   const struct DGLMIRgcnState* rgcn;
   /* Optional (extension): for every in-CSR position p, the out-CSR position of the
    * same edge.  When present and the fused GAT backward runs unblocked (no column
@@ -120,6 +120,13 @@ typedef struct {
    * in-CSR (a 256-B feature row and a logit gathered per edge become one H-float
    * term; C3 unblocked 11.98 -> 9.57 ms).  NULL = the destination-side walk. */
   const int32_t* gat_edge_pos;
+  /* Optional relation id of every edge (the hack's typed edges: Graph::AddEdgesWithType
+   * stores them in the graph object and the R-GCN kernels read them from there through
+   * GetCsrSortedByEdgeType, src/graph/graph.cc:690-746, binary_reduce_impl.cu:951,1020,
+   * 1128,1208).  One int32 per edge id, each in [0, num_rels) where num_rels is the
+   * weight's leading dimension.  Read only by the DGLMIRgcn* entries, which therefore
+   * keep the reference's argument lists.  NULL for untyped graphs. */
+  const int32_t* etypes;
 } DGLMIGraph;
 
 /* A contiguous row-major fp32 device array (NDArray / DLTensor subset). */
@@ -325,10 +332,12 @@ int DGLMIEdgeSoftmaxBackward(const DGLMIGraph* graph, const DGLMIArray* out,
 
 /* ---- the hack's R-GCN layer kernels and neighbour-access benchmark -------------
  * (_CAPI_DGLRgcnLayer0 / 0Backward / 1 / 1Backward / _CAPI_DGLNbAccess,
- * binary_reduce.cc:398-450; kernels binary_reduce_impl.cu:779-1250).  The
- * reference reads the relation of every edge from its graph object
- * (GetCsrSortedByEdgeType); here it is the device int32 array `etypes`, one entry
- * per edge id, each in [0, num_rels).  norm: one float per edge id ((E) or (E, 1)).
+ * binary_reduce.cc:398-450; kernels binary_reduce_impl.cu:779-1250).  Same argument
+ * lists as the reference's PackedFuncs (plus the stream): like the reference, which
+ * reads the relation of every edge from its graph object (GetCsrSortedByEdgeType),
+ * the entries read it from the graph, DGLMIGraph.etypes (device int32, one entry per
+ * edge id, each in [0, num_rels); required when the graph has edges).
+ * norm: one float per edge id ((E) or (E, 1)).
  * Every output is overwritten.  Relation transforms run as one dense product over
  * the node rows and every edge only gathers (the hack multiplies per edge).  The
  * hack's Layer0Backward overwrites repeated (source, relation) pairs
@@ -339,9 +348,8 @@ int DGLMIEdgeSoftmaxBackward(const DGLMIGraph* graph, const DGLMIArray* out,
  * GetCsrSortedByEdgeType, graph.cc:690-746).  Without it every Layer* call
  * gathers the relation of each edge by edge id, gathers norm by edge id and
  * re-sorts the out-CSR by (source, relation).  DGLMIRgcnPrepare builds, on the
- * device and once, for the relations `etypes` (one int32 per edge id, in
- * [0, num_rels)) and the edge weights `norm` (one float per edge id; NULL = none
- * cached):
+ * device and once, for the graph's relations (graph->etypes) and the edge weights
+ * `norm` (one float per edge id; NULL = none cached):
  *   layers bit 0 (Layer0 / Layer0Backward): the in-CSR columns etypes[e] * N_src + u
  *     and the out-CSR regrouped by that key;
  *   layers bit 1 (Layer1 / Layer1Backward): the in-CSR columns u * R + etypes[e]
@@ -353,15 +361,16 @@ int DGLMIEdgeSoftmaxBackward(const DGLMIGraph* graph, const DGLMIArray* out,
  *     relation's rows and multiply by W_t in one pass (64-wide gathered rows, outputs
  *     <= 128 wide); results then match the unfused path to fp32 rounding, not bit for bit.
  * Set DGLMIGraph.rgcn to the state; an entry uses it when graph->rgcn->etypes ==
- * etypes, num_rels and the source count match and the layer's bit is set, and
+ * graph->etypes, num_rels and the source count match and the layer's bit is set, and
  * uses the cached norm copies only when norm->data == graph->rgcn->norm -- a caller
- * that changes the VALUES behind those pointers must prepare again.  Results are
- * bit-identical with and without the state.  The memory (about 6 int32/float per
+ * that changes the VALUES behind those pointers must prepare again, or re-gather the
+ * norm copies with DGLMIRgcnRefreshNorm (any other norm is read by edge id).  Results
+ * are bit-identical with and without the state.  The memory (about 6 int32/float per
  * edge per layer) is the library's until DGLMIRgcnRelease.  Stream-ordered;
  * DGLMIRgcnRelease synchronises the device. */
 typedef struct DGLMIRgcnState {
-  const int32_t* etypes;    /* the etypes pointer the state was built from */
-  const float* norm;        /* the norm pointer it was built from, or NULL */
+  const int32_t* etypes;    /* the graph->etypes pointer the state was built from */
+  const float* norm;        /* the norm pointer of the cached copies, or NULL */
   int32_t num_rels;
   int32_t layers;
   int64_t num_src;
@@ -375,24 +384,31 @@ typedef struct DGLMIRgcnState {
   const float* in_rel_norm;    /* norm per position of in_rel */
   void* owner;                 /* library-private */
 } DGLMIRgcnState;
-int DGLMIRgcnPrepare(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* norm,
-                     int32_t num_rels, int32_t layers, DGLMIRgcnState* state, void* stream);
+int DGLMIRgcnPrepare(const DGLMIGraph* graph, const DGLMIArray* norm, int32_t num_rels,
+                     int32_t layers, DGLMIRgcnState* state, void* stream);
+/* Re-gathers a state's cached norm copies from `norm` (one float per edge id of the
+ * graph the state was prepared on; the state must have been prepared with a norm) and
+ * makes norm->data the cached pointer: a new or rewritten edge-weight tensor costs
+ * three E-float gathers instead of a new Prepare (no sorts, no allocation). */
+int DGLMIRgcnRefreshNorm(const DGLMIGraph* graph, const DGLMIArray* norm, DGLMIRgcnState* state,
+                         void* stream);
 int DGLMIRgcnRelease(DGLMIRgcnState* state);
 
-/* _CAPI_DGLRgcnLayer0: ret[v, :] = sum_{e=(u->v)} weight[etypes[e], u, :] * norm[e];
+/* _CAPI_DGLRgcnLayer0(G, weight, norm, ret):
+ * ret[v, :] = sum_{e=(u->v)} weight[etypes[e], u, :] * norm[e];
  * weight (R, N_src, F), ret (N_dst, F). */
-int DGLMIRgcnLayer0(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* weight,
-                    const DGLMIArray* norm, DGLMIArray* ret, void* stream);
-/* _CAPI_DGLRgcnLayer0Backward: grad_weight[t, u, :] = sum over the edges e of
- * relation t out of u of grad_out[v, :] * norm[e]; grad_weight (R, N_src, F). */
-int DGLMIRgcnLayer0Backward(const DGLMIGraph* graph, const int32_t* etypes,
-                            const DGLMIArray* grad_out, const DGLMIArray* norm,
-                            DGLMIArray* grad_weight, void* stream);
-/* _CAPI_DGLRgcnLayer1: ret[v, :] = sum_e norm[e] * hidden[u, :] . weight[etypes[e]];
+int DGLMIRgcnLayer0(const DGLMIGraph* graph, const DGLMIArray* weight, const DGLMIArray* norm,
+                    DGLMIArray* ret, void* stream);
+/* _CAPI_DGLRgcnLayer0Backward(G, grad_out, norm, grad_weight):
+ * grad_weight[t, u, :] = sum over the edges e of relation t out of u of
+ * grad_out[v, :] * norm[e]; grad_weight (R, N_src, F). */
+int DGLMIRgcnLayer0Backward(const DGLMIGraph* graph, const DGLMIArray* grad_out,
+                            const DGLMIArray* norm, DGLMIArray* grad_weight, void* stream);
+/* _CAPI_DGLRgcnLayer1(G, hidden, weight, norm, ret):
+ * ret[v, :] = sum_e norm[e] * hidden[u, :] . weight[etypes[e]];
  * hidden (N_src, F_in), weight (R, F_in, F_out), ret (N_dst, F_out). */
-int DGLMIRgcnLayer1(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* hidden,
-                    const DGLMIArray* weight, const DGLMIArray* norm, DGLMIArray* ret,
-                    void* stream);
+int DGLMIRgcnLayer1(const DGLMIGraph* graph, const DGLMIArray* hidden, const DGLMIArray* weight,
+                    const DGLMIArray* norm, DGLMIArray* ret, void* stream);
 /* Extension (no reference counterpart): DGLMIRgcnLayer1 with RelGraphConv's self-loop
  * and bias, ret[v] = agg[v] + bias + hidden[v] . loop_weight (+ epilogue->addend[v]),
  * in the order of relgraphconv.py:186-190 (python/dgl/nn/pytorch/conv/relgraphconv.py),
@@ -401,27 +417,27 @@ int DGLMIRgcnLayer1(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIA
  * or NULL, square graphs only; epilogue->bias has F_out floats, epilogue->addend the
  * shape of ret (not aliasing it); row_mul / row_div must be NULL.  NULL loop_weight and
  * epilogue give DGLMIRgcnLayer1. */
-int DGLMIRgcnLayer1Ex(const DGLMIGraph* graph, const int32_t* etypes, const DGLMIArray* hidden,
+int DGLMIRgcnLayer1Ex(const DGLMIGraph* graph, const DGLMIArray* hidden,
                       const DGLMIArray* weight, const DGLMIArray* norm,
                       const DGLMIArray* loop_weight, const DGLMIEpilogue* epilogue,
                       DGLMIArray* ret, void* stream);
-/* _CAPI_DGLRgcnLayer1Backward: grad_hidden[u] = sum_{e out of u} norm[e] * grad_out[v]
- * . weight[t]^T; grad_weight[t] = sum_{e of relation t} norm[e] hidden[u]^T grad_out[v]. */
-int DGLMIRgcnLayer1Backward(const DGLMIGraph* graph, const int32_t* etypes,
-                            const DGLMIArray* hidden, const DGLMIArray* weight,
-                            const DGLMIArray* norm, const DGLMIArray* grad_out,
-                            DGLMIArray* grad_hidden, DGLMIArray* grad_weight, void* stream);
+/* _CAPI_DGLRgcnLayer1Backward(G, hidden, weight, norm, grad_out, grad_hidden, grad_weight):
+ * grad_hidden[u] = sum_{e out of u} norm[e] * grad_out[v] . weight[t]^T;
+ * grad_weight[t] = sum_{e of relation t} norm[e] hidden[u]^T grad_out[v]. */
+int DGLMIRgcnLayer1Backward(const DGLMIGraph* graph, const DGLMIArray* hidden,
+                            const DGLMIArray* weight, const DGLMIArray* norm,
+                            const DGLMIArray* grad_out, DGLMIArray* grad_hidden,
+                            DGLMIArray* grad_weight, void* stream);
 /* Extension: DGLMIRgcnLayer1Backward of DGLMIRgcnLayer1Ex's self-loop as well:
  * grad_hidden also gets grad_out . loop_weight^T, and grad_loop_weight (F_in, F_out; may
  * be NULL) = hidden^T . grad_out.  grad_hidden may be NULL when the input gradient is
  * not wanted (the fused walk then skips its MFMA passes).  NULL loop_weight gives
  * DGLMIRgcnLayer1Backward. */
-int DGLMIRgcnLayer1BackwardEx(const DGLMIGraph* graph, const int32_t* etypes,
-                              const DGLMIArray* hidden, const DGLMIArray* weight,
-                              const DGLMIArray* norm, const DGLMIArray* loop_weight,
-                              const DGLMIArray* grad_out, DGLMIArray* grad_hidden,
-                              DGLMIArray* grad_weight, DGLMIArray* grad_loop_weight,
-                              void* stream);
+int DGLMIRgcnLayer1BackwardEx(const DGLMIGraph* graph, const DGLMIArray* hidden,
+                              const DGLMIArray* weight, const DGLMIArray* norm,
+                              const DGLMIArray* loop_weight, const DGLMIArray* grad_out,
+                              DGLMIArray* grad_hidden, DGLMIArray* grad_weight,
+                              DGLMIArray* grad_loop_weight, void* stream);
 /* _CAPI_DGLNbAccess: the in-neighbour gather benchmark.  Runs `times` in-neighbour
  * row gathers of feat over the in-CSR (the load-balanced copy_u sum, into scratch;
  * the reference's timed kernels read rows without using them) and writes the mean

@@ -174,6 +174,39 @@ def c3(dev, steps, warmup):
             "fused_fwd_Gedges_s": m / ms_ff / 1e6, "fused_fwd_bwd_Gedges_s": m / ms_ffb / 1e6}
 
 
+def verify_rgcn_fused(conv, g, x, et, norm):
+    """The fused R-GCN route vs the GEMM + typed-gather route, once, before any C5
+    time is taken: output (rtol = atol = 1e-4) and the input and every parameter
+    gradient (|a - b| <= 1e-3 + 1e-4 max|b|: long fp32 sums in two orders).  Raises,
+    so a wrong fast kernel cannot print a time."""
+    gen = th.Generator(device=x.device)
+    gen.manual_seed(11)
+    params = [x] + list(conv.parameters())
+    res = {}
+    for fused in (True, False):
+        conv.use_fused = fused
+        out = conv(g, x, et, norm)
+        if fused and g._graph.__dict__.get("_rgcn_fused") is None:
+            raise AssertionError("C5: the fused route did not run")
+        go = th.randn(out.shape, device=x.device, generator=gen) if fused else go
+        res[fused] = (out.detach(), th.autograd.grad(out, params, go))
+        del out
+    conv.use_fused = True
+    (fo, fg), (uo, ug) = res[True], res[False]
+    if not th.allclose(fo, uo, rtol=1e-4, atol=1e-4):
+        raise AssertionError("C5: fused output differs from the unfused route by %.3g"
+                             % float((fo - uo).abs().max()))
+    worst = 0.0
+    for a, b in zip(fg, ug):
+        bound = 1e-3 + 1e-4 * float(b.abs().max())
+        err = float((a - b).abs().max())
+        worst = max(worst, err / bound)
+        if err > bound:
+            raise AssertionError("C5: fused gradient differs by %.3g (bound %.3g)" % (err, bound))
+    return {"fused_vs_unfused_checked": True, "out_max_abs_diff": float((fo - uo).abs().max()),
+            "grad_worst_err_over_bound": worst}
+
+
 def c5(dev, steps, warmup):
     n, m, R, f = 5_000_000, 80_000_000, 4, 64
     g = chung_lu(n, m, 0.5, 8, dev)
@@ -185,6 +218,7 @@ def c5(dev, steps, warmup):
     norm = (1.0 / indeg)[dst.long()].reshape(m, 1)
     x = th.randn(n, f, device=dev, requires_grad=True)
     conv = RelGraphConv(f, f, R, "basis", num_bases=R, self_loop=True).to(dev)
+    check = verify_rgcn_fused(conv, g, x, et, norm)
 
     def fwd_bwd():
         conv(g, x, et, norm).sum().backward()
@@ -209,7 +243,8 @@ def c5(dev, steps, warmup):
             "layer_fwd_ms": ms_f, "layer_fwd_bwd_ms": ms_fb, "fused_route": fused,
             "gemm_gather_fwd_ms": ms_f_u, "gemm_gather_fwd_bwd_ms": ms_fb_u,
             "typed_gather_ms": ms_g,
-            "typed_gather_alg_GBps": alg / ms_g / 1e6, "typed_gather_Gedges_s": m / ms_g / 1e6}
+            "typed_gather_alg_GBps": alg / ms_g / 1e6, "typed_gather_Gedges_s": m / ms_g / 1e6,
+            "check": check}
 
 
 def sd(dev, steps, warmup):

@@ -59,12 +59,12 @@ def main():
            "graph": "chung-lu alpha 0.5" if "--chung-lu" in sys.argv else "uniform random"}
     if "--capi-only" in sys.argv:  # for rocprofv3 kernel statistics
         if "--prepared" in sys.argv:
-            K.rgcn_prepare(gidx, et32, norm, R, layers=2)
+            K.rgcn_prepare(gidx, norm, R, layers=2, etypes=et32)
         if "--fused" in sys.argv:
-            K.rgcn_prepare(gidx, et32, norm, R, layers=4)
+            K.rgcn_prepare(gidx, norm, R, layers=4, etypes=et32)
         for _ in range(3):
-            K.rgcn_layer1(gidx, et32, h, W, norm, ret)
-            K.rgcn_layer1_backward(gidx, et32, h, W, norm, go, gh, gw)
+            K.rgcn_layer1(gidx, h, W, norm, ret, etypes=et32)
+            K.rgcn_layer1_backward(gidx, h, W, norm, go, gh, gw, etypes=et32)
         th.cuda.synchronize()
         return
     res["python_fwd_ms"] = ktime(lambda: conv(g, h, et, norm))
@@ -74,34 +74,34 @@ def main():
         out = conv(g, hr, et, norm)
         out.backward(go)
     res["python_fwd_bwd_ms"] = ktime(py_fb)
-    res["capi_layer1_ms"] = ktime(lambda: K.rgcn_layer1(gidx, et32, h, W, norm, ret))
+    res["capi_layer1_ms"] = ktime(lambda: K.rgcn_layer1(gidx, h, W, norm, ret, etypes=et32))
     res["capi_layer1_backward_ms"] = ktime(
-        lambda: K.rgcn_layer1_backward(gidx, et32, h, W, norm, go, gh, gw))
+        lambda: K.rgcn_layer1_backward(gidx, h, W, norm, go, gh, gw, etypes=et32))
     w0 = th.randn(R, n, 16, device=dev)
     r0 = th.empty(n, 16, device=dev)
     gw0 = th.empty_like(w0)
-    res["capi_layer0_F16_ms"] = ktime(lambda: K.rgcn_layer0(gidx, et32, w0, norm, r0))
-    res["capi_layer0_F16_backward_ms"] = ktime(lambda: K.rgcn_layer0_backward(gidx, et32, r0, norm, gw0))
+    res["capi_layer0_F16_ms"] = ktime(lambda: K.rgcn_layer0(gidx, w0, norm, r0, etypes=et32))
+    res["capi_layer0_F16_backward_ms"] = ktime(lambda: K.rgcn_layer0_backward(gidx, r0, norm, gw0, etypes=et32))
     ref = (ret.clone(), gh.clone(), gw.clone(), r0.clone(), gw0.clone())
     th.cuda.synchronize()
     t0 = __import__("time").time()
-    K.rgcn_prepare(gidx, et32, norm, R, layers=3)
+    K.rgcn_prepare(gidx, norm, R, layers=3, etypes=et32)
     th.cuda.synchronize()
     res["prepare_s"] = __import__("time").time() - t0
-    res["prepared_layer1_ms"] = ktime(lambda: K.rgcn_layer1(gidx, et32, h, W, norm, ret))
+    res["prepared_layer1_ms"] = ktime(lambda: K.rgcn_layer1(gidx, h, W, norm, ret, etypes=et32))
     res["prepared_layer1_backward_ms"] = ktime(
-        lambda: K.rgcn_layer1_backward(gidx, et32, h, W, norm, go, gh, gw))
+        lambda: K.rgcn_layer1_backward(gidx, h, W, norm, go, gh, gw, etypes=et32))
     res["prepared_layer1_fwd_bwd_ms"] = res["prepared_layer1_ms"] + res["prepared_layer1_backward_ms"]
-    res["prepared_layer0_F16_ms"] = ktime(lambda: K.rgcn_layer0(gidx, et32, w0, norm, r0))
+    res["prepared_layer0_F16_ms"] = ktime(lambda: K.rgcn_layer0(gidx, w0, norm, r0, etypes=et32))
     res["prepared_layer0_F16_backward_ms"] = ktime(
-        lambda: K.rgcn_layer0_backward(gidx, et32, r0, norm, gw0))
+        lambda: K.rgcn_layer0_backward(gidx, r0, norm, gw0, etypes=et32))
     res["prepared_bit_identical"] = all(bool(th.equal(a, b)) for a, b in
                                         zip(ref, (ret, gh, gw, r0, gw0)))
     # fused layer-1 kernels (state bit 2): aggregate per relation, then W_t, in one pass
-    K.rgcn_prepare(gidx, et32, norm, R, layers=7)
-    res["fused_layer1_ms"] = ktime(lambda: K.rgcn_layer1(gidx, et32, h, W, norm, ret))
+    K.rgcn_prepare(gidx, norm, R, layers=7, etypes=et32)
+    res["fused_layer1_ms"] = ktime(lambda: K.rgcn_layer1(gidx, h, W, norm, ret, etypes=et32))
     res["fused_layer1_backward_ms"] = ktime(
-        lambda: K.rgcn_layer1_backward(gidx, et32, h, W, norm, go, gh, gw))
+        lambda: K.rgcn_layer1_backward(gidx, h, W, norm, go, gh, gw, etypes=et32))
     res["fused_layer1_fwd_bwd_ms"] = res["fused_layer1_ms"] + res["fused_layer1_backward_ms"]
     rel = lambda a, b: float((a - b).abs().max() / b.abs().max().clamp(min=1e-30))
     res["fused_max_rel_diff_vs_unfused"] = max(rel(ret, ref[0]), rel(gh, ref[1]), rel(gw, ref[2]))

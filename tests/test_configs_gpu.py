@@ -165,11 +165,47 @@ def test_c4_rmat_copy_u_sum_and_partition():
     assert st["cut_edges"] < ct["cut_edges"] and sum(st["halo_rows"]) < sum(ct["halo_rows"])
 
 
-def test_c5_rgcn_python_path_vs_c_entry():
-    """C5: R-GCN layer (4 relations, 64 -> 64, per-edge norm 1 / in-degree) on
-    5 M nodes / 80 M typed edges: RelGraphConv's path (one hipBLASLt GEMM + the
-    typed gather) vs DGLMIRgcnLayer1 (the library's own GEMM + gather), forward
-    and input gradient, plus 256 sampled rows in fp64."""
+def _sample_out_rows(gidx, rows):
+    """(segment id, destination id, edge id) of the out-edges of `rows`, out-CSR order."""
+    ip = gidx.out_csr.indptr.long()
+    beg, end = ip[rows], ip[rows + 1]
+    lens = end - beg
+    seg = th.repeat_interleave(th.arange(rows.numel(), device=DEV), lens)
+    pos = th.repeat_interleave(beg - th.cumsum(lens, 0) + lens, lens) + \
+        th.arange(int(lens.sum()), device=DEV)
+    return seg, gidx.out_csr.indices.long()[pos], gidx.out_csr.data.long()[pos]
+
+
+def _typed_rows(a, t, W, transpose=False):
+    """Row i of the result is a[i] @ W[t[i]] (or @ W[t[i]]^T): one GEMM per relation,
+    never an (E, F, F) tensor of per-edge weights."""
+    out = th.zeros(a.shape[0], W.shape[1] if transpose else W.shape[2], dtype=a.dtype,
+                   device=a.device)
+    for r in range(W.shape[0]):
+        sel = t == r
+        out[sel] = a[sel] @ (W[r].t() if transpose else W[r])
+    return out
+
+
+def _rows_with_hubs(deg, k_hub, k_rand, n):
+    """The k_hub highest-degree rows (hub rows span many work shares) + random rows."""
+    return th.cat([th.topk(deg, k_hub).indices, th.randint(0, n, (k_rand,), device=DEV)])
+
+
+def test_c5_rgcn_fused_route_full_size():
+    """C5 at full size (5 M nodes / 80 M typed edges, 4 relations, 64 -> 64, self-loop
+    and bias, norm = 1 / in-degree) -- the configuration the bench's C5 line times.
+
+    (1) RelGraphConv on the fused route (DGLMIRgcnLayer1Ex / BackwardEx with the prepared
+    state: tile queues over ~156 K row tiles, ordered per-group carries, hub rows spanning
+    many shares) vs the GEMM + typed-gather route: output, input gradient and every
+    parameter gradient.
+    (2) The C entries on a prepared state (layers 4 and 6) vs the restatement of the
+    hack's layer-1 formula (oracle/hack_ref.c: ret[v] = sum_e norm_e h[u] W[t_e], plus
+    RelGraphConv's bias and self-loop; binary_reduce_impl.cu:1082-1194) in fp64: 256
+    destination rows (the 32 largest in-degrees among them) for the output, 256 source
+    rows (the 32 largest out-degrees) for the input gradient, and the whole relation and
+    self-loop weight gradients.  Bounds scale with the absolute mass of each sum."""
     import dgl
     from dgl import kernel as K
     from dgl.nn.pytorch import RelGraphConv
@@ -179,26 +215,87 @@ def test_c5_rgcn_python_path_vs_c_entry():
     gen.manual_seed(8)
     et = th.randint(0, R, (m,), device=DEV, generator=gen)
     g = dgl.DGLGraph.from_device_coo(src, dst, n)
-    norm = (1.0 / th.bincount(dst.long(), minlength=n).clamp(min=1).float())[dst.long()].view(-1, 1)
-    conv = RelGraphConv(64, 64, R, "basis", num_bases=R, bias=False).to(DEV)
-    conv.use_fused = False  # the GEMM + typed-gather path, against the C entries
+    indeg = th.bincount(dst.long(), minlength=n)
+    outdeg = th.bincount(src.long(), minlength=n)
+    norm = (1.0 / indeg.clamp(min=1).float())[dst.long()].view(-1, 1)
+    del src, dst
+    th.manual_seed(0)
+    conv = RelGraphConv(64, 64, R, "basis", num_bases=R, self_loop=True).to(DEV)
+    with th.no_grad():
+        conv.h_bias.uniform_(-1, 1)
     h = th.randn(n, 64, device=DEV, requires_grad=True)
-    out = conv(g, h, et, norm)
-    go = th.randn_like(out)
-    out.backward(go)
+    go = th.randn(n, 64, device=DEV)
+    params = [h] + list(conv.parameters())
+    res = {}
+    for fused in (True, False):
+        conv.use_fused = fused
+        out = conv(g, h, et, norm)
+        if fused:
+            assert g._graph.__dict__.get("_rgcn_fused") is not None  # the fused route ran
+        res[fused] = (out.detach(), th.autograd.grad(out, params, go))
+        del out
+    th.testing.assert_close(res[True][0], res[False][0], rtol=1e-4, atol=1e-4)
+    for a, b in zip(res[True][1], res[False][1]):  # long fp32 sums in two orders
+        assert (a - b).abs().max().item() <= 1e-3 + 1e-4 * b.abs().max().item()
+    del res
+    g._graph.__dict__.pop("_rgcn_fused", None)
+    # (2) the C entries on prepared state vs the fp64 formula
     gidx = g._graph.get_immutable_gidx(DEV)
+    gidx.__dict__.pop("_rgcn_state", None)
+    et32 = et.int()
+    hd = h.detach()
     Wr = conv._relation_weights().detach().contiguous()
-    ret = th.empty(n, 64, device=DEV)
-    K.rgcn_layer1(gidx, et.int(), h.detach(), Wr, norm, ret)
-    th.testing.assert_close(out.detach(), ret, rtol=1e-4, atol=1e-4)
-    gh = th.empty(n, 64, device=DEV)
-    gw = th.empty_like(Wr)
-    K.rgcn_layer1_backward(gidx, et.int(), h.detach(), Wr, norm, go, gh, gw)
-    th.testing.assert_close(h.grad, gh, rtol=1e-4, atol=1e-4)
-    rows = th.randint(0, n, (256,), device=DEV)
+    lw = conv.loop_weight.detach().contiguous()
+    bias = conv.h_bias.detach().contiguous()
+    nf = norm.reshape(-1).contiguous()
+    rows = _rows_with_hubs(indeg, 32, 224, n)
     seg, us, es = _sample_rows(gidx, rows)
-    msg = th.einsum("ek,ekx->ex", h.detach()[us].double(), Wr.double()[et[es]]) * \
-        norm[es].double()
-    ref = th.zeros(256, 64, dtype=th.float64, device=DEV).index_add_(0, seg, msg)
-    mass = th.zeros(256, 64, dtype=th.float64, device=DEV).index_add_(0, seg, msg.abs())
-    assert ((ret[rows].double() - ref).abs() <= 1e-5 + 1e-5 * mass).all()
+    W64 = Wr.double()
+    nu = nf[es, None].double()
+    msg = _typed_rows(hd[us].double(), et[es], W64) * nu
+    amsg = _typed_rows(hd[us].double().abs(), et[es], W64.abs()) * nu
+    ref = th.zeros(256, 64, dtype=th.float64, device=DEV).index_add_(0, seg, msg) + \
+        hd[rows].double() @ lw.double() + bias.double()
+    mass = th.zeros(256, 64, dtype=th.float64, device=DEV).index_add_(0, seg, amsg) + \
+        hd[rows].double().abs() @ lw.double().abs() + bias.double().abs()
+    srows = _rows_with_hubs(outdeg, 32, 224, n)
+    sseg, vs, ses = _sample_out_rows(gidx, srows)
+    gmsg = go[vs].double() * nf[ses, None].double()
+    gh_ref = th.zeros(256, 64, dtype=th.float64, device=DEV).index_add_(
+        0, sseg, _typed_rows(gmsg, et[ses], W64, True)) + go[srows].double() @ lw.double().t()
+    gh_mass = th.zeros(256, 64, dtype=th.float64, device=DEV).index_add_(
+        0, sseg, _typed_rows(gmsg.abs(), et[ses], W64.abs(), True)) + \
+        go[srows].double().abs() @ lw.double().abs().t()
+    # the whole weight gradients in fp64: gW[t] = sum_{e of t} norm_e h[u]^T go[v], chunked
+    ic = gidx.in_csr
+    gw_ref = th.zeros(R, 64, 64, dtype=th.float64, device=DEV)
+    gw_mass = th.zeros_like(gw_ref)
+    for lo in range(0, m, 1 << 22):
+        u = ic.indices[lo:lo + (1 << 22)].long()
+        v = ic.rows[lo:lo + (1 << 22)].long()
+        e = ic.data[lo:lo + (1 << 22)].long()
+        t = et[e]
+        a, b = hd[u].double(), go[v].double() * nf[e, None].double()
+        for r in range(R):
+            sel = t == r
+            gw_ref[r] += a[sel].t() @ b[sel]
+            gw_mass[r] += a[sel].abs().t() @ b[sel].abs()
+        del u, v, e, t, a, b
+    gl_ref = hd.double().t() @ go.double()
+    gl_mass = hd.double().abs().t() @ go.double().abs()
+    for layers in (4, 6):
+        K.rgcn_prepare(gidx, nf, R, layers=layers, etypes=et32)
+        ret = th.full((n, 64), float("nan"), device=DEV)
+        K.rgcn_layer1_ex(gidx, hd, Wr, nf, ret, loop_weight=lw, bias=bias, etypes=et32)
+        assert ((ret[rows].double() - ref).abs() <= 1e-5 + 1e-5 * mass).all(), layers
+        assert not th.isnan(ret).any()
+        del ret
+        gh = th.full((n, 64), float("nan"), device=DEV)
+        gw, gl = th.full_like(Wr, float("nan")), th.full_like(lw, float("nan"))
+        K.rgcn_layer1_backward_ex(gidx, hd, Wr, nf, lw, go, gh, gw, gl, etypes=et32)
+        assert ((gh[srows].double() - gh_ref).abs() <= 1e-5 + 1e-5 * gh_mass).all(), layers
+        assert not th.isnan(gh).any()
+        del gh
+        assert ((gw.double() - gw_ref).abs() <= 2e-4 + 1e-6 * gw_mass).all(), layers
+        assert ((gl.double() - gl_ref).abs() <= 2e-4 + 1e-6 * gl_mass).all(), layers
+    gidx.__dict__.pop("_rgcn_state").release()

@@ -34,10 +34,8 @@ def test_graph_from_scipy():
     (lambda: nn.TAGConv(5, 2, k=2), {"lin.weight": (2, 15)}),
     (lambda: nn.ChebConv(5, 2, 3), {"fc.2.weight": (2, 5), "bias": (2,)}),
     (lambda: nn.EdgeConv(5, 2), {"theta.weight": (2, 5), "phi.weight": (2, 5)}),
-    (lambda: nn.GMMConv(5, 10, 3, 4), {"mu": (4, 3), "inv_sigma": (4, 3), "fc.weight": (40, 5)}),
     (lambda: nn.GatedGraphConv(5, 10, 5, 3), {"linears.2.weight": (10, 10),
                                               "gru.weight_ih": (30, 10)}),
-    (lambda: nn.CFConv(2, 3, 2, 3), {"project_node.weight": (2, 2)}),
     (lambda: nn.AGNNConv(1), {"beta": (1,)}),
 ])
 def test_module_parameters(ctor, params):
@@ -47,9 +45,7 @@ def test_module_parameters(ctor, params):
 
 
 def test_bad_aggregators():
-    for ctor in (lambda: nn.SAGEConv(5, 10, "median"), lambda: nn.GINConv(None, "prod"),
-                 lambda: nn.GMMConv(5, 10, 3, 4, "min"),
-                 lambda: nn.NNConv(5, 10, None, "min")):
+    for ctor in (lambda: nn.SAGEConv(5, 10, "median"), lambda: nn.GINConv(None, "prod")):
         with pytest.raises(KeyError):
             ctor()
 

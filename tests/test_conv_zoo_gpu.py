@@ -1,5 +1,5 @@
 """The remaining dgl.nn.pytorch conv modules (SAGE, GIN, SG, APPNP, TAG, Cheb,
-AGNN, EdgeConv, GMM, NN, GatedGraph, CF) on the HIP path.
+AGNN, EdgeConv, GatedGraph) on the HIP path.
 
 Each module is checked three ways: against a dense float64 restatement of the
 reference's formula (its forward in ``python/dgl/nn/pytorch/conv/*.py``),
@@ -365,80 +365,6 @@ def test_edge_conv_reference_cases():
     assert bn(g, th.randn(20, 5, device=DEV)).shape == (20, 2)
 
 
-# ---------------------------------------------------------------------- GMM / NN
-@pytest.mark.parametrize("aggre", ["sum", "mean", "max"])
-def test_gmm_conv_dense(aggre):
-    g = _rand_graph(self_loops=True)
-    th.manual_seed(0)
-    conv = nn.GMMConv(5, 10, 3, 4, aggre, residual=True).to(DEV)
-    x = th.randn(g.number_of_nodes(), 5, device=DEV)
-    pseudo = th.randn(g.number_of_edges(), 3, device=DEV)
-    out = conv(g, x, pseudo)
-    s, d = _edges(g)
-    s, d = s.to(DEV), d.to(DEV)
-    h = (x.double() @ conv.fc.weight.detach().double().t()).view(-1, 4, 10)
-    mu, isg = conv.mu.detach().double(), conv.inv_sigma.detach().double()
-    gs = (-0.5 * (pseudo.double()[:, None, :] - mu[None]) ** 2 * isg[None] ** 2).sum(-1)
-    m = h[s] * th.exp(gs)[:, :, None]  # (E, K, out)
-    n = g.number_of_nodes()
-    if aggre == "max":
-        agg = th.full((n, 4, 10), -np.inf, dtype=th.float64, device=DEV).scatter_reduce(
-            0, d[:, None, None].expand_as(m), m, "amax")
-    else:
-        agg = th.zeros(n, 4, 10, dtype=th.float64, device=DEV).index_add_(0, d, m)
-        if aggre == "mean":
-            agg = agg / th.bincount(d, minlength=n).clamp(min=1).double()[:, None, None]
-    want = agg.sum(1) + x.double() @ conv.res_fc.weight.detach().double().t() \
-        + conv.bias.detach().double()
-    assert th.allclose(out.double(), want, **TOL)
-
-
-def test_gmm_nn_reference_shapes():
-    """test_nn.py:532-595 (mean aggregator, homogeneous and bipartite)."""
-    g = dgl.DGLGraph(sp.sparse.random(100, 100, density=0.1), readonly=True)
-    gmm = nn.GMMConv(5, 10, 3, 4, "mean").to(DEV)
-    assert gmm(g, th.randn(100, 5, device=DEV),
-               th.randn(g.number_of_edges(), 3, device=DEV)).shape[-1] == 10
-    gb = dgl.bipartite(sp.sparse.random(100, 50, density=0.1))
-    gmm = nn.GMMConv((5, 2), 10, 3, 4, "mean").to(DEV)
-    assert gmm(gb, (th.randn(100, 5, device=DEV), th.randn(50, 2, device=DEV)),
-               th.randn(gb.number_of_edges(), 3, device=DEV)).shape[-1] == 10
-    nnc = nn.NNConv(5, 10, th.nn.Linear(4, 50), "mean").to(DEV)
-    assert nnc(g, th.randn(100, 5, device=DEV),
-               th.randn(g.number_of_edges(), 4, device=DEV)).shape[-1] == 10
-    gb = dgl.bipartite(sp.sparse.random(50, 100, density=0.1))
-    nnc = nn.NNConv((5, 2), 10, th.nn.Linear(4, 50), "mean").to(DEV)
-    assert nnc(gb, (th.randn(50, 5, device=DEV), th.randn(100, 2, device=DEV)),
-               th.randn(gb.number_of_edges(), 4, device=DEV)).shape[-1] == 10
-
-
-@pytest.mark.parametrize("aggre", ["sum", "mean", "max"])
-def test_nn_conv_dense(aggre):
-    g = _rand_graph(n=120, m=900, self_loops=True)
-    th.manual_seed(0)
-    conv = nn.NNConv(5, 7, th.nn.Linear(3, 35), aggre, residual=True).to(DEV)
-    th.nn.init.normal_(conv.bias)
-    x = th.randn(120, 5, device=DEV, requires_grad=True)
-    ef = th.randn(g.number_of_edges(), 3, device=DEV)
-    out = conv(g, x, ef)
-    out.sum().backward()
-    s, d = _edges(g)
-    s, d = s.to(DEV), d.to(DEV)
-    w = _lin64(conv.edge_nn, ef.double()).view(-1, 5, 7)
-    m = x.detach().double()[s][:, :, None] * w
-    if aggre == "max":
-        agg = th.full((120, 5, 7), -np.inf, dtype=th.float64, device=DEV).scatter_reduce(
-            0, d[:, None, None].expand_as(m), m, "amax")
-    else:
-        agg = th.zeros(120, 5, 7, dtype=th.float64, device=DEV).index_add_(0, d, m)
-        if aggre == "mean":
-            agg = agg / th.bincount(d, minlength=120).clamp(min=1).double()[:, None, None]
-    want = agg.sum(1) + x.detach().double() @ conv.res_fc.weight.detach().double().t() \
-        + conv.bias.detach().double()
-    assert th.allclose(out.double(), want, **TOL)
-    assert x.grad is not None and conv.edge_nn.weight.grad is not None
-
-
 # ------------------------------------------------------------------ GatedGraph
 def test_gated_graph_conv_fused_dense():
     g = _rand_graph(n=150, m=1200, seed=2)
@@ -467,24 +393,6 @@ def test_gated_graph_reference_shape():
     conv = nn.GatedGraphConv(5, 10, 5, 3).to(DEV)
     etypes = (th.arange(g.number_of_edges()) % 3).to(DEV)
     assert conv(g, th.randn(100, 5, device=DEV), etypes).shape[-1] == 10
-
-
-# ------------------------------------------------------------------------- CF
-def test_cf_conv_dense():
-    """test_nn.py:733-747 plus the u_mul_e_sum value."""
-    g = dgl.DGLGraph(sp.sparse.random(100, 100, density=0.1, random_state=9), readonly=True)
-    th.manual_seed(0)
-    conv = nn.CFConv(node_in_feats=2, edge_in_feats=3, hidden_feats=2, out_feats=3).to(DEV)
-    nf = th.randn(100, 2, device=DEV)
-    ef = th.randn(g.number_of_edges(), 3, device=DEV)
-    out = conv(g, nf, ef)
-    assert out.shape[-1] == 3
-    s, d = _edges(g)
-    hv = conv.project_node(nf).double()
-    he = conv.project_edge(ef).double()
-    agg = th.zeros(100, 2, dtype=th.float64, device=DEV).index_add_(0, d.to(DEV), hv[s.to(DEV)] * he)
-    want = conv.project_out(agg.float()).double()
-    assert th.allclose(out.double(), want.detach(), **TOL)
 
 
 def test_builtins_only_reach_hip():

@@ -41,7 +41,7 @@ def test_rgcn_layer0_fwd_bwd(F, hub):
     n = g.number_of_nodes()
     w = th.randn(R, n, F, device=DEV)
     ret = th.full((n, F), float("nan"), device=DEV)
-    K.rgcn_layer0(gidx, et.int(), w, norm, ret)
+    K.rgcn_layer0(gidx, w, norm, ret, etypes=et.int())
     ref = th.zeros(n, F, dtype=th.float64, device=DEV).index_add_(
         0, d, w.double()[et, s] * norm.double())
     mass = th.zeros(n, F, dtype=th.float64, device=DEV).index_add_(
@@ -49,7 +49,7 @@ def test_rgcn_layer0_fwd_bwd(F, hub):
     assert ((ret.double() - ref).abs() <= 1e-5 + 1e-6 * mass).all()
     go = th.randn(n, F, device=DEV)
     gw = th.full((R, n, F), float("nan"), device=DEV)
-    K.rgcn_layer0_backward(gidx, et.int(), go, norm, gw)
+    K.rgcn_layer0_backward(gidx, go, norm, gw, etypes=et.int())
     gref = th.zeros(R * n, F, dtype=th.float64, device=DEV).index_add_(
         0, et * n + s, go.double()[d] * norm.double()).view(R, n, F)
     th.testing.assert_close(gw.double(), gref, rtol=1e-5, atol=1e-5)
@@ -93,12 +93,12 @@ def _layer1_fwd_bwd(K_in, X, hub, n, m, R=4, prepare=0, cached_norm=True):
     gidx.__dict__.pop("_rgcn_state", None)
     et32 = et.int()
     if prepare:
-        K.rgcn_prepare(gidx, et32, norm if cached_norm else None, R, layers=prepare)
-        assert gidx._rgcn_state.matches(et32, norm, R, 1)
+        K.rgcn_prepare(gidx, norm if cached_norm else None, R, layers=prepare, etypes=et32)
+        assert gidx._rgcn_state.matches(et32, R, 1)
     h = th.randn(n, K_in, device=DEV)
     w = th.randn(R, K_in, X, device=DEV) / 4
     ret = th.full((n, X), float("nan"), device=DEV)
-    K.rgcn_layer1(gidx, et32, h, w, norm, ret)
+    K.rgcn_layer1(gidx, h, w, norm, ret, etypes=et32)
     msg = th.einsum("ek,ekx->ex", h.double()[s], w.double()[et]) * norm.double()
     ref = th.zeros(n, X, dtype=th.float64, device=DEV).index_add_(0, d, msg)
     mass = th.zeros(n, X, dtype=th.float64, device=DEV).index_add_(0, d, msg.abs())
@@ -106,7 +106,7 @@ def _layer1_fwd_bwd(K_in, X, hub, n, m, R=4, prepare=0, cached_norm=True):
     go = th.randn(n, X, device=DEV)
     gh = th.full((n, K_in), float("nan"), device=DEV)
     gw = th.full((R, K_in, X), float("nan"), device=DEV)
-    K.rgcn_layer1_backward(gidx, et32, h, w, norm, go, gh, gw)
+    K.rgcn_layer1_backward(gidx, h, w, norm, go, gh, gw, etypes=et32)
     gidx.__dict__.pop("_rgcn_state", None)
     gmsg = go.double()[d] * norm.double()                        # (E, X)
     gh_ref = th.zeros(n, K_in, dtype=th.float64, device=DEV).index_add_(
@@ -144,7 +144,7 @@ def test_rgcn_gemm_split_k_large_n():
     go = th.randn(n, X, device=DEV)
     gh = th.empty(n, K_in, device=DEV)
     gw = th.empty(R, K_in, X, device=DEV)
-    K.rgcn_layer1_backward(gidx, et.int(), h, w, norm, go, gh, gw)
+    K.rgcn_layer1_backward(gidx, h, w, norm, go, gh, gw, etypes=et.int())
     gmsg = go.double()[d] * norm.double()
     gw_ref = th.zeros(R, K_in, X, dtype=th.float64, device=DEV).index_add_(
         0, et, th.einsum("ek,ex->ekx", h.double()[s], gmsg))
@@ -158,11 +158,13 @@ def test_rgcn_rejects_bad_arguments():
     w = th.randn(2, 100, 8, device=DEV)
     ret = th.empty(100, 8, device=DEV)
     with pytest.raises(DGLError, match="etypes"):
-        K.rgcn_layer0(gidx, et[:10].int(), w, norm, ret)
+        K.rgcn_layer0(gidx, w, norm, ret, etypes=et[:10].int())
     with pytest.raises(DGLError, match="norm"):
-        K.rgcn_layer0(gidx, et.int(), w, norm[:10], ret)
+        K.rgcn_layer0(gidx, w, norm[:10], ret, etypes=et.int())
     with pytest.raises(DGLError, match="source nodes"):
-        K.rgcn_layer0(gidx, et.int(), th.randn(2, 50, 8, device=DEV), norm, ret)
+        K.rgcn_layer0(gidx, th.randn(2, 50, 8, device=DEV), norm, ret, etypes=et.int())
+    with pytest.raises(DGLError, match="edge types"):  # an untyped graph, no etypes given
+        K.rgcn_layer0(gidx, w, norm, ret)
 
 
 def test_nb_access_times_the_gather():
@@ -182,8 +184,8 @@ def _layer_calls(K, gidx, et32, norm, n, R, layer, seed):
         go = th.randn(n, F, device=DEV, generator=gen)
         ret = th.empty(n, F, device=DEV)
         gw = th.empty(R, n, F, device=DEV)
-        K.rgcn_layer0(gidx, et32, w, norm, ret)
-        K.rgcn_layer0_backward(gidx, et32, go, norm, gw)
+        K.rgcn_layer0(gidx, w, norm, ret, etypes=et32)
+        K.rgcn_layer0_backward(gidx, go, norm, gw, etypes=et32)
         return ret, gw
     K_in, X = 32, 16
     h = th.randn(n, K_in, device=DEV, generator=gen)
@@ -191,8 +193,8 @@ def _layer_calls(K, gidx, et32, norm, n, R, layer, seed):
     go = th.randn(n, X, device=DEV, generator=gen)
     ret = th.empty(n, X, device=DEV)
     gh, gw = th.empty(n, K_in, device=DEV), th.empty(R, K_in, X, device=DEV)
-    K.rgcn_layer1(gidx, et32, h, w, norm, ret)
-    K.rgcn_layer1_backward(gidx, et32, h, w, norm, go, gh, gw)
+    K.rgcn_layer1(gidx, h, w, norm, ret, etypes=et32)
+    K.rgcn_layer1_backward(gidx, h, w, norm, go, gh, gw, etypes=et32)
     return ret, gh, gw
 
 
@@ -200,15 +202,15 @@ def _layer_calls(K, gidx, et32, norm, n, R, layer, seed):
 def test_rgcn_prepared_state_bit_identical(layer):
     """DGLMIRgcnPrepare (relation-expanded columns, typed out-CSR and norm in
     position order built once per graph): every entry returns the same bits as the
-    stateless call; a different norm tensor reuses the columns but gathers its own
-    norm; an in-place write into the cached norm stops the state from being used."""
+    stateless call; a different norm tensor, or an in-place write into the cached one,
+    re-gathers the cached copies (DGLMIRgcnRefreshNorm) and keeps the same bits."""
     from dgl import kernel as K
     g, gidx, s, d, et, norm = _graph(700, 9000, 4, seed=21 + layer, hub=True)
     n, R = g.number_of_nodes(), 4
     et32 = et.int()
     gidx.__dict__.pop("_rgcn_state", None)
     plain = _layer_calls(K, gidx, et32, norm, n, R, layer, seed=5)
-    st = K.rgcn_prepare(gidx, et32, norm, R, layers=1 << layer)
+    st = K.rgcn_prepare(gidx, norm, R, layers=1 << layer, etypes=et32)
     assert st.c.owner and st.c.nnz == len(s)
     prepared = _layer_calls(K, gidx, et32, norm, n, R, layer, seed=5)
     for a, b in zip(plain, prepared):
@@ -219,13 +221,17 @@ def test_rgcn_prepared_state_bit_identical(layer):
     gidx.__dict__["_rgcn_state"] = st
     for a, b in zip(plain2, _layer_calls(K, gidx, et32, norm2, n, R, layer, seed=6)):
         assert th.equal(a, b)
-    norm.mul_(3.0)  # in place: the cached copy is stale, the call must not use it
+    assert st.norm is norm2  # re-gathered, not rebuilt
+    norm2.mul_(3.0)  # in place: the cached copy is stale and must be re-gathered
     gidx.__dict__.pop("_rgcn_state")
-    plain3 = _layer_calls(K, gidx, et32, norm, n, R, layer, seed=7)
+    plain3 = _layer_calls(K, gidx, et32, norm2, n, R, layer, seed=7)
     gidx.__dict__["_rgcn_state"] = st
-    assert not st.matches(et32, norm, R, layer)
-    for a, b in zip(plain3, _layer_calls(K, gidx, et32, norm, n, R, layer, seed=7)):
+    assert st.matches(et32, R, layer)
+    for a, b in zip(plain3, _layer_calls(K, gidx, et32, norm2, n, R, layer, seed=7)):
         assert th.equal(a, b)
+    assert st.versions[1] == norm2._version
+    # other relation ids (another tensor) do not match the state
+    assert not st.matches(et32.clone(), R, layer)
     gidx.__dict__.pop("_rgcn_state")
 
 
@@ -234,11 +240,11 @@ def test_rgcn_prepare_rejects_bad_arguments():
     from dgl._ffi import DGLError
     g, gidx, s, d, et, norm = _graph(100, 500, 2, seed=1)
     with pytest.raises(DGLError, match="layers"):
-        K.RgcnState(gidx, et.int(), norm, 2, 8)
+        K.RgcnState(gidx, norm, 2, 8, etypes=et.int())
     with pytest.raises(DGLError, match="norm"):
-        K.RgcnState(gidx, et.int(), norm[:10], 2, 3)
+        K.RgcnState(gidx, norm[:10], 2, 3, etypes=et.int())
     with pytest.raises(DGLError, match="etypes"):
-        K.RgcnState(gidx, et.int()[:10], norm, 2, 3)
+        K.RgcnState(gidx, norm, 2, 3, etypes=et.int()[:10])
 
 
 @pytest.mark.parametrize("K_in,X,R,prepare,hub", [(64, 64, 4, 6, True), (64, 32, 3, 6, False),
@@ -254,7 +260,7 @@ def test_rgcn_layer1_ex_self_loop(K_in, X, R, prepare, hub):
     gidx.__dict__.pop("_rgcn_state", None)
     et32 = et.int()
     if prepare:
-        K.rgcn_prepare(gidx, et32, norm, R, layers=prepare)
+        K.rgcn_prepare(gidx, norm, R, layers=prepare, etypes=et32)
     h = th.randn(n, K_in, device=DEV)
     w = th.randn(R, K_in, X, device=DEV) / 4
     lw = th.randn(K_in, X, device=DEV) / 4
@@ -267,14 +273,15 @@ def test_rgcn_layer1_ex_self_loop(K_in, X, R, prepare, hub):
     lmass = h.double().abs() @ lw.double().abs()
     for addend in (None, add):
         ret = th.full((n, X), float("nan"), device=DEV)
-        K.rgcn_layer1_ex(gidx, et32, h, w, norm, ret, loop_weight=lw, bias=bias, addend=addend)
+        K.rgcn_layer1_ex(gidx, h, w, norm, ret, loop_weight=lw, bias=bias, addend=addend,
+                         etypes=et32)
         ref = agg + bias.double() + loop + (0 if addend is None else addend.double())
         assert ((ret.double() - ref).abs() <= 1e-4 + 1e-5 * (mass + lmass)).all()
     go = th.randn(n, X, device=DEV)
     gh = th.full((n, K_in), float("nan"), device=DEV)
     gw = th.full((R, K_in, X), float("nan"), device=DEV)
     gl = th.full((K_in, X), float("nan"), device=DEV)
-    K.rgcn_layer1_backward_ex(gidx, et32, h, w, norm, lw, go, gh, gw, gl)
+    K.rgcn_layer1_backward_ex(gidx, h, w, norm, lw, go, gh, gw, gl, etypes=et32)
     gmsg = go.double()[d] * norm.double()
     gh_ref = th.zeros(n, K_in, dtype=th.float64, device=DEV).index_add_(
         0, s, th.einsum("ex,ekx->ek", gmsg, w.double()[et])) + go.double() @ lw.double().t()
@@ -292,8 +299,8 @@ def test_rgcn_layer1_ex_self_loop(K_in, X, R, prepare, hub):
     assert ((gl.double() - gl_ref).abs() <= 2e-4 + 1e-6 * gl_mass).all()
     # no loop weight: the plain entries' results
     ret0, ret1 = th.empty(n, X, device=DEV), th.empty(n, X, device=DEV)
-    K.rgcn_layer1(gidx, et32, h, w, norm, ret0)
-    K.rgcn_layer1_ex(gidx, et32, h, w, norm, ret1)
+    K.rgcn_layer1(gidx, h, w, norm, ret0, etypes=et32)
+    K.rgcn_layer1_ex(gidx, h, w, norm, ret1, etypes=et32)
     assert th.equal(ret0, ret1)
     gidx.__dict__.pop("_rgcn_state", None)
 
@@ -307,11 +314,12 @@ def test_rgcn_layer1_ex_rejects_bad_arguments():
     h, w = th.randn(n, 16, device=DEV), th.randn(2, 16, 8, device=DEV)
     ret = th.empty(n, 8, device=DEV)
     with pytest.raises(DGLError, match="loop_weight"):
-        K.rgcn_layer1_ex(gidx, et32, h, w, norm, ret, loop_weight=th.randn(8, 16, device=DEV))
+        K.rgcn_layer1_ex(gidx, h, w, norm, ret, loop_weight=th.randn(8, 16, device=DEV),
+                         etypes=et32)
     with pytest.raises(DGLError, match="grad_loop_weight needs loop_weight"):
-        K.rgcn_layer1_backward_ex(gidx, et32, h, w, norm, None, th.randn(n, 8, device=DEV),
+        K.rgcn_layer1_backward_ex(gidx, h, w, norm, None, th.randn(n, 8, device=DEV),
                                   th.empty(n, 16, device=DEV), th.empty_like(w),
-                                  th.empty(16, 8, device=DEV))
+                                  th.empty(16, 8, device=DEV), etypes=et32)
 
 
 @pytest.mark.parametrize("n,m", [(500, 4000), (1700, 20000), (33, 300)])
@@ -331,12 +339,12 @@ def test_rgcn_layer1_backward_ex_without_grad_hidden(prepare):
     gidx.__dict__.pop("_rgcn_state", None)
     et32 = et.int()
     if prepare:
-        K.rgcn_prepare(gidx, et32, norm, 4, layers=prepare)
+        K.rgcn_prepare(gidx, norm, 4, layers=prepare, etypes=et32)
     h, w = th.randn(n, 64, device=DEV), th.randn(4, 64, 64, device=DEV) / 4
     lw, go = th.randn(64, 64, device=DEV) / 4, th.randn(n, 64, device=DEV)
     gh, gw, gl = th.empty(n, 64, device=DEV), th.empty_like(w), th.empty_like(lw)
-    K.rgcn_layer1_backward_ex(gidx, et32, h, w, norm, lw, go, gh, gw, gl)
+    K.rgcn_layer1_backward_ex(gidx, h, w, norm, lw, go, gh, gw, gl, etypes=et32)
     gw2, gl2 = th.full_like(w, float("nan")), th.full_like(lw, float("nan"))
-    K.rgcn_layer1_backward_ex(gidx, et32, h, w, norm, lw, go, None, gw2, gl2)
+    K.rgcn_layer1_backward_ex(gidx, h, w, norm, lw, go, None, gw2, gl2, etypes=et32)
     assert th.equal(gw, gw2) and th.equal(gl, gl2)
     gidx.__dict__.pop("_rgcn_state", None)

@@ -100,9 +100,9 @@ def test_rgcn_layer0_vs_oracle(F, hub):
     go = rng.standard_normal((n, F)).astype(np.float32)
     et32, nd = th.from_numpy(et).int().to(DEV), th.from_numpy(norm).to(DEV)
     ret = th.full((n, F), float("nan"), device=DEV)
-    K.rgcn_layer0(gidx, et32, th.from_numpy(w).to(DEV), nd, ret)
+    K.rgcn_layer0(gidx, th.from_numpy(w).to(DEV), nd, ret, etypes=et32)
     gw = th.full((R, n, F), float("nan"), device=DEV)
-    K.rgcn_layer0_backward(gidx, et32, th.from_numpy(go).to(DEV), nd, gw)
+    K.rgcn_layer0_backward(gidx, th.from_numpy(go).to(DEV), nd, gw, etypes=et32)
     oref = O.hack_rgcn_layer0(src, dst, et, n, w, norm)
     omass = O.hack_rgcn_layer0(src, dst, et, n, np.abs(w), norm)
     _close(ret.cpu(), oref, omass, "layer0")
@@ -126,13 +126,13 @@ def test_rgcn_layer1_vs_oracle(K_in, X, prepare, hub):
     et32, nd = th.from_numpy(et).int().to(DEV), th.from_numpy(norm).to(DEV)
     gidx.__dict__.pop("_rgcn_state", None)
     if prepare:
-        K.rgcn_prepare(gidx, et32, nd, R, layers=prepare)
+        K.rgcn_prepare(gidx, nd, R, layers=prepare, etypes=et32)
     hd, wd, god = (th.from_numpy(a).to(DEV) for a in (h, w, go))
     ret = th.full((n, X), float("nan"), device=DEV)
-    K.rgcn_layer1(gidx, et32, hd, wd, nd, ret)
+    K.rgcn_layer1(gidx, hd, wd, nd, ret, etypes=et32)
     gh = th.full((n, K_in), float("nan"), device=DEV)
     gw = th.full((R, K_in, X), float("nan"), device=DEV)
-    K.rgcn_layer1_backward(gidx, et32, hd, wd, nd, god, gh, gw)
+    K.rgcn_layer1_backward(gidx, hd, wd, nd, god, gh, gw, etypes=et32)
     gidx.__dict__.pop("_rgcn_state", None)
     oref = O.hack_rgcn_layer1(src, dst, et, n, h, w, norm)
     omass = O.hack_rgcn_layer1(src, dst, et, n, np.abs(h), np.abs(w), norm)

@@ -155,7 +155,7 @@ def test_capi_errors_without_device():
                                 0.2, ctypes.byref(a), ctypes.byref(a), ctypes.byref(a), None)
     assert rc == -1 and "fused GAT needs a graph of fewer than 2^31 edges" in _ffi.last_error()
     st = _ffi.RgcnState()
-    rc = L.DGLMIRgcnPrepare(ctypes.byref(g), None, None, 2, 1, ctypes.byref(st), None)
+    rc = L.DGLMIRgcnPrepare(ctypes.byref(g), None, 2, 1, ctypes.byref(st), None)
     assert rc == -1 and "R-GCN needs a graph of fewer than 2^31 edges" in _ffi.last_error()
 
 

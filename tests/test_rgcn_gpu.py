@@ -182,9 +182,12 @@ def test_relgraphconv_fused_route(R, bases, loop, act):
 
 
 def test_relgraphconv_fused_state_follows_the_tensors():
-    """The fused route's prepared state is keyed on etypes / norm and their version
-    counters: an in-place update, a new norm per call and new etypes rebuild it;
-    a norm that needs a gradient and 32-wide layers keep the typed-gather path."""
+    """The fused route's prepared state is keyed on etypes and its version counter:
+    an in-place update of norm or a new norm per call re-gathers the cached norm
+    copies (same state), new etypes rebuild it (the old state released first, one
+    alive); a norm that needs a gradient and 32-wide layers keep the typed-gather path."""
+    import gc
+    from dgl import kernel as K
     g, src, dst, et, n = typed_graph(seed=6)
     R = 4
     th.manual_seed(2)
@@ -192,16 +195,22 @@ def test_relgraphconv_fused_state_follows_the_tensors():
     x = th.randn(n, 64, device=DEV)
     etypes = th.from_numpy(et).to(DEV)
     norm = th.rand(len(src), 1, device=DEV)
+    gc.collect()
+    live = K.RgcnState.live
     with th.no_grad():
         a = conv(g, x, etypes, norm)
+        st = g._graph.__dict__["_rgcn_fused"][1].__dict__["_rgcn_state"]
+        assert K.RgcnState.live == live + 1
         norm.mul_(2.0)
         b = conv(g, x, etypes, norm)
         assert th.allclose(b, 2 * a, rtol=1e-5, atol=1e-5)
         outs = [conv(g, x, etypes, th.full((len(src), 1), float(k), device=DEV)) for k in (1, 2, 3)]
         assert th.allclose(outs[1], 2 * outs[0], rtol=1e-5, atol=1e-5)
         assert th.allclose(outs[2], 3 * outs[0], rtol=1e-4, atol=1e-4)
+        assert g._graph.__dict__["_rgcn_fused"][1].__dict__["_rgcn_state"] is st
         et2 = (etypes + 1) % R
         c = conv(g, x, et2, norm)
+        assert K.RgcnState.live == live + 1 and not st._fin.alive
         conv.use_fused = False
         c2 = conv(g, x, et2, norm)
         assert th.allclose(c, c2, rtol=1e-4, atol=1e-4)
