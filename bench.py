@@ -167,8 +167,21 @@ def measure_c4(world, rank, dist, cdev, device, args):
     th.cuda.synchronize()
     res = {"workload": "C4: RMAT scale 24 (ids >= 10M rejected), %d nodes, %d edges, feat %d"
                        % (C4_N, C4_E, FEAT), "scaling": "strong", "n_gpus": world,
+           "target": "north_star's >= 6x edges/s at 8 GPUs vs 1 is read from this line: a fixed "
+                     "graph split over the ranks, the halo exchange inside every step",
            "setup_s": None}
     steps = max(1, args.steps)
+    if world > 1:
+        # the N = 1 step on the same box in the same run: the whole graph's copy_u_sum
+        # on each rank's own GPU (max over ranks) -> speedup_vs_n1
+        out1 = th.empty_like(out_full)
+        one = lambda: K.copy_reduce("sum", gidx, 0, x, out1)
+        for _ in range(2):
+            one()
+        n1_ms = _max_over_ranks(_timed(one, steps, None, None) * 1e3 / steps, dist, cdev)
+        res["n1_ms_per_step"] = n1_ms
+        res["n1_edges_per_s"] = C4_E / (n1_ms * 1e-3)
+        del out1
     if world == 1:
         out = th.empty_like(out_full)
         step = lambda: K.copy_reduce("sum", gidx, 0, x, out)
@@ -178,7 +191,7 @@ def measure_c4(world, rank, dist, cdev, device, args):
         if not th.equal(out, out_full):
             raise SystemExit("C4 copy_u_sum not deterministic")
         res.update({"value": C4_E * steps / el, "unit": "edges/s",
-                    "ms_per_step": el * 1e3 / steps, "partitioner": None,
+                    "ms_per_step": el * 1e3 / steps, "speedup_vs_n1": 1.0, "partitioner": None,
                     "setup_s": time.time() - t0})
         return res
     t1 = time.time()
@@ -252,6 +265,7 @@ def measure_c4(world, rank, dist, cdev, device, args):
     dist.all_gather(works, work)
     works = [int(w.item()) for w in works]
     res.update({"value": C4_E * steps / el, "unit": "edges/s", "ms_per_step": el * 1e3 / steps,
+                "speedup_vs_n1": res["n1_ms_per_step"] / (el * 1e3 / steps),
                 "exchange": "hybrid: pulled rows + pushed partial sums (tau %d), two "
                             "all-to-all-v (%s) overlapped with the owned-source SpMM"
                             % (args.c4_tau, dist.get_backend()),
@@ -272,6 +286,153 @@ def measure_c4(world, rank, dist, cdev, device, args):
                                          "cut_fraction": stats_ct["cut_edges"] / C4_E},
                 "setup_s": time.time() - t0})
     return res
+
+
+C5_NODES = 5_000_000
+C5_EDGES = 80_000_000
+C5_RELS = 4
+
+
+def _allreduce_sum(tensors, dist, cdev):
+    """Sum of the tensors over the ranks, in place (one flat collective; host
+    staging for gloo)."""
+    flat = th.cat([t.reshape(-1) for t in tensors])
+    if cdev == "cpu":
+        f = flat.cpu()
+        dist.all_reduce(f)
+        flat.copy_(f)
+    else:
+        dist.all_reduce(flat)
+    off = 0
+    for t in tensors:
+        t.copy_(flat[off:off + t.numel()].view_as(t))
+        off += t.numel()
+
+
+def measure_c5(world, rank, dist, cdev, device, args):
+    """C5 at N > 1 (BASELINE.json config 5: R-GCN on a 4-relation 5 M-node / 80 M-edge
+    graph on 4 MI355X): DistRelGraphConv (64 -> 64, basis, self-loop, bias, norm = 1 /
+    in-degree) on each rank's block of the device label-propagation partition
+    (METIS stand-in), the fused R-GCN kernels on the local block.  A step = forward
+    (halo all-to-all-v of the remote input rows) + backward (the reverse exchange of
+    the halo rows' gradients) + the weight-gradient all-reduce -- the reference's
+    multi-GPU pattern (examples/pytorch/graphsage/train_sampling_multi_gpu.py:193-265)
+    on a full-graph partition.  Before timing, every rank runs the single-GPU module
+    on the whole graph and the partitioned outputs, input gradients and all-reduced
+    weight gradients must match it; that whole-graph step, timed on each rank's own
+    GPU, is the N = 1 figure of speedup_vs_n1.  Strong scaling: value = 80 M edges /
+    step time."""
+    from dgl import distributed as D
+    from dgl.nn.pytorch import RelGraphConv
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import bench_configs as bc
+    t0 = time.time()
+    n, m, R, f = args.c5_nodes, args.c5_edges, C5_RELS, FEAT
+    g = bc.chung_lu(n, m, 0.5, 8, device)  # the graph of the N = 1 configs line
+    src, dst = g._graph._device_only
+    gen = th.Generator(device=device)
+    gen.manual_seed(8)
+    et = th.randint(0, R, (m,), generator=gen, device=device)
+    indeg = th.bincount(dst.long(), minlength=n).float().clamp(min=1)
+    norm = (1.0 / indeg)[dst.long()].reshape(m, 1)
+    del indeg
+    gen.manual_seed(9)
+    x = th.randn(n, f, generator=gen, device=device)
+    go = th.randn(n, f, generator=gen, device=device)
+    th.manual_seed(0)
+    conv = RelGraphConv(f, f, R, "basis", num_bases=R, self_loop=True).to(device)
+    with th.no_grad():
+        conv.h_bias.uniform_(-0.5, 0.5)
+    params = list(conv.parameters())
+    xr = x.clone().requires_grad_()
+    out_full = conv(g, xr, et, norm)
+    grads_full = th.autograd.grad(out_full, [xr] + params, go)
+    out_full = out_full.detach()
+
+    def step1():
+        th.autograd.grad(conv(g, xr, et, norm), [xr] + params, go)
+    steps = max(1, min(args.steps, 10))
+    for _ in range(2):
+        step1()
+    n1_ms = _max_over_ranks(_timed(step1, steps, None, None) * 1e3 / steps, dist, cdev)
+    del xr
+    log("C5: whole-graph module + N = 1 timing (%.1fs)" % (time.time() - t0))
+    gidx = g._graph.get_immutable_gidx(device)
+    t1 = time.time()
+    assign, info = D.partition_labelprop(gidx, world, rounds=args.c4_rounds, slack=args.c4_slack)
+    th.cuda.synchronize()
+    lp_s = time.time() - t1
+    h = (assign.long() * th.arange(1, n + 1, device=device) % 1000003).sum()
+    hs = th.tensor([float(h.item())], device=cdev, dtype=th.float64)
+    hmax, hmin = hs.clone(), hs.clone()
+    dist.all_reduce(hmax, op=dist.ReduceOp.MAX)
+    dist.all_reduce(hmin, op=dist.ReduceOp.MIN)
+    if float(hmax.item()) != float(hmin.item()):
+        raise SystemExit("C5: ranks disagree on the partition")
+    part = D.build_partition_from_assignment(src, dst, assign, rank, None, world)
+    keep = assign[dst.long()] == rank  # local edge order = the global order of kept edges
+    et_l, norm_l = et[keep].contiguous(), norm[keep].contiguous()
+    del keep, src, dst, assign
+    g._graph.__dict__.pop("_rgcn_fused", None)  # the whole graph's prepared state
+    gidx.__dict__.pop("_rgcn_state", None)
+    log("C5: partition (%.1fs)" % (time.time() - t0))
+    dr = D.DistRelGraphConv(f, f, R, "basis", num_bases=R, self_loop=True).to(device)
+    dr.conv.load_state_dict(conv.state_dict())
+    inner = part.inner_global.long()
+    xi = x[inner].contiguous().requires_grad_()
+    go_i = go[inner].contiguous()
+    params_d = list(dr.parameters())
+    out_d = dr(part, xi, et_l, norm_l)
+    fused = part.local_graph(device)._graph.__dict__.get("_rgcn_fused") is not None
+    grads_d = list(th.autograd.grad(out_d, [xi] + params_d, go_i))
+    _allreduce_sum(grads_d[1:], dist, cdev)
+    ref = out_full[inner]
+    out_err = float(((out_d.detach() - ref).abs() / (1e-4 + 1e-4 * ref.abs())).max())
+    gx_ref = grads_full[0][inner]
+    errs = [float((grads_d[0] - gx_ref).abs().max()) / (1e-3 + 1e-4 * float(gx_ref.abs().max()))]
+    for a, b in zip(grads_d[1:], grads_full[1:]):
+        errs.append(float((a - b).abs().max()) / (1e-3 + 1e-4 * float(b.abs().max())))
+    worst = _max_over_ranks(max([out_err] + errs), dist, cdev)
+    all_fused = _max_over_ranks(0.0 if fused else 1.0, dist, cdev) == 0.0
+    if worst > 1.0:
+        raise SystemExit("C5: the partitioned R-GCN layer differs from the single-GPU module "
+                         "(worst error / bound %.3g)" % worst)
+    del out_d, grads_d, out_full, grads_full, ref, gx_ref, g, gidx, x, go
+    th.cuda.empty_cache()
+
+    def dstep():
+        for p in params_d:
+            p.grad = None
+        xi.grad = None
+        dr(part, xi, et_l, norm_l).backward(go_i)
+        D.allreduce_gradients(params_d, average=False)
+
+    def fstep():
+        with th.no_grad():
+            dr(part, xi, et_l, norm_l)
+    for _ in range(2):
+        dstep()
+        fstep()
+    el = _timed(dstep, steps, dist, cdev)
+    fel = _timed(fstep, steps, dist, cdev)
+    halo = th.tensor([float(part.n_halo)], device=cdev, dtype=th.float64)
+    dist.all_reduce(halo)
+    ms = el * 1e3 / steps
+    return {"workload": "C5: R-GCN RelGraphConv 4 relations basis 64->64, self-loop + bias, "
+                        "norm 1/in-degree, Chung-Lu(0.5) %d nodes / %d typed edges" % (n, m),
+            "scaling": "strong", "n_gpus": world, "value": m * steps / el, "unit": "edges/s",
+            "ms_per_step": ms, "fwd_ms": fel * 1e3 / steps,
+            "step": "DistRelGraphConv forward (halo all-to-all-v) + backward (reverse halo "
+                    "exchange) + weight-gradient all-reduce (%s)" % dist.get_backend(),
+            "n1_ms_per_step": n1_ms, "n1_step": "RelGraphConv forward + backward on the whole "
+                                                "graph, each rank's own GPU, max over ranks",
+            "speedup_vs_n1": n1_ms / ms, "fused_route_all_ranks": all_fused,
+            "check_worst_err_over_bound": worst,
+            "check": "partitioned output (rtol = atol = 1e-4), input gradient and all-reduced "
+                     "weight gradients (1e-3 + 1e-4 max|ref|) vs the whole-graph module",
+            "partitioner": "device label propagation, %d rounds, slack %g (%.2fs)"
+                           % (args.c4_rounds, args.c4_slack, lp_s),
+            "halo_rows_all_ranks": int(halo.item()), "setup_s": time.time() - t0}
 
 
 def make_local_graph(n_src, n_dst, src, dst, device):
@@ -360,42 +521,88 @@ def _rocprof():
                                          if os.path.exists("/opt/rocm/bin/rocprofv3") else None)
 
 
-def pmc_child():
-    """Body of one rocprofv3 --pmc pass (``bench.py --pmc-child``): the M1 launch
-    pair 3 times, then 3 launches over a calibration graph whose bytes are known
-    exactly (a random permutation: every source row gathered once, no reuse)."""
+def pmc_child(world=1, rank=0, edges_per_gpu=EDGES_PER_GPU, scale0=SCALE):
+    """Body of one rocprofv3 --pmc pass (``bench.py --pmc-child``): this rank's M1
+    launch pair (its row block of the world-size graph, as the timed run builds it)
+    3 times, then 3 launches over a calibration graph whose bytes are known exactly
+    (a random permutation of the same node table: every source row gathered once, no
+    reuse).  The parent makes the rank's GPU the only visible one (cuda:0 here)."""
     import dgl  # noqa: F401
     from dgl import kernel as K
     from dgl.graph_index import device_block_gidx
     device = "cuda:0"
     th.cuda.set_device(0)
-    n, n_dst, src, dst, x = build_workload(1, 0, device)
+    n, n_dst, src, dst, x = build_workload(world, rank, device, edges_per_gpu, scale0)
     g, _ = make_local_graph(n, n_dst, src, dst, device)
     del src, dst
     out = th.empty(n_dst, FEAT, device=device)
     for _ in range(3):
         K.copy_reduce("sum", g, 0, x, out)
     th.cuda.synchronize()
-    del g
+    del g, out
     gp = th.Generator(device=device)
     gp.manual_seed(11)
     csrc = th.randperm(n, generator=gp, device=device).to(th.int32)
     cdst = th.arange(n, dtype=th.int32, device=device)
     gc = device_block_gidx(n, n, csrc, cdst)
+    out = th.empty(n, FEAT, device=device)
     for _ in range(3):
         K.copy_reduce("sum", gc, 0, x, out)
     th.cuda.synchronize()
 
 
-def pmc_traffic_live(timeout_s=150):
-    """Fabric bytes of the M1 copy_u_sum launch pair, measured now by rocprofv3 PMC
-    passes over ``bench.py --pmc-child`` (one counter group per pass, as
-    MI355X_MICROARCH.md §rocprofv3 prescribes), run BEFORE this process touches
-    the GPU.  gfx950 FETCH_SIZE under-reports wide reads (MI355X_MICROARCH.md
-    §HBM), so its scale is calibrated in the same pass on a permutation gather
-    whose read bytes are known exactly (4F per source row + 8 per edge);
-    WRITE_SIZE is exact for 16-B stores.  Returns a dict or None."""
+def pmc_phase_values(rows, n_passes, launches=3):
+    """Counter values of the PMC child's launches by phase.  rows: (pass, dispatch id,
+    is_reduce, counter, value) of the k_chunk_reduce / k_chunk_fixup dispatches.
+    Within each pass, dispatch order tells the phases apart: the first `launches`
+    reduce launches and the fixups after them are the rank's M1 launches ("m1"), the
+    rest the calibration graph's ("cal").  Returns {(phase, counter): [values]}."""
+    vals = {}
+    for i in range(n_passes):
+        disp = sorted({(d, red) for pi, d, red, _, _ in rows if pi == i})
+        phase, nred, phase_of = "m1", 0, {}
+        for d, red in disp:
+            if red:
+                nred += 1
+                phase = "m1" if nred <= launches else "cal"
+            phase_of[d] = phase
+        for pi, d, red, cname, v in rows:
+            if pi == i:
+                vals.setdefault((phase_of[d], cname), []).append(v)
+    return vals
+
+
+def _child_device_env(local):
+    """Environment that leaves a child process exactly one GPU: this rank's.  The
+    rank's device is the `local`-th one this process would see (ROCR_VISIBLE_DEVICES
+    and then HIP_/CUDA_VISIBLE_DEVICES filter it), pinned through ROCR_VISIBLE_DEVICES
+    so the profiler's agent list holds that GPU alone."""
+    env = dict(os.environ)
+    idx = str(local)
+    for var in ("CUDA_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
+        lst = env.pop(var, None)
+        if lst:
+            idx = lst.split(",")[int(idx)]
+    rocr = env.get("ROCR_VISIBLE_DEVICES")
+    env["ROCR_VISIBLE_DEVICES"] = rocr.split(",")[int(idx)] if rocr else idx
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR",
+              "MASTER_PORT", "GROUP_RANK", "ROLE_RANK"):
+        env.pop(k, None)
+    return env
+
+
+def pmc_traffic_live(world=1, rank=0, local=0, edges_per_gpu=EDGES_PER_GPU, scale0=SCALE,
+                     timeout_s=240):
+    """Fabric bytes of this rank's copy_u_sum launch pair, measured now by rocprofv3
+    PMC passes over ``bench.py --pmc-child`` (one counter group per pass, as
+    MI355X_MICROARCH.md §rocprofv3 prescribes) on this rank's own GPU, run BEFORE
+    this process touches the GPU.  gfx950 FETCH_SIZE under-reports wide reads
+    (MI355X_MICROARCH.md §HBM), so its scale is calibrated in the same pass on a
+    permutation gather whose read bytes are known exactly (4F per source row + 8 per
+    edge); WRITE_SIZE is exact for 16-B stores.  Ranks sharing one GPU (a
+    --same-device rehearsal) take turns through a lock file.  Returns a dict or None."""
     import csv
+    import fcntl
     import glob
     import shutil
     import signal
@@ -404,15 +611,21 @@ def pmc_traffic_live(timeout_s=150):
     prof = _rocprof()
     if prof is None:
         return None
+    env = _child_device_env(local)
     tmp = tempfile.mkdtemp(prefix="dglmi_pmc_")
-    vals = {}
+    lock = open(os.path.join(tempfile.gettempdir(), "dglmi_pmc_gpu%s.lock"
+                             % env["ROCR_VISIBLE_DEVICES"]), "w")
+    fcntl.flock(lock, fcntl.LOCK_EX)
+    rows = []
     try:
         for i, counters in enumerate(PMC_PASSES):
             d = os.path.join(tmp, "p%d" % i)
             cmd = [prof, "--pmc", *counters, "-d", d, "-o", "run", "--output-format", "csv", "--",
-                   sys.executable, os.path.abspath(__file__), "--pmc-child"]
+                   sys.executable, os.path.abspath(__file__), "--pmc-child",
+                   "--pmc-world", str(world), "--pmc-rank", str(rank),
+                   "--edges-per-gpu", str(edges_per_gpu), "--scale", str(scale0)]
             p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
-                                 start_new_session=True, cwd=ROOT)
+                                 start_new_session=True, cwd=ROOT, env=env)
             try:
                 _, err = p.communicate(timeout=timeout_s)
             except subprocess.TimeoutExpired:
@@ -429,40 +642,39 @@ def pmc_traffic_live(timeout_s=150):
                 return None
             for r in csv.DictReader(open(files[0])):
                 name = r["Kernel_Name"]
-                if "k_chunk_reduce" not in name and "k_chunk_fixup" not in name:
-                    continue
-                key = (int(r["Grid_Size"]), "reduce" if "k_chunk_reduce" in name else "fixup",
-                       r["Counter_Name"])
-                vals.setdefault(key, []).append(float(r["Counter_Value"]))
+                if "k_chunk_reduce" in name or "k_chunk_fixup" in name:
+                    rows.append((i, int(r["Dispatch_Id"]), "k_chunk_reduce" in name,
+                                 r["Counter_Name"], float(r["Counter_Value"])))
     finally:
+        fcntl.flock(lock, fcntl.LOCK_UN)
+        lock.close()
         shutil.rmtree(tmp, ignore_errors=True)
-    grids = sorted({k[0] for k in vals if k[1] == "reduce"})
-    if len(grids) < 2:
-        return None
-    m1_grid, cal_grid = grids[-1], grids[0]
+    vals = pmc_phase_values(rows, len(PMC_PASSES))
 
-    def per_launch(grid, counter):  # mean per dispatch, reduce + fixup
-        return sum(float(np.mean(v)) for k, v in vals.items() if k[0] == grid and k[2] == counter)
+    def per_launch(phase, counter):  # mean per launch pair (reduce + fixup sums / 3)
+        v = vals.get((phase, counter))
+        return float(np.sum(v)) / 3.0 if v else 0.0
 
-    n = 1 << SCALE
+    n = 1 << (scale0 + int(round(math.log2(world))))
     cal_known_read = 4 * FEAT * n + 8 * n  # every X row once + rows/indices stream
-    fetch_cal = per_launch(cal_grid, "FETCH_SIZE") * 1024
-    fetch = per_launch(m1_grid, "FETCH_SIZE") * 1024
-    write = per_launch(m1_grid, "WRITE_SIZE") * 1024
+    fetch_cal = per_launch("cal", "FETCH_SIZE") * 1024
+    fetch = per_launch("m1", "FETCH_SIZE") * 1024
+    write = per_launch("m1", "WRITE_SIZE") * 1024
     if fetch_cal <= 0 or fetch <= 0:
         return None
     scale = cal_known_read / fetch_cal
-    hit = per_launch(m1_grid, "TCC_HIT_sum")
-    miss = per_launch(m1_grid, "TCC_MISS_sum")
+    hit = per_launch("m1", "TCC_HIT_sum")
+    miss = per_launch("m1", "TCC_MISS_sum")
     return {"bytes_per_launch": scale * fetch + write, "read_bytes": scale * fetch,
             "write_bytes": write, "fetch_size_bytes_raw": fetch, "fetch_scale": scale,
             "fetch_scale_from": "permutation gather, %d known read bytes, FETCH_SIZE %d"
                                 % (cal_known_read, fetch_cal),
             "l2_hit_rate": hit / (hit + miss) if hit + miss > 0 else None,
-            "passes": [list(c) for c in PMC_PASSES],
-            "method": "rocprofv3 --pmc per pass over `bench.py --pmc-child` (M1 launch pair x3), "
-                      "read = FETCH_SIZE x calibrated scale, + WRITE_SIZE; Infinity-Cache hits "
-                      "included (they leave L2)"}
+            "passes": [list(c) for c in PMC_PASSES], "rank": rank,
+            "device": "ROCR_VISIBLE_DEVICES=%s" % env["ROCR_VISIBLE_DEVICES"],
+            "method": "rocprofv3 --pmc per pass over `bench.py --pmc-child` (this rank's launch "
+                      "pair x3 on its own GPU), read = FETCH_SIZE x calibrated scale, + "
+                      "WRITE_SIZE; Infinity-Cache hits included (they leave L2)"}
 
 
 def _max_over_ranks(v, dist, cdev):
@@ -620,6 +832,12 @@ class SideLines:
         elif self.rank == 0:
             print(json.dumps(self.res), flush=True)
         return SIDE_LINE_RC if self.res.get("side_line_errors") else 0
+
+
+def gc_collect():
+    import gc
+    gc.collect()
+    th.cuda.empty_cache()
 
 
 def _free_port():
@@ -832,25 +1050,42 @@ def measure_update_all(g, x, out_ref, args):
             "path": "DGLGraph.update_all(fn.copy_u, fn.sum) incl. output allocation"}
 
 
-def measure_configs(device, steps=5, warmup=2):
+def measure_configs(device, steps=5, warmup=2, budgets=(("c2", 120), ("c3", 300), ("c5", 360)),
+                    script=None):
     """The other single-GPU BASELINE configs at N = 1, timed on this box beside the
     headline (scripts/bench_configs.py): C2 arxiv-size copy_u_sum and GraphConv layer,
     C3 Reddit-size fused GATConv forward / forward + backward, C5 RelGraphConv on the
-    fused R-GCN entries.  Informational: a config that fails is recorded under its key
-    and does not change the job's status (the headline contract is the M1 line)."""
-    import gc
-    sys.path.insert(0, os.path.join(ROOT, "scripts"))
-    import bench_configs as bc
-    out = {"steps": steps, "warmup": warmup, "source": "scripts/bench_configs.py"}
-    for name in ("c2", "c3", "c5"):
+    fused R-GCN entries (checked against the unfused route before it is timed).
+    Informational, and isolated: each config runs in a child process of its own under
+    a time limit (killed with its process group when it overruns), so an import error,
+    a GPU fault or a stall there is recorded under its key and can neither change the
+    job's status nor stop the headline line from printing."""
+    import signal
+    import subprocess
+    out = {"steps": steps, "warmup": warmup, "source": "scripts/bench_configs.py, one child "
+                                                        "process per config"}
+    script = script or os.path.join(ROOT, "scripts", "bench_configs.py")
+    for name, budget in budgets:
         t0 = time.time()
+        cmd = [sys.executable, script, "--configs", name, "--steps", str(steps),
+               "--warmup", str(warmup)]
+        p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                             start_new_session=True, cwd=ROOT)
         try:
-            out[name] = getattr(bc, name)(device, steps, warmup)
-        except Exception as exc:  # noqa: BLE001 -- informational only
-            out[name] = {"error": repr(exc)[:300]}
+            so, se = p.communicate(timeout=budget)
+            lines = [ln for ln in so.decode(errors="replace").splitlines() if ln.startswith("{")]
+            if p.returncode == 0 and lines:
+                out[name] = json.loads(lines[-1])
+            else:
+                out[name] = {"error": "rc %d: %s" % (p.returncode,
+                                                     se.decode(errors="replace")[-300:])}
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+            out[name] = {"error": "exceeded %d s" % budget}
+        except ValueError as exc:
+            out[name] = {"error": "unparsable output: %r" % exc}
         out[name]["wall_s"] = time.time() - t0
-        gc.collect()
-        th.cuda.empty_cache()
         log("configs %s: %s" % (name, json.dumps(out[name])))
     return out
 
@@ -877,6 +1112,10 @@ def main():
                     help="skip the fixed-size C4 (10M / 200M, partitioned, with exchange) line")
     ap.add_argument("--no-configs", action="store_true",
                     help="N=1: skip the informational C2 / C3 / C5 config timings")
+    ap.add_argument("--no-c5", action="store_true",
+                    help="N>1: skip the partitioned C5 R-GCN line")
+    ap.add_argument("--c5-nodes", type=int, default=C5_NODES, help=argparse.SUPPRESS)
+    ap.add_argument("--c5-edges", type=int, default=C5_EDGES, help=argparse.SUPPRESS)
     ap.add_argument("--c4-nodes", type=int, default=C4_NODES, help=argparse.SUPPRESS)
     ap.add_argument("--c4-edges", type=int, default=C4_EDGES, help=argparse.SUPPRESS)
     ap.add_argument("--c4-rounds", type=int, default=24,
@@ -888,12 +1127,14 @@ def main():
                     help="C4 hybrid exchange: push a partial sum when a part holds >= tau "
                          "sources of a destination")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-world", type=int, default=1, help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-rank", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--launch-grace", type=float, default=60.0,
                     help="self-launched N > 1: seconds the other ranks get after one fails")
     ap.add_argument("--launcher-stub", default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.pmc_child:
-        pmc_child()
+        pmc_child(args.pmc_world, args.pmc_rank, args.edges_per_gpu, args.scale)
         return 0
     if args.gpus < 1:
         log("--gpus must be >= 1")
@@ -917,15 +1158,17 @@ def main():
     m1 = world == 1 and args.edges_per_gpu == EDGES_PER_GPU and args.scale == SCALE
     pmc = None
     under_profiler = any(k.startswith("ROCPROF") for k in os.environ)
-    if m1 and not args.no_pmc and not under_profiler:
-        # counters first, in child processes, before this process touches the GPU
+    local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
+    if not args.no_pmc and not under_profiler:
+        # counters first, in child processes on this rank's own GPU, before this
+        # process touches the GPU (every rank measures its own launch pair)
         t0 = time.time()
         try:
-            pmc = pmc_traffic_live()
+            pmc = pmc_traffic_live(world, rank, local, args.edges_per_gpu, args.scale)
         except Exception as exc:  # the counters must never take the GPU line down
             log("pmc passes failed: %r" % exc)
+        trace("pmc passes: %s (%.1fs)" % ("ok" if pmc else "unavailable", time.time() - t0))
         log("pmc passes: %s (%.1fs)" % ("ok" if pmc else "unavailable", time.time() - t0))
-    local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
     th.cuda.set_device(local)
     device = "cuda:%d" % local
     dist = None
@@ -1026,6 +1269,19 @@ def main():
     elapsed = time.perf_counter() - t_start
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     edges_total = m_local
+    if pmc is None and m1:
+        # no live counters (profiler unavailable, or this run is itself under
+        # rocprofv3): the committed passes of the same launch at this head
+        try:
+            pmc = dict(json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json"))))
+            pmc["source"] = "profiles/pmc_traffic.json (committed rocprofv3 passes, same launch)"
+        except (OSError, ValueError):
+            pmc = None
+    # per-rank launch record: kernel time, edges and the fabric bytes of this rank's
+    # own launch pair (its PMC passes) -> its roofline fraction
+    per_rank = [{"rank": rank, "kernel_ms": kernel_ms, "edges": int(m_local), "n_dst": int(n_dst),
+                 "traffic": pmc["bytes_per_launch"] if pmc else None,
+                 "l2_hit_rate": pmc.get("l2_hit_rate") if pmc else None}]
     if dist is not None:
         t = th.tensor([elapsed], device=cdev, dtype=th.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -1036,6 +1292,12 @@ def main():
         e = th.tensor([m_local], device=cdev, dtype=th.float64)
         dist.all_reduce(e)
         edges_total = int(e.item())
+        gathered = [None] * world
+        dist.all_gather_object(gathered, per_rank[0])
+        per_rank = gathered
+    for r in per_rank:
+        r["achieved_GBps"] = r["traffic"] / (r["kernel_ms"] * 1e-3) / 1e9 if r["traffic"] else None
+        r["frac"] = r["achieved_GBps"] / HBM_PEAK_GBPS if r["achieved_GBps"] else None
 
     ms_per_step = elapsed * 1000.0 / args.steps
     value = edges_total * args.steps / elapsed
@@ -1055,28 +1317,32 @@ def main():
     compulsory = 4 * (n_dst + 1) + 4 * m_local + 4 * FEAT * n + 4 * FEAT * n_dst
     alg_gbps = alg_bytes / (kernel_ms * 1e-3) / 1e9
     comp_gbps = compulsory / (kernel_ms * 1e-3) / 1e9
-    if pmc is None and m1:
-        # no live counters (profiler unavailable, or this run is itself under
-        # rocprofv3): the committed passes of the same launch at this head
-        try:
-            pmc = dict(json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json"))))
-            pmc["source"] = "profiles/pmc_traffic.json (committed rocprofv3 passes, same launch)"
-        except (OSError, ValueError):
-            pmc = None
-    traffic = pmc["bytes_per_launch"] if pmc else None
-    achieved = traffic / (kernel_ms * 1e-3) / 1e9 if traffic else None
+    # the line's roofline: at N = 1 the launch's own; at N > 1 the rank with the
+    # highest fraction (per_rank lists every rank's, frac_min the lowest)
+    fr = [r for r in per_rank if r["frac"] is not None]
+    best = max(fr, key=lambda r: r["frac"]) if fr else None
+    traffic = best["traffic"] if best else None
+    achieved = best["achieved_GBps"] if best else None
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBPS if achieved else None, "traffic": traffic,
+            "frac": best["frac"] if best else None, "traffic": traffic,
             "kernel": "k_chunk_reduce + k_chunk_fixup (one copy_u_sum launch pair)",
             "kernel_ms": kernel_ms,
-            "achieved_from": "fabric bytes per launch (rocprofv3 PMC, this run) / HIP-event "
-                             "kernel time" if traffic else "no counters this run",
+            "achieved_from": ("fabric bytes per launch (rocprofv3 PMC, this run%s) / HIP-event "
+                              "kernel time" % ("" if world == 1 else
+                                               ", each rank on its own GPU; the rank with the "
+                                               "highest fraction")) if traffic else
+                             "no counters this run",
             "alg_bytes_per_launch": alg_bytes, "alg_GBps": alg_gbps,
             "alg_note": "SURVEY §8d model: counts L2-served re-reads of hub rows, above peak",
             "compulsory_bytes_per_launch": compulsory, "compulsory_GBps": comp_gbps,
             "compulsory_frac": comp_gbps / HBM_PEAK_GBPS}
+    if world > 1:
+        roof["per_rank"] = per_rank
+        roof["frac_min"] = min(r["frac"] for r in fr) if fr else None
+        roof["alg_note"] += "; per rank: this rank's row block of the world-size graph"
     if pmc:
-        roof["pmc"] = pmc
+        roof["pmc"] = pmc if world == 1 else {k: v for k, v in pmc.items()
+                                              if k in ("method", "passes", "fetch_scale")}
     res = {
         "metric": "edges/sec + achieved HBM GB/s, GCN copy_u_sum on 100M-edge graph, 1/2/4/8 MI355X",
         "value": value,
@@ -1134,7 +1400,11 @@ def main():
             del part
         th.cuda.empty_cache()
         lines.run("c4", lambda: measure_c4(world, rank, dist, cdev, device, args))
+    if world > 1 and not args.no_c5 and not under_profiler:
+        gc_collect()
+        lines.run("c5", lambda: measure_c5(world, rank, dist, cdev, device, args))
     if world == 1 and not under_profiler and not args.no_configs:
+        gc_collect()
         res["configs"] = measure_configs(device)
     rc = lines.finish()
     if dist is not None:

@@ -973,13 +973,31 @@ int DGLMIFusedGatSupported(int64_t heads, int64_t head_dim) {
   return gat_supported(heads, head_dim) ? 1 : 0;
 }
 
-int DGLMIFusedGatForward(const DGLMIGraph* graph, const DGLMIArray* feat_src, const DGLMIArray* el,
-                         const DGLMIArray* er, float negative_slope, DGLMIArray* out,
-                         DGLMIArray* max_out, DGLMIArray* sum_out, void* stream) {
+}  // extern "C"
+
+namespace {
+// the optional slope aggregates of DGLMIFusedGatForwardEx / BackwardEx
+void gat_check_ls(const GatArgs& a, const DGLMIArray* lf, const DGLMIArray* ls) {
+  DGLMI_CHECK((lf == nullptr) == (ls == nullptr), "slope_feat and slope_sum go together");
+  if (lf == nullptr) return;
+  check_array(lf, "slope_feat");
+  check_array(ls, "slope_sum");
+  DGLMI_CHECK(lf->shape[0] == a.num_rows && feat_numel(lf) == a.F, "slope_feat must be (N_dst, H, D)");
+  DGLMI_CHECK(ls->shape[0] == a.num_rows && feat_numel(ls) == a.H, "slope_sum must be (N_dst, H)");
+  DGLMI_CHECK(aligned16(lf->data), "slope_feat must be 16-byte aligned");
+}
+
+int gat_forward_impl(const DGLMIGraph* graph, const DGLMIArray* feat_src, const DGLMIArray* el,
+                     const DGLMIArray* er, float negative_slope, DGLMIArray* out,
+                     DGLMIArray* max_out, DGLMIArray* sum_out, DGLMIArray* lf, DGLMIArray* ls,
+                     void* stream) {
   API_BEGIN();
   check_graph32(graph, "fused GAT");
   DeviceGuard guard(graph->device);
   GatArgs a = gat_args(graph, feat_src, el, er, negative_slope, out, max_out, sum_out);
+  gat_check_ls(a, lf, ls);
+  a.lf = lf ? lf->data : nullptr;
+  a.ls = ls ? ls->data : nullptr;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const DGLMICsr& walk = graph->in_csr;
   if (a.num_rows * a.F == 0) return 0;
@@ -987,14 +1005,20 @@ int DGLMIFusedGatForward(const DGLMIGraph* graph, const DGLMIArray* feat_src, co
     launch_fill(out->data, a.num_rows * a.F, 0.0f, s);
     launch_fill(max_out->data, a.num_rows * a.H, 0.0f, s);
     launch_fill(sum_out->data, a.num_rows * a.H, 0.0f, s);
+    if (lf) {
+      launch_fill(lf->data, a.num_rows * a.F, 0.0f, s);
+      launch_fill(ls->data, a.num_rows * a.H, 0.0f, s);
+    }
     return 0;
   }
+  // carry record per chunk: acc, m, l (+ lf, ls)
+  const int64_t cw = lf ? 2 * a.F + 3 * a.H : a.F + 2 * a.H;
   const int nb = gat_blocks(graph);
   if (nb > 1) {
     // column-blocked: one raw (unnormalised) launch per source block into its own
     // partial buffers, then the in-order merge
     const int64_t N = a.num_rows;
-    const int64_t part_floats = nb * N * (a.F + 2 * a.H);
+    const int64_t part_floats = nb * N * cw;
     int64_t max_chunks = 0;
     for (int b = 0; b < nb; ++b) {
       const int64_t c = graph->in_col_blocks[b].nnz;
@@ -1002,11 +1026,14 @@ int DGLMIFusedGatForward(const DGLMIGraph* graph, const DGLMIArray* feat_src, co
                                             gat_chunk_edges(std::max<int64_t>(c, 1)));
     }
     const int64_t part_bytes = (part_floats * static_cast<int64_t>(sizeof(float)) + 255) & ~int64_t(255);
-    const int64_t carry_bytes = (max_chunks * (a.F + 2 * a.H) * static_cast<int64_t>(sizeof(float)) + 15) & ~int64_t(15);
+    const int64_t carry_bytes = (max_chunks * cw * static_cast<int64_t>(sizeof(float)) + 15) & ~int64_t(15);
     Scratch ws(graph, part_bytes + carry_bytes + max_chunks * static_cast<int64_t>(sizeof(int32_t)), s);
+    // [out parts][lf parts][m parts][l parts][ls parts]: the float4 arrays first
     float* out_part = static_cast<float*>(ws.ptr);
-    float* m_part = out_part + nb * N * a.F;
+    float* lf_part = lf ? out_part + nb * N * a.F : nullptr;
+    float* m_part = out_part + nb * N * a.F * (lf ? 2 : 1);
     float* l_part = m_part + nb * N * a.H;
+    float* ls_part = lf ? l_part + nb * N * a.H : nullptr;
     for (int b = 0; b < nb; ++b) {
       const DGLMICsr& c = graph->in_col_blocks[b];
       GatArgs ab = a;
@@ -1018,18 +1045,23 @@ int DGLMIFusedGatForward(const DGLMIGraph* graph, const DGLMIArray* feat_src, co
       ab.out = out_part + b * N * a.F;
       ab.m = m_part + b * N * a.H;
       ab.l = l_part + b * N * a.H;
+      if (lf) {
+        ab.lf = lf_part + b * N * a.F;
+        ab.ls = ls_part + b * N * a.H;
+      }
       ab.raw = 1;
       ab.carry = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + part_bytes);
       ab.seg_cnt = reinterpret_cast<int32_t*>(static_cast<char*>(ws.ptr) + part_bytes + carry_bytes);
       launch_gat_forward(ab, s);
     }
     launch_gat_merge(out_part, m_part, l_part, nb, N, a.H, a.D, out->data, max_out->data,
-                     sum_out->data, s);
+                     sum_out->data, s, lf_part, ls_part, lf ? lf->data : nullptr,
+                     ls ? ls->data : nullptr);
     check_hip(hipGetLastError(), "fused GAT forward (blocked) launch");
     return 0;
   }
   const int64_t chunks = (walk.nnz + a.chunk - 1) / a.chunk;
-  const int64_t carry_bytes = (chunks * (a.F + 2 * a.H) * static_cast<int64_t>(sizeof(float)) + 15) & ~int64_t(15);
+  const int64_t carry_bytes = (chunks * cw * static_cast<int64_t>(sizeof(float)) + 15) & ~int64_t(15);
   Scratch carry(graph, carry_bytes + chunks * static_cast<int64_t>(sizeof(int32_t)), s);
   a.carry = static_cast<float*>(carry.ptr);
   a.seg_cnt = reinterpret_cast<int32_t*>(static_cast<char*>(carry.ptr) + carry_bytes);
@@ -1037,12 +1069,33 @@ int DGLMIFusedGatForward(const DGLMIGraph* graph, const DGLMIArray* feat_src, co
   check_hip(hipGetLastError(), "fused GAT forward launch");
   API_END();
 }
+}  // namespace
 
-int DGLMIFusedGatBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src, const DGLMIArray* el,
-                          const DGLMIArray* er, float negative_slope, const DGLMIArray* out,
-                          const DGLMIArray* max_in, const DGLMIArray* sum_in,
-                          const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
-                          DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream) {
+extern "C" {
+
+int DGLMIFusedGatForward(const DGLMIGraph* graph, const DGLMIArray* feat_src, const DGLMIArray* el,
+                         const DGLMIArray* er, float negative_slope, DGLMIArray* out,
+                         DGLMIArray* max_out, DGLMIArray* sum_out, void* stream) {
+  return gat_forward_impl(graph, feat_src, el, er, negative_slope, out, max_out, sum_out, nullptr,
+                          nullptr, stream);
+}
+
+int DGLMIFusedGatForwardEx(const DGLMIGraph* graph, const DGLMIArray* feat_src, const DGLMIArray* el,
+                           const DGLMIArray* er, float negative_slope, DGLMIArray* out,
+                           DGLMIArray* max_out, DGLMIArray* sum_out, DGLMIArray* slope_feat,
+                           DGLMIArray* slope_sum, void* stream) {
+  return gat_forward_impl(graph, feat_src, el, er, negative_slope, out, max_out, sum_out, slope_feat,
+                          slope_sum, stream);
+}
+
+}  // extern "C"
+
+namespace {
+int gat_backward_impl(const DGLMIGraph* graph, const DGLMIArray* feat_src, const DGLMIArray* el,
+                      const DGLMIArray* er, float negative_slope, const DGLMIArray* out,
+                      const DGLMIArray* max_in, const DGLMIArray* sum_in, const DGLMIArray* lf_in,
+                      const DGLMIArray* ls_in, const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
+                      DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream) {
   API_BEGIN();
   check_graph32(graph, "fused GAT");
   DeviceGuard guard(graph->device);
@@ -1076,6 +1129,7 @@ int DGLMIFusedGatBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src, c
   a.g_er = grad_er->data;
   a.g_el = grad_el->data;
   a.g_ft = grad_feat_src->data;
+  gat_check_ls(a, lf_in, ls_in);
   const int nb = gat_blocks(graph);
   // Edge-position backward (DGLMIGraph.gat_edge_pos): no destination-side walk.  The
   // stats come from a dense pass, the source-side walk stores every edge's grad_er
@@ -1101,6 +1155,31 @@ int DGLMIFusedGatBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src, c
   a.stats = static_cast<float4*>(ws.ptr);
   a.carry = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + ((stats_bytes + 255) & ~int64_t(255)));
   a.seg_cnt = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(a.carry) + carry_bytes);
+  if (lf_in != nullptr) {
+    // the forward kept the slope aggregates: stats and grad_er from one dense pass, then
+    // the source-side walk(s) only -- no destination-side walk, no per-edge terms
+    a.lf = lf_in->data;
+    a.ls = ls_in->data;
+    launch_gat_stats(a, s);
+    a.lf = a.ls = nullptr;
+    auto src_walk = [&](const DGLMICsr& c, bool accumulate) {
+      GatArgs b = a;
+      b.indptr = c.indptr;
+      b.rows = c.rows;
+      b.indices = c.indices;
+      b.nnz = c.nnz;
+      b.num_rows = c.num_rows;
+      b.chunk = gat_bwd_chunk_edges(std::max<int64_t>(c.nnz, 1));
+      b.accumulate = accumulate;
+      launch_gat_backward_src(b, s);
+    };
+    if (nb > 1)
+      for (int b = 0; b < nb; ++b) src_walk(graph->out_col_blocks[b], b > 0);
+    else
+      src_walk(outc, false);
+    check_hip(hipGetLastError(), "fused GAT backward (slope aggregates) launch");
+    return 0;
+  }
   if (pos_path) {
     DGLMIGraph nows;  // t must not alias the caller's workspace (the reduce's carries)
     std::memset(&nows, 0, sizeof(nows));
@@ -1168,6 +1247,30 @@ int DGLMIFusedGatBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src, c
   API_END();
 }
 
+}  // namespace
+
+extern "C" {
+
+int DGLMIFusedGatBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src, const DGLMIArray* el,
+                          const DGLMIArray* er, float negative_slope, const DGLMIArray* out,
+                          const DGLMIArray* max_in, const DGLMIArray* sum_in,
+                          const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
+                          DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream) {
+  return gat_backward_impl(graph, feat_src, el, er, negative_slope, out, max_in, sum_in, nullptr,
+                           nullptr, grad_out, grad_feat_src, grad_el, grad_er, stream);
+}
+
+int DGLMIFusedGatBackwardEx(const DGLMIGraph* graph, const DGLMIArray* feat_src,
+                            const DGLMIArray* el, const DGLMIArray* er, float negative_slope,
+                            const DGLMIArray* out, const DGLMIArray* max_in,
+                            const DGLMIArray* sum_in, const DGLMIArray* slope_feat,
+                            const DGLMIArray* slope_sum, const DGLMIArray* grad_out,
+                            DGLMIArray* grad_feat_src, DGLMIArray* grad_el, DGLMIArray* grad_er,
+                            void* stream) {
+  return gat_backward_impl(graph, feat_src, el, er, negative_slope, out, max_in, sum_in, slope_feat,
+                           slope_sum, grad_out, grad_feat_src, grad_el, grad_er, stream);
+}
+
 // The reference's argument order (_CAPI_DGLFusedGatKernel /
 // _CAPI_DGLKernelBackwardFusedGat, binary_reduce.cc:380-396, 529-549) over the
 // kernels above.  The caller owns `sum` (N, H[, 1]) and `exp` (E, H[, 1]) and
@@ -1186,14 +1289,25 @@ bool gat_exp_holds_max(const DGLMIGraph* g, const DGLMIArray* feat_src, const DG
   DGLMI_CHECK(sum->shape[0] == g->in_csr.num_rows && feat_numel(sum) == H, "sum must be (N_dst, H[, 1])");
   return g->in_csr.nnz >= g->in_csr.num_rows;
 }
-DGLMIArray gat_state_view(float* data, int64_t rows, int64_t H) {
+DGLMIArray gat_state_view(float* data, int64_t rows, int64_t H, int64_t D = 0) {
   DGLMIArray v;
   std::memset(&v, 0, sizeof(v));
   v.data = data;
-  v.ndim = 2;
+  v.ndim = D > 0 ? 3 : 2;
   v.shape[0] = rows;
   v.shape[1] = H;
+  v.shape[2] = D;
   return v;
+}
+// exp (E, H) also holds the slope aggregates after the running max: slope_feat
+// (N, H, D) from float round_up(N H, 4), then slope_sum (N, H) -- room for all three
+// when E >= N (D + 2) about (C3: E / N ~ 490); then the backward runs no
+// destination-side walk (DGLMIFusedGatForwardEx)
+int64_t gat_lf_offset(int64_t N, int64_t H) { return (N * H + 3) & ~int64_t(3); }
+bool gat_exp_holds_slopes(const DGLMIGraph* g, const DGLMIArray* feat_src, const DGLMIArray* exp) {
+  const int64_t N = g->in_csr.num_rows, E = g->in_csr.nnz;
+  const int64_t H = feat_src->shape[1], D = feat_src->shape[2];
+  return aligned16(exp->data) && E * H >= gat_lf_offset(N, H) + N * H * D + N * H;
 }
 }  // namespace
 
@@ -1208,8 +1322,15 @@ int DGLMIFusedGatKernel(const DGLMIGraph* graph, const DGLMIArray* feat_src, con
   DGLMIArray l = gat_state_view(sum->data, N, H);
   if (gat_exp_holds_max(graph, feat_src, sum, exp)) {
     DGLMIArray m = gat_state_view(exp->data, N, H);
-    if (DGLMIFusedGatForward(graph, feat_src, el, er, slope, ret, &m, &l, stream) != 0)
+    if (gat_exp_holds_slopes(graph, feat_src, exp)) {
+      const int64_t D = feat_src->shape[2];
+      DGLMIArray lf = gat_state_view(exp->data + gat_lf_offset(N, H), N, H, D);
+      DGLMIArray ls = gat_state_view(lf.data + N * H * D, N, H);
+      if (DGLMIFusedGatForwardEx(graph, feat_src, el, er, slope, ret, &m, &l, &lf, &ls, stream) != 0)
+        throw Error(g_last_error);
+    } else if (DGLMIFusedGatForward(graph, feat_src, el, er, slope, ret, &m, &l, stream) != 0) {
       throw Error(g_last_error);
+    }
   } else {
     DGLMIGraph no_ws = *graph;  // the max must not alias the kernels' workspace
     no_ws.workspace = nullptr;
@@ -1238,9 +1359,17 @@ int DGLMIKernelBackwardFusedGat(const DGLMIGraph* graph, const DGLMIArray* feat_
   if (gat_exp_holds_max(graph, feat_src, sum, exp)) {
     const DGLMIArray m = gat_state_view(exp->data, N, H);
     const DGLMIArray l = gat_state_view(sum->data, N, H);
-    if (DGLMIFusedGatBackward(graph, feat_src, el, er, slope, ret, &m, &l, grad_out, grad_feat_src,
-                              grad_el, grad_er, stream) != 0)
+    if (gat_exp_holds_slopes(graph, feat_src, exp)) {
+      const int64_t D = feat_src->shape[2];
+      const DGLMIArray lf = gat_state_view(exp->data + gat_lf_offset(N, H), N, H, D);
+      const DGLMIArray ls = gat_state_view(lf.data + N * H * D, N, H);
+      if (DGLMIFusedGatBackwardEx(graph, feat_src, el, er, slope, ret, &m, &l, &lf, &ls, grad_out,
+                                  grad_feat_src, grad_el, grad_er, stream) != 0)
+        throw Error(g_last_error);
+    } else if (DGLMIFusedGatBackward(graph, feat_src, el, er, slope, ret, &m, &l, grad_out,
+                                     grad_feat_src, grad_el, grad_er, stream) != 0) {
       throw Error(g_last_error);
+    }
   } else {
     // sum holds max + log(sum): attention = exp(s - lse) / 1
     DGLMIGraph no_ws = *graph;
@@ -1619,7 +1748,7 @@ int rgcn_layer1_impl(const DGLMIGraph* graph, const DGLMIArray* hidden,
       rgcn_fused_walk(fs, fs->in_rel, fs->in_rel_norm, norm->data, &eids, &w);
       launch_rgcn_fused(false, fs->in_rel.indptr, fs->in_rel.indices, fs->in_rel.rows, eids, w,
                         hidden->data, weight->data, K * X, X, 1, ret->data, nullptr, in.num_rows, R,
-                        X, s, bias, addend, loop ? loop->data : nullptr);
+                        X, s, bias, addend, loop ? loop->data : nullptr, in.num_cols);
       check_hip(hipGetLastError(), "rgcn fused layer1 launch");
       return 0;
     }
@@ -1727,7 +1856,7 @@ int rgcn_layer1_backward_impl(const DGLMIGraph* graph,
     launch_rgcn_fused(true, fs->out_typed[0].indptr, fs->out_typed[0].indices, fs->out_typed[0].rows,
                       eids, w, grad_out->data, weight->data, K * X, 1, X,
                       grad_hidden ? grad_hidden->data : nullptr, static_cast<float*>(gy.ptr), N, R,
-                      K, s, nullptr, nullptr, loop ? loop->data : nullptr);
+                      K, s, nullptr, nullptr, loop ? loop->data : nullptr, graph->in_csr.num_rows);
     launch_gemm(hidden->data, 1, K, static_cast<float*>(gy.ptr), MG, 1, static_cast<float*>(gw.ptr),
                 K, MG, N, splits, static_cast<float*>(parts.ptr), s);
     if (!loop) {

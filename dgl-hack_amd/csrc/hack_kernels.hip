@@ -11,6 +11,7 @@
 // the C entries keep the library free of a second BLAS runtime in the caller's
 // process and use the kernel below -- these shapes (K, F <= a few hundred) are
 // bound by reading X and writing Y, not by the FMAs.
+#include <cstdlib>
 #include <stdexcept>
 
 #include "internal.h"
@@ -352,6 +353,22 @@ constexpr int kFusedWsFloats = 20480;
 constexpr int kTileGrab = 2;
 constexpr int kCtrStride = 32;
 
+// Lane u of each 16-lane row (DPP row_newbcast; u folds to a constant once unrolled):
+// what __shfl(v, u, 16) returns, without the ds_bpermute round trip through the LDS
+__device__ __forceinline__ int row_bcast16(int v, int u) {
+#if DGLMI_PROBES
+  return __shfl(v, u, 16);  // probe build: the round-3 walk (ds_bpermute), for A/B timing
+#endif
+  switch (u & 15) {
+#define DGLMI_RB(U) case U: return __builtin_amdgcn_update_dpp(0, v, 0x150 + U, 0xF, 0xF, false);
+    DGLMI_RB(0) DGLMI_RB(1) DGLMI_RB(2) DGLMI_RB(3) DGLMI_RB(4) DGLMI_RB(5) DGLMI_RB(6)
+    DGLMI_RB(7) DGLMI_RB(8) DGLMI_RB(9) DGLMI_RB(10) DGLMI_RB(11) DGLMI_RB(12) DGLMI_RB(13)
+    DGLMI_RB(14) DGLMI_RB(15)
+#undef DGLMI_RB
+  }
+  return 0;
+}
+
 // the slot's rows -> gy[v][t * 64 + c], gy rows `mats` blocks of 64 wide (the weight
 // gradients' operand: G_t per relation, then the tile's own rows for the self-loop)
 __device__ __forceinline__ void store_gy(const float* slot, float* gy, int64_t v0, int g, int q,
@@ -496,9 +513,10 @@ __global__ void __launch_bounds__(kGemmThreads) k_rgcn_fused(
           int rj[8];
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
-            const int c = __shfl(my_col, j0 + u, 16);
-            rj[u] = __shfl(my_row, j0 + u, 16);
-            wj[u] = __shfl(my_w, j0 + u, 16);
+            // the group's edge j0 + u: DPP row broadcasts (VALU, no LDS round trip)
+            const int c = row_bcast16(my_col, j0 + u);
+            rj[u] = row_bcast16(my_row, j0 + u);
+            wj[u] = __int_as_float(row_bcast16(__float_as_int(my_w), j0 + u));
             x[u] = *reinterpret_cast<const float4*>(T + static_cast<int64_t>(c) * kFusedW + 4 * q);
           }
 #pragma unroll
@@ -544,6 +562,221 @@ __global__ void __launch_bounds__(kGemmThreads) k_rgcn_fused(
         if (bias) v += bias[n];
         if (addend) v += addend[m * out_w + n];
         __builtin_nontemporal_store(v, out + m * out_w + n);
+      }
+    }
+  }
+}
+
+// The same fused layer-1 walk on 16-row tiles, 16 waves per CU (round 4).  The
+// 32-row kernel above holds one 8-wave block per CU: W (80 KB at 4 + 1 matrices of
+// 64 x 64) plus eight 8.3 KB slots fill the 160 KB LDS, so each SIMD has two waves to
+// cover the gathers' latency with (0.52 of 8 TB/s past L2, 24 % MFMA busy, waves
+// waiting 57 %).  Here a wave owns 16-row tiles and multiplies them by
+// v_mfma_f32_16x16x4_f32 (same f32 rate): its slot is 4 KB, so sixteen slots and W fit
+// one 1024-thread block -- four waves per SIMD, without re-walking the CSR.
+//  * Slots and W are XOR-swizzled by float4 (no padding: 159744 B of LDS), so the MFMA
+//    operand reads are conflict-free ds_read_b128: the k order inside the sum is
+//    permuted (lane group kq covers k = 16 kq + 4 s + j over the 16 instructions of a
+//    64-deep pass), which lets every lane take four k-steps of A and of B in one read.
+//  * W is stored transposed, Wt[t][n][k], for the same reason.
+//  * Two tiles per queue grab on the same eight queues (twice the tiles).
+// Everything else -- equal edge shares per 16-lane group with in-order carries, the
+// self-loop pass, gy stores, the epilogue -- is the 32-row kernel's.
+constexpr int kR16Threads = 1024;
+constexpr int kR16Grab = 4;
+
+// float index of (row, col) in a 16 x 64 swizzled slot / a 64-float Wt row
+__device__ __forceinline__ int swz(int row, int col) {
+  return ((((col >> 2) ^ row) & 15) << 2) | (col & 3) | (col & ~63);
+}
+
+template <bool BWD, int NB16>
+__global__ void __launch_bounds__(kR16Threads) k_rgcn_fused16(
+    const int32_t* __restrict__ ptr, const int32_t* __restrict__ cols,
+    const int32_t* __restrict__ rows, const int32_t* __restrict__ eids, const float* __restrict__ w,
+    const float* __restrict__ T, const float* __restrict__ W, int64_t ws_t, int64_t ws_k,
+    int64_t ws_n, float* __restrict__ out, float* __restrict__ gy, int64_t num_rows, int R,
+    int out_w, const float* __restrict__ bias, const float* __restrict__ addend,
+    const float* __restrict__ Lw, unsigned* __restrict__ tile_ctr) {
+  using f32x4 = __attribute__((ext_vector_type(4))) float;
+  constexpr int SW = NB16 * 16;  // output columns held (out_w rounded up to 32)
+  // row gathers in flight per lane: as many as fit 128 VGPRs without spills (the
+  // backward keeps more state live; hipcc -Rpass-analysis=kernel-resource-usage)
+  constexpr int GU = (!BWD && NB16 <= 4) ? 8 : ((BWD && NB16 == 8) ? 2 : 4);
+  __shared__ float Ws[kFusedWsFloats];
+  __shared__ float slots[16][16 * kFusedW];
+  __shared__ float carries[16][3][kFusedW];
+  const int RL = R + (Lw != nullptr);
+  // Wt[t][n][k] (k swizzled by float4 against n & 15)
+  for (int i = threadIdx.x; i < RL * kFusedW * SW; i += kR16Threads) {
+    const int t = i / (kFusedW * SW), k = (i / SW) % kFusedW, n = i % SW;
+    const float v = n >= out_w ? 0.0f
+                               : (t < R ? W[t * ws_t + k * ws_k + n * ws_n] : Lw[k * ws_k + n * ws_n]);
+    Ws[t * kFusedW * SW + n * kFusedW + swz(n & 15, k)] = v;
+  }
+  __syncthreads();  // the only block barrier
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int m = lane & 15, kq = lane >> 4;  // MFMA: A row / B, C column; k group
+  const int g = lane >> 4, q = lane & 15;   // gather: 16-lane group, float4 column
+  float* slot = slots[wv];
+  float* carry = carries[wv][0];
+  // the gathered table by a buffer resource: 32-bit byte offsets (the launcher takes this
+  // kernel for tables under 4 GiB), one VGPR per gather in flight instead of two
+  const __amdgpu_buffer_rsrc_t trs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(T), 0, -1, 0x00020000);
+  const int64_t tiles = (num_rows + 15) / 16;
+  const int nq = gridDim.x < 8 ? static_cast<int>(gridDim.x) : 8;
+  const int64_t qid = blockIdx.x % nq;
+  unsigned* ctr = tile_ctr + qid * kCtrStride;
+  const int64_t qtiles = tiles > qid ? (tiles - qid + nq - 1) / nq : 0;
+  for (int64_t k0 = 0;;) {
+    if ((k0 & (kR16Grab - 1)) == 0) {
+      unsigned tv = 0;
+      if (lane == 0) tv = atomicAdd(ctr, static_cast<unsigned>(kR16Grab));
+      k0 = static_cast<unsigned>(__builtin_amdgcn_readfirstlane(static_cast<int>(tv)));
+    }
+    if (k0 >= qtiles) break;
+    const int64_t tile = qid + nq * k0;
+    ++k0;
+    const int64_t v0 = tile * 16;
+    const int tile_rows = num_rows - v0 < 16 ? static_cast<int>(num_rows - v0) : 16;
+    f32x4 acc[NB16];
+#pragma unroll
+    for (int nb = 0; nb < NB16; ++nb) acc[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int t = 0; t < RL; ++t) {
+      if (t == R) {
+        // self-loop: the tile's own rows of T (coalesced), 4 rows per group
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = 4 * g + i;
+          const int64_t v = v0 + row;
+          const float4 a = v < num_rows ? *reinterpret_cast<const float4*>(T + v * kFusedW + 4 * q)
+                                        : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+          *reinterpret_cast<float4*>(slot + row * kFusedW + swz(row, 4 * q)) = a;
+        }
+      } else {
+        const int64_t base = static_cast<int64_t>(t) * num_rows + v0;
+        const int64_t pb = ptr[base], pe = ptr[base + tile_rows];
+        if (!BWD && pb == pe) continue;  // no relation-t edge into the tile
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = 4 * g + i;
+          *reinterpret_cast<float4*>(slot + row * kFusedW + swz(row, 4 * q)) =
+              make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        }
+        const int64_t share = (pe - pb + 3) / 4;
+        const int64_t gb = pb + g * share < pe ? pb + g * share : pe;
+        const int64_t ge = gb + share < pe ? gb + share : pe;
+        const bool cont = gb < ge && gb > pb && rows[gb - 1] == rows[gb];  // never group 0
+        bool first = true;
+        int crow = -1;
+        float4 a4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        int cur = -1;
+        auto flush = [&]() {
+          float* d = (first && cont) ? carry + (g - 1) * kFusedW + 4 * q
+                                     : slot + cur * kFusedW + swz(cur, 4 * q);
+          if (first && cont) crow = cur;
+          *reinterpret_cast<float4*>(d) = a4;
+          first = false;
+        };
+        for (int64_t p = gb; p < ge; p += 16) {
+          const int n = ge - p < 16 ? static_cast<int>(ge - p) : 16;
+          int my_col = 0, my_row = -1;
+          float my_w = 0.0f;
+          if (q < n) {
+            my_col = cols[p + q];
+            my_row = static_cast<int>(rows[p + q] - base);
+            my_w = w[eids ? eids[p + q] : p + q];
+          }
+#pragma unroll
+          for (int j0 = 0; j0 < 16; j0 += GU) {
+            float4 x[GU];
+            float wj[GU];
+            int rj[GU];
+#pragma unroll
+            for (int u = 0; u < GU; ++u) {
+              const int c = row_bcast16(my_col, j0 + u);
+              rj[u] = row_bcast16(my_row, j0 + u);
+              wj[u] = __int_as_float(row_bcast16(__float_as_int(my_w), j0 + u));
+              const uint32_t off = (static_cast<uint32_t>(c) * kFusedW + 4u * q) * 4u;
+              typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+              const u32x4v r4 = __builtin_amdgcn_raw_buffer_load_b128(trs, static_cast<int>(off), 0, 0);
+              x[u] = make_float4(__uint_as_float(r4.x), __uint_as_float(r4.y), __uint_as_float(r4.z),
+                                 __uint_as_float(r4.w));
+            }
+#pragma unroll
+            for (int u = 0; u < GU; ++u) {
+              if (rj[u] < 0) break;  // past the batch (group-uniform)
+              if (rj[u] != cur) {
+                if (cur >= 0) flush();
+                a4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                cur = rj[u];
+              }
+              a4.x += wj[u] * x[u].x;
+              a4.y += wj[u] * x[u].y;
+              a4.z += wj[u] * x[u].z;
+              a4.w += wj[u] * x[u].w;
+            }
+          }
+        }
+        if (cur >= 0) flush();
+        wave_lds_sync();
+        // carries into their rows, in group order (deterministic)
+#pragma unroll
+        for (int gg = 1; gg < 4; ++gg) {
+          const int cr = __builtin_amdgcn_readlane(crow, gg * 16);
+          if (cr >= 0) slot[cr * kFusedW + swz(cr, lane)] += carry[(gg - 1) * kFusedW + lane];
+        }
+      }
+      wave_lds_sync();
+      if constexpr (BWD) {
+        // the slot's rows -> gy[v][t * 64 + c] (the weight gradients' operand)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = 4 * g + i;
+          if (row >= tile_rows) break;
+          const float4 v = *reinterpret_cast<const float4*>(slot + row * kFusedW + swz(row, 4 * q));
+          float* d = gy + (v0 + row) * (static_cast<int64_t>(RL) * kFusedW) + t * kFusedW + 4 * q;
+          __builtin_nontemporal_store(v.x, d);
+          __builtin_nontemporal_store(v.y, d + 1);
+          __builtin_nontemporal_store(v.z, d + 2);
+          __builtin_nontemporal_store(v.w, d + 3);
+        }
+      }
+      if (out != nullptr) {
+        // acc[nb] += slot (16 x 64) . W_t (64 x 16 nb..): k = 16 kq + 4 s + j
+        const float* wt = Ws + t * kFusedW * SW;
+#pragma unroll 1
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int c = 16 * kq + 4 * s4;
+          const float4 a = *reinterpret_cast<const float4*>(slot + m * kFusedW + swz(m, c));
+#pragma unroll
+          for (int nb = 0; nb < NB16; ++nb) {
+            const int n = nb * 16 + m;
+            const float4 b = *reinterpret_cast<const float4*>(wt + n * kFusedW + swz(m, c));
+            acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc[nb], 0, 0, 0);
+            acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc[nb], 0, 0, 0);
+            acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc[nb], 0, 0, 0);
+            acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc[nb], 0, 0, 0);
+          }
+        }
+      }
+      wave_lds_sync();  // the slot is read; the next relation may overwrite it
+    }
+    if (out == nullptr) continue;  // BWD without grad_hidden: only gy was wanted
+    // C[row 4 kq + i][col nb * 16 + m]
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t mrow = v0 + 4 * kq + i;
+      if (mrow >= num_rows) continue;
+#pragma unroll
+      for (int nb = 0; nb < NB16; ++nb) {
+        const int n = nb * 16 + m;
+        if (n >= out_w) continue;
+        float v = acc[nb][i];
+        if (bias) v += bias[n];
+        if (addend) v += addend[mrow * out_w + n];
+        __builtin_nontemporal_store(v, out + mrow * out_w + n);
       }
     }
   }
@@ -681,6 +914,13 @@ bool try_tn(const float* A, int64_t a_rs, int64_t a_cs, const float* B, int64_t 
 
 }  // namespace
 
+// Tile height of the fused layer-1 kernels: 16 (k_rgcn_fused16, 16 waves per CU) or,
+// with DGLMI_RGCN_TILE=32, the 8-wave 32-row kernel (A/B and fallback).
+int rgcn_tile_rows() {
+  const char* e = std::getenv("DGLMI_RGCN_TILE");  // read per launch: tests switch it
+  return e != nullptr && std::atoi(e) == 32 ? 32 : 16;
+}
+
 bool rgcn_fused_ok(int64_t gathered_w, int64_t out_w, int64_t R) {
   if (gathered_w != kFusedW || out_w < 1 || out_w > 128 || R < 1) return false;
   const int64_t nb = out_w <= 32 ? 1 : (out_w <= 64 ? 2 : 4);
@@ -691,8 +931,10 @@ void launch_rgcn_fused(bool bwd, const int32_t* ptr, const int32_t* cols, const 
                        const int32_t* eids, const float* w, const float* T, const float* W,
                        int64_t ws_t, int64_t ws_k, int64_t ws_n, float* out, float* gy,
                        int64_t num_rows, int64_t R, int64_t out_w, hipStream_t s,
-                       const float* bias, const float* addend, const float* loop_w) {
+                       const float* bias, const float* addend, const float* loop_w,
+                       int64_t t_rows) {
   if (num_rows <= 0) return;
+  if (t_rows < 0) t_rows = num_rows;
   const int64_t tiles = (num_rows + 31) / 32;
   const int64_t want = (tiles + 7) / 8;
   const dim3 grid(static_cast<unsigned>(want < 256 ? want : 256)), block(kGemmThreads);
@@ -703,6 +945,29 @@ void launch_rgcn_fused(bool bwd, const int32_t* ptr, const int32_t* cols, const 
   if (hipMallocAsync(reinterpret_cast<void**>(&ctr), ctr_bytes, s) != hipSuccess ||
       hipMemsetAsync(ctr, 0, ctr_bytes, s) != hipSuccess)
     throw std::runtime_error("rgcn fused: tile counter allocation failed");
+  // gathered table T: the rows of the relation-major walk's columns (num_rows of them
+  // forward, the source rows backward: at most the larger of the two row counts)
+  if (rgcn_tile_rows() == 16 && (num_rows + 1) * kFusedW * 4 < (int64_t(1) << 32) &&
+      t_rows * kFusedW * 4 < (int64_t(1) << 32)) {
+    const int64_t t16 = (num_rows + 15) / 16;
+    const int64_t want16 = (t16 + 15) / 16;
+    const dim3 grid16(static_cast<unsigned>(want16 < 256 ? want16 : 256)), block16(kR16Threads);
+#define DGLMI_RGCN_FUSED16(B_, NB_)                                                               \
+  hipLaunchKernelGGL((k_rgcn_fused16<B_, NB_>), grid16, block16, 0, s, ptr, cols, rows, eids, w, T, \
+                     W, ws_t, ws_k, ws_n, out, gy, num_rows, Ri, ow, bias, addend, loop_w, ctr)
+    if (bwd) {
+      if (out_w <= 32) DGLMI_RGCN_FUSED16(true, 2);
+      else if (out_w <= 64) DGLMI_RGCN_FUSED16(true, 4);
+      else DGLMI_RGCN_FUSED16(true, 8);
+    } else {
+      if (out_w <= 32) DGLMI_RGCN_FUSED16(false, 2);
+      else if (out_w <= 64) DGLMI_RGCN_FUSED16(false, 4);
+      else DGLMI_RGCN_FUSED16(false, 8);
+    }
+#undef DGLMI_RGCN_FUSED16
+    (void)hipFreeAsync(ctr, s);
+    return;
+  }
 #define DGLMI_RGCN_FUSED(B_, NB_)                                                               \
   hipLaunchKernelGGL((k_rgcn_fused<B_, NB_>), grid, block, 0, s, ptr, cols, rows, eids, w, T, W, \
                      ws_t, ws_k, ws_n, out, gy, num_rows, Ri, ow, bias, addend, loop_w, ctr)

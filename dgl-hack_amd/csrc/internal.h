@@ -350,6 +350,12 @@ struct GatArgs {
   // edge's grad_er term at t[(t_off + position) * H + h]; NULL = not stored
   float* t;
   int64_t t_off;
+  // slope aggregates (DGLMIFusedGatForwardEx): the forward writes, per destination row
+  // and head, lf = sum_in a_e lrelu'(pre_e) ft[u] (N_dst, H, D) and ls = sum_in a_e
+  // lrelu'(pre_e) (N_dst, H); with them the backward's k_gat_stats also writes grad_er
+  // and no destination-side walk runs.  NULL = not kept.
+  float* lf;
+  float* ls;
 };
 bool gat_supported(int64_t H, int64_t D);
 int64_t gat_chunk_edges(int64_t nnz);
@@ -357,12 +363,16 @@ void launch_gat_forward(const GatArgs& a, hipStream_t s);
 void launch_gat_backward_dst(const GatArgs& a, hipStream_t s);
 void launch_gat_backward_src(const GatArgs& a, hipStream_t s);
 // stats[v, h] = {er, m, 1/l, <grad_out[v,h,:], out[v,h,:]>} for every destination row
-// (dense; replaces the destination-side walk's stats when gat_edge_pos is given)
+// (dense; replaces the destination-side walk's stats when gat_edge_pos is given); with
+// a.lf / a.ls (the forward's slope aggregates) also grad_er = <grad_out, lf> - delta ls
 void launch_gat_stats(const GatArgs& a, hipStream_t s);
 // out[r] = merge over blocks b of the unnormalised partials (out_part[b], m_part[b],
-// l_part[b]), normalised; m / l of the merged softmax (blocks in order)
+// l_part[b]), normalised; m / l of the merged softmax (blocks in order); lf / ls from
+// lf_part / ls_part the same way (all four NULL: none)
 void launch_gat_merge(const float* out_part, const float* m_part, const float* l_part, int nb,
-                      int64_t num_rows, int H, int D, float* out, float* m, float* l, hipStream_t s);
+                      int64_t num_rows, int H, int D, float* out, float* m, float* l, hipStream_t s,
+                      const float* lf_part = nullptr, const float* ls_part = nullptr,
+                      float* lf = nullptr, float* ls = nullptr);
 // l[i] = m[i] + log(l[i]) for i < n (one log-sum-exp per row and head)
 void launch_gat_fold_lse(const float* m, float* l, int64_t n, hipStream_t s);
 
@@ -387,7 +397,7 @@ void launch_rgcn_fused(bool bwd, const int32_t* ptr, const int32_t* cols, const 
                        int64_t ws_t, int64_t ws_k, int64_t ws_n, float* out, float* gy,
                        int64_t num_rows, int64_t R, int64_t out_w, hipStream_t s,
                        const float* bias = nullptr, const float* addend = nullptr,
-                       const float* loop_w = nullptr);
+                       const float* loop_w = nullptr, int64_t t_rows = -1);
 // out[i] += a[i], i < n
 void launch_add_into(float* out, const float* a, int64_t n, hipStream_t s);
 // out[p] = v[idx[p]]; out[p] = p

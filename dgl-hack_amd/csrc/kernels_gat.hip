@@ -24,6 +24,13 @@
 //   grad_ft[u] = sum_out a_e grad_out[v],  grad_el[u] = sum_out dpre
 //                              (out-CSR walk, src-owner)
 // Everything owner-computes: no atomics.
+//
+// Forward with the slope aggregates (GatArgs::lf / ls, DGLMIFusedGatForwardEx):
+// the same pass also keeps, per row and head,
+//   ls[v] = sum_in a_e lrelu'(pre_e),   lf[v] = sum_in a_e lrelu'(pre_e) ft[u]
+// (lrelu' = 1 or slope, so one more running sum beside out's, rescaled with it), and
+//   grad_er[v] = sum_in dpre_e = <grad_out[v], lf[v]> - delta_v ls[v]
+// becomes a dense per-row pass (k_gat_stats): the backward needs no in-CSR walk.
 #include "internal.h"
 
 #include <climits>
@@ -82,7 +89,8 @@ __device__ __forceinline__ float head_sum(float x, int d4) {
 // ---------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------
-template <int L, int NV, bool O32>
+// LS: also the slope aggregates lf / ls (carry record [acc F][m H][l H][lf F][ls H])
+template <int L, int NV, bool O32, bool LS>
 __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
   static_assert(L >= 1 && L <= 64, "a lane group must fit in one wavefront");
   constexpr int G = kBlock / L;
@@ -100,7 +108,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
   if (a.seg_cnt != nullptr && lane == 0) a.seg_cnt[chunk] = 0;  // the fixup's counters
   const int F4 = static_cast<int>(a.F / 4);
   const int H = a.H, D = a.D;
-  const int64_t CW = a.F + 2 * H;  // carry record: acc[F], m[H], l[H]
+  const int64_t CW = LS ? 2 * a.F + 3 * H : a.F + 2 * H;  // carry record, see above
   int hd[NV], fl[NV];
   bool ok4[NV], lead[NV];
 #pragma unroll
@@ -116,21 +124,25 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       if (ok4[v]) st4g(a.out + r * a.F + 4 * (lane + v * L), Z);
+      if (LS && ok4[v]) st4g(a.lf + r * a.F + 4 * (lane + v * L), Z);
       if (lead[v]) {
         a.m[r * H + hd[v]] = 0.0f;
         a.l[r * H + hd[v]] = 0.0f;
+        if (LS) a.ls[r * H + hd[v]] = 0.0f;
       }
     }
   };
   int64_t cur = a.rows[p0];
   bool cont = p0 > 0 && a.rows[p0 - 1] == cur;
-  float mx[NV], sm[NV], erv[NV];
-  float4 acc[NV];
+  float mx[NV], sm[NV], erv[NV], qs[NV];
+  float4 acc[NV], qa[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     mx[v] = kNegInf;
     sm[v] = 0.0f;
     acc[v] = Z;
+    qs[v] = 0.0f;
+    qa[v] = Z;
     erv[v] = ok4[v] ? a.er[cur * H + hd[v]] : 0.0f;
   }
   // write a finished / partial row.  final: normalise; else raw (m, l, acc)
@@ -142,20 +154,27 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
       if (is_cont) {
         float* c = a.carry + chunk * CW;
         st4g(c + 4 * f4, acc[v]);
+        if (LS) st4g(c + a.F + 2 * H + 4 * f4, qa[v]);
         if (lead[v]) {
           c[a.F + hd[v]] = mx[v];
           c[a.F + H + hd[v]] = sm[v];
+          if (LS) c[2 * a.F + 2 * H + hd[v]] = qs[v];
         }
       } else {
-        float4 o = acc[v];
+        float4 o = acc[v], q = qa[v];
+        float qsv = qs[v];
         if (final && !a.raw) {
           const float inv = sm[v] > 0.0f ? 1.0f / sm[v] : 0.0f;
           o = make_float4(o.x * inv, o.y * inv, o.z * inv, o.w * inv);
+          q = make_float4(q.x * inv, q.y * inv, q.z * inv, q.w * inv);
+          qsv *= inv;
         }
         st4g(a.out + r * a.F + 4 * f4, o);
+        if (LS) st4g(a.lf + r * a.F + 4 * f4, q);
         if (lead[v]) {
           a.m[r * H + hd[v]] = mx[v];
           a.l[r * H + hd[v]] = sm[v];
+          if (LS) a.ls[r * H + hd[v]] = qsv;
         }
       }
     }
@@ -198,16 +217,23 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
             mx[v] = kNegInf;
             sm[v] = 0.0f;
             acc[v] = Z;
+            qs[v] = 0.0f;
+            qa[v] = Z;
             erv[v] = ok4[v] ? a.er[cur * H + hd[v]] : 0.0f;
           }
         }
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
-          const float s = leaky(elv[u][v] + erv[v], a.slope);
+          const float pre = elv[u][v] + erv[v];
+          const float s = leaky(pre, a.slope);
           if (s > mx[v]) {
             const float sc = fexp(mx[v] - s);
             acc[v] = make_float4(acc[v].x * sc, acc[v].y * sc, acc[v].z * sc, acc[v].w * sc);
             sm[v] *= sc;
+            if (LS) {
+              qa[v] = make_float4(qa[v].x * sc, qa[v].y * sc, qa[v].z * sc, qa[v].w * sc);
+              qs[v] *= sc;
+            }
             mx[v] = s;
           }
           const float pe = fexp(s - mx[v]);
@@ -215,6 +241,12 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
           acc[v] = make_float4(acc[v].x + pe * x.x, acc[v].y + pe * x.y, acc[v].z + pe * x.z,
                                acc[v].w + pe * x.w);
           sm[v] += pe;
+          if (LS) {
+            const float pd = pe * dleaky(pre, a.slope);
+            qa[v] = make_float4(qa[v].x + pd * x.x, qa[v].y + pd * x.y, qa[v].z + pd * x.z,
+                                qa[v].w + pd * x.w);
+            qs[v] += pd;
+          }
         }
       }
     }
@@ -225,7 +257,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
   fill_empty_rows(a.indptr, a.num_rows, chunk, (a.nnz + K - 1) / K, L, lane, zero_row);
 }
 
-template <int L, int NV>
+template <int L, int NV, bool LS>
 __global__ void __launch_bounds__(kBlock) k_gat_fwd_fixup(GatArgs a) {
   static_assert(L >= 1 && L <= 64, "a lane group must fit in one wavefront");
   constexpr int G = kBlock / L;
@@ -246,9 +278,11 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_fixup(GatArgs a) {
   const int64_t cend = nseg == 1 ? last : (chunk + kFixSeg - 1 < last ? chunk + kFixSeg - 1 : last);
   const int F4 = static_cast<int>(a.F / 4);
   const int H = a.H;
-  const int64_t CW = a.F + 2 * H;
-  // online-softmax merge of carry record c into (acc, mx, sm)
-  auto merge = [&](float4& acc, float& mx, float& sm, int64_t c, int f4, int h) {
+  const int64_t CW = LS ? 2 * a.F + 3 * H : a.F + 2 * H;
+  // online-softmax merge of carry record c into (acc, mx, sm) (and the slope
+  // aggregates (qa, qs), rescaled by the same factors)
+  auto merge = [&](float4& acc, float& mx, float& sm, float4& qa, float& qs, int64_t c, int f4,
+                   int h) {
     const float* cr = a.carry + c * CW;
     const float4 ca = ld4g(cr + 4 * f4);
     const float cm = cr[a.F + h], cl = cr[a.F + H + h];
@@ -257,6 +291,12 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_fixup(GatArgs a) {
     acc = make_float4(acc.x * f1 + ca.x * f2, acc.y * f1 + ca.y * f2, acc.z * f1 + ca.z * f2,
                       acc.w * f1 + ca.w * f2);
     sm = sm * f1 + cl * f2;
+    if (LS) {
+      const float4 cq = ld4g(cr + a.F + 2 * H + 4 * f4);
+      qa = make_float4(qa.x * f1 + cq.x * f2, qa.y * f1 + cq.y * f2, qa.z * f1 + cq.z * f2,
+                       qa.w * f1 + cq.w * f2);
+      qs = qs * f1 + cr[2 * a.F + 2 * H + h] * f2;
+    }
     mx = mn;
   };
   if (nseg > 1) {
@@ -268,11 +308,15 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_fixup(GatArgs a) {
       float* cr = a.carry + chunk * CW;
       float4 acc = ld4g(cr + 4 * f4);
       float mx = cr[a.F + h], sm = cr[a.F + H + h];
-      for (int64_t c = chunk + 1; c <= cend; ++c) merge(acc, mx, sm, c, f4, h);
+      float4 qa = LS ? ld4g(cr + a.F + 2 * H + 4 * f4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      float qs = LS ? cr[2 * a.F + 2 * H + h] : 0.0f;
+      for (int64_t c = chunk + 1; c <= cend; ++c) merge(acc, mx, sm, qa, qs, c, f4, h);
       st4g(cr + 4 * f4, acc);
+      if (LS) st4g(cr + a.F + 2 * H + 4 * f4, qa);
       if ((4 * f4) % a.D == 0) {
         cr[a.F + h] = mx;
         cr[a.F + H + h] = sm;
+        if (LS) cr[2 * a.F + 2 * H + h] = qs;
       }
     }
     if (!seg_arrive_last(a.seg_cnt + first, nseg, L, lane)) return;
@@ -284,15 +328,19 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_fixup(GatArgs a) {
     const int h = (4 * f4) / a.D;
     float4 acc = ld4g(a.out + r * a.F + 4 * f4);
     float mx = a.m[r * H + h], sm = a.l[r * H + h];
+    float4 qa = LS ? ld4g(a.lf + r * a.F + 4 * f4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float qs = LS ? a.ls[r * H + h] : 0.0f;
     if (nseg > 1)
-      for (int64_t sg = 0; sg < nseg; ++sg) merge(acc, mx, sm, first + sg * kFixSeg, f4, h);
+      for (int64_t sg = 0; sg < nseg; ++sg) merge(acc, mx, sm, qa, qs, first + sg * kFixSeg, f4, h);
     else
-      for (int64_t c = first; c <= last; ++c) merge(acc, mx, sm, c, f4, h);
+      for (int64_t c = first; c <= last; ++c) merge(acc, mx, sm, qa, qs, c, f4, h);
     const float inv = a.raw ? 1.0f : (sm > 0.0f ? 1.0f / sm : 0.0f);
     st4g(a.out + r * a.F + 4 * f4, make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv));
+    if (LS) st4g(a.lf + r * a.F + 4 * f4, make_float4(qa.x * inv, qa.y * inv, qa.z * inv, qa.w * inv));
     if ((4 * f4) % a.D == 0) {
       a.m[r * H + h] = mx;
       a.l[r * H + h] = sm;
+      if (LS) a.ls[r * H + h] = qs * inv;
     }
   }
 }
@@ -626,12 +674,17 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_fixup(GatArgs a, float* vec_
 
 // Merge the unnormalised per-block softmax partials of a column-blocked forward
 // (blocks in order; a block that saw no edge of the row has l = 0 and is skipped).
+// lf_part / ls_part (may be NULL): the blocks' raw slope aggregates, merged into lf / ls
+// with the same factors.
 __global__ void __launch_bounds__(kBlock) k_gat_merge(const float* __restrict__ out_part,
                                                      const float* __restrict__ m_part,
                                                      const float* __restrict__ l_part, int nb,
                                                      int64_t num_rows, int H, int D,
                                                      float* __restrict__ out, float* __restrict__ m,
-                                                     float* __restrict__ l) {
+                                                     float* __restrict__ l,
+                                                     const float* __restrict__ lf_part,
+                                                     const float* __restrict__ ls_part,
+                                                     float* __restrict__ lf, float* __restrict__ ls) {
   const int64_t F = static_cast<int64_t>(H) * D;
   const int64_t F4 = F / 4;
   const int64_t total = num_rows * F4;
@@ -640,31 +693,42 @@ __global__ void __launch_bounds__(kBlock) k_gat_merge(const float* __restrict__ 
     const int64_t r = i / F4;
     const int f4 = static_cast<int>(i - r * F4);
     const int h = (4 * f4) / D;
-    float mx = kNegInf, sm = 0.0f;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    float mx = kNegInf, sm = 0.0f, qs = 0.0f;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f), qa = acc;
     for (int b = 0; b < nb; ++b) {
       const int64_t hi = (static_cast<int64_t>(b) * num_rows + r) * H + h;
       const float lb = l_part[hi];
       if (!(lb > 0.0f)) continue;
       const float mb = m_part[hi];
-      const float4 ab = ld4g(out_part + (static_cast<int64_t>(b) * num_rows + r) * F + 4 * f4);
+      const int64_t vi = (static_cast<int64_t>(b) * num_rows + r) * F + 4 * f4;
+      const float4 ab = ld4g(out_part + vi);
       const float mn = fmaxf(mx, mb);
       const float f1 = expf(mx - mn), f2 = expf(mb - mn);
       acc = make_float4(acc.x * f1 + ab.x * f2, acc.y * f1 + ab.y * f2, acc.z * f1 + ab.z * f2,
                         acc.w * f1 + ab.w * f2);
       sm = sm * f1 + lb * f2;
+      if (lf_part != nullptr) {
+        const float4 qb = ld4g(lf_part + vi);
+        qa = make_float4(qa.x * f1 + qb.x * f2, qa.y * f1 + qb.y * f2, qa.z * f1 + qb.z * f2,
+                         qa.w * f1 + qb.w * f2);
+        qs = qs * f1 + ls_part[hi] * f2;
+      }
       mx = mn;
     }
     const float inv = sm > 0.0f ? 1.0f / sm : 0.0f;
     st4g(out + r * F + 4 * f4, make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv));
+    if (lf_part != nullptr)
+      st4g(lf + r * F + 4 * f4, make_float4(qa.x * inv, qa.y * inv, qa.z * inv, qa.w * inv));
     if ((4 * f4) % D == 0) {
       m[r * H + h] = sm > 0.0f ? mx : 0.0f;
       l[r * H + h] = sm;
+      if (lf_part != nullptr) ls[r * H + h] = qs * inv;
     }
   }
 }
 
-// Destination stats without a destination-side walk (edge-position backward): one
+// Destination stats without a destination-side walk (edge-position backward, and the
+// backward after a forward with slope aggregates, which also gets grad_er here): one
 // thread per float4 slot of a row, the head's D4 slots adjacent and aligned in the
 // wavefront, so delta is reduced by the same head_sum as the destination walk's
 // (bit-identical stats).  Every lane reaches the shuffles (no early exit).
@@ -682,10 +746,14 @@ __global__ void k_gat_stats(GatArgs a) {
     const float4 g = ok ? ld4g(a.go + r * a.F + 4 * f4) : Z;
     const float4 o = ok ? ld4g(a.fo + r * a.F + 4 * f4) : Z;
     const float d = head_sum(dot4(g, o), D4);
+    // with the forward's slope aggregates: grad_er = <grad_out, lf> - delta ls (no walk)
+    const float4 q = (a.lf != nullptr && ok) ? ld4g(a.lf + r * a.F + 4 * f4) : Z;
+    const float e = a.lf != nullptr ? head_sum(dot4(g, q), D4) : 0.0f;
     if (ok && f4 % D4 == 0) {
       const int64_t j = r * a.H + f4 / D4;
       const float l = a.l_in[j];
       a.stats[j] = make_float4(a.er[j], a.m_in[j], l > 0.0f ? 1.0f / l : 0.0f, d);
+      if (a.lf != nullptr) a.g_er[j] = e - d * a.ls[j];
     }
   }
 }
@@ -709,11 +777,19 @@ void fwd_cfg(const GatArgs& a, hipStream_t s) {
   constexpr int G = kBlock / L;
   const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
   const unsigned blocks = static_cast<unsigned>((chunks + G - 1) / G);
-  if (a.o32)
-    hipLaunchKernelGGL((k_gat_fwd<L, NV, true>), dim3(blocks), dim3(kBlock), 0, s, a);
-  else
-    hipLaunchKernelGGL((k_gat_fwd<L, NV, false>), dim3(blocks), dim3(kBlock), 0, s, a);
-  if (chunks > 1) hipLaunchKernelGGL((k_gat_fwd_fixup<L, NV>), dim3(blocks), dim3(kBlock), 0, s, a);
+  const bool ls = a.lf != nullptr;
+#define DGLMI_GAT_FWD(O_, LS_) \
+  hipLaunchKernelGGL((k_gat_fwd<L, NV, O_, LS_>), dim3(blocks), dim3(kBlock), 0, s, a)
+  if (a.o32) {
+    if (ls) DGLMI_GAT_FWD(true, true); else DGLMI_GAT_FWD(true, false);
+  } else {
+    if (ls) DGLMI_GAT_FWD(false, true); else DGLMI_GAT_FWD(false, false);
+  }
+#undef DGLMI_GAT_FWD
+  if (chunks > 1) {
+    if (ls) hipLaunchKernelGGL((k_gat_fwd_fixup<L, NV, true>), dim3(blocks), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((k_gat_fwd_fixup<L, NV, false>), dim3(blocks), dim3(kBlock), 0, s, a);
+  }
 }
 
 template <int L, int NV>
@@ -773,13 +849,14 @@ int64_t gat_chunk_edges(int64_t nnz) { return fast_chunk_edges(nnz, 64); }
 
 void launch_gat_forward(const GatArgs& a, hipStream_t s) { DGLMI_GAT_DISPATCH(fwd_cfg, a, s); }
 void launch_gat_merge(const float* out_part, const float* m_part, const float* l_part, int nb,
-                      int64_t num_rows, int H, int D, float* out, float* m, float* l, hipStream_t s) {
+                      int64_t num_rows, int H, int D, float* out, float* m, float* l, hipStream_t s,
+                      const float* lf_part, const float* ls_part, float* lf, float* ls) {
   const int64_t total = num_rows * (static_cast<int64_t>(H) * D / 4);
   if (total <= 0) return;
   const int64_t want = (total + kBlock - 1) / kBlock;
   const unsigned blocks = static_cast<unsigned>(want < 65536 ? want : 65536);
   hipLaunchKernelGGL(k_gat_merge, dim3(blocks), dim3(kBlock), 0, s, out_part, m_part, l_part, nb,
-                     num_rows, H, D, out, m, l);
+                     num_rows, H, D, out, m, l, lf_part, ls_part, lf, ls);
 }
 // l[i] = m[i] + log(l[i]): the softmax state of a row as one log-sum-exp, so the
 // backward's attention exp(s - m) / l becomes exp(s - lse) / 1 (the reference-order

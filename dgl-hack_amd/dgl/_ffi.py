@@ -176,6 +176,15 @@ _SIGS = {
         ctypes.c_float, ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.c_void_p]),
+    "DGLMIFusedGatForwardEx": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_float, ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.c_void_p]),
+    "DGLMIFusedGatBackwardEx": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_float, ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.c_void_p]),
     "DGLMIFusedGatKernel": (ctypes.c_int, [
         ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.c_float,

@@ -17,6 +17,8 @@ and its PyTorch implementation (``backend/pytorch/tensor.py:291-381,
 """
 from __future__ import annotations
 
+import os
+
 import torch as th
 
 from . import kernel as K
@@ -371,7 +373,11 @@ def gcn_norm_aggregate(gidx, x, norm, bias=None, n_dst=None):
 
 
 class FusedGat(th.autograd.Function):
-    """tensor.py:383-413 (FusedGat), max-stabilised and without per-edge buffers."""
+    """tensor.py:383-413 (FusedGat), max-stabilised and without per-edge buffers.  When
+    a gradient will be wanted, the forward also keeps the attention's slope aggregates
+    (DGLMIFusedGatForwardEx: N x H x D + N x H floats), and the backward is a dense pass
+    plus the source-side walk -- no destination-side walk.
+    DGLMI_GAT_SLOPES=0 keeps the round-3 backward (destination walk / edge positions)."""
 
     @staticmethod
     def forward(ctx, gidx, feat_src, el, er, slope):
@@ -381,20 +387,30 @@ class FusedGat(th.autograd.Function):
         out = feat_src.new_empty((n_dst, H, D))
         mx = feat_src.new_empty((n_dst, H))
         sm = feat_src.new_empty((n_dst, H))
-        K.fused_gat_forward(gidx, feat_src, el, er, slope, out, mx, sm)
+        lf = ls = None
+        if any(ctx.needs_input_grad[1:4]) and os.environ.get("DGLMI_GAT_SLOPES", "1") != "0":
+            lf = feat_src.new_empty((n_dst, H, D))
+            ls = feat_src.new_empty((n_dst, H))
+        K.fused_gat_forward(gidx, feat_src, el, er, slope, out, mx, sm, lf, ls)
         ctx.gidx, ctx.slope = gidx, slope
-        ctx.save_for_backward(feat_src, el, er, out, mx, sm)
+        ctx.slopes = lf is not None
+        if lf is not None:
+            ctx.save_for_backward(feat_src, el, er, out, mx, sm, lf, ls)
+        else:
+            ctx.save_for_backward(feat_src, el, er, out, mx, sm)
         return out
 
     @staticmethod
     def backward(ctx, grad_out):
-        feat_src, el, er, out, mx, sm = ctx.saved_tensors
+        saved = ctx.saved_tensors
+        feat_src, el, er, out, mx, sm = saved[:6]
+        lf, ls = saved[6:] if ctx.slopes else (None, None)
         grad_out = grad_out.contiguous()
         g_ft = th.empty_like(feat_src)
         g_el = th.empty_like(el)
         g_er = th.empty_like(er)
         K.fused_gat_backward(ctx.gidx, feat_src, el, er, ctx.slope, out, mx, sm, grad_out, g_ft,
-                             g_el, g_er)
+                             g_el, g_er, lf, ls)
         return None, g_ft, g_el, g_er, None
 
 

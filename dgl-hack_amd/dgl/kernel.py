@@ -314,25 +314,42 @@ def _gat_bwd_cgraph(graph, feat_src):
     return graph.cstruct(None, col_blocks=nb, edge_pos=gat_edge_pos(graph, nb))
 
 
-def fused_gat_forward(graph, feat_src, el, er, slope, out, max_out, sum_out):
-    """_CAPI_DGLFusedGatKernel (binary_reduce.cc:380-396) -> DGLMIFusedGatForward."""
+def fused_gat_forward(graph, feat_src, el, er, slope, out, max_out, sum_out, slope_feat=None,
+                      slope_sum=None):
+    """_CAPI_DGLFusedGatKernel (binary_reduce.cc:380-396) -> DGLMIFusedGatForward, or
+    with ``slope_feat`` (N, H, D) / ``slope_sum`` (N, H) DGLMIFusedGatForwardEx: the
+    forward also keeps the attention's slope aggregates, so the backward needs no
+    destination-side walk."""
     _check_ctx(graph, [("feat_src", feat_src), ("el", el), ("er", er), ("out", out)])
     g = graph.cstruct(None, col_blocks=gat_col_blocks(graph, feat_src))
-    check_call(_ffi.lib().DGLMIFusedGatForward(
-        ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"),
-        float(slope), _arr(out, "out"), _arr(max_out, "max_out"), _arr(sum_out, "sum_out"),
-        _stream(out)))
+    args = [ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"),
+            float(slope), _arr(out, "out"), _arr(max_out, "max_out"), _arr(sum_out, "sum_out")]
+    if slope_feat is None:
+        check_call(_ffi.lib().DGLMIFusedGatForward(*args, _stream(out)))
+    else:
+        check_call(_ffi.lib().DGLMIFusedGatForwardEx(
+            *args, _arr(slope_feat, "slope_feat"), _arr(slope_sum, "slope_sum"), _stream(out)))
     return out
 
 
 def fused_gat_backward(graph, feat_src, el, er, slope, out, max_in, sum_in, grad_out,
-                       grad_feat_src, grad_el, grad_er):
-    """_CAPI_DGLKernelBackwardFusedGat (binary_reduce.cc:529-549) -> DGLMIFusedGatBackward."""
+                       grad_feat_src, grad_el, grad_er, slope_feat=None, slope_sum=None):
+    """_CAPI_DGLKernelBackwardFusedGat (binary_reduce.cc:529-549) -> DGLMIFusedGatBackward
+    (or DGLMIFusedGatBackwardEx with the forward's slope aggregates)."""
     _check_ctx(graph, [("feat_src", feat_src), ("grad_out", grad_out)])
-    g = _gat_bwd_cgraph(graph, feat_src)
-    check_call(_ffi.lib().DGLMIFusedGatBackward(
+    if slope_feat is None:
+        g = _gat_bwd_cgraph(graph, feat_src)
+        check_call(_ffi.lib().DGLMIFusedGatBackward(
+            ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"),
+            float(slope), _arr(out, "out"), _arr(max_in, "max_in"), _arr(sum_in, "sum_in"),
+            _arr(grad_out, "grad_out"), _arr(grad_feat_src, "grad_feat_src"),
+            _arr(grad_el, "grad_el"), _arr(grad_er, "grad_er"), _stream(grad_out)))
+        return
+    g = graph.cstruct(None, col_blocks=gat_col_blocks(graph, feat_src, backward=True))
+    check_call(_ffi.lib().DGLMIFusedGatBackwardEx(
         ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"), float(slope),
         _arr(out, "out"), _arr(max_in, "max_in"), _arr(sum_in, "sum_in"),
+        _arr(slope_feat, "slope_feat"), _arr(slope_sum, "slope_sum"),
         _arr(grad_out, "grad_out"), _arr(grad_feat_src, "grad_feat_src"), _arr(grad_el, "grad_el"),
         _arr(grad_er, "grad_er"), _stream(grad_out)))
 

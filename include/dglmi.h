@@ -291,6 +291,26 @@ int DGLMIFusedGatBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src, c
                           const DGLMIArray* max_in, const DGLMIArray* sum_in,
                           const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
                           DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream);
+/* Extension: the forward also keeps, per destination row v and head h, the slope
+ * aggregates of the attention (lrelu' = 1 where the logit's pre-activation el + er is
+ * positive, else the negative slope):
+ *   slope_sum[v, h]     = sum_{e into v} a_e * lrelu'(pre_e)                 (N_dst, H)
+ *   slope_feat[v, h, :] = sum_{e into v} a_e * lrelu'(pre_e) * feat_src[u, h, :]  (N_dst, H, D)
+ * (16-byte aligned), one more running sum beside the output's.  Handed to
+ * DGLMIFusedGatBackwardEx they give grad_er[v, h] = <grad_out[v, h], slope_feat[v, h]>
+ * - delta[v, h] * slope_sum[v, h] (delta = <grad_out[v, h], out[v, h]>) from one dense
+ * pass: the backward runs only the source-side walk over the out-CSR. */
+int DGLMIFusedGatForwardEx(const DGLMIGraph* graph, const DGLMIArray* feat_src, const DGLMIArray* el,
+                           const DGLMIArray* er, float negative_slope, DGLMIArray* out,
+                           DGLMIArray* max_out, DGLMIArray* sum_out, DGLMIArray* slope_feat,
+                           DGLMIArray* slope_sum, void* stream);
+int DGLMIFusedGatBackwardEx(const DGLMIGraph* graph, const DGLMIArray* feat_src,
+                            const DGLMIArray* el, const DGLMIArray* er, float negative_slope,
+                            const DGLMIArray* out, const DGLMIArray* max_in,
+                            const DGLMIArray* sum_in, const DGLMIArray* slope_feat,
+                            const DGLMIArray* slope_sum, const DGLMIArray* grad_out,
+                            DGLMIArray* grad_feat_src, DGLMIArray* grad_el, DGLMIArray* grad_er,
+                            void* stream);
 /* The same two kernels in the reference's argument order, for a binding of the hack's
  * PackedFuncs that keeps its Python caller unchanged (tensor.py:383-420):
  *   _CAPI_DGLFusedGatKernel(G, feat_src, el, er, sum, exp, ret, slope)
@@ -300,8 +320,11 @@ int DGLMIFusedGatBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src, c
  * caller-allocated state passed from the forward to the backward unchanged; their
  * contents are this library's softmax state, not the hack's per-edge exponentials:
  * when E >= N_dst, exp's first N_dst * H floats keep the running max and sum the sum
- * of exp(s - max) (bit-identical to DGLMIFusedGatForward / Backward); otherwise sum
- * keeps max + log(sum) and exp is not touched.  ret (N_dst, H, D) is overwritten, and
+ * of exp(s - max) (bit-identical to DGLMIFusedGatForward / Backward), and when also
+ * E >= about N_dst * (D + 2) (a 16-byte aligned exp), the slope aggregates of
+ * DGLMIFusedGatForwardEx follow the max in exp (from float round_up(N_dst * H, 4)) and
+ * the backward skips its destination-side walk; otherwise sum keeps max + log(sum)
+ * and exp is not touched.  ret (N_dst, H, D) is overwritten, and
  * the three gradients are overwritten (the hack's caller zero-fills them first). */
 int DGLMIFusedGatKernel(const DGLMIGraph* graph, const DGLMIArray* feat_src, const DGLMIArray* el,
                         const DGLMIArray* er, DGLMIArray* sum, DGLMIArray* exp, DGLMIArray* ret,

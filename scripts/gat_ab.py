@@ -60,21 +60,26 @@ def run(args):
     for blocks in (os.environ.get("GAT_AB_BLOCKS", "auto 1")).split():
         if blocks != "auto":
             os.environ["DGLMI_GAT_BLOCKS"] = blocks
-        # GAT_AB_POS: the backward's edge-position path (1) and destination-side walk (0)
-        for pos in (os.environ.get("GAT_AB_POS", "1")).split():
-            os.environ["DGLMI_GAT_EDGE_POS"] = pos
-            key = blocks if pos == "1" else blocks + "_dstwalk"
-            fwd = lambda: K.fused_gat_forward(gidx, ft, el, er, 0.2, out, mx, sm)
-            bwd = lambda: K.fused_gat_backward(gidx, ft, el, er, 0.2, out, mx, sm, go, gft, gel, ger)
+        # GAT_AB_POS: the backward's edge-position path (1), destination-side walk (0), or
+        # the forward's slope aggregates and no destination walk at all ("slopes")
+        lf, ls = th.empty_like(out), th.empty_like(mx)
+        for pos in (os.environ.get("GAT_AB_POS", "slopes 1")).split():
+            os.environ["DGLMI_GAT_EDGE_POS"] = "1" if pos == "slopes" else pos
+            key = blocks + {"slopes": "_slopes", "1": "", "0": "_dstwalk"}[pos]
+            sl = (lf, ls) if pos == "slopes" else (None, None)
+            fwd = lambda: K.fused_gat_forward(gidx, ft, el, er, 0.2, out, mx, sm, *sl)
+            bwd = lambda: K.fused_gat_backward(gidx, ft, el, er, 0.2, out, mx, sm, go, gft, gel, ger,
+                                               *sl)
             res["fwd_ms_" + key] = ev_time(fwd)
             res["bwd_ms_" + key] = ev_time(bwd)
             fwd()
             bwd()
             th.cuda.synchronize()
             saved[key] = [t.cpu().clone() for t in (out, mx, sm, gft, gel, ger)]
-            if key.endswith("_dstwalk") and blocks in saved:
+            if key != blocks and blocks in saved:
                 d = (saved[key][5].double() - saved[blocks][5].double()).abs()
-                res["g_er_maxabs_pos_vs_dstwalk_" + blocks] = float(d.max())
+                res["g_er_maxabs_%s_vs_pos" % key] = float(d.max())
+                res["g_ft_equal_%s_vs_pos" % key] = bool(th.equal(saved[key][3], saved[blocks][3]))
     os.environ.pop("DGLMI_GAT_BLOCKS", None)
     os.environ.pop("DGLMI_GAT_EDGE_POS", None)
     if args.save:

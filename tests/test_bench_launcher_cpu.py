@@ -74,3 +74,63 @@ def test_side_line_failure_sets_status_and_list():
     assert res["value"] == 1.0 and res["n_gpus"] == 2
     assert "injected side-line failure" in res["c4"]["error"]
     assert [e["line"] for e in res["side_line_errors"]] == ["c4"]
+
+
+def _bench():
+    sys.path.insert(0, ROOT)
+    import bench
+    return bench
+
+
+def test_pmc_child_env_pins_the_rank_gpu(monkeypatch):
+    """The PMC child of rank r sees only rank r's GPU, through the chain of visibility
+    variables the rank itself sees (ROCR_VISIBLE_DEVICES, then HIP_/CUDA_VISIBLE_DEVICES)."""
+    b = _bench()
+    for k in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    monkeypatch.setenv("RANK", "2")
+    env = b._child_device_env(2)
+    assert env["ROCR_VISIBLE_DEVICES"] == "2" and "WORLD_SIZE" not in env and "RANK" not in env
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "4,5,6,7")
+    assert b._child_device_env(1)["ROCR_VISIBLE_DEVICES"] == "5"
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "3,2")
+    env = b._child_device_env(0)
+    assert env["ROCR_VISIBLE_DEVICES"] == "7" and "HIP_VISIBLE_DEVICES" not in env
+
+
+def test_pmc_phases_by_dispatch_order():
+    """Each pass: 3 M1 launch pairs (reduce + fixup) then 3 calibration pairs; the
+    phases come from dispatch order, whatever the grid sizes."""
+    b = _bench()
+    rows = []
+    for p in range(2):
+        d = 100 * p
+        for phase_val in (10.0, 1.0):            # m1 launches, then calibration
+            for _ in range(3):
+                rows.append((p, d, True, "FETCH_SIZE", phase_val))
+                rows.append((p, d + 1, False, "FETCH_SIZE", phase_val / 10))
+                d += 2
+    vals = b.pmc_phase_values(rows, 2)
+    assert sorted(vals[("m1", "FETCH_SIZE")]) == sorted([10.0] * 6 + [1.0] * 6)
+    assert sorted(vals[("cal", "FETCH_SIZE")]) == sorted([1.0] * 6 + [0.1] * 6)
+
+
+def test_configs_run_isolated(tmp_path):
+    """measure_configs: every config in a child process of its own under a time limit --
+    a crash, a stall or garbage is recorded under its key and the others still run."""
+    b = _bench()
+    stub = tmp_path / "stub.py"
+    stub.write_text(
+        "import json, sys, time\n"
+        "name = sys.argv[sys.argv.index('--configs') + 1]\n"
+        "if name == 'crash': raise RuntimeError('boom')\n"
+        "if name == 'hang': time.sleep(60)\n"
+        "print(json.dumps({'config': name, 'ms': 1.0}))\n")
+    t0 = __import__("time").time()
+    out = b.measure_configs("cpu", budgets=(("crash", 20), ("hang", 3), ("ok", 20)),
+                            script=str(stub))
+    assert "boom" in out["crash"]["error"]
+    assert out["hang"]["error"] == "exceeded 3 s"
+    assert out["ok"]["config"] == "ok" and out["ok"]["ms"] == 1.0
+    assert __import__("time").time() - t0 < 40

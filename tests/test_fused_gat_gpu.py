@@ -122,12 +122,15 @@ def test_fused_gat_deterministic():
     assert th.equal(B.fused_gat(g, ft, el, er, 0.2), B.fused_gat(g, ft, el, er, 0.2))
 
 
-@pytest.mark.parametrize("nb", [2, 4, 8])
-def test_fused_gat_column_blocks_vs_dense(nb, monkeypatch):
+@pytest.mark.parametrize("nb,slopes", [(2, "1"), (4, "1"), (8, "1"), (4, "0"), (8, "0")])
+def test_fused_gat_column_blocks_vs_dense(nb, slopes, monkeypatch):
     """Column-blocked launches (DGLMIGraph.num_col_blocks): per-block softmax
-    partials merged in block order (forward), gradients accumulated block by block
-    (backward), against the fp64 restatement, incl. rows empty in some blocks."""
+    partials merged in block order (forward; with the slope aggregates merged the
+    same way), gradients accumulated block by block (backward: the source-side walk
+    only, or -- slopes "0" -- the destination-side walk too), against the fp64
+    restatement, incl. rows empty in some blocks."""
     monkeypatch.setenv("DGLMI_GAT_BLOCKS", str(nb))
+    monkeypatch.setenv("DGLMI_GAT_SLOPES", slopes)
     src, dst, n = powerlaw(20000, 300000, seed=13)
     g = dgl.DGLGraph()
     g.add_nodes(n)
@@ -210,12 +213,13 @@ def test_gatconv_padded_head_width_matches_unfused(heads, out):
 
 @pytest.mark.parametrize("H,D", [(8, 8), (3, 16), (16, 4)])
 def test_fused_gat_edge_position_backward(H, D, monkeypatch):
-    """The unblocked backward without its destination-side walk (DGLMIGraph
-    .gat_edge_pos): dense stats, grad_er terms stored in out-CSR order by the
-    source-side walk, one gather-sum over the in-CSR.  The feature and el gradients
-    equal the destination-walk backward bit for bit (the same source-side walk);
-    grad_er differs only in summation order; all three match the fp64
-    restatement, hub rows included."""
+    """The unblocked backward's three forms: with the forward's slope aggregates
+    (default: grad_er = <grad_out, slope_feat> - delta slope_sum from a dense pass), the
+    edge-position path (DGLMIGraph.gat_edge_pos: grad_er terms stored in out-CSR order
+    by the source-side walk, one gather-sum over the in-CSR) and the destination-side
+    walk.  The feature and el gradients are bit-identical across the three (the same
+    source-side walk and stats); grad_er differs only in how its sum is formed; all
+    match the fp64 restatement, hub rows included."""
     src, dst, n = powerlaw(20000, 300000, seed=29)
     g = dgl.DGLGraph()
     g.add_nodes(n)
@@ -226,18 +230,59 @@ def test_fused_gat_edge_position_backward(H, D, monkeypatch):
     er = (3 * th.randn(n, H, 1, device=DEV, generator=gen)).requires_grad_()
     go = None
     grads = {}
-    for mode in ("1", "0"):
+    for slopes, mode in (("1", "1"), ("0", "1"), ("0", "0")):
+        monkeypatch.setenv("DGLMI_GAT_SLOPES", slopes)
         monkeypatch.setenv("DGLMI_GAT_EDGE_POS", mode)
         out = B.fused_gat(g, ft, el, er, 0.2)
         if go is None:
             go = th.randn(out.shape, device=DEV, generator=gen)
-        grads[mode] = th.autograd.grad(out, (ft, el, er), go)
+        grads[slopes + mode] = th.autograd.grad(out, (ft, el, er), go)
     gidx = g._graph.get_immutable_gidx(th.device(DEV))
     assert getattr(gidx, "_gat_pos", None) is not None  # the edge-position path ran
-    assert th.equal(grads["1"][0], grads["0"][0]) and th.equal(grads["1"][1], grads["0"][1])
-    assert th.allclose(grads["1"][2], grads["0"][2], rtol=1e-5, atol=1e-5)
+    for k in ("11", "01"):
+        assert th.equal(grads[k][0], grads["00"][0]) and th.equal(grads[k][1], grads["00"][1])
+        assert th.allclose(grads[k][2], grads["00"][2], rtol=1e-5, atol=1e-5)
     fd, eld, erd = (t.detach().double().requires_grad_() for t in (ft, el, er))
     ref = dense_gat(src, dst, n, fd, eld, erd, 0.2)
     gr = th.autograd.grad(ref, (fd, eld, erd), go.double())
-    for a, b, name in zip(grads["1"], gr, ("ft", "el", "er")):
-        assert th.allclose(a.double(), b, rtol=1e-3, atol=1e-3), name
+    for k in ("11", "01"):
+        for a, b, name in zip(grads[k], gr, ("ft", "el", "er")):
+            assert th.allclose(a.double(), b, rtol=1e-3, atol=1e-3), (k, name)
+
+
+@pytest.mark.parametrize("H,D", [(8, 8), (2, 32)])
+def test_fused_gat_slope_aggregates_known_answers(H, D):
+    """DGLMIFusedGatForwardEx's slope aggregates against their definition in fp64
+    (slope_sum = sum_e a_e lrelu'(pre_e), slope_feat = sum_e a_e lrelu'(pre_e) ft[u]),
+    with mixed-sign logits so both slopes occur, split rows and empty rows."""
+    from dgl import kernel as K
+    src, dst, n = powerlaw(20000, 300000, seed=31)
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    gidx = g._graph.get_immutable_gidx(th.device(DEV))
+    gen = th.Generator(device=DEV).manual_seed(4)
+    ft = th.randn(n, H, D, device=DEV, generator=gen)
+    el = 2 * th.randn(n, H, 1, device=DEV, generator=gen)
+    er = 2 * th.randn(n, H, 1, device=DEV, generator=gen)
+    out, mx, sm = th.empty(n, H, D, device=DEV), th.empty(n, H, device=DEV), th.empty(n, H, device=DEV)
+    lf, ls = th.full((n, H, D), float("nan"), device=DEV), th.full((n, H), float("nan"), device=DEV)
+    K.fused_gat_forward(gidx, ft, el, er, 0.2, out, mx, sm, lf, ls)
+    s, d = th.from_numpy(src).to(DEV), th.from_numpy(dst).to(DEV)
+    pre = el.double()[s, :, 0] + er.double()[d, :, 0]
+    e = th.nn.functional.leaky_relu(pre, 0.2)
+    emax = th.full((n, H), -1e300, dtype=th.float64, device=DEV).index_reduce(0, d, e, "amax")
+    ex = th.exp(e - emax[d])
+    a = ex / th.zeros(n, H, dtype=th.float64, device=DEV).index_add(0, d, ex)[d]
+    slope = th.where(pre > 0, 1.0, 0.2).double()
+    ls_ref = th.zeros(n, H, dtype=th.float64, device=DEV).index_add(0, d, a * slope)
+    lf_ref = th.zeros(n, H, D, dtype=th.float64, device=DEV).index_add(
+        0, d, (a * slope)[:, :, None] * ft.double()[s])
+    assert th.allclose(ls.double(), ls_ref, rtol=1e-4, atol=1e-5)
+    assert th.allclose(lf.double(), lf_ref, rtol=1e-4, atol=1e-4)
+    zero = th.from_numpy(np.bincount(dst, minlength=n) == 0).to(DEV)
+    assert (ls[zero] == 0).all() and (lf[zero] == 0).all()
+    # the plain forward's outputs are unchanged by keeping them
+    out2 = th.empty_like(out)
+    K.fused_gat_forward(gidx, ft, el, er, 0.2, out2, th.empty_like(mx), th.empty_like(sm))
+    assert th.equal(out, out2)

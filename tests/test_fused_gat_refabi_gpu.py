@@ -76,7 +76,15 @@ def test_reference_order_matches_dense_and_native(H, D):
     # native entry, so the results are bit-identical to dgl.backend.fused_gat
     src, dst, n = powerlaw(20000, 300000, seed=17)
     g, (ft, el, er), out, gf, go = _check(src, dst, n, H, D, seed=4)
-    nat = B.fused_gat(g, ft, el, er, 0.2)
+    # exp also holds the slope aggregates when E * H >= round_up(N H, 4) + N H (D + 1)
+    # (dglmi.h); the native entry then keeps them too, else neither does
+    holds = len(src) * H >= ((n * H + 3) // 4) * 4 + n * H * (D + 1)
+    import os
+    os.environ["DGLMI_GAT_SLOPES"] = "1" if holds else "0"
+    try:
+        nat = B.fused_gat(g, ft, el, er, 0.2)
+    finally:
+        os.environ.pop("DGLMI_GAT_SLOPES")
     assert th.equal(nat, out)
     gn = th.autograd.grad(nat, (ft, el, er), go)
     for a, b in zip(gn, gf):

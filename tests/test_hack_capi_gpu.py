@@ -76,13 +76,16 @@ def test_rgcn_layer1_tall_gemms(K_in, X):
     _layer1_fwd_bwd(K_in, X, False, 40001, 200000)
 
 
-@pytest.mark.parametrize("X,R,hub,cached_norm", [(64, 4, False, True), (64, 4, True, False),
-                                                 (32, 2, False, True), (100, 2, True, True)])
-def test_rgcn_layer1_fused(X, R, hub, cached_norm):
+@pytest.mark.parametrize("X,R,hub,cached_norm,tile", [
+    (64, 4, False, True, "16"), (64, 4, True, False, "16"), (32, 2, False, True, "16"),
+    (100, 2, True, True, "16"), (64, 4, True, True, "32"), (100, 2, False, False, "32")])
+def test_rgcn_layer1_fused(X, R, hub, cached_norm, tile, monkeypatch):
     """The fused layer-1 kernels (prepared state bit 2: relation-major CSRs; each
     relation's rows aggregated into LDS, then one MFMA pass by W_t -- no Y = X W_cat
     table): forward and both gradients vs the fp64 restatement and the Python path,
-    with the norm streamed from the state or gathered by edge id."""
+    with the norm streamed from the state or gathered by edge id, on 16-row tiles
+    (k_rgcn_fused16, the default) and 32-row tiles (DGLMI_RGCN_TILE=32)."""
+    monkeypatch.setenv("DGLMI_RGCN_TILE", tile)
     _layer1_fwd_bwd(64, X, hub, 40001, 200000, R=R, prepare=4, cached_norm=cached_norm)
 
 
@@ -247,14 +250,17 @@ def test_rgcn_prepare_rejects_bad_arguments():
         K.RgcnState(gidx, norm, 2, 3, etypes=et.int()[:10])
 
 
-@pytest.mark.parametrize("K_in,X,R,prepare,hub", [(64, 64, 4, 6, True), (64, 32, 3, 6, False),
-                                                  (64, 64, 4, 0, False), (24, 16, 2, 2, True)])
-def test_rgcn_layer1_ex_self_loop(K_in, X, R, prepare, hub):
+@pytest.mark.parametrize("K_in,X,R,prepare,hub,tile", [
+    (64, 64, 4, 6, True, "16"), (64, 32, 3, 6, False, "16"), (64, 64, 4, 0, False, "16"),
+    (24, 16, 2, 2, True, "16"), (64, 64, 4, 6, True, "32"), (64, 100, 2, 6, False, "16")])
+def test_rgcn_layer1_ex_self_loop(K_in, X, R, prepare, hub, tile, monkeypatch):
     """DGLMIRgcnLayer1Ex / BackwardEx: the relation sum + hidden . loop_weight + bias
     (+ addend) forward, and grad_hidden with the self-loop term plus grad_loop_weight,
     vs fp64 -- on the fused kernels (64-wide rows, prepared state: the self-loop is one
-    more MFMA pass over the tile's own rows) and on the GEMM + gather path."""
+    more MFMA pass over the tile's own rows; 16- and 32-row tiles) and on the GEMM +
+    gather path."""
     from dgl import kernel as K
+    monkeypatch.setenv("DGLMI_RGCN_TILE", tile)
     g, gidx, s, d, et, norm = _graph(20001, 150000, R, seed=K_in + X + R, hub=hub)
     n = g.number_of_nodes()
     gidx.__dict__.pop("_rgcn_state", None)
@@ -322,10 +328,12 @@ def test_rgcn_layer1_ex_rejects_bad_arguments():
                                   th.empty(16, 8, device=DEV), etypes=et32)
 
 
-@pytest.mark.parametrize("n,m", [(500, 4000), (1700, 20000), (33, 300)])
-def test_rgcn_layer1_fused_small_grids(n, m):
-    """Graphs of fewer than 57 row tiles launch the fused kernels on fewer than eight
-    blocks: the tile queues shrink to the grid (every queue has a server)."""
+@pytest.mark.parametrize("n,m,tile", [(500, 4000, "16"), (1700, 20000, "16"), (33, 300, "16"),
+                                      (17, 200, "16"), (500, 4000, "32"), (33, 300, "32")])
+def test_rgcn_layer1_fused_small_grids(n, m, tile, monkeypatch):
+    """Graphs of few row tiles launch the fused kernels on fewer than eight blocks: the
+    tile queues shrink to the grid (every queue has a server); partial last tiles."""
+    monkeypatch.setenv("DGLMI_RGCN_TILE", tile)
     _layer1_fwd_bwd(64, 64, False, n, m, R=4, prepare=4)
 
 
