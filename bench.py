@@ -199,12 +199,7 @@ def measure_c4(world, rank, dist, cdev, device, args):
     th.cuda.synchronize()
     lp_s = time.time() - t1
     # every rank computed the same labels (deterministic kernels); make sure of it
-    h = (assign.long() * th.arange(1, C4_N + 1, device=device) % 1000003).sum()
-    hs = th.tensor([float(h.item())], device=cdev, dtype=th.float64)
-    hmax, hmin = hs.clone(), hs.clone()
-    dist.all_reduce(hmax, op=dist.ReduceOp.MAX)
-    dist.all_reduce(hmin, op=dist.ReduceOp.MIN)
-    if float(hmax.item()) != float(hmin.item()):
+    if not _ranks_agree(assign, dist, cdev):
         raise SystemExit("ranks disagree on the partition")
     trace("C4: hash check done")
     log("C4: label propagation %.2fs" % lp_s)
@@ -333,6 +328,9 @@ def measure_c5(world, rank, dist, cdev, device, args):
     gen = th.Generator(device=device)
     gen.manual_seed(8)
     et = th.randint(0, R, (m,), generator=gen, device=device)
+    if not (_ranks_agree(src, dist, cdev) and _ranks_agree(dst, dist, cdev)
+            and _ranks_agree(et, dist, cdev)):
+        raise SystemExit("C5: ranks built different graphs")
     indeg = th.bincount(dst.long(), minlength=n).float().clamp(min=1)
     norm = (1.0 / indeg)[dst.long()].reshape(m, 1)
     del indeg
@@ -362,12 +360,7 @@ def measure_c5(world, rank, dist, cdev, device, args):
     assign, info = D.partition_labelprop(gidx, world, rounds=args.c4_rounds, slack=args.c4_slack)
     th.cuda.synchronize()
     lp_s = time.time() - t1
-    h = (assign.long() * th.arange(1, n + 1, device=device) % 1000003).sum()
-    hs = th.tensor([float(h.item())], device=cdev, dtype=th.float64)
-    hmax, hmin = hs.clone(), hs.clone()
-    dist.all_reduce(hmax, op=dist.ReduceOp.MAX)
-    dist.all_reduce(hmin, op=dist.ReduceOp.MIN)
-    if float(hmax.item()) != float(hmin.item()):
+    if not _ranks_agree(assign, dist, cdev):
         raise SystemExit("C5: ranks disagree on the partition")
     part = D.build_partition_from_assignment(src, dst, assign, rank, None, world)
     keep = assign[dst.long()] == rank  # local edge order = the global order of kept edges
@@ -684,6 +677,17 @@ def _max_over_ranks(v, dist, cdev):
     t = th.tensor([float(v)], device=cdev, dtype=th.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def _ranks_agree(t, dist, cdev):
+    """True when an integer device tensor is the same on every rank (a position-weighted
+    checksum mod a prime, compared by max and min over the ranks)."""
+    h = (t.reshape(-1).long() * th.arange(1, t.numel() + 1, device=t.device) % 1000003).sum()
+    hs = th.tensor([float(h.item())], device=cdev, dtype=th.float64)
+    hmax, hmin = hs.clone(), hs.clone()
+    dist.all_reduce(hmax, op=dist.ReduceOp.MAX)
+    dist.all_reduce(hmin, op=dist.ReduceOp.MIN)
+    return float(hmax.item()) == float(hmin.item())
 
 
 def _timed(fn, steps, dist, cdev):

@@ -47,13 +47,8 @@ CONFIGS = {
 def chung_lu(n, m, alpha, seed, device):
     """Power-law edge list (same draw as scripts/bench_configs.py), identical on
     every rank."""
-    g = th.Generator(device=device)
-    g.manual_seed(seed)
-    w = th.arange(1, n + 1, device=device, dtype=th.float64).pow(-alpha)
-    w = w[th.randperm(n, generator=g, device=device)].float()
-    src = th.multinomial(w, m, replacement=True, generator=g).to(th.int32)
-    dst = th.multinomial(w, m, replacement=True, generator=g).to(th.int32)
-    return src, dst
+    from dgl.data.synthetic import chung_lu_edges
+    return chung_lu_edges(n, m, alpha, seed, device)
 
 
 def main():

@@ -33,12 +33,8 @@ from dgl.nn.pytorch import GraphConv, GATConv, FusedGATConv, RelGraphConv  # noq
 
 
 def chung_lu(n, m, alpha, seed, device, self_loops=False):
-    g = th.Generator(device=device)
-    g.manual_seed(seed)
-    w = th.arange(1, n + 1, device=device, dtype=th.float64).pow(-alpha)
-    w = w[th.randperm(n, generator=g, device=device)]
-    src = th.multinomial(w.float(), m, replacement=True, generator=g).to(th.int32)
-    dst = th.multinomial(w.float(), m, replacement=True, generator=g).to(th.int32)
+    from dgl.data.synthetic import chung_lu_edges
+    src, dst = chung_lu_edges(n, m, alpha, seed, device)  # the same draw on every rank
     if self_loops:
         ar = th.arange(n, device=device, dtype=th.int32)
         src = th.cat([src, ar])

@@ -59,7 +59,9 @@ def dense_gat(src, dst, n, ft, el, er, slope):
     d = th.from_numpy(dst).to(DEV)
     H = ft.shape[1]
     e = th.nn.functional.leaky_relu(el[s, :, 0] + er[d, :, 0], slope)
-    emax = th.full((n, H), -1e300, dtype=th.float64, device=DEV).index_reduce(0, d, e, "amax")
+    # the shift cancels in the softmax, so it carries no gradient (the amax backward
+    # over a star's hub row took ~30 s)
+    emax = th.full((n, H), -1e300, dtype=th.float64, device=DEV).index_reduce(0, d, e.detach(), "amax")
     ex = th.exp(e - emax[d])
     den = th.zeros(n, H, dtype=th.float64, device=DEV).index_add(0, d, ex)
     a = ex / den[d]

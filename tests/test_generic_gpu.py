@@ -97,6 +97,10 @@ SHAPES = [(1,), (3,), (8,), (6,), (4, 4), (8, 8), (2, 256), (512,), (3, 5)]
 @pytest.mark.parametrize("op", ["add", "sub", "mul", "div", "dot"])
 @pytest.mark.parametrize("lhs,rhs", [("u", "v"), ("e", "v"), ("u", "e")])
 def test_sddmm(sk, lhs, rhs, op, shape):
+    if shape in ((2, 256), (512,)) and op in ("add", "sub"):
+        # the wide rows' vector path is op-independent; mul / div / dot cover it (the
+        # fp64 checks of a 512-wide row over 100 K edges take ~5 s a case)
+        pytest.skip("wide rows: covered by mul / div / dot")
     src, dst, n, g, ref = sk
     m = len(src)
     lv, rv = _feats(n, m, lhs, rhs, op, shape, seed=zlib.crc32(repr((lhs, rhs, op, shape)).encode()) % 1000)
