@@ -78,7 +78,8 @@ def test_rgcn_layer1_tall_gemms(K_in, X):
 
 @pytest.mark.parametrize("X,R,hub,cached_norm,tile", [
     (64, 4, False, True, "16"), (64, 4, True, False, "16"), (32, 2, False, True, "16"),
-    (100, 2, True, True, "16"), (64, 4, True, True, "32"), (100, 2, False, False, "32")])
+    (100, 2, True, True, "16"), (64, 4, True, True, "16"), (64, 4, True, True, "32"),
+    (100, 2, False, False, "32")])
 def test_rgcn_layer1_fused(X, R, hub, cached_norm, tile, monkeypatch):
     """The fused layer-1 kernels (prepared state bit 2: relation-major CSRs; each
     relation's rows aggregated into LDS, then one MFMA pass by W_t -- no Y = X W_cat
@@ -116,7 +117,13 @@ def _layer1_fwd_bwd(K_in, X, hub, n, m, R=4, prepare=0, cached_norm=True):
         0, s, th.einsum("ex,ekx->ek", gmsg, w.double()[et]))
     gw_ref = th.zeros(R, K_in, X, dtype=th.float64, device=DEV).index_add_(
         0, et, th.einsum("ek,ex->ekx", h.double()[s], gmsg))
-    th.testing.assert_close(gh.double(), gh_ref, rtol=1e-4, atol=1e-4)
+    # a hub source's gradient sums thousands of out-edge terms: the bound scales with
+    # their absolute mass, like the forward's (a flat rtol = 1e-4 failed one hub entry at
+    # 1.7e-4 relative, 8.8e-4 absolute, on 16-row tiles)
+    gh_mass = th.zeros(n, K_in, dtype=th.float64, device=DEV).index_add_(
+        0, s, th.einsum("ex,ekx->ek", gmsg.abs(), w.double()[et].abs()))
+    assert ((gh.double() - gh_ref).abs() <= 1e-4 + 1e-5 * gh_mass).all(), \
+        float(((gh.double() - gh_ref).abs() / (1e-4 + 1e-5 * gh_mass)).max())
     # the weight gradient sums tens of thousands of terms per entry: the bound scales
     # with their absolute mass, as for the other long fp32 sums
     gw_mass = th.zeros(R, K_in, X, dtype=th.float64, device=DEV).index_add_(
@@ -130,8 +137,6 @@ def _layer1_fwd_bwd(K_in, X, hub, n, m, R=4, prepare=0, cached_norm=True):
     out.backward(go)
     # (two fp32 summation orders, e.g. the fused path's aggregate-then-transform:
     # bounds scaled by the absolute mass of the sums, as against fp64 above)
-    gh_mass = th.zeros(n, K_in, dtype=th.float64, device=DEV).index_add_(
-        0, s, th.einsum("ex,ekx->ek", gmsg.abs(), w.double()[et].abs()))
     assert ((out.detach().double() - ret.double()).abs() <= 2e-4 + 2e-5 * mass).all()
     assert ((hr.grad.double() - gh.double()).abs() <= 2e-4 + 2e-5 * gh_mass).all()
     assert ((wr.grad.double() - gw.double()).abs() <= 4e-4 + 2e-6 * gw_mass).all()
