@@ -361,7 +361,9 @@ void run_fast(const DGLMIGraph* g, const DGLMICsr& walk, int kind, int red, cons
   a.indptr = idx(g, walk.indptr);
   a.rows = walk.rows;
   a.indices = walk.indices;
-  a.eids = idx(g, walk.data);
+  // a position view's walk (DGLMIGraph.eid_identity): edge p's operand sits at p
+  const int id_bit = &walk == &g->in_csr ? 1 : (&walk == &g->out_csr ? 2 : 0);
+  a.eids = (g->eid_identity & id_bit) != 0 ? IdxPtr{nullptr, wide(g) ? 1 : 0} : idx(g, walk.data);
   a.nnz = walk.nnz;
   a.num_rows = walk.num_rows;
   a.x = x;
@@ -389,6 +391,10 @@ void run_fast(const DGLMIGraph* g, const DGLMICsr& walk, int kind, int red, cons
     a.bias = epi->bias;
     a.addend = epi->addend;
   }
+  // one weight per edge, read at the position: staged with the walk (FAST_COL_MUL_POS)
+  if (kind == FAST_COL_MUL_EDGE_BCAST && !a.eids && head_dim == F && w_map == nullptr &&
+      red == RED_SUM)
+    kind = FAST_COL_MUL_POS;
   Scratch carry(g, fast_workspace_bytes(walk.nnz, F), s);
   a.carry = static_cast<float*>(carry.ptr);
   a.seg_cnt = reinterpret_cast<int32_t*>(static_cast<char*>(carry.ptr) + fast_carry_bytes(walk.nnz, F));

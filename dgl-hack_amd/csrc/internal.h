@@ -271,6 +271,7 @@ enum FastKind : int {
   FAST_COL_MUL_EDGE = 2,        // v = X[col] * E[eid]            (same feature shape)
   FAST_COL_MUL_EDGE_BCAST = 3,  // v = X[col, h, :] * E[eid, h]   (E broadcast over the last dim)
   FAST_COL_TIE = 4,     // v = XR[row] == W[col] ? X[col] : 0  (max / min gradient, tie mask)
+  FAST_COL_MUL_POS = 5, // v = X[col] * W[p], one weight per position (identity edge ids; sum)
 };
 struct FastArgs {
   IdxPtr indptr;

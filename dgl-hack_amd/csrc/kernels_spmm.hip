@@ -159,7 +159,10 @@ __global__ void __launch_bounds__(kBlock) k_lane_reduce(FastArgs a) {
       r[0] = r0.x; r[1] = r0.y; r[2] = r0.z; r[3] = r0.w; r[4] = r1.x; r[5] = r1.y; r[6] = r1.z; r[7] = r1.w;
       c[0] = c0.x; c[1] = c0.y; c[2] = c0.z; c[3] = c0.w; c[4] = c1.x; c[5] = c1.y; c[6] = c1.z; c[7] = c1.w;
       if constexpr (needs_eid<KIND>()) {
-        if (a.eids.wide) {
+        if (!a.eids) {  // identity edge ids (a position view's walk)
+#pragma unroll
+          for (int u = 0; u < U; ++u) e[u] = base + u;
+        } else if (a.eids.wide) {
 #pragma unroll
           for (int u = 0; u < U; ++u) e[u] = a.eids[base + u];
         } else {
@@ -175,7 +178,7 @@ __global__ void __launch_bounds__(kBlock) k_lane_reduce(FastArgs a) {
         const bool ok = base + u < p1;
         r[u] = ok ? a.rows[base + u] : INT_MAX;
         c[u] = ok ? a.indices[base + u] : 0;
-        if constexpr (needs_eid<KIND>()) e[u] = ok ? a.eids[base + u] : 0;
+        if constexpr (needs_eid<KIND>()) e[u] = ok ? (a.eids ? a.eids[base + u] : base + u) : 0;
       }
     }
     float v[U][F];
@@ -276,14 +279,17 @@ void run_lane_f(const FastArgs& a, hipStream_t s) {
 
 template <int KIND, int RED>
 void run_cfg(const FastArgs& a, IdxPtr indptr, hipStream_t s) {
+  // FAST_COL_MUL_POS has its own kernel only for float4 rows; elsewhere it is the
+  // broadcast kind with identity edge ids (the same values, the per-lane weight load)
+  constexpr int K2 = KIND == FAST_COL_MUL_POS ? FAST_COL_MUL_EDGE_BCAST : KIND;
   if (a.F < 16 && lane_kernel_width(a.F)) {
-    run_lane_f<KIND, RED>(a, s);
+    run_lane_f<K2, RED>(a, s);
     return;
   }
-  switch (fast_vw(a.F, KIND, a.head_dim)) {
+  switch (fast_vw(a.F, K2, a.head_dim)) {
     case 4: run_vw<KIND, RED, 4>(a, indptr, s); break;
-    case 2: launch_fast_chunk_vw2(KIND, RED, a, s); break;
-    default: launch_fast_chunk_vw1(KIND, RED, a, s); break;
+    case 2: launch_fast_chunk_vw2(K2, RED, a, s); break;
+    default: launch_fast_chunk_vw1(K2, RED, a, s); break;
   }
 }
 
@@ -367,6 +373,7 @@ void launch_fast_reduce(int kind, int red, const FastArgs& a, hipStream_t s) {
       break;
     case FAST_COL_MUL_EDGE: run_cfg<FAST_COL_MUL_EDGE, RED_SUM>(a, indptr, s); break;
     case FAST_COL_TIE: run_cfg<FAST_COL_TIE, RED_SUM>(a, indptr, s); break;
+    case FAST_COL_MUL_POS: run_cfg<FAST_COL_MUL_POS, RED_SUM>(a, indptr, s); break;
     default: run_cfg<FAST_COL_MUL_EDGE_BCAST, RED_SUM>(a, indptr, s); break;
   }
 }

@@ -77,6 +77,12 @@ __device__ __forceinline__ typename VecT<VW>::T vident() {
   else if constexpr (VW == 2) return make_float2(v, v);
   else return v;
 }
+template <int VW>
+__device__ __forceinline__ typename VecT<VW>::T vone() {
+  if constexpr (VW == 4) return make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+  else if constexpr (VW == 2) return make_float2(1.0f, 1.0f);
+  else return 1.0f;
+}
 __device__ __forceinline__ float4 vscale(float4 a, float m) { return make_float4(a.x * m, a.y * m, a.z * m, a.w * m); }
 __device__ __forceinline__ float2 vscale(float2 a, float m) { return make_float2(a.x * m, a.y * m); }
 __device__ __forceinline__ float vscale(float a, float m) { return a * m; }
@@ -113,7 +119,7 @@ __device__ __forceinline__ float4 buf_ld4(__amdgpu_buffer_rsrc_t r, uint32_t off
 
 template <int KIND>
 constexpr bool needs_eid() {
-  return KIND != FAST_COPY_COL && KIND != FAST_COL_TIE;
+  return KIND != FAST_COPY_COL && KIND != FAST_COL_TIE && KIND != FAST_COL_MUL_POS;
 }
 
 // Value of one edge for VW-float slot fv of the output row.  `hs` (bcast kind):
@@ -161,6 +167,11 @@ __device__ __forceinline__ int64_t ld_stream(IdxPtr q, int64_t p) {
   }
   return ld_stream<VAR>(static_cast<const int32_t*>(q.p) + p);
 }
+template <int VAR>
+__device__ __forceinline__ float ld_stream_f(const float* p) {
+  if constexpr (VAR & 1) return __builtin_nontemporal_load(p);
+  else return *p;
+}
 template <int VAR, typename V>
 __device__ __forceinline__ void st_out(float* p, V v) {
   if constexpr (VAR & 2) vst_nt(p, v);
@@ -198,6 +209,11 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, IdxPtr indp
   __shared__ int32_t s_row[G][B];
   __shared__ int32_t s_col[G][B];
   __shared__ int64_t s_eid[needs_eid<KIND>() ? G : 1][needs_eid<KIND>() ? B : 1];
+  // FAST_COL_MUL_POS: one scalar edge value per position (u_mul_e with one weight per
+  // edge, edge ids = the positions of a position view), staged with the rows and
+  // columns by one coalesced load instead of a per-lane load behind a staged edge id
+  constexpr bool kScalarW = KIND == FAST_COL_MUL_POS;
+  __shared__ float s_w[kScalarW ? G : 1][kScalarW ? B : 1];
 
   const int g = threadIdx.x / L;
   const int lane = threadIdx.x % L;
@@ -231,14 +247,61 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, IdxPtr indp
       const bool ok = p < p1;
       s_row[g][q] = ok ? ld_stream<VAR>(a.rows + p) : INT_MAX;
       s_col[g][q] = ok ? ld_stream<VAR>(a.indices + p) : 0;
-      if constexpr (needs_eid<KIND>()) s_eid[needs_eid<KIND>() ? g : 0][q] = ok ? ld_stream<VAR>(a.eids, p) : 0;
+      // identity edge ids (a position view's walk, a.eids null): no `data` stream
+      if constexpr (needs_eid<KIND>())
+        s_eid[needs_eid<KIND>() ? g : 0][q] = ok ? (a.eids ? ld_stream<VAR>(a.eids, p) : p) : 0;
+      if constexpr (kScalarW) s_w[kScalarW ? g : 0][kScalarW ? q : 0] = ok ? ld_stream_f<VAR>(a.w + p) : 0.0f;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the mul kinds load both operands in the gather loop and multiply in the
+    // accumulation loop: a product inside the bounds-checked gather made the compiler
+    // wait for each gather before issuing the next (s_waitcnt vmcnt(0) per edge)
+    constexpr bool kMulVec = KIND == FAST_COL_MUL_EDGE;
+    constexpr bool kMulScl = KIND == FAST_COL_MUL_EDGE_BCAST || KIND == FAST_COL_MUL_POS;
 #pragma unroll
     for (int ub = 0; ub < B; ub += U) {
       V val[U][NV];
+      [[maybe_unused]] V wv[kMulVec ? U : 1][kMulVec ? NV : 1];
+      [[maybe_unused]] float wsc[kMulScl ? U : 1][kMulScl ? NV : 1];
+      bool fast_mul = false;
+      if constexpr (kMulVec || kMulScl) fast_mul = a.x_map == nullptr && a.w_map == nullptr;
+      if (fast_mul) {
+        if constexpr (kMulVec || kMulScl) {
+        // (sum only: I = 0; positions past the chunk are never accumulated; no maps:
+        // a map load in flight made the compiler wait for every earlier gather)
+        // every gather first, then the weights
+        int64_t cc[U], ee[U];
+        bool okk[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          cc[u] = s_col[g][ub + u];
+          okk[u] = s_row[g][ub + u] != INT_MAX;
+          if constexpr (!kScalarW) ee[u] = s_eid[needs_eid<KIND>() ? g : 0][ub + u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int v = 0; v < NV; ++v) {
+            const int f4 = lane + v * L;
+            val[u][v] = (okk[u] && f4 < F4) ? vld<VW>(a.x + cc[u] * a.F + VW * f4) : I;
+          }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int v = 0; v < NV; ++v) {
+            const int f4 = lane + v * L;
+            const bool in = okk[u] && f4 < F4;
+            if constexpr (kScalarW)
+              wsc[u][kMulScl ? v : 0] = s_w[kScalarW ? g : 0][kScalarW ? ub + u : 0];
+            else if constexpr (kMulScl)
+              wsc[u][kMulScl ? v : 0] = in ? a.w[ee[u] * wn + hsel[v]] : 0.0f;
+            else
+              wv[kMulVec ? u : 0][kMulVec ? v : 0] = in ? vld<VW>(a.w + ee[u] * a.F + VW * f4) : I;
+          }
+        }
+      } else {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int32_t col = s_col[g][ub + u];
@@ -268,8 +331,12 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, IdxPtr indp
             val[u][v] = (ok && f4 < F4) ? (nt ? vld_nt<VW>(px) : vld<VW>(px)) : I;
           } else {
             val[u][v] = (ok && f4 < F4) ? edge_value<KIND, VW>(a, col, eid, f4, hsel[v], wn, s_row[g][ub + u]) : I;
+            // (mapped mul kinds: the product is already in val)
+            if constexpr (kMulScl) wsc[u][kMulScl ? v : 0] = 1.0f;
+            if constexpr (kMulVec) wv[kMulVec ? u : 0][kMulVec ? v : 0] = vone<VW>();
           }
         }
+      }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -288,7 +355,11 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, IdxPtr indp
           cont = false;
         }
 #pragma unroll
-        for (int v = 0; v < NV; ++v) acc[v] = vred<RED>(acc[v], val[u][v]);
+        for (int v = 0; v < NV; ++v) {
+          if constexpr (kMulVec) acc[v] = vred<RED>(acc[v], vmul(val[u][v], wv[kMulVec ? u : 0][kMulVec ? v : 0]));
+          else if constexpr (kMulScl) acc[v] = vred<RED>(acc[v], vscale(val[u][v], wsc[u][kMulScl ? v : 0]));
+          else acc[v] = vred<RED>(acc[v], val[u][v]);
+        }
       }
     }
     __builtin_amdgcn_wave_barrier();

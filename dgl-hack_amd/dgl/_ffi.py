@@ -50,6 +50,7 @@ class Graph(ctypes.Structure):
         ("rgcn", ctypes.c_void_p),
         ("gat_edge_pos", ctypes.c_void_p),
         ("etypes", ctypes.c_void_p),
+        ("eid_identity", ctypes.c_int32),
     ]
 
 

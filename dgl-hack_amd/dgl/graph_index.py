@@ -92,6 +92,8 @@ class ImmutableGraphIndex:
         self._coo = None
         self._gather_cols = None
         self._col_blocks = {}
+        # "in" / "out" for a position view (position_view): edge ids = that walk's positions
+        self.position_of = None
         # relation id per edge id (int32 on the device) for the R-GCN entries, which
         # read it from the graph like the reference (DGLMIGraph.etypes); None = untyped
         self.etypes = None
@@ -232,9 +234,11 @@ class ImmutableGraphIndex:
             wv = DeviceCSR(walk.indptr, walk.indices, pos, walk.rows, walk.num_cols)
             ov = DeviceCSR(other.indptr, other.indices, inv[other.data.long()], other.rows,
                            other.num_cols)
-            self._pos_views[direction] = ImmutableGraphIndex(
+            view = ImmutableGraphIndex(
                 wv if direction == "in" else ov, ov if direction == "in" else wv,
                 self.num_src, self.num_dst, self.device, eid_perm=True)
+            view.position_of = direction  # its edge ids are this walk's positions
+            self._pos_views[direction] = view
         return self._pos_views[direction]
 
     def gcn_edge_weights(self, norm):
@@ -330,6 +334,8 @@ class ImmutableGraphIndex:
         g.device = self.device.index if self.device.index is not None else th.cuda.current_device()
         g.workspace = None
         g.workspace_bytes = 0
+        # a position view's walk has data[p] == p (DGLMIGraph.eid_identity)
+        g.eid_identity = {"in": 1, "out": 2}.get(self.position_of, 0)
         return g
 
     def workspace_bytes(self, feat_len):

@@ -127,6 +127,13 @@ typedef struct {
    * weight's leading dimension.  Read only by the DGLMIRgcn* entries, which therefore
    * keep the reference's argument lists.  NULL for untyped graphs. */
   const int32_t* etypes;
+  /* Optional (extension): bit 0 set when in_csr.data[p] == p for every position p,
+   * bit 1 the same for out_csr -- a view whose edge ids are one walk's positions, with
+   * per-edge operands permuted into that order (dgl's position_view).  The
+   * load-balanced reduce then takes edge p's operand at p without streaming `data`, and
+   * a per-edge scalar operand is staged with the walk's rows and columns instead of
+   * gathered per lane.  0 = read `data`. */
+  int32_t eid_identity;
 } DGLMIGraph;
 
 /* A contiguous row-major fp32 device array (NDArray / DLTensor subset). */

@@ -55,6 +55,8 @@ def main():
     res["copy_u_sum_ms"] = ktime(lambda: g.update_all(fn.copy_u("h", "m"), fn.sum("m", "o")), steps)
     res["u_mul_e_sum_ms"] = ktime(lambda: g.update_all(fn.u_mul_e("h", "w", "m"), fn.sum("m", "o")),
                                   steps)
+    from dgl import backend as B
+    res["gcn_norm_aggregate_ms"] = ktime(lambda: B.gcn_norm_aggregate(gidx, x, "both"), steps)
     W = th.randn(R, f, f, device=dev) * 0.1
     Lw = th.randn(f, f, device=dev) * 0.1
     bias = th.randn(f, device=dev)

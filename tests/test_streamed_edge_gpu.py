@@ -1,0 +1,99 @@
+"""u_op_e / e_op_u reductions whose edge operand needs no gradient (fixed edge weights,
+R-GCN / GCN norms) stream the operand in walk order on large graphs
+(``dgl.backend._StreamedEdgeReduce``): the results and the node gradient must equal the
+edge-id walk bit for bit -- the same values in the same summation order -- for every
+reducer, both operand orders and broadcast edge operands; an in-place write into the
+operand must be seen (the permuted copy is keyed on the version counter).  The edge-id
+walk itself is oracle-checked in test_kernels_gpu.py / test_generic_gpu.py."""
+import pytest
+import torch as th
+
+import dgl
+import dgl.function as fn
+from dgl import backend as B
+from graphs import powerlaw
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def big():
+    src, dst, n = powerlaw(200_000, 1_300_000, seed=21)  # past STREAM_EDGE_MIN_EDGES
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    return g, n, len(src)
+
+
+def _run(g, msg, red, x, w, streamed, monkeypatch):
+    monkeypatch.setenv("DGLMI_STREAM_EDGE", "1" if streamed else "0")
+    xr = x.clone().requires_grad_()
+    g.ndata["x"] = xr
+    g.edata["w"] = w
+    g.update_all(msg, red)
+    out = g.ndata.pop("h")
+    go = th.randn(out.shape, device=DEV, generator=th.Generator(device=DEV).manual_seed(5))
+    (gx,) = th.autograd.grad(out, (xr,), go)
+    return out.detach(), gx
+
+
+@pytest.mark.parametrize("op,red,order,shape", [
+    ("mul", "sum", "ue", (16,)), ("mul", "mean", "ue", (16,)), ("mul", "max", "ue", (8,)),
+    ("add", "min", "eu", (8,)), ("mul", "sum", "eu", (4, 8)), ("sub", "sum", "ue", (4, 8)),
+    ("mul", "sum", "ue", (64,))])
+def test_streamed_edge_operand_bit_identical(big, op, red, order, shape, monkeypatch):
+    g, n, m = big
+    gen = th.Generator(device=DEV).manual_seed(3)
+    x = th.randn((n,) + shape, device=DEV, generator=gen)
+    wshape = (m, 1) if len(shape) == 1 else (m, shape[0], 1)
+    w = th.rand(wshape, device=DEV, generator=gen) + 0.5
+    msg = getattr(fn, ("u_%s_e" if order == "ue" else "e_%s_u") % op)
+    mf = msg("x", "w", "m") if order == "ue" else msg("w", "x", "m")
+    rf = getattr(fn, red)("m", "h")
+    taken = []
+    orig = B._StreamedEdgeReduce.apply
+
+    def spy(*a):
+        taken.append(True)
+        return orig(*a)
+    monkeypatch.setattr(B._StreamedEdgeReduce, "apply", spy)
+    o1, g1 = _run(g, mf, rf, x, w, True, monkeypatch)
+    assert taken, "the streamed route was not taken"
+    o0, g0 = _run(g, mf, rf, x, w, False, monkeypatch)
+    assert len(taken) == 1
+    assert th.equal(o1, o0)
+    assert th.equal(g1, g0)
+
+
+def test_streamed_edge_operand_sees_inplace_writes(big, monkeypatch):
+    g, n, m = big
+    x = th.randn(n, 16, device=DEV)
+    w = th.rand(m, 1, device=DEV)
+    mf, rf = fn.u_mul_e("x", "w", "m"), fn.sum("m", "h")
+    a, _ = _run(g, mf, rf, x, w, True, monkeypatch)
+    w.mul_(2.0)  # same storage, new version: the cached permuted copy must be rebuilt
+    b, _ = _run(g, mf, rf, x, w, True, monkeypatch)
+    c, _ = _run(g, mf, rf, x, w, False, monkeypatch)
+    assert th.equal(b, c)
+    assert th.equal(b, 2.0 * a)  # exact: scaling by 2 commutes with fp32 rounding
+
+
+def test_edge_operand_with_grad_keeps_edge_id_walk(big, monkeypatch):
+    """An operand that needs a gradient (attention weights) is read by edge id as before,
+    and its gradient is the u_dot_v of the fused backward."""
+    g, n, m = big
+    monkeypatch.setenv("DGLMI_STREAM_EDGE", "1")
+    x = th.randn(n, 8, device=DEV)
+    w = th.rand(m, 1, device=DEV).requires_grad_()
+    called = []
+    monkeypatch.setattr(B._StreamedEdgeReduce, "apply", lambda *a: called.append(1))
+    g.ndata["x"] = x
+    g.edata["w"] = w
+    g.update_all(fn.u_mul_e("x", "w", "m"), fn.sum("m", "h"))
+    out = g.ndata.pop("h")
+    (gw,) = th.autograd.grad(out, (w,), th.ones_like(out))
+    assert not called
+    src, dst = (th.as_tensor(t).long().to(DEV) for t in g.all_edges())
+    ref = x[src].sum(1, keepdim=True)
+    assert th.allclose(gw, ref, rtol=1e-5, atol=1e-5)
