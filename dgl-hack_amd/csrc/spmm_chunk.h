@@ -260,15 +260,19 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, IdxPtr indp
     // wait for each gather before issuing the next (s_waitcnt vmcnt(0) per edge)
     constexpr bool kMulVec = KIND == FAST_COL_MUL_EDGE;
     constexpr bool kMulScl = KIND == FAST_COL_MUL_EDGE_BCAST || KIND == FAST_COL_MUL_POS;
+    // the max / min gradient: both gathered rows first, the tie test (against the
+    // walk row's own value) in the accumulation loop
+    constexpr bool kTie = KIND == FAST_COL_TIE;
+    constexpr bool kTwo = kMulVec || kTie;  // a second gathered row per edge
 #pragma unroll
     for (int ub = 0; ub < B; ub += U) {
       V val[U][NV];
-      [[maybe_unused]] V wv[kMulVec ? U : 1][kMulVec ? NV : 1];
+      [[maybe_unused]] V wv[kTwo ? U : 1][kTwo ? NV : 1];
       [[maybe_unused]] float wsc[kMulScl ? U : 1][kMulScl ? NV : 1];
       bool fast_mul = false;
-      if constexpr (kMulVec || kMulScl) fast_mul = a.x_map == nullptr && a.w_map == nullptr;
+      if constexpr (kMulVec || kMulScl || kTie) fast_mul = a.x_map == nullptr && a.w_map == nullptr;
       if (fast_mul) {
-        if constexpr (kMulVec || kMulScl) {
+        if constexpr (kMulVec || kMulScl || kTie) {
         // (sum only: I = 0; positions past the chunk are never accumulated; no maps:
         // a map load in flight made the compiler wait for every earlier gather)
         // every gather first, then the weights
@@ -278,7 +282,7 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, IdxPtr indp
         for (int u = 0; u < U; ++u) {
           cc[u] = s_col[g][ub + u];
           okk[u] = s_row[g][ub + u] != INT_MAX;
-          if constexpr (!kScalarW) ee[u] = s_eid[needs_eid<KIND>() ? g : 0][ub + u];
+          if constexpr (!kScalarW && !kTie) ee[u] = s_eid[needs_eid<KIND>() ? g : 0][ub + u];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -297,8 +301,10 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, IdxPtr indp
               wsc[u][kMulScl ? v : 0] = s_w[kScalarW ? g : 0][kScalarW ? ub + u : 0];
             else if constexpr (kMulScl)
               wsc[u][kMulScl ? v : 0] = in ? a.w[ee[u] * wn + hsel[v]] : 0.0f;
+            else if constexpr (kTie)
+              wv[kTwo ? u : 0][kTwo ? v : 0] = in ? vld<VW>(a.w + cc[u] * a.F + VW * f4) : I;
             else
-              wv[kMulVec ? u : 0][kMulVec ? v : 0] = in ? vld<VW>(a.w + ee[u] * a.F + VW * f4) : I;
+              wv[kTwo ? u : 0][kTwo ? v : 0] = in ? vld<VW>(a.w + ee[u] * a.F + VW * f4) : I;
           }
         }
       } else {
@@ -333,7 +339,7 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, IdxPtr indp
             val[u][v] = (ok && f4 < F4) ? edge_value<KIND, VW>(a, col, eid, f4, hsel[v], wn, s_row[g][ub + u]) : I;
             // (mapped mul kinds: the product is already in val)
             if constexpr (kMulScl) wsc[u][kMulScl ? v : 0] = 1.0f;
-            if constexpr (kMulVec) wv[kMulVec ? u : 0][kMulVec ? v : 0] = vone<VW>();
+            if constexpr (kMulVec) wv[kTwo ? u : 0][kTwo ? v : 0] = vone<VW>();
           }
         }
       }
@@ -356,7 +362,15 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, IdxPtr indp
         }
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
-          if constexpr (kMulVec) acc[v] = vred<RED>(acc[v], vmul(val[u][v], wv[kMulVec ? u : 0][kMulVec ? v : 0]));
+          if constexpr (kMulVec) acc[v] = vred<RED>(acc[v], vmul(val[u][v], wv[kTwo ? u : 0][kTwo ? v : 0]));
+          else if constexpr (kTie) {
+            // (mapped fallback: val already holds the masked value)
+            const int f4 = lane + v * L;
+            acc[v] = vred<RED>(acc[v], fast_mul && f4 < F4
+                                           ? vtie(vld<VW>(a.xr + static_cast<int64_t>(r) * a.F + VW * f4),
+                                                  wv[kTwo ? u : 0][kTwo ? v : 0], val[u][v])
+                                           : val[u][v]);
+          }
           else if constexpr (kMulScl) acc[v] = vred<RED>(acc[v], vscale(val[u][v], wsc[u][kMulScl ? v : 0]));
           else acc[v] = vred<RED>(acc[v], val[u][v]);
         }

@@ -167,7 +167,10 @@ def _streams_edge_operand(reducer, op, graph, lhs, rhs, lhs_data, rhs_data, out_
     caches (C5 graph: u_mul_e_sum 5.55 ms against copy_u_sum's 3.47 ms), so it is
     streamed in the walk's position order instead (ImmutableGraphIndex.position_operand:
     a permuted copy, built once per direction and cached while the tensor and its
-    version counter are unchanged).  Narrow operands only: the copy costs its size."""
+    version counter are unchanged).  Narrow operands only: the copy costs its size;
+    and only from an operand's second use on (a tensor made fresh every call, such as
+    an attention computed without grad, keeps the edge-id walk: permuting it each
+    call cost the C3 unfused GAT forward 21 -> 44 ms)."""
     if reducer not in ("sum", "mean", "max", "min") or op == "dot":
         return False
     if sorted((lhs, rhs)) != [SRC, EDGE]:
@@ -182,7 +185,8 @@ def _streams_edge_operand(reducer, op, graph, lhs, rhs, lhs_data, rhs_data, out_
         return False
     ic = graph.in_csr
     return (ic.nnz >= STREAM_EDGE_MIN_EDGES and edge.shape[0] == ic.nnz
-            and out_size == ic.num_rows and edge[0].numel() <= STREAM_EDGE_MAX_WIDTH)
+            and out_size == ic.num_rows and edge[0].numel() <= STREAM_EDGE_MAX_WIDTH
+            and graph.reused_operand(edge))
 
 
 class _StreamedEdgeReduce(th.autograd.Function):

@@ -58,10 +58,14 @@ def test_streamed_edge_operand_bit_identical(big, op, red, order, shape, monkeyp
         taken.append(True)
         return orig(*a)
     monkeypatch.setattr(B._StreamedEdgeReduce, "apply", spy)
+    # the first use of an operand keeps the edge-id walk; from the second on it streams
+    o_first, _ = _run(g, mf, rf, x, w, True, monkeypatch)
+    assert not taken
     o1, g1 = _run(g, mf, rf, x, w, True, monkeypatch)
     assert taken, "the streamed route was not taken"
     o0, g0 = _run(g, mf, rf, x, w, False, monkeypatch)
     assert len(taken) == 1
+    assert th.equal(o_first, o0)
     assert th.equal(o1, o0)
     assert th.equal(g1, g0)
 
@@ -71,12 +75,30 @@ def test_streamed_edge_operand_sees_inplace_writes(big, monkeypatch):
     x = th.randn(n, 16, device=DEV)
     w = th.rand(m, 1, device=DEV)
     mf, rf = fn.u_mul_e("x", "w", "m"), fn.sum("m", "h")
-    a, _ = _run(g, mf, rf, x, w, True, monkeypatch)
+    for _ in range(2):  # the second call streams (and caches) the operand
+        a, _ = _run(g, mf, rf, x, w, True, monkeypatch)
     w.mul_(2.0)  # same storage, new version: the cached permuted copy must be rebuilt
-    b, _ = _run(g, mf, rf, x, w, True, monkeypatch)
+    for _ in range(2):
+        b, _ = _run(g, mf, rf, x, w, True, monkeypatch)
     c, _ = _run(g, mf, rf, x, w, False, monkeypatch)
     assert th.equal(b, c)
     assert th.equal(b, 2.0 * a)  # exact: scaling by 2 commutes with fp32 rounding
+
+
+def test_fresh_operand_per_call_keeps_edge_id_walk(big, monkeypatch):
+    """A new operand tensor every call (an attention computed without grad) is never
+    permuted, even when the allocator hands it the previous one's address."""
+    g, n, m = big
+    x = th.randn(n, 16, device=DEV)
+    called = []
+    orig = B._StreamedEdgeReduce.apply
+    monkeypatch.setattr(B._StreamedEdgeReduce, "apply",
+                        lambda *a: called.append(1) or orig(*a))
+    for i in range(3):
+        w = th.full((m, 1), float(i + 1), device=DEV)
+        _run(g, fn.u_mul_e("x", "w", "m"), fn.sum("m", "h"), x, w, True, monkeypatch)
+        del w
+    assert not called
 
 
 def test_edge_operand_with_grad_keeps_edge_id_walk(big, monkeypatch):
