@@ -180,8 +180,11 @@ def _streams_edge_operand(reducer, op, graph, lhs, rhs, lhs_data, rhs_data, out_
     edge = rhs_data if rhs == EDGE else lhs_data
     if edge.requires_grad or not edge.is_cuda or os.environ.get("DGLMI_STREAM_EDGE", "1") == "0":
         return False
-    # whole graphs only (edge ids a permutation of [0, nnz)), and not a position view
+    # whole graphs only (edge ids a permutation of [0, nnz)), not a position view, and
+    # not a graph whose in-CSR already holds its edges in id order (read at the position)
     if not getattr(graph, "eid_perm", False) or getattr(graph, "position_of", None) is not None:
+        return False
+    if graph.eid_identity_bits() & 1:
         return False
     ic = graph.in_csr
     return (ic.nnz >= STREAM_EDGE_MIN_EDGES and edge.shape[0] == ic.nnz

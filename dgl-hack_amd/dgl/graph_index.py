@@ -359,9 +359,28 @@ class ImmutableGraphIndex:
         g.device = self.device.index if self.device.index is not None else th.cuda.current_device()
         g.workspace = None
         g.workspace_bytes = 0
-        # a position view's walk has data[p] == p (DGLMIGraph.eid_identity)
-        g.eid_identity = {"in": 1, "out": 2}.get(self.position_of, 0)
+        g.eid_identity = self.eid_identity_bits()
         return g
+
+    def eid_identity_bits(self):
+        """DGLMIGraph.eid_identity: bit 0 when the in-CSR's edge ids are its positions,
+        bit 1 the same for the out-CSR -- a position view's walk, or a whole graph whose
+        edges came sorted by destination (by source): its edge operands are then read
+        at the walk position, streamed, instead of gathered by edge id.  Checked once
+        on the device and cached (DGLMI_EID_IDENTITY=0 turns the detection off)."""
+        if self.position_of is not None:
+            return {"in": 1, "out": 2}[self.position_of]
+        bits = getattr(self, "_eid_id_bits", None)
+        if bits is None:
+            bits = 0
+            if self.eid_perm and self.in_csr.nnz and os.environ.get("DGLMI_EID_IDENTITY", "1") != "0":
+                for bit, c in ((1, self.in_csr), (2, self.out_csr)):
+                    iota = th.arange(c.nnz, device=c.data.device, dtype=c.data.dtype)
+                    if bool(th.equal(c.data, iota)):
+                        bits |= bit
+                    del iota
+            self._eid_id_bits = bits
+        return bits
 
     def workspace_bytes(self, feat_len):
         cache = self.__dict__.setdefault("_ws_bytes", {})

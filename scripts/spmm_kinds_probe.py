@@ -41,11 +41,23 @@ def main():
         g = dgl.DGLGraph.from_device_coo(src, dst, n)
         del src, dst
         m = g.number_of_edges()
+    elif "sorted" in sys.argv:
+        # the C5 graph with its edges in destination order: edge ids = in-CSR positions
+        # (DGLMIGraph.eid_identity); DGLMI_EID_IDENTITY=0 in the environment for the A/B
+        from dgl.data.synthetic import chung_lu_edges
+        n, m = 5_000_000, 80_000_000
+        src, dst = chung_lu_edges(n, m, 0.5, 8, dev)
+        order = th.sort(dst.long() * n + src.long()).indices  # (destination, source) order
+        g = dgl.DGLGraph.from_device_coo(src[order].contiguous(), dst[order].contiguous(), n)
+        del src, dst, order
+        x = th.randn(n, 64, device=dev)
     else:
         n, m = 5_000_000, 80_000_000
         g = chung_lu(n, m, 0.5, 8, dev)
         x = th.randn(n, 64, device=dev)
-    res = {"graph": "m1" if "m1" in sys.argv else "c5 chung-lu", "nodes": n, "edges": m}
+    res = {"graph": "m1" if "m1" in sys.argv else ("c5 chung-lu, dst-sorted edge ids" if "sorted" in sys.argv
+                                                    else "c5 chung-lu"), "nodes": n, "edges": m,
+           "eid_identity": g._graph.get_immutable_gidx(dev).eid_identity_bits()}
     g.ndata["x"] = x
     g.edata["w"] = th.rand(m, 1, device=dev)
     res["copy_u_sum_ms"] = ktime(lambda: g.update_all(fn.copy_u("x", "m"), fn.sum("m", "o")))

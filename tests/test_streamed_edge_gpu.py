@@ -119,3 +119,37 @@ def test_edge_operand_with_grad_keeps_edge_id_walk(big, monkeypatch):
     src, dst = (th.as_tensor(t).long().to(DEV) for t in g.all_edges())
     ref = x[src].sum(1, keepdim=True)
     assert th.allclose(gw, ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("msg", ["u_mul_e", "copy_e"])
+def test_dst_sorted_graph_reads_edge_operands_at_positions(msg, monkeypatch):
+    """Edges added in (destination, source) order: the in-CSR's edge ids are its positions
+    (DGLMIGraph.eid_identity bit 0, detected once per graph), so edge operands are read
+    at the walk position -- the same values in the same order as through the ids."""
+    import numpy as np
+    src, dst, n = powerlaw(50_000, 400_000, seed=5)
+    order = np.lexsort((src, dst))  # (destination, source) order: the in-CSR's own
+    src, dst = src[order], dst[order]
+    graphs = []
+    for detect in ("1", "0"):
+        monkeypatch.setenv("DGLMI_EID_IDENTITY", detect)
+        g = dgl.DGLGraph()
+        g.add_nodes(n)
+        g.add_edges(src, dst)
+        gidx = g._graph.get_immutable_gidx(DEV)
+        assert bool(gidx.eid_identity_bits() & 1) == (detect == "1")
+        graphs.append(g)
+    gen = th.Generator(device=DEV).manual_seed(9)
+    x = th.randn(n, 4, 8, device=DEV, generator=gen)
+    e = th.rand(len(src), 4, 1 if msg == "u_mul_e" else 8, device=DEV, generator=gen)
+    outs = []
+    for g in graphs:
+        xr, er = x.clone().requires_grad_(), e.clone().requires_grad_()
+        g.ndata["x"], g.edata["e"] = xr, er
+        mf = fn.u_mul_e("x", "e", "m") if msg == "u_mul_e" else fn.copy_e("e", "m")
+        g.update_all(mf, fn.sum("m", "h"))
+        out = g.ndata.pop("h")
+        grads = th.autograd.grad(out, (xr, er) if msg == "u_mul_e" else (er,), th.ones_like(out))
+        outs.append((out.detach(),) + tuple(grads))
+    for a, b in zip(*outs):
+        assert th.equal(a, b)
