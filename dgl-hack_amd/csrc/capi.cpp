@@ -993,15 +993,28 @@ void gat_check_ls(const GatArgs& a, const DGLMIArray* lf, const DGLMIArray* ls) 
   DGLMI_CHECK(aligned16(lf->data), "slope_feat must be 16-byte aligned");
 }
 
+// attention dropout parameters of the GatArgs (p = 0: off)
+void gat_set_dropout(GatArgs& a, float p, uint64_t seed) {
+  DGLMI_CHECK(p >= 0.0f && p < 1.0f, "attn_drop must be in [0, 1)");
+  a.drop = p > 0.0f ? 1 : 0;
+  if (!a.drop) return;
+  const double t = static_cast<double>(p) * 4294967296.0;
+  a.drop_thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : static_cast<uint32_t>(t);
+  a.drop_scale = 1.0f / (1.0f - p);
+  a.drop_seed = seed;
+}
+
 int gat_forward_impl(const DGLMIGraph* graph, const DGLMIArray* feat_src, const DGLMIArray* el,
                      const DGLMIArray* er, float negative_slope, DGLMIArray* out,
                      DGLMIArray* max_out, DGLMIArray* sum_out, DGLMIArray* lf, DGLMIArray* ls,
-                     void* stream) {
+                     void* stream, float attn_drop = 0.0f, uint64_t seed = 0) {
   API_BEGIN();
   check_graph32(graph, "fused GAT");
   DeviceGuard guard(graph->device);
   GatArgs a = gat_args(graph, feat_src, el, er, negative_slope, out, max_out, sum_out);
   gat_check_ls(a, lf, ls);
+  gat_set_dropout(a, attn_drop, seed);
+  a.eids = graph->in_csr.data;
   a.lf = lf ? lf->data : nullptr;
   a.ls = ls ? ls->data : nullptr;
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1046,6 +1059,7 @@ int gat_forward_impl(const DGLMIGraph* graph, const DGLMIArray* feat_src, const 
       ab.indptr = c.indptr;
       ab.rows = c.rows;
       ab.indices = c.indices;
+      ab.eids = c.data;
       ab.nnz = c.nnz;
       ab.chunk = gat_chunk_edges(std::max<int64_t>(c.nnz, 1));
       ab.out = out_part + b * N * a.F;
@@ -1101,12 +1115,17 @@ int gat_backward_impl(const DGLMIGraph* graph, const DGLMIArray* feat_src, const
                       const DGLMIArray* er, float negative_slope, const DGLMIArray* out,
                       const DGLMIArray* max_in, const DGLMIArray* sum_in, const DGLMIArray* lf_in,
                       const DGLMIArray* ls_in, const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
-                      DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream) {
+                      DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream, float attn_drop = 0.0f,
+                      uint64_t seed = 0) {
   API_BEGIN();
   check_graph32(graph, "fused GAT");
   DeviceGuard guard(graph->device);
   GatArgs a = gat_args(graph, feat_src, el, er, negative_slope, const_cast<DGLMIArray*>(out),
                        const_cast<DGLMIArray*>(max_in), const_cast<DGLMIArray*>(sum_in));
+  gat_set_dropout(a, attn_drop, seed);
+  // with dropout only the slope-aggregate backward (no destination-side walk) applies
+  DGLMI_CHECK(!a.drop || lf_in != nullptr,
+              "attention dropout needs the forward's slope aggregates (slope_feat / slope_sum)");
   hipStream_t s = static_cast<hipStream_t>(stream);
   a.chunk = gat_bwd_chunk_edges(std::max<int64_t>(graph->in_csr.nnz, 1));
   check_array(grad_out, "grad_out");
@@ -1173,6 +1192,7 @@ int gat_backward_impl(const DGLMIGraph* graph, const DGLMIArray* feat_src, const
       b.indptr = c.indptr;
       b.rows = c.rows;
       b.indices = c.indices;
+      b.eids = c.data;
       b.nnz = c.nnz;
       b.num_rows = c.num_rows;
       b.chunk = gat_bwd_chunk_edges(std::max<int64_t>(c.nnz, 1));
@@ -1275,6 +1295,27 @@ int DGLMIFusedGatBackwardEx(const DGLMIGraph* graph, const DGLMIArray* feat_src,
                             void* stream) {
   return gat_backward_impl(graph, feat_src, el, er, negative_slope, out, max_in, sum_in, slope_feat,
                            slope_sum, grad_out, grad_feat_src, grad_el, grad_er, stream);
+}
+
+int DGLMIFusedGatDropoutForward(const DGLMIGraph* graph, const DGLMIArray* feat_src,
+                                const DGLMIArray* el, const DGLMIArray* er, float negative_slope,
+                                float attn_drop, uint64_t seed, DGLMIArray* out, DGLMIArray* max_out,
+                                DGLMIArray* sum_out, DGLMIArray* slope_feat, DGLMIArray* slope_sum,
+                                void* stream) {
+  return gat_forward_impl(graph, feat_src, el, er, negative_slope, out, max_out, sum_out, slope_feat,
+                          slope_sum, stream, attn_drop, seed);
+}
+
+int DGLMIFusedGatDropoutBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src,
+                                 const DGLMIArray* el, const DGLMIArray* er, float negative_slope,
+                                 float attn_drop, uint64_t seed, const DGLMIArray* out,
+                                 const DGLMIArray* max_in, const DGLMIArray* sum_in,
+                                 const DGLMIArray* slope_feat, const DGLMIArray* slope_sum,
+                                 const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
+                                 DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream) {
+  return gat_backward_impl(graph, feat_src, el, er, negative_slope, out, max_in, sum_in, slope_feat,
+                           slope_sum, grad_out, grad_feat_src, grad_el, grad_er, stream, attn_drop,
+                           seed);
 }
 
 // The reference's argument order (_CAPI_DGLFusedGatKernel /

@@ -357,7 +357,28 @@ struct GatArgs {
   // and no destination-side walk runs.  NULL = not kept.
   float* lf;
   float* ls;
+  // attention dropout (DGLMIFusedGatDropout*): edge e, head h keeps its weight, scaled by
+  // 1 / (1 - p), when gat_drop_hash(seed, eid * H + h) >= drop_thresh; the walk's edge
+  // ids in `eids` (its CSR's data).  drop = 0: off.
+  int drop;
+  uint32_t drop_thresh;
+  float drop_scale;
+  uint64_t drop_seed;
+  const int32_t* eids;
 };
+// the dropout mask's hash (two rounds of a 32-bit avalanche mix keyed by the seed's
+// halves; mirrored in numpy by dgl.kernel.gat_dropout_keep for the tests)
+__host__ __device__ __forceinline__ uint32_t gat_mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+__host__ __device__ __forceinline__ uint32_t gat_drop_hash(uint64_t seed, uint32_t key) {
+  return gat_mix32(gat_mix32(key ^ static_cast<uint32_t>(seed)) ^ static_cast<uint32_t>(seed >> 32));
+}
 bool gat_supported(int64_t H, int64_t D);
 int64_t gat_chunk_edges(int64_t nnz);
 void launch_gat_forward(const GatArgs& a, hipStream_t s);

@@ -98,6 +98,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
   constexpr int U = NV == 1 ? 8 : 4;
   __shared__ int32_t s_row[G][B];
   __shared__ int32_t s_col[G][B];
+  __shared__ int32_t s_eid[G][B];  // attention dropout: the positions' edge ids
   const int g = threadIdx.x / L;
   const int lane = threadIdx.x % L;
   const int64_t chunk = (int64_t)blockIdx.x * G + g;
@@ -109,6 +110,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
   const int F4 = static_cast<int>(a.F / 4);
   const int H = a.H, D = a.D;
   const int64_t CW = LS ? 2 * a.F + 3 * H : a.F + 2 * H;  // carry record, see above
+  const bool drop = a.drop != 0;
   int hd[NV], fl[NV];
   bool ok4[NV], lead[NV];
 #pragma unroll
@@ -185,6 +187,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
       const bool ok = p < p1;
       s_row[g][q] = ok ? a.rows[p] : INT_MAX;
       s_col[g][q] = ok ? a.indices[p] : 0;
+      if (drop) s_eid[g][q] = ok ? a.eids[p] : 0;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -237,15 +240,24 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
             mx[v] = s;
           }
           const float pe = fexp(s - mx[v]);
+          // dropout: the output and lf take the kept, rescaled weight; the softmax
+          // denominator and ls the plain one
+          float pk = pe;
+          if (drop) {
+            const uint32_t key = static_cast<uint32_t>(s_eid[g][ub + u]) * static_cast<uint32_t>(H) +
+                                 static_cast<uint32_t>(hd[v]);
+            pk = gat_drop_hash(a.drop_seed, key) >= a.drop_thresh ? pe * a.drop_scale : 0.0f;
+          }
           const float4 x = val[u][v];
-          acc[v] = make_float4(acc[v].x + pe * x.x, acc[v].y + pe * x.y, acc[v].z + pe * x.z,
-                               acc[v].w + pe * x.w);
+          acc[v] = make_float4(acc[v].x + pk * x.x, acc[v].y + pk * x.y, acc[v].z + pk * x.z,
+                               acc[v].w + pk * x.w);
           sm[v] += pe;
           if (LS) {
-            const float pd = pe * dleaky(pre, a.slope);
+            const float dl = dleaky(pre, a.slope);
+            const float pd = pk * dl;
             qa[v] = make_float4(qa[v].x + pd * x.x, qa[v].y + pd * x.y, qa[v].z + pd * x.z,
                                 qa[v].w + pd * x.w);
-            qs[v] += pd;
+            qs[v] += pe * dl;
           }
         }
       }
@@ -485,6 +497,8 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
   constexpr int U = NV == 1 ? 8 : 4;
   __shared__ int32_t s_row[G][B];
   __shared__ int32_t s_col[G][B];
+  __shared__ int32_t s_eid[G][B];  // attention dropout: the positions' edge ids
+  const bool drop = a.drop != 0;
   const int g = threadIdx.x / L;
   const int lane = threadIdx.x % L;
   const int64_t chunk = (int64_t)blockIdx.x * G + g;
@@ -555,6 +569,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
       const bool ok = p < p1;
       s_row[g][q] = ok ? a.rows[p] : INT_MAX;
       s_col[g][q] = ok ? a.indices[p] : 0;
+      if (drop) s_eid[g][q] = ok ? a.eids[p] : 0;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -588,13 +603,22 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
           const float att = fexp(leaky(pre, a.slope) - sv.y) * sv.z;
           const float4 gv = gov[u][v];
           const float ge = head_sum(dot4(gv, ftv[v]), D4);
-          const float te = att * (ge - sv.w) * dleaky(pre, a.slope);
+          // dropout: d = kept ? 1 / (1 - p) : 0 scales the edge's message, not the
+          // softmax (grad of the logit: att (d <grad_out, ft> - delta) lrelu')
+          float dk = 1.0f;
+          if (drop) {
+            const uint32_t key = static_cast<uint32_t>(s_eid[g][ub + u]) * static_cast<uint32_t>(H) +
+                                 static_cast<uint32_t>(hd[v]);
+            dk = gat_drop_hash(a.drop_seed, key) >= a.drop_thresh ? a.drop_scale : 0.0f;
+          }
+          const float te = att * (dk * ge - sv.w) * dleaky(pre, a.slope);
           acce[v] += te;
           // the edge's grad_er term, in this walk's position order (edge-position
           // backward: grad_er is then one gather-sum over the in-CSR)
           if (a.t != nullptr && lead[v]) a.t[(a.t_off + base + ub + u) * H + hd[v]] = te;
-          accf[v] = make_float4(accf[v].x + att * gv.x, accf[v].y + att * gv.y,
-                                accf[v].z + att * gv.z, accf[v].w + att * gv.w);
+          const float ad = att * dk;
+          accf[v] = make_float4(accf[v].x + ad * gv.x, accf[v].y + ad * gv.y,
+                                accf[v].z + ad * gv.z, accf[v].w + ad * gv.w);
         }
       }
     }

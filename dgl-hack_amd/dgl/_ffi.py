@@ -186,6 +186,17 @@ _SIGS = {
         ctypes.c_float, ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.c_void_p]),
+    "DGLMIFusedGatDropoutForward": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_float, ctypes.c_float, ctypes.c_uint64, ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_void_p]),
+    "DGLMIFusedGatDropoutBackward": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_float, ctypes.c_float, ctypes.c_uint64, ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_void_p]),
     "DGLMIFusedGatKernel": (ctypes.c_int, [
         ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.c_float,

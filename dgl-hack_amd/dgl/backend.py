@@ -466,10 +466,13 @@ class FusedGat(th.autograd.Function):
     a gradient will be wanted, the forward also keeps the attention's slope aggregates
     (DGLMIFusedGatForwardEx: N x H x D + N x H floats), and the backward is a dense pass
     plus the source-side walk -- no destination-side walk.
-    DGLMI_GAT_SLOPES=0 keeps the round-3 backward (destination walk / edge positions)."""
+    DGLMI_GAT_SLOPES=0 keeps the round-3 backward (destination walk / edge positions).
+    ``attn_drop`` > 0: GATConv's attention dropout (gatconv.py:154) inside the same
+    kernels, the mask a hash of ``seed`` and the edge id, recomputed by the backward
+    (DGLMIFusedGatDropout*; always with the slope aggregates)."""
 
     @staticmethod
-    def forward(ctx, gidx, feat_src, el, er, slope):
+    def forward(ctx, gidx, feat_src, el, er, slope, attn_drop=0.0, seed=0):
         feat_src, el, er = feat_src.contiguous(), el.contiguous(), er.contiguous()
         n_dst = er.shape[0]
         H, D = feat_src.shape[1], feat_src.shape[2]
@@ -477,11 +480,14 @@ class FusedGat(th.autograd.Function):
         mx = feat_src.new_empty((n_dst, H))
         sm = feat_src.new_empty((n_dst, H))
         lf = ls = None
-        if any(ctx.needs_input_grad[1:4]) and os.environ.get("DGLMI_GAT_SLOPES", "1") != "0":
+        if any(ctx.needs_input_grad[1:4]) and (
+                attn_drop > 0.0 or os.environ.get("DGLMI_GAT_SLOPES", "1") != "0"):
             lf = feat_src.new_empty((n_dst, H, D))
             ls = feat_src.new_empty((n_dst, H))
-        K.fused_gat_forward(gidx, feat_src, el, er, slope, out, mx, sm, lf, ls)
+        K.fused_gat_forward(gidx, feat_src, el, er, slope, out, mx, sm, lf, ls,
+                            attn_drop=attn_drop, seed=seed)
         ctx.gidx, ctx.slope = gidx, slope
+        ctx.attn_drop, ctx.seed = attn_drop, seed
         ctx.slopes = lf is not None
         if lf is not None:
             ctx.save_for_backward(feat_src, el, er, out, mx, sm, lf, ls)
@@ -499,17 +505,22 @@ class FusedGat(th.autograd.Function):
         g_el = th.empty_like(el)
         g_er = th.empty_like(er)
         K.fused_gat_backward(ctx.gidx, feat_src, el, er, ctx.slope, out, mx, sm, grad_out, g_ft,
-                             g_el, g_er, lf, ls)
-        return None, g_ft, g_el, g_er, None
+                             g_el, g_er, lf, ls, attn_drop=ctx.attn_drop, seed=ctx.seed)
+        return None, g_ft, g_el, g_er, None, None, None
 
 
-def fused_gat(graph, feat_src, el, er, slope):
+def fused_gat(graph, feat_src, el, er, slope, attn_drop=0.0, seed=None):
     """backend.py:1235 / tensor.py:415-420: softmax attention + aggregation in one kernel.
 
     ``graph`` is a DGLGraph (or an ImmutableGraphIndex); feat_src (N, H, D), el / er
-    (N, H, 1).  Returns (N, H, D)."""
+    (N, H, 1).  Returns (N, H, D).  ``attn_drop``: dropout on the attention weights
+    (GATConv in training); ``seed`` (default: drawn from torch's default generator, so
+    ``torch.manual_seed`` reproduces the mask) keys the mask."""
     gidx = graph if hasattr(graph, "in_csr") else graph._graph.get_immutable_gidx(feat_src.device)
-    return FusedGat.apply(gidx, feat_src, el, er, float(slope))
+    attn_drop = float(attn_drop)
+    if attn_drop > 0.0 and seed is None:
+        seed = int(th.randint(0, 2 ** 62, (1,)).item())
+    return FusedGat.apply(gidx, feat_src, el, er, float(slope), attn_drop, int(seed or 0))
 
 
 # --------------------------------------------------------------------------- #

@@ -11,6 +11,7 @@ from __future__ import annotations
 import ctypes
 import os
 
+import numpy as np
 import torch as th
 
 from . import _ffi
@@ -314,14 +315,45 @@ def _gat_bwd_cgraph(graph, feat_src):
     return graph.cstruct(None, col_blocks=nb, edge_pos=gat_edge_pos(graph, nb))
 
 
+def gat_dropout_keep(seed, eids, num_heads, p):
+    """The fused GAT's attention-dropout mask (DGLMIFusedGatDropout*; internal.h
+    gat_drop_hash) on the host, for tests: a (len(eids), num_heads) bool array, True where
+    edge eids[i], head h keeps its weight.  numpy uint32 arithmetic wraps like the
+    kernel's."""
+    seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    lo, hi = np.uint32(seed & 0xFFFFFFFF), np.uint32(seed >> 32)
+    key = (np.asarray(eids, dtype=np.uint64)[:, None] * np.uint64(num_heads)
+           + np.arange(num_heads, dtype=np.uint64)[None, :]).astype(np.uint32)
+
+    def mix(x):
+        x = x ^ (x >> np.uint32(16))
+        x = x * np.uint32(0x7FEB352D)
+        x = x ^ (x >> np.uint32(15))
+        x = x * np.uint32(0x846CA68B)
+        return x ^ (x >> np.uint32(16))
+    with np.errstate(over="ignore"):
+        h = mix(mix(key ^ lo) ^ hi)
+    t = p * 4294967296.0
+    thresh = np.uint32(0xFFFFFFFF if t >= 4294967295.0 else int(t))
+    return h >= thresh
+
+
 def fused_gat_forward(graph, feat_src, el, er, slope, out, max_out, sum_out, slope_feat=None,
-                      slope_sum=None):
+                      slope_sum=None, attn_drop=0.0, seed=0):
     """_CAPI_DGLFusedGatKernel (binary_reduce.cc:380-396) -> DGLMIFusedGatForward, or
     with ``slope_feat`` (N, H, D) / ``slope_sum`` (N, H) DGLMIFusedGatForwardEx: the
     forward also keeps the attention's slope aggregates, so the backward needs no
-    destination-side walk."""
+    destination-side walk.  ``attn_drop`` > 0: DGLMIFusedGatDropoutForward (GATConv's
+    attention dropout in the same pass, the mask a hash of ``seed`` and the edge id)."""
     _check_ctx(graph, [("feat_src", feat_src), ("el", el), ("er", er), ("out", out)])
     g = graph.cstruct(None, col_blocks=gat_col_blocks(graph, feat_src))
+    if attn_drop > 0.0:
+        check_call(_ffi.lib().DGLMIFusedGatDropoutForward(
+            ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"),
+            float(slope), float(attn_drop), ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF),
+            _arr(out, "out"), _arr(max_out, "max_out"), _arr(sum_out, "sum_out"),
+            _arr(slope_feat, "slope_feat"), _arr(slope_sum, "slope_sum"), _stream(out)))
+        return out
     args = [ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"),
             float(slope), _arr(out, "out"), _arr(max_out, "max_out"), _arr(sum_out, "sum_out")]
     if slope_feat is None:
@@ -333,10 +365,24 @@ def fused_gat_forward(graph, feat_src, el, er, slope, out, max_out, sum_out, slo
 
 
 def fused_gat_backward(graph, feat_src, el, er, slope, out, max_in, sum_in, grad_out,
-                       grad_feat_src, grad_el, grad_er, slope_feat=None, slope_sum=None):
+                       grad_feat_src, grad_el, grad_er, slope_feat=None, slope_sum=None,
+                       attn_drop=0.0, seed=0):
     """_CAPI_DGLKernelBackwardFusedGat (binary_reduce.cc:529-549) -> DGLMIFusedGatBackward
-    (or DGLMIFusedGatBackwardEx with the forward's slope aggregates)."""
+    (or DGLMIFusedGatBackwardEx with the forward's slope aggregates; with ``attn_drop`` > 0
+    DGLMIFusedGatDropoutBackward, the forward's seed)."""
     _check_ctx(graph, [("feat_src", feat_src), ("grad_out", grad_out)])
+    if attn_drop > 0.0:
+        if slope_feat is None:
+            raise DGLError("fused GAT dropout backward needs the forward's slope aggregates")
+        g = graph.cstruct(None, col_blocks=gat_col_blocks(graph, feat_src, backward=True))
+        check_call(_ffi.lib().DGLMIFusedGatDropoutBackward(
+            ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"),
+            float(slope), float(attn_drop), ctypes.c_uint64(int(seed) & 0xFFFFFFFFFFFFFFFF),
+            _arr(out, "out"), _arr(max_in, "max_in"), _arr(sum_in, "sum_in"),
+            _arr(slope_feat, "slope_feat"), _arr(slope_sum, "slope_sum"),
+            _arr(grad_out, "grad_out"), _arr(grad_feat_src, "grad_feat_src"),
+            _arr(grad_el, "grad_el"), _arr(grad_er, "grad_er"), _stream(grad_out)))
+        return
     if slope_feat is None:
         g = _gat_bwd_cgraph(graph, feat_src)
         check_call(_ffi.lib().DGLMIFusedGatBackward(

@@ -3,8 +3,10 @@
 GATConv whose attention softmax and aggregation run as one fused HIP kernel
 (``dgl.backend.fused_gat``, csrc/kernels_gat.hip).  Falls back to the
 unfused GATConv composition when the head size is not supported by the fused
-kernel or attention dropout is active (the fused kernel has no per-edge
-buffer to drop out).  The reference's timing prints are not reproduced.
+kernel.  The reference's module builds ``attn_drop`` but never applies it
+(fusedGatConv.py:80, 152); here it is applied in training, inside the fused
+kernel (a hashed per-edge, per-head mask; ``dgl.backend.fused_gat``).  The
+reference's timing prints are not reproduced.
 """
 
 from .... import backend as B
@@ -30,7 +32,7 @@ class FusedGATConv(GATConv):
             feat_src = feat_dst = B.project(h_src, self.fc.weight.t()).view(-1, self._num_heads, self._out_feats)
         el = (feat_src * self.attn_l).sum(dim=-1).unsqueeze(-1)
         er = (feat_dst * self.attn_r).sum(dim=-1).unsqueeze(-1)
-        rst = B.fused_gat(graph, feat_src, el, er, self.negative_slope)
+        rst = self._fused(graph, feat_src, el, er)
         if self.res_fc is not None:
             resval = self.res_fc(h_dst).view(h_dst.shape[0], -1, self._out_feats)
             rst = rst + resval

@@ -3,11 +3,14 @@
 Same parameters, initialisation and math as the reference: projection
 (torch GEMM), el / er attention terms, ``u_add_v`` SDDMM, LeakyReLU,
 max-stabilised ``edge_softmax`` and ``u_mul_e_sum`` with the attention
-broadcast over the head dimension (the load-balanced HIP kernel).  When no
-attention dropout is active and the head size suits the fused kernel, the
-middle of that chain (u_add_v .. u_mul_e_sum) runs as ONE fused HIP kernel
-(``dgl.backend.fused_gat``; same math, max-stabilised in both forms) --
-set ``use_fused = False`` on the module to force the unfused composition.
+broadcast over the head dimension (the load-balanced HIP kernel).  When the
+head size suits the fused kernel, the middle of that chain (u_add_v ..
+u_mul_e_sum) runs as ONE fused HIP kernel (``dgl.backend.fused_gat``; same math,
+max-stabilised in both forms), attention dropout in training included (its mask
+drawn inside the kernel from a per-call seed: the same Bernoulli(1 - p) per edge
+and head, scaled by 1 / (1 - p), as ``nn.Dropout`` on the softmax output, not the
+same draws) -- set ``use_fused = False`` on the module to force the unfused
+composition.
 The reference's unconditional ``th.cuda.synchronize()`` + timing prints
 (:146-170) are not reproduced.
 """
@@ -59,7 +62,9 @@ class GATConv(nn.Module):
         self.use_fused = True
 
     def _fused_ok(self):
-        if not self.use_fused or (self.training and self.attn_drop.p > 0):
+        # attention dropout in training runs inside the fused kernels (the mask a hash
+        # of a per-call seed and the edge id; dgl.backend.fused_gat)
+        if not self.use_fused:
             return False
         return self._fused_dim() is not None
 
@@ -72,10 +77,11 @@ class GATConv(nn.Module):
 
     def _fused(self, graph, feat_src, el, er):
         d = self._fused_dim()
+        p = self.attn_drop.p if self.training else 0.0
         if d == self._out_feats:
-            return B.fused_gat(graph, feat_src, el, er, self.negative_slope)
+            return B.fused_gat(graph, feat_src, el, er, self.negative_slope, attn_drop=p)
         ft = th.nn.functional.pad(feat_src, (0, d - self._out_feats))
-        return B.fused_gat(graph, ft, el, er, self.negative_slope)[..., :self._out_feats]
+        return B.fused_gat(graph, ft, el, er, self.negative_slope, attn_drop=p)[..., :self._out_feats]
 
     def reset_parameters(self):
         gain = nn.init.calculate_gain("relu")

@@ -318,6 +318,29 @@ int DGLMIFusedGatBackwardEx(const DGLMIGraph* graph, const DGLMIArray* feat_src,
                             const DGLMIArray* slope_sum, const DGLMIArray* grad_out,
                             DGLMIArray* grad_feat_src, DGLMIArray* grad_el, DGLMIArray* grad_er,
                             void* stream);
+
+/* Fused GAT with attention dropout (GATConv's attn_drop in training, gatconv.py:154:
+ * dropout on the softmax weights, per edge and head).  Edge e, head h keeps its weight,
+ * scaled by 1 / (1 - attn_drop), when a counter hash of (seed, e * H + h) clears the
+ * threshold attn_drop * 2^32 -- a mask no buffer holds: the backward recomputes it from
+ * the same seed and the walks' edge ids.  The softmax denominator (sum_out) is the plain
+ * one; out and slope_feat carry the kept, rescaled weights.  The backward needs the
+ * forward's slope aggregates.  attn_drop = 0 equals DGLMIFusedGatForwardEx /
+ * BackwardEx bit for bit.  Extension: the reference has no fused dropout (its
+ * FusedGATConv runs without one; GATConv composes dropout between edge_softmax and
+ * u_mul_e_sum). */
+int DGLMIFusedGatDropoutForward(const DGLMIGraph* graph, const DGLMIArray* feat_src,
+                                const DGLMIArray* el, const DGLMIArray* er, float negative_slope,
+                                float attn_drop, uint64_t seed, DGLMIArray* out, DGLMIArray* max_out,
+                                DGLMIArray* sum_out, DGLMIArray* slope_feat, DGLMIArray* slope_sum,
+                                void* stream);
+int DGLMIFusedGatDropoutBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src,
+                                 const DGLMIArray* el, const DGLMIArray* er, float negative_slope,
+                                 float attn_drop, uint64_t seed, const DGLMIArray* out,
+                                 const DGLMIArray* max_in, const DGLMIArray* sum_in,
+                                 const DGLMIArray* slope_feat, const DGLMIArray* slope_sum,
+                                 const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
+                                 DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream);
 /* The same two kernels in the reference's argument order, for a binding of the hack's
  * PackedFuncs that keeps its Python caller unchanged (tensor.py:383-420):
  *   _CAPI_DGLFusedGatKernel(G, feat_src, el, er, sum, exp, ret, slope)

@@ -164,10 +164,23 @@ def c3(dev, steps, warmup):
         fgat(g, x).sum().backward()
     ms_ff = timeit(ffwd, steps, warmup)
     ms_ffb = timeit(ffwd_bwd, steps, warmup)
+    # training with the reference GAT example's attention dropout (train.py --attn-drop
+    # 0.6): the composition applies nn.Dropout to the softmax; GATConv now keeps it in
+    # the fused kernels
+    dgat = GATConv(602, 8, 8, attn_drop=0.6).to(dev)
+    dgat.load_state_dict(gat.state_dict())
+    dgat.train()
+
+    def dfwd_bwd():
+        dgat(g, x).sum().backward()
+    ms_dfb = timeit(dfwd_bwd, steps, warmup)
+    dgat.use_fused = False
+    ms_dufb = timeit(dfwd_bwd, steps, warmup)
     return {"config": "C3 Reddit-size GATConv 602 -> 8x8", "nodes": n, "edges": m,
             "unfused_fwd_ms": ms_f, "unfused_fwd_bwd_ms": ms_fb,
             "fused_fwd_ms": ms_ff, "fused_fwd_bwd_ms": ms_ffb,
-            "fused_fwd_Gedges_s": m / ms_ff / 1e6, "fused_fwd_bwd_Gedges_s": m / ms_ffb / 1e6}
+            "fused_fwd_Gedges_s": m / ms_ff / 1e6, "fused_fwd_bwd_Gedges_s": m / ms_ffb / 1e6,
+            "attn_drop_0.6_fused_fwd_bwd_ms": ms_dfb, "attn_drop_0.6_unfused_fwd_bwd_ms": ms_dufb}
 
 
 def verify_rgcn_fused(conv, g, x, et, norm):

@@ -1,6 +1,7 @@
-"""The seeded Chung-Lu edge lists every rank of a multi-GPU bench builds on its own
-(dgl.data.synthetic.chung_lu_edges): the same draw on every call, in range, and
-skewed like the power law it samples."""
+"""Host-side seeded draws: the Chung-Lu edge lists every rank of a multi-GPU bench
+builds on its own (dgl.data.synthetic.chung_lu_edges: the same draw on every call, in
+range, skewed like the power law it samples) and the fused GAT's attention-dropout
+mask (dgl.kernel.gat_dropout_keep)."""
 import torch as th
 
 from dgl.data.synthetic import chung_lu_edges
@@ -22,3 +23,20 @@ def test_chung_lu_edges_repeatable_and_skewed():
     assert 1000 < int(deg.max()) < 2000
     # the two ends are independent draws
     assert not th.equal(a[0], a[1])
+
+
+def test_gat_dropout_keep_mask_statistics():
+    """The fused GAT's attention-dropout mask (host mirror of the kernel's hash): the
+    kept share is 1 - p, heads and seeds give independent draws."""
+    import numpy as np
+    from dgl.kernel import gat_dropout_keep
+    eids = np.arange(250_000)
+    for p in (0.1, 0.5, 0.6):
+        k = gat_dropout_keep(12345, eids, 8, p)
+        assert k.shape == (250_000, 8)
+        assert abs(k.mean() - (1 - p)) < 0.005
+        # neighbouring heads of one edge are not correlated
+        assert abs((k[:, 0] & k[:, 1]).mean() - (1 - p) ** 2) < 0.005
+    a, b = gat_dropout_keep(1, eids, 4, 0.5), gat_dropout_keep(2, eids, 4, 0.5)
+    assert abs((a == b).mean() - 0.5) < 0.01
+    assert gat_dropout_keep(7, eids[:10], 4, 0.0).all()
