@@ -86,6 +86,26 @@ __device__ __forceinline__ float head_sum(float x, int d4) {
   return x;
 }
 
+// Attention dropout, staged per position: the H keep bits of the position's edge (one
+// hash per edge and head, computed by the one lane that stages the position, instead of
+// by every lane of the head in the edge loop: 16 lanes per row at 8 x 8), or the edge
+// id itself for more than 32 heads (hashed per lane then).
+__device__ __forceinline__ uint32_t gat_stage_keep(const GatArgs& a, int64_t p) {
+  const uint32_t e = static_cast<uint32_t>(a.eids[p]);
+  if (a.H > 32) return e;
+  uint32_t kb = 0;
+  for (int h = 0; h < a.H; ++h)
+    kb |= (gat_drop_hash(a.drop_seed, e * static_cast<uint32_t>(a.H) + static_cast<uint32_t>(h)) >=
+           a.drop_thresh ? 1u : 0u) << h;
+  return kb;
+}
+__device__ __forceinline__ bool gat_kept(const GatArgs& a, uint32_t staged, int h) {
+  if (a.H > 32)
+    return gat_drop_hash(a.drop_seed, staged * static_cast<uint32_t>(a.H) + static_cast<uint32_t>(h)) >=
+           a.drop_thresh;
+  return (staged >> h) & 1u;
+}
+
 // ---------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------
@@ -98,7 +118,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
   constexpr int U = NV == 1 ? 8 : 4;
   __shared__ int32_t s_row[G][B];
   __shared__ int32_t s_col[G][B];
-  __shared__ int32_t s_eid[G][B];  // attention dropout: the positions' edge ids
+  __shared__ uint32_t s_keep[G][B];  // attention dropout: keep bits (gat_stage_keep)
   const int g = threadIdx.x / L;
   const int lane = threadIdx.x % L;
   const int64_t chunk = (int64_t)blockIdx.x * G + g;
@@ -187,7 +207,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
       const bool ok = p < p1;
       s_row[g][q] = ok ? a.rows[p] : INT_MAX;
       s_col[g][q] = ok ? a.indices[p] : 0;
-      if (drop) s_eid[g][q] = ok ? a.eids[p] : 0;
+      if (drop) s_keep[g][q] = ok ? gat_stage_keep(a, p) : 0u;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -243,11 +263,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
           // dropout: the output and lf take the kept, rescaled weight; the softmax
           // denominator and ls the plain one
           float pk = pe;
-          if (drop) {
-            const uint32_t key = static_cast<uint32_t>(s_eid[g][ub + u]) * static_cast<uint32_t>(H) +
-                                 static_cast<uint32_t>(hd[v]);
-            pk = gat_drop_hash(a.drop_seed, key) >= a.drop_thresh ? pe * a.drop_scale : 0.0f;
-          }
+          if (drop) pk = gat_kept(a, s_keep[g][ub + u], hd[v]) ? pe * a.drop_scale : 0.0f;
           const float4 x = val[u][v];
           acc[v] = make_float4(acc[v].x + pk * x.x, acc[v].y + pk * x.y, acc[v].z + pk * x.z,
                                acc[v].w + pk * x.w);
@@ -497,7 +513,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
   constexpr int U = NV == 1 ? 8 : 4;
   __shared__ int32_t s_row[G][B];
   __shared__ int32_t s_col[G][B];
-  __shared__ int32_t s_eid[G][B];  // attention dropout: the positions' edge ids
+  __shared__ uint32_t s_keep[G][B];  // attention dropout: keep bits (gat_stage_keep)
   const bool drop = a.drop != 0;
   const int g = threadIdx.x / L;
   const int lane = threadIdx.x % L;
@@ -569,7 +585,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
       const bool ok = p < p1;
       s_row[g][q] = ok ? a.rows[p] : INT_MAX;
       s_col[g][q] = ok ? a.indices[p] : 0;
-      if (drop) s_eid[g][q] = ok ? a.eids[p] : 0;
+      if (drop) s_keep[g][q] = ok ? gat_stage_keep(a, p) : 0u;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -606,11 +622,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
           // dropout: d = kept ? 1 / (1 - p) : 0 scales the edge's message, not the
           // softmax (grad of the logit: att (d <grad_out, ft> - delta) lrelu')
           float dk = 1.0f;
-          if (drop) {
-            const uint32_t key = static_cast<uint32_t>(s_eid[g][ub + u]) * static_cast<uint32_t>(H) +
-                                 static_cast<uint32_t>(hd[v]);
-            dk = gat_drop_hash(a.drop_seed, key) >= a.drop_thresh ? a.drop_scale : 0.0f;
-          }
+          if (drop) dk = gat_kept(a, s_keep[g][ub + u], hd[v]) ? a.drop_scale : 0.0f;
           const float te = att * (dk * ge - sv.w) * dleaky(pre, a.slope);
           acce[v] += te;
           // the edge's grad_er term, in this walk's position order (edge-position

@@ -30,8 +30,10 @@ def dense_gat_dropout(src, dst, n, ft, el, er, slope, keep, p):
     return th.zeros(n, H, ft.shape[2], dtype=th.float64, device=DEV).index_add(0, d, ft[s] * a[:, :, None])
 
 
-@pytest.mark.parametrize("nb,p", [(1, 0.5), (1, 0.1), (4, 0.6), (8, 0.3)])
-def test_fused_gat_dropout_vs_dense(nb, p, monkeypatch):
+@pytest.mark.parametrize("nb,p,H,D", [(1, 0.5, 8, 8), (1, 0.1, 8, 8), (4, 0.6, 8, 8),
+                                      (8, 0.3, 8, 8), (1, 0.5, 64, 4), (2, 0.4, 3, 16)])
+def test_fused_gat_dropout_vs_dense(nb, p, H, D, monkeypatch):
+    """(more than 32 heads: the mask is hashed per lane instead of staged as bits)"""
     monkeypatch.setenv("DGLMI_GAT_BLOCKS", str(nb))
     src, dst, n = powerlaw(20000, 300000, seed=13)
     g = dgl.DGLGraph()
@@ -41,7 +43,6 @@ def test_fused_gat_dropout_vs_dense(nb, p, monkeypatch):
         ib, ob = g._graph.get_immutable_gidx(th.device(DEV)).col_blocks(nb)
         assert all(c.nnz > 0 for c in ib + ob)
     gen = th.Generator(device=DEV).manual_seed(5)
-    H, D = 8, 8
     ft = th.randn(n, H, D, device=DEV, generator=gen).requires_grad_()
     el = (3 * th.randn(n, H, 1, device=DEV, generator=gen)).requires_grad_()
     er = (3 * th.randn(n, H, 1, device=DEV, generator=gen)).requires_grad_()
