@@ -121,14 +121,17 @@ def test_edge_operand_with_grad_keeps_edge_id_walk(big, monkeypatch):
     assert th.allclose(gw, ref, rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("msg", ["u_mul_e", "copy_e"])
-def test_dst_sorted_graph_reads_edge_operands_at_positions(msg, monkeypatch):
+@pytest.mark.parametrize("msg,order_by", [("u_mul_e", "dst"), ("copy_e", "dst"), ("u_mul_e", "src")])
+def test_dst_sorted_graph_reads_edge_operands_at_positions(msg, order_by, monkeypatch):
     """Edges added in (destination, source) order: the in-CSR's edge ids are its positions
     (DGLMIGraph.eid_identity bit 0, detected once per graph), so edge operands are read
     at the walk position -- the same values in the same order as through the ids."""
     import numpy as np
     src, dst, n = powerlaw(50_000, 400_000, seed=5)
-    order = np.lexsort((src, dst))  # (destination, source) order: the in-CSR's own
+    # (destination, source) order: the in-CSR's own (bit 0); (source, destination): the
+    # out-CSR's (bit 1, the node gradient's walk)
+    order = np.lexsort((src, dst)) if order_by == "dst" else np.lexsort((dst, src))
+    bit = 1 if order_by == "dst" else 2
     src, dst = src[order], dst[order]
     graphs = []
     for detect in ("1", "0"):
@@ -137,7 +140,7 @@ def test_dst_sorted_graph_reads_edge_operands_at_positions(msg, monkeypatch):
         g.add_nodes(n)
         g.add_edges(src, dst)
         gidx = g._graph.get_immutable_gidx(DEV)
-        assert bool(gidx.eid_identity_bits() & 1) == (detect == "1")
+        assert bool(gidx.eid_identity_bits() & bit) == (detect == "1")
         graphs.append(g)
     gen = th.Generator(device=DEV).manual_seed(9)
     x = th.randn(n, 4, 8, device=DEV, generator=gen)
