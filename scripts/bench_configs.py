@@ -108,6 +108,8 @@ def c2(dev, steps, warmup):
     ms_spmm = timeit(lambda: dgl.kernel.copy_reduce("sum", gidx, 0, x.detach(), out), steps, warmup)
 
     def layer():
+        x.grad = None  # as after zero_grad(set_to_none=True)
+        conv.zero_grad(set_to_none=True)
         conv(g, x).sum().backward()
     ms = timeit(layer, steps, warmup)
     alg = 4 * (n + 1) + 4 * m + 4 * f * m + 4 * f * n
@@ -230,6 +232,10 @@ def c5(dev, steps, warmup):
     check = verify_rgcn_fused(conv, g, x, et, norm)
 
     def fwd_bwd():
+        # gradients start from None each step, as after an optimizer's
+        # zero_grad(set_to_none=True): no accumulation pass over x.grad (5 M x 64)
+        x.grad = None
+        conv.zero_grad(set_to_none=True)
         conv(g, x, et, norm).sum().backward()
 
     def fwd():
