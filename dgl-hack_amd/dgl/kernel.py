@@ -333,7 +333,7 @@ def gat_dropout_keep(seed, eids, num_heads, p):
         return x ^ (x >> np.uint32(16))
     with np.errstate(over="ignore"):
         h = mix(mix(key ^ lo) ^ hi)
-    t = p * 4294967296.0
+    t = float(np.float32(p)) * 4294967296.0  # the C entry takes p as a float
     thresh = np.uint32(0xFFFFFFFF if t >= 4294967295.0 else int(t))
     return h >= thresh
 
