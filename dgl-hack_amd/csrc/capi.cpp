@@ -998,6 +998,7 @@ void gat_set_dropout(GatArgs& a, float p, uint64_t seed) {
   DGLMI_CHECK(p >= 0.0f && p < 1.0f, "attn_drop must be in [0, 1)");
   a.drop = p > 0.0f ? 1 : 0;
   if (!a.drop) return;
+  DGLMI_CHECK(a.o32, "attention dropout needs gathered tables below 2^31 elements");
   const double t = static_cast<double>(p) * 4294967296.0;
   a.drop_thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : static_cast<uint32_t>(t);
   a.drop_scale = 1.0f / (1.0f - p);

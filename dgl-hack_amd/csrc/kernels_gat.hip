@@ -110,7 +110,8 @@ __device__ __forceinline__ bool gat_kept(const GatArgs& a, uint32_t staged, int 
 // forward
 // ---------------------------------------------------------------------------
 // LS: also the slope aggregates lf / ls (carry record [acc F][m H][l H][lf F][ls H])
-template <int L, int NV, bool O32, bool LS>
+// DROP: attention dropout (a separate instance, so the plain walk's code is untouched)
+template <int L, int NV, bool O32, bool LS, bool DROP = false>
 __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
   static_assert(L >= 1 && L <= 64, "a lane group must fit in one wavefront");
   constexpr int G = kBlock / L;
@@ -118,7 +119,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
   constexpr int U = NV == 1 ? 8 : 4;
   __shared__ int32_t s_row[G][B];
   __shared__ int32_t s_col[G][B];
-  __shared__ uint32_t s_keep[G][B];  // attention dropout: keep bits (gat_stage_keep)
+  __shared__ uint32_t s_keep[DROP ? G : 1][DROP ? B : 1];  // dropout keep bits (gat_stage_keep)
   const int g = threadIdx.x / L;
   const int lane = threadIdx.x % L;
   const int64_t chunk = (int64_t)blockIdx.x * G + g;
@@ -130,7 +131,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
   const int F4 = static_cast<int>(a.F / 4);
   const int H = a.H, D = a.D;
   const int64_t CW = LS ? 2 * a.F + 3 * H : a.F + 2 * H;  // carry record, see above
-  const bool drop = a.drop != 0;
+  constexpr bool drop = DROP;
   int hd[NV], fl[NV];
   bool ok4[NV], lead[NV];
 #pragma unroll
@@ -207,7 +208,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
       const bool ok = p < p1;
       s_row[g][q] = ok ? a.rows[p] : INT_MAX;
       s_col[g][q] = ok ? a.indices[p] : 0;
-      if (drop) s_keep[g][q] = ok ? gat_stage_keep(a, p) : 0u;
+      if constexpr (drop) s_keep[drop ? g : 0][drop ? q : 0] = ok ? gat_stage_keep(a, p) : 0u;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -263,7 +264,8 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
           // dropout: the output and lf take the kept, rescaled weight; the softmax
           // denominator and ls the plain one
           float pk = pe;
-          if (drop) pk = gat_kept(a, s_keep[g][ub + u], hd[v]) ? pe * a.drop_scale : 0.0f;
+          if constexpr (drop)
+            pk = gat_kept(a, s_keep[drop ? g : 0][drop ? ub + u : 0], hd[v]) ? pe * a.drop_scale : 0.0f;
           const float4 x = val[u][v];
           acc[v] = make_float4(acc[v].x + pk * x.x, acc[v].y + pk * x.y, acc[v].z + pk * x.z,
                                acc[v].w + pk * x.w);
@@ -505,7 +507,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_dst(GatArgs a) {
 // ---------------------------------------------------------------------------
 // backward, source side (out-CSR): grad_ft, grad_el
 // ---------------------------------------------------------------------------
-template <int L, int NV, bool O32>
+template <int L, int NV, bool O32, bool DROP = false>
 __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
   static_assert(L >= 1 && L <= 64, "a lane group must fit in one wavefront");
   constexpr int G = kBlock / L;
@@ -513,8 +515,8 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
   constexpr int U = NV == 1 ? 8 : 4;
   __shared__ int32_t s_row[G][B];
   __shared__ int32_t s_col[G][B];
-  __shared__ uint32_t s_keep[G][B];  // attention dropout: keep bits (gat_stage_keep)
-  const bool drop = a.drop != 0;
+  __shared__ uint32_t s_keep[DROP ? G : 1][DROP ? B : 1];  // dropout keep bits (gat_stage_keep)
+  constexpr bool drop = DROP;
   const int g = threadIdx.x / L;
   const int lane = threadIdx.x % L;
   const int64_t chunk = (int64_t)blockIdx.x * G + g;
@@ -585,7 +587,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
       const bool ok = p < p1;
       s_row[g][q] = ok ? a.rows[p] : INT_MAX;
       s_col[g][q] = ok ? a.indices[p] : 0;
-      if (drop) s_keep[g][q] = ok ? gat_stage_keep(a, p) : 0u;
+      if constexpr (drop) s_keep[drop ? g : 0][drop ? q : 0] = ok ? gat_stage_keep(a, p) : 0u;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -622,7 +624,8 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
           // dropout: d = kept ? 1 / (1 - p) : 0 scales the edge's message, not the
           // softmax (grad of the logit: att (d <grad_out, ft> - delta) lrelu')
           float dk = 1.0f;
-          if (drop) dk = gat_kept(a, s_keep[g][ub + u], hd[v]) ? a.drop_scale : 0.0f;
+          if constexpr (drop)
+            dk = gat_kept(a, s_keep[drop ? g : 0][drop ? ub + u : 0], hd[v]) ? a.drop_scale : 0.0f;
           const float te = att * (dk * ge - sv.w) * dleaky(pre, a.slope);
           acce[v] += te;
           // the edge's grad_er term, in this walk's position order (edge-position
@@ -816,7 +819,10 @@ void fwd_cfg(const GatArgs& a, hipStream_t s) {
   const bool ls = a.lf != nullptr;
 #define DGLMI_GAT_FWD(O_, LS_) \
   hipLaunchKernelGGL((k_gat_fwd<L, NV, O_, LS_>), dim3(blocks), dim3(kBlock), 0, s, a)
-  if (a.o32) {
+  if (a.drop) {  // dropout instances for 32-bit offsets only (checked by the C entry)
+    if (ls) hipLaunchKernelGGL((k_gat_fwd<L, NV, true, true, true>), dim3(blocks), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((k_gat_fwd<L, NV, true, false, true>), dim3(blocks), dim3(kBlock), 0, s, a);
+  } else if (a.o32) {
     if (ls) DGLMI_GAT_FWD(true, true); else DGLMI_GAT_FWD(true, false);
   } else {
     if (ls) DGLMI_GAT_FWD(false, true); else DGLMI_GAT_FWD(false, false);
@@ -847,7 +853,9 @@ void bwd_src_cfg(const GatArgs& a, hipStream_t s) {
   constexpr int G = kBlock / L;
   const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
   const unsigned blocks = static_cast<unsigned>((chunks + G - 1) / G);
-  if (a.o32)
+  if (a.drop)  // dropout instances for 32-bit offsets only (checked by the C entry)
+    hipLaunchKernelGGL((k_gat_bwd_src<L, NV, true, true>), dim3(blocks), dim3(kBlock), 0, s, a);
+  else if (a.o32)
     hipLaunchKernelGGL((k_gat_bwd_src<L, NV, true>), dim3(blocks), dim3(kBlock), 0, s, a);
   else
     hipLaunchKernelGGL((k_gat_bwd_src<L, NV, false>), dim3(blocks), dim3(kBlock), 0, s, a);
