@@ -361,9 +361,12 @@ void run_fast(const DGLMIGraph* g, const DGLMICsr& walk, int kind, int red, cons
   a.indptr = idx(g, walk.indptr);
   a.rows = walk.rows;
   a.indices = walk.indices;
-  // a position view's walk (DGLMIGraph.eid_identity): edge p's operand sits at p
+  // a position view's walk (DGLMIGraph.eid_identity), or an internal walk whose edge
+  // ids are its positions (data NULL: the R-GCN state's position-ordered walks): edge
+  // p's operand sits at p
   const int id_bit = &walk == &g->in_csr ? 1 : (&walk == &g->out_csr ? 2 : 0);
-  a.eids = (g->eid_identity & id_bit) != 0 ? IdxPtr{nullptr, wide(g) ? 1 : 0} : idx(g, walk.data);
+  a.eids = ((g->eid_identity & id_bit) != 0 || walk.data == nullptr) ? IdxPtr{nullptr, wide(g) ? 1 : 0}
+                                                                      : idx(g, walk.data);
   a.nnz = walk.nnz;
   a.num_rows = walk.num_rows;
   a.x = x;
@@ -1662,7 +1665,7 @@ DGLMICsr rgcn_in_walk(const DGLMIGraph* g, const DGLMIRgcnState* st, int layer, 
   walk.num_cols = num_cols;
   *w = norm;
   if (st->norm != nullptr && st->norm == norm && st->in_norm != nullptr) {
-    walk.data = st->positions;
+    walk.data = nullptr;  // edge ids = positions (run_fast reads the norm at the position)
     *w = st->in_norm;
   }
   return walk;
@@ -1672,7 +1675,7 @@ DGLMICsr rgcn_out_walk(const DGLMIRgcnState* st, int layer, const float* norm, c
   DGLMICsr walk = st->out_typed[layer];
   *w = norm;
   if (st->norm != nullptr && st->norm == norm && st->out_norm[layer] != nullptr) {
-    walk.data = st->positions;
+    walk.data = nullptr;  // edge ids = positions (run_fast reads the norm at the position)
     *w = st->out_norm[layer];
   }
   return walk;
