@@ -934,7 +934,7 @@ class DistGATConv(th.nn.Module):
         ft_full = full[:, :H * D].reshape(-1, H, D)
         el_full = full[:, H * D:].reshape(-1, H, 1)
         gidx = part.gidx(feat.device)
-        if c._fused_ok():
+        if c._fused_route(gidx, ft_full.shape[0]):
             rst = c._fused(gidx, ft_full.contiguous(), el_full.contiguous(), er)
         else:
             g = part.local_graph(feat.device).local_var()

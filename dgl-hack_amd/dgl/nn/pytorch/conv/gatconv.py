@@ -68,6 +68,25 @@ class GATConv(nn.Module):
             return False
         return self._fused_dim() is not None
 
+    def _fused_route(self, graph, n_rows):
+        """Whether this call takes the fused kernels: the head size suits them, the
+        graph has 32-bit device indices (a 2^31+-edge graph takes the composition,
+        whose kernels have 64-bit offsets) and, with attention dropout in training,
+        the gathered tables stay below 2^31 elements (the dropout walks are built with
+        32-bit offsets only; ``capi.cpp`` gat_set_dropout).  ``graph``: a DGLGraph or
+        an ImmutableGraphIndex; ``n_rows``: the larger of its source / destination
+        row counts."""
+        if not self._fused_ok():
+            return False
+        if hasattr(graph, "in_csr"):  # an ImmutableGraphIndex: its device CSRs
+            if graph.in_csr.bits != 32:
+                return False
+        elif getattr(graph._graph, "device_bits", lambda: 32)() != 32:
+            return False
+        if self.training and self.attn_drop.p > 0:
+            return n_rows * self._num_heads * self._fused_dim() < (1 << 31)
+        return True
+
     def _fused_dim(self):
         """Head width for the fused kernel (the output width itself, or padded to
         the next supported one; see dgl.kernel.fused_gat_head_dim)."""
@@ -107,9 +126,7 @@ class GATConv(nn.Module):
             feat_src = feat_dst = B.project(h_src, self.fc.weight.t()).view(-1, self._num_heads, self._out_feats)
         el = (feat_src * self.attn_l).sum(dim=-1).unsqueeze(-1)
         er = (feat_dst * self.attn_r).sum(dim=-1).unsqueeze(-1)
-        # the fused kernels are int32-only: a 64-bit graph (2^31+ edges) takes the
-        # composition, whose kernels have 64-bit offsets
-        if self._fused_ok() and getattr(graph._graph, "device_bits", lambda: 32)() == 32:
+        if self._fused_route(graph, max(feat_src.shape[0], feat_dst.shape[0])):
             rst = self._fused(graph, feat_src, el, er)
         else:
             graph.srcdata.update({"ft": feat_src, "el": el})

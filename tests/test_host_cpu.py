@@ -237,3 +237,23 @@ def test_rgcn_fused_ok_matches_the_kernel_rule():
     assert K.rgcn_fused_ok(64, 128, 2) and not K.rgcn_fused_ok(64, 128, 3)
     assert K.rgcn_fused_ok(64, 32, 10) and not K.rgcn_fused_ok(64, 32, 11)
     assert not K.rgcn_fused_ok(32, 64, 1) and not K.rgcn_fused_ok(64, 129, 1)
+
+
+def test_gatconv_fused_route_limits():
+    """GATConv takes the fused kernels only where they apply: 32-bit device CSRs, and
+    with attention dropout in training gathered tables below 2^31 elements (the
+    dropout walks have 32-bit offsets only, capi.cpp gat_set_dropout)."""
+    from types import SimpleNamespace
+    from dgl.nn.pytorch import GATConv, FusedGATConv
+    g32 = SimpleNamespace(in_csr=SimpleNamespace(bits=32))
+    g64 = SimpleNamespace(in_csr=SimpleNamespace(bits=64))
+    for cls in (GATConv, FusedGATConv):
+        conv = cls(16, 8, 8, attn_drop=0.5)
+        big = (1 << 31) // 64
+        conv.train()
+        assert conv._fused_route(g32, big - 1) and not conv._fused_route(g32, big)
+        assert not conv._fused_route(g64, 10)
+        conv.eval()
+        assert conv._fused_route(g32, big)
+        conv.use_fused = False
+        assert not conv._fused_route(g32, 10)
