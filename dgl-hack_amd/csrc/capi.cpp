@@ -1466,8 +1466,8 @@ int DGLMIEdgeSoftmaxSupported(int64_t values_per_edge) {
 
 int64_t DGLMIEdgeSoftmaxWorkspaceBytes(const DGLMICsr* in_csr, int64_t values_per_edge) {
   if (in_csr == nullptr || in_csr->nnz <= 0 || values_per_edge <= 0) return 0;
-  const int64_t chunks = (in_csr->nnz + softmax_chunk_edges(in_csr->nnz) - 1) /
-                         softmax_chunk_edges(in_csr->nnz);
+  const int64_t K = softmax_chunk_edges(in_csr->nnz, values_per_edge);
+  const int64_t chunks = (in_csr->nnz + K - 1) / K;
   const int64_t stats = ((2 * in_csr->num_rows * values_per_edge * 4) + 255) & ~int64_t(255);
   // carries, then one segmented-fixup counter per chunk
   return stats + ((chunks * 2 * values_per_edge * 4 + 15) & ~int64_t(15)) + chunks * 4;
@@ -1493,7 +1493,7 @@ int64_t softmax_setup(const DGLMIGraph* g, const DGLMIArray* x, const char* name
   a.nnz = in.nnz;
   a.num_rows = in.num_rows;
   a.H = static_cast<int>(H);
-  a.chunk = softmax_chunk_edges(in.nnz);
+  a.chunk = softmax_chunk_edges(in.nnz, H);
   return H;
 }
 }  // namespace

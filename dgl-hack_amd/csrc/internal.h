@@ -261,7 +261,7 @@ struct SoftmaxArgs {
   int32_t* seg_cnt;        // num_chunks counters after the carries (segmented fixup), or null
 };
 bool softmax_supported(int64_t H);
-int64_t softmax_chunk_edges(int64_t nnz);
+int64_t softmax_chunk_edges(int64_t nnz, int64_t H);
 void launch_edge_softmax(const SoftmaxArgs& a, bool backward, hipStream_t s);
 
 // Load-balanced reduce-to-row kernels (kernels_spmm.hip).

@@ -13,8 +13,7 @@
 //   backward = k_sm_rows<DOTSUM> (S[v] = sum_e a[e] * ga[e]) + fixup, then
 //              k_sm_edges<GRAD> (gs[e] = a[e] ga[e] - a[e] S[v], the
 //              reference's order of operations, softmax.py:103-112).
-// Row work is cut into fixed chunks of CSR positions (one lane per chunk,
-// whole H-row in registers), rows cut by a chunk boundary are merged in chunk
+// Row work is cut into fixed chunks of CSR positions (one wave per chunk), rows cut by a chunk boundary are merged in chunk
 // order by the fixup -- deterministic, no atomics.
 #include "internal.h"
 
@@ -65,71 +64,113 @@ __device__ __forceinline__ void merge(float& m, float& l, float m2, float l2) {
   m = mn;
 }
 
+// merge() with one exponential: the larger maximum's own factor is exp(0) = 1.  The
+// same (m, l) for finite values; a NaN or +inf anywhere leaves l NaN (so the row's
+// softmax is NaN, as with the reference's exp(score - max)); two empty states
+// (m = -inf, l = 0) stay empty.
+__device__ __forceinline__ void merge1(float& m, float& l, float m2, float l2) {
+  const bool ge = m >= m2;
+  const float hi = ge ? m : m2, lo = ge ? m2 : m;
+  const float lhi = ge ? l : l2, llo = ge ? l2 : l;
+  if (hi == -INFINITY) return;
+  l = lhi + llo * expf(lo - hi);
+  m = hi;
+}
+
+// One wave per chunk of K CSR positions, walked L = 64 / H positions at a time with
+// lane (j, h) on position base + j and head h: every load instruction reads L
+// consecutive positions' row ids and edge ids and, when the edge ids are the
+// positions (a position view), one contiguous 256-byte run of logits.  (A lane per
+// chunk walking its own positions -- the round-1 form -- kept 64 streams per wave
+// whose lines left L2 before the lane came back: 6 ms for 1.4 GB at H = 1.)  The
+// positions of one step are reduced by a segmented inclusive scan over j (rows are
+// sorted, so equal row ids are one segment); each finished segment is written out,
+// the step's last one carries into the next step.  Outputs per chunk as before: a row
+// continued from the previous chunk goes to the chunk's carry, every other row to
+// the row statistics, and k_sm_fixup merges the carries in chunk order --
+// deterministic, no atomics.
 template <int H, int MODE>
 __global__ void __launch_bounds__(kBlock) k_sm_rows(SoftmaxArgs a) {
-  const int64_t chunk = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  constexpr int L = 64 / H;      // positions per step
+  constexpr int U = L >= 16 ? 2 : 4;  // steps whose loads are issued together
+  const int lane = threadIdx.x & 63, j = lane / H, h = lane % H;
+  const int64_t chunk = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
   const int64_t K = a.chunk;
   const int64_t p0 = chunk * K;
   if (p0 >= a.nnz) return;
   const int64_t p1 = p0 + K < a.nnz ? p0 + K : a.nnz;
-  if (a.seg_cnt != nullptr) a.seg_cnt[chunk] = 0;  // k_sm_fixup's counters
-  int64_t cur = a.rows[p0];
-  bool cont = p0 > 0 && a.rows[p0 - 1] == cur;
-  float m[H], l[H];
-#pragma unroll
-  for (int h = 0; h < H; ++h) {
-    m[h] = MODE == SM_STATS ? -INFINITY : 0.0f;
-    l[h] = 0.0f;
-  }
-  auto flush = [&]() {
-    float* pm = cont ? a.carry + chunk * 2 * H : a.stat0 + cur * H;
-    strow<H>(pm, m);
-    if constexpr (MODE == SM_STATS) strow<H>(cont ? pm + H : a.stat1 + cur * H, l);
+  if (a.seg_cnt != nullptr && lane == 0) a.seg_cnt[chunk] = 0;  // k_sm_fixup's counters
+  const int first_row = a.rows[p0];
+  const bool cont = p0 > 0 && a.rows[p0 - 1] == first_row;
+  auto put = [&](int row, float m, float l) {
+    const bool carry = cont && row == first_row;
+    float* pm = carry ? a.carry + chunk * 2 * H : a.stat0 + (int64_t)row * H;
+    pm[h] = m;
+    if constexpr (MODE == SM_STATS) (carry ? pm + H : a.stat1 + (int64_t)row * H)[h] = l;
   };
-  constexpr int U = 4;
-  for (int64_t base = p0; base < p1; base += U) {
-    int64_t rr[U];
-    float s[U][H], g[U][H];
+  int run_row = -1;  // the row the previous step ended in, and its partial state
+  float run_m = MODE == SM_STATS ? -INFINITY : 0.0f, run_l = 0.0f;
+  for (int64_t base = p0; base < p1; base += U * L) {
+    int r[U];
+    float x[U], g[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t p = base + u < p1 ? base + u : p1 - 1;
-      rr[u] = a.rows[p];
-      const int64_t e = a.eids[p];
-      ldrow<H>(a.s + e * H, s[u]);
-      if constexpr (MODE == SM_DOTSUM) ldrow<H>(a.ga + e * H, g[u]);
+      const int64_t p = base + u * L + j;
+      r[u] = -1;
+      x[u] = MODE == SM_STATS ? -INFINITY : 0.0f;
+      g[u] = 0.0f;
+      if (p < p1) {
+        r[u] = a.rows[p];
+        const int64_t e = a.eids[p];
+        x[u] = a.s[e * H + h];
+        if constexpr (MODE == SM_DOTSUM) g[u] = a.ga[e * H + h];
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (base + u >= p1) break;
-      if (rr[u] != cur) {
-        flush();
-#pragma unroll
-        for (int h = 0; h < H; ++h) {
-          m[h] = MODE == SM_STATS ? -INFINITY : 0.0f;
-          l[h] = 0.0f;
-        }
-        cur = rr[u];
-        cont = false;
+      const int64_t sb = base + u * L;
+      if (sb >= p1) break;  // wave-uniform
+      const int jl = p1 - sb < L ? static_cast<int>(p1 - sb) - 1 : L - 1;  // last valid j
+      float m, l;
+      if constexpr (MODE == SM_STATS) {
+        m = x[u];
+        l = x[u] == INFINITY ? __builtin_nanf("") : (x[u] == -INFINITY ? 0.0f : 1.0f);
+      } else {
+        m = x[u] * g[u];
+        l = 0.0f;
       }
-#pragma unroll
-      for (int h = 0; h < H; ++h) {
-        if constexpr (MODE == SM_STATS) {
-          const float x = s[u][h];
-          if (x > m[h]) {
-            // the new maximum's own term exp(x - x): 1, or NaN for x = +inf as in
-            // the reference's exp(score - max) (softmax.py:70-72)
-            l[h] = l[h] * expf(m[h] - x) + (x == INFINITY ? __builtin_nanf("") : 1.0f);
-            m[h] = x;
-          } else if (x != -INFINITY) {  // a masked logit adds exp(-inf) = 0
-            l[h] += expf(x - m[h]);
+      // the previous step's last row: continued by this step's first segment, or done
+      const int r0 = __shfl(r[u], h);
+      if (run_row >= 0) {
+        if (r0 == run_row) {
+          if (j == 0) {
+            if constexpr (MODE == SM_STATS) merge1(m, l, run_m, run_l);
+            else m += run_m;
           }
-        } else {
-          m[h] += s[u][h] * g[u][h];
+        } else if (j == 0) {
+          put(run_row, run_m, run_l);
         }
       }
+#pragma unroll
+      for (int d = 1; d < L; d <<= 1) {
+        const float m2 = __shfl_up(m, d * H);
+        const float l2 = MODE == SM_STATS ? __shfl_up(l, d * H) : 0.0f;
+        const int r2 = __shfl_up(r[u], d * H);
+        if (j >= d && r2 == r[u]) {
+          if constexpr (MODE == SM_STATS) merge1(m, l, m2, l2);
+          else m += m2;
+        }
+      }
+      const int rn = __shfl_down(r[u], H);
+      const int rl = __shfl(r[u], jl * H + h);
+      const bool seg_end = j <= jl && (j == jl || rn != r[u]);
+      if (seg_end && r[u] != rl) put(r[u], m, l);
+      run_row = rl;
+      run_m = __shfl(m, jl * H + h);
+      run_l = MODE == SM_STATS ? __shfl(l, jl * H + h) : 0.0f;
     }
   }
-  flush();
+  if (j == 0) put(run_row, run_m, run_l);
 }
 
 template <int H, int MODE>
@@ -178,7 +219,9 @@ __global__ void __launch_bounds__(kBlock) k_sm_fixup(SoftmaxArgs a) {
   if constexpr (MODE == SM_STATS) strow<H>(a.stat1 + r * H, l);
 }
 
-// One lane per edge; items in edge-id order (coo_dst) or in-CSR order.
+// One lane per edge; items in edge-id order (coo_dst) or in-CSR order.  (Two or four
+// edges in flight per lane, loads issued before any store, measured no faster: 2.98
+// against 2.73 ms at H = 8 on the C3 graph.)
 template <int H, int MODE>
 __global__ void __launch_bounds__(kBlock) k_sm_edges(SoftmaxArgs a) {
   const int64_t stride = (int64_t)gridDim.x * kBlock;
@@ -213,14 +256,16 @@ template <int H>
 void run(const SoftmaxArgs& a, bool backward, hipStream_t st) {
   const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
   const dim3 rb(static_cast<unsigned>((chunks + kBlock - 1) / kBlock)), blk(kBlock);
+  // k_sm_rows: one wave per chunk
+  const dim3 rrb(static_cast<unsigned>((chunks + kBlock / 64 - 1) / (kBlock / 64)));
   const int64_t eb = (a.nnz + kBlock - 1) / kBlock;
   const dim3 ebl(static_cast<unsigned>(eb < 256 * 64 ? eb : 256 * 64));
   if (!backward) {
-    hipLaunchKernelGGL((k_sm_rows<H, SM_STATS>), rb, blk, 0, st, a);
+    hipLaunchKernelGGL((k_sm_rows<H, SM_STATS>), rrb, blk, 0, st, a);
     if (chunks > 1) hipLaunchKernelGGL((k_sm_fixup<H, SM_STATS>), rb, blk, 0, st, a);
     hipLaunchKernelGGL((k_sm_edges<H, SM_NORMALIZE>), ebl, blk, 0, st, a);
   } else {
-    hipLaunchKernelGGL((k_sm_rows<H, SM_DOTSUM>), rb, blk, 0, st, a);
+    hipLaunchKernelGGL((k_sm_rows<H, SM_DOTSUM>), rrb, blk, 0, st, a);
     if (chunks > 1) hipLaunchKernelGGL((k_sm_fixup<H, SM_DOTSUM>), rb, blk, 0, st, a);
     hipLaunchKernelGGL((k_sm_edges<H, SM_GRAD>), ebl, blk, 0, st, a);
   }
@@ -230,10 +275,13 @@ void run(const SoftmaxArgs& a, bool backward, hipStream_t st) {
 
 bool softmax_supported(int64_t H) { return H == 1 || H == 2 || H == 4 || H == 8 || H == 16; }
 
-int64_t softmax_chunk_edges(int64_t nnz) {
-  int64_t k = 128;
-  while (k > 16 && nnz / k < 256 * 64 * 16) k >>= 1;
-  return k;
+// positions per chunk (one wave each): 16 steps of 64 / H positions, fewer while the
+// graph would give fewer than 2048 waves
+int64_t softmax_chunk_edges(int64_t nnz, int64_t H) {
+  const int64_t L = H >= 1 && H <= 64 ? 64 / H : 1;
+  int64_t steps = 16;
+  while (steps > 1 && nnz / (L * steps) < 2048) steps >>= 1;
+  return L * steps;
 }
 
 void launch_edge_softmax(const SoftmaxArgs& a, bool backward, hipStream_t s) {

@@ -21,6 +21,11 @@ from .... import backend as B
 from .... import function as fn
 from .... import kernel as K
 from ..softmax import edge_softmax
+from ..softmax import _apply as _edge_softmax_on
+
+# run the unfused composition in in-CSR position order (GATConv._position_space);
+# False: edge-id order throughout, as the reference
+POSITION_SPACE = True
 
 
 def expand_as_pair(x):
@@ -87,6 +92,31 @@ class GATConv(nn.Module):
             return n_rows * self._num_heads * self._fused_dim() < (1 << 31)
         return True
 
+    def _position_space(self, graph, feat_src):
+        """Whether the composition may run with edge ids = in-CSR positions: the logits
+        and attention are internal to this call (the reference sets them on a
+        ``local_var`` graph), so they can live in the walk's order instead of edge-id
+        order -- every per-edge read and write streams instead of landing on a random
+        line per edge.  Whole graphs only (edge ids a permutation), and not while
+        attention dropout is active (``nn.Dropout`` then draws its mask in edge-id
+        order, as the reference's composition does)."""
+        if not POSITION_SPACE or not feat_src.is_cuda or (self.training and self.attn_drop.p > 0):
+            return False
+        gidx = graph._graph.get_immutable_gidx(feat_src.device)
+        return gidx.eid_perm and gidx.in_csr.nnz > 0
+
+    def _composed_in_positions(self, graph, feat_src, el, er):
+        """u_add_v, LeakyReLU, edge_softmax and u_mul_e_sum -- the reference's
+        composition, the same kernels -- on the graph's in-CSR position view
+        (ImmutableGraphIndex.position_view): the same values summed in the same order,
+        bit-identical to the edge-id composition (tests/test_nn_gpu.py)."""
+        gidx = graph._graph.get_immutable_gidx(feat_src.device)
+        view = gidx.position_view("in")
+        n_dst, m = view.num_dst, view.number_of_edges()
+        e = B.binary_reduce("none", "add", view, B.SRC, B.DST, el, er, m)
+        a = self.attn_drop(_edge_softmax_on(view, self.leaky_relu(e), n_dst))
+        return B.binary_reduce("sum", "mul", view, B.SRC, B.EDGE, feat_src, a, n_dst)
+
     def _fused_dim(self):
         """Head width for the fused kernel (the output width itself, or padded to
         the next supported one; see dgl.kernel.fused_gat_head_dim)."""
@@ -128,6 +158,8 @@ class GATConv(nn.Module):
         er = (feat_dst * self.attn_r).sum(dim=-1).unsqueeze(-1)
         if self._fused_route(graph, max(feat_src.shape[0], feat_dst.shape[0])):
             rst = self._fused(graph, feat_src, el, er)
+        elif not isinstance(feat, tuple) and self._position_space(graph, feat_src):
+            rst = self._composed_in_positions(graph, feat_src, el, er)
         else:
             graph.srcdata.update({"ft": feat_src, "el": el})
             graph.dstdata.update({"er": er})

@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Fused edge softmax on the C3 graph (232,965 nodes / 114.6 M edges), H = 8 and
+H = 1: forward and backward HIP-event medians on the graph and on its in-CSR position
+view, plus a digest of every output (run against two builds of the library to
+show bit-identity)."""
+import hashlib
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "dgl-hack_amd"))
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+
+import numpy as np  # noqa: E402
+import torch as th  # noqa: E402
+
+
+def ktime(fn, steps=5):
+    fn()
+    ev = [(th.cuda.Event(enable_timing=True), th.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for a, b in ev:
+        a.record()
+        fn()
+        b.record()
+    th.cuda.synchronize()
+    return float(np.median([a.elapsed_time(b) for a, b in ev]))
+
+
+def main():
+    from bench_configs import chung_lu
+    from dgl import kernel as K
+    dev = "cuda:0"
+    g = chung_lu(232965, 114615892, 0.4, 3, dev)
+    gidx = g._graph.get_immutable_gidx(dev)
+    res = {"lib": os.environ.get("DGL_LIBRARY_PATH", "in-tree")}
+    dig = hashlib.sha256()
+    for H in (8, 1):
+        gen = th.Generator(device=dev).manual_seed(H)
+        s = th.randn(gidx.number_of_edges(), H, 1, device=dev, generator=gen) * 3
+        ga = th.randn(s.shape, device=dev, generator=gen)
+        for name, gi in (("graph", gidx), ("view", gidx.position_view("in"))):
+            out, gs = th.empty_like(s), th.empty_like(s)
+            res["H%d_%s_fwd_ms" % (H, name)] = ktime(lambda: K.edge_softmax_forward(gi, s, out))
+            res["H%d_%s_bwd_ms" % (H, name)] = ktime(lambda: K.edge_softmax_backward(gi, out, ga, gs))
+            for t in (out, gs):
+                dig.update(t.cpu().numpy().tobytes())
+    res["digest"] = dig.hexdigest()
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -338,3 +338,41 @@ def test_graph_conv_fused_epilogue_matches_reference_steps(norm, fin, fout, bloc
         # the unblocked epilogue path keeps the order)
         if blocks is None:
             assert th.equal(res[0][0], res[1][0])
+
+
+@pytest.mark.parametrize("H,D", [(8, 8), (3, 5), (1, 16)])
+def test_gat_composition_position_space_bit_identical(H, D, monkeypatch):
+    """GATConv's unfused composition run on the in-CSR position view (logits and
+    attention in walk order, GATConv._position_space) gives the same bits as the
+    edge-id composition: output and every gradient.  (3 heads: the edge softmax's
+    decomposition rather than its fused kernel.)"""
+    from dgl.nn.pytorch.conv import gatconv
+    from graphs import powerlaw
+    src, dst, n = powerlaw(20000, 300000, seed=21)
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    th.manual_seed(3)
+    gat = nn.GATConv(32, D, H).to(DEV)
+    gat.use_fused = False
+    x = th.randn(n, 32, device=DEV, requires_grad=True)
+    go = th.randn(n, H, D, device=DEV)
+    res = []
+    for pos in (True, False):
+        monkeypatch.setattr(gatconv, "POSITION_SPACE", pos)
+        calls = []
+        orig = gat._composed_in_positions
+        monkeypatch.setattr(gat, "_composed_in_positions", lambda *a: calls.append(1) or orig(*a))
+        gat.zero_grad()
+        x.grad = None
+        out = gat(g, x)
+        out.backward(go)
+        assert bool(calls) == pos
+        res.append([out.detach().clone(), x.grad.clone()] + [p.grad.clone() for p in gat.parameters()])
+    for a, b in zip(*res):
+        assert th.equal(a, b), float((a - b).abs().max())
+    # attention dropout in training keeps the edge-id order (nn.Dropout's draws)
+    gd = nn.GATConv(32, D, H, attn_drop=0.5).to(DEV)
+    gd.use_fused = False
+    monkeypatch.setattr(gatconv, "POSITION_SPACE", True)
+    assert not gd._position_space(g, x) and gd.eval()._position_space(g, x)
