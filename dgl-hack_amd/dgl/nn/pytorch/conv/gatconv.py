@@ -102,6 +102,8 @@ class GATConv(nn.Module):
         order, as the reference's composition does)."""
         if not POSITION_SPACE or not feat_src.is_cuda or (self.training and self.attn_drop.p > 0):
             return False
+        if not hasattr(getattr(graph, "_graph", None), "get_immutable_gidx"):
+            return False
         gidx = graph._graph.get_immutable_gidx(feat_src.device)
         return gidx.eid_perm and gidx.in_csr.nnz > 0
 
