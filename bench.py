@@ -48,6 +48,11 @@ SCALE = 23
 EDGES_PER_GPU = 100_000_000
 FEAT = 64
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# xGMI: 7 point-to-point links per GPU at ~153 GB/s each (the task brief's figure; the
+# local microarchitecture guide quotes none).  Counted here as ONE direction of one
+# link, so the exchange fractions below are, if anything, understated.  In an
+# all-to-all over N GPUs of one node a rank uses N - 1 links (one per peer).
+XGMI_LINK_GBPS = 153.0
 
 
 def log(*a):
@@ -259,7 +264,10 @@ def measure_c4(world, rank, dist, cdev, device, args):
     works = [th.zeros_like(work) for _ in range(world)]
     dist.all_gather(works, work)
     works = [int(w.item()) for w in works]
+    per_rank, ex_sum, model = c4_decomposition(part, x_inner, bufs, out, steps, rank, world,
+                                               dist, cdev)
     res.update({"value": C4_E * steps / el, "unit": "edges/s", "ms_per_step": el * 1e3 / steps,
+                "per_rank": per_rank, "exchange_aggregate": ex_sum, "model": model,
                 "speedup_vs_n1": res["n1_ms_per_step"] / (el * 1e3 / steps),
                 "exchange": "hybrid: pulled rows + pushed partial sums (tau %d), two "
                             "all-to-all-v (%s) overlapped with the owned-source SpMM"
@@ -281,6 +289,73 @@ def measure_c4(world, rank, dist, cdev, device, args):
                                          "cut_fraction": stats_ct["cut_edges"] / C4_E},
                 "setup_s": time.time() - t0})
     return res
+
+
+def c4_decomposition(part, x_inner, bufs, out, steps, rank, world, dist, cdev):
+    """The hybrid C4 step taken apart on every rank (round 5): each block's copy_u_sum
+    alone (owned, push, receive) with its algorithmic bytes and HBM fraction, the two
+    all-to-all-v alone (pulled rows, then partial rows; send buffers filled once) with
+    the bytes this rank sends and receives and their rate against the xGMI links, and
+    the step the schedule predicts from those parts -- the exchange in flight from the
+    start, the push and owned SpMMs meanwhile, the receive pass after both:
+    max(t_push + t_own, t_exchange) + t_recv, max over ranks -- to set beside the
+    measured step."""
+    from dgl import distributed as D
+    from dgl import kernel as K
+    f = FEAT
+    send, recv, pout, tmp = bufs["send"], bufs["recv"], bufs["pout"], bufs["tmp"]
+    th.index_select(x_inner, 0, part.send_idx, out=send)
+    blocks = (("own", part.g_own, x_inner, tmp, None),
+              ("push", part.g_push, x_inner, pout, None),
+              ("recv", part.g_recv, recv, out, (None, None, None, tmp)))
+    spmm = {}
+    for name, gi, src, dst, epi in blocks:
+        if gi is None:
+            spmm[name] = {"edges": 0, "alg_bytes": 0, "ms": 0.0, "GBps": None, "frac": None}
+            continue
+        fn = (lambda gi=gi, src=src, dst=dst, epi=epi:
+              K.copy_reduce("sum", gi, 0, src, dst, epilogue=epi))
+        fn()
+        t = _timed(fn, steps, None, None) * 1e3 / steps
+        b = spmm_alg_bytes(gi, f, addend=epi is not None)
+        spmm[name] = {"edges": int(gi.in_csr.nnz), "alg_bytes": b, "ms": t,
+                      "GBps": b / (t * 1e-3) / 1e9, "frac": b / (t * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+    if part.g_push is not None:  # the partial rows the peers will receive
+        K.copy_reduce("sum", part.g_push, 0, x_inner, pout)
+    rc, sc = part.recv_counts.tolist(), part.send_counts.tolist()
+    pc, oc = part.pin_counts.tolist(), part.pout_counts.tolist()
+
+    def exchange():
+        D._a2av(recv[:part.n_halo], send, rc, sc, None)
+        D._a2av(recv[part.n_halo:], pout, pc, oc, None)
+    exchange()
+    ex_mine, _ = _timed_local(exchange, steps, dist, cdev)
+    ex_ms = ex_mine * 1e3 / steps
+    sent = int(part.send_counts.sum()) + int(part.pout_counts.sum())
+    got = int(part.n_halo) + int(part.n_pin)
+    sp_bytes = sum(v["alg_bytes"] for v in spmm.values())
+    sp_ms = sum(v["ms"] for v in spmm.values())
+    rec = {"rank": rank, "spmm_edges": sum(v["edges"] for v in spmm.values()),
+           "spmm_alg_bytes": sp_bytes, "spmm_ms": sp_ms,
+           "spmm_GBps": sp_bytes / (sp_ms * 1e-3) / 1e9 if sp_ms > 0 else None,
+           "spmm_frac": sp_bytes / (sp_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS if sp_ms > 0 else None,
+           "blocks": spmm, "rows_sent": sent, "rows_received": got,
+           "bytes_sent": sent * 4 * f, "bytes_received": got * 4 * f, "exchange_ms": ex_ms,
+           "model_ms": max(spmm["push"]["ms"] + spmm["own"]["ms"], ex_ms) + spmm["recv"]["ms"]}
+    per_rank = gather_ranks(rec, dist)
+    ex_sum = exchange_summary(per_rank, world)
+    tot_b = sum(r["spmm_alg_bytes"] for r in per_rank)
+    t_max = max(r["spmm_ms"] for r in per_rank)
+    model = {"step_ms": max(r["model_ms"] for r in per_rank),
+             "rule": "max over ranks of max(t_push + t_own, t_exchange) + t_recv, each part "
+                     "timed alone on the rank (owned SpMM and exchange overlap; push before, "
+                     "receive pass after)",
+             "spmm_aggregate": {"alg_bytes": tot_b, "max_rank_ms": t_max,
+                                "GBps": tot_b / (t_max * 1e-3) / 1e9 if t_max > 0 else None,
+                                "frac": (tot_b / (t_max * 1e-3) / 1e9 / (world * HBM_PEAK_GBPS)
+                                         if t_max > 0 else None),
+                                "peak_GBps": world * HBM_PEAK_GBPS}}
+    return per_rank, ex_sum, model
 
 
 C5_NODES = 5_000_000
@@ -411,6 +486,49 @@ def measure_c5(world, rank, dist, cdev, device, args):
     halo = th.tensor([float(part.n_halo)], device=cdev, dtype=th.float64)
     dist.all_reduce(halo)
     ms = el * 1e3 / steps
+    # the step taken apart on every rank (round 5): the layer's forward + backward on
+    # the local block with the halo rows already in place, and the two exchanges alone
+    # (the forward's all-to-all-v of halo input rows, the backward's reverse one)
+    g_loc = part.local_graph(device)
+    x_full = D.halo_exchange(xi.detach(), part).detach().requires_grad_()
+    n_in = part.n_inner
+
+    def cstep():
+        th.autograd.grad(dr.conv(g_loc, x_full, et_l, norm_l)[:n_in], [x_full] + params_d, go_i)
+    cstep()
+    c_ms = _timed(cstep, steps, None, None) * 1e3 / steps
+    idx = part.device_plan(xi.device)
+    send = xi.detach().index_select(0, idx).contiguous()
+    recv = xi.new_empty((part.n_halo, f))
+    rc, sc = part.recv_counts.tolist(), part.send_counts.tolist()
+
+    def xstep():
+        D._a2av(recv, send, rc, sc, None)   # forward: halo input rows in
+        D._a2av(send, recv, sc, rc, None)   # backward: their gradients back out
+    xstep()
+    x_mine, _ = _timed_local(xstep, steps, dist, cdev)
+    x_ms = x_mine * 1e3 / steps
+    e_loc = int(g_loc.number_of_edges())
+    rows = int(part.n_halo) + int(sum(sc))
+    # bytes model of the fused R-GCN walks: one gathered 4F-byte row per edge each way
+    # (forward: the relation-transformed source row; backward: the gradient row) plus
+    # 12 B of column id, edge type and norm per edge each way
+    b_model = 2 * e_loc * (4 * f + 12)
+    rec = {"rank": rank, "local_edges": e_loc, "halo_rows": int(part.n_halo),
+           "compute_ms": c_ms, "compute_edges_per_s": e_loc / (c_ms * 1e-3),
+           "compute_alg_bytes": b_model,
+           "compute_GBps": b_model / (c_ms * 1e-3) / 1e9,
+           "compute_frac": b_model / (c_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+           "rows_exchanged": rows,
+           # forward: n_halo rows in, sum(sc) out; backward: the reverse
+           "bytes_received": rows * 4 * f, "bytes_sent": rows * 4 * f,
+           "exchange_ms": x_ms}
+    per_rank = gather_ranks(rec, dist)
+    ex_sum = exchange_summary(per_rank, world)
+    n1_rate = m / (n1_ms * 1e-3)
+    for r in per_rank:
+        r["compute_rate_vs_n1"] = r["compute_edges_per_s"] / n1_rate
+    del x_full, send, recv
     return {"workload": "C5: R-GCN RelGraphConv 4 relations basis 64->64, self-loop + bias, "
                         "norm 1/in-degree, Chung-Lu(0.5) %d nodes / %d typed edges" % (n, m),
             "scaling": "strong", "n_gpus": world, "value": m * steps / el, "unit": "edges/s",
@@ -425,7 +543,13 @@ def measure_c5(world, rank, dist, cdev, device, args):
                      "weight gradients (1e-3 + 1e-4 max|ref|) vs the whole-graph module",
             "partitioner": "device label propagation, %d rounds, slack %g (%.2fs)"
                            % (args.c4_rounds, args.c4_slack, lp_s),
-            "halo_rows_all_ranks": int(halo.item()), "setup_s": time.time() - t0}
+            "halo_rows_all_ranks": int(halo.item()), "per_rank": per_rank,
+            "exchange_aggregate": ex_sum,
+            "model": {"step_ms": max(r["compute_ms"] + r["exchange_ms"] for r in per_rank),
+                      "rule": "max over ranks of compute (local block, halo rows in place) + "
+                              "exchange (forward rows in, backward gradients out), each timed "
+                              "alone: the layer's exchanges are not overlapped"},
+            "setup_s": time.time() - t0}
 
 
 def make_local_graph(n_src, n_dst, src, dst, device):
@@ -707,6 +831,65 @@ def _timed(fn, steps, dist, cdev):
         dist.all_reduce(v, op=dist.ReduceOp.MAX)
         el = float(v.item())
     return el
+
+
+def _timed_local(fn, steps, dist, cdev):
+    """As _timed, but returns (this rank's own seconds, max over ranks)."""
+    if dist is not None:
+        dist.barrier()
+    th.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    th.cuda.synchronize()
+    mine = time.perf_counter() - t
+    if dist is not None:
+        dist.barrier()
+    return mine, _max_over_ranks(mine, dist, cdev)
+
+
+def spmm_alg_bytes(gi, feat, addend=False):
+    """SURVEY §8(d)'s algorithmic bytes of one copy_u_sum over block ``gi``: indptr +
+    column ids + one gathered 4F-byte source row per edge + one 4F-byte output row per
+    destination (+ the epilogue's addend row)."""
+    if gi is None:
+        return 0
+    c = gi.in_csr
+    rows, nnz = int(c.num_rows), int(c.nnz)
+    return 4 * (rows + 1) + 4 * nnz + 4 * feat * nnz + 4 * feat * rows * (2 if addend else 1)
+
+
+def gather_ranks(rec, dist):
+    """Every rank's record (a dict) on every rank, in rank order."""
+    if dist is None:
+        return [rec]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, rec)
+    return out
+
+
+def exchange_summary(per_rank, world, bytes_key_in="bytes_received", bytes_key_out="bytes_sent",
+                     ms_key="exchange_ms"):
+    """Per-rank achieved exchange rates against the xGMI links a rank uses in an
+    all-to-all (N - 1, one per peer) and the job's aggregate: the bytes that crossed
+    the fabric (each row counted once, at its receiver) over the slowest rank's
+    exchange time, against N (N - 1) links.  Adds fields to ``per_rank`` in place."""
+    links = max(world - 1, 1)
+    for r in per_rank:
+        t = r.get(ms_key) or 0.0
+        r["exchange_in_GBps"] = r[bytes_key_in] / (t * 1e-3) / 1e9 if t > 0 else None
+        r["exchange_out_GBps"] = r[bytes_key_out] / (t * 1e-3) / 1e9 if t > 0 else None
+        r["xgmi_peak_GBps"] = links * XGMI_LINK_GBPS
+        busy = max(r["exchange_in_GBps"] or 0.0, r["exchange_out_GBps"] or 0.0)
+        r["exchange_frac"] = busy / r["xgmi_peak_GBps"] if t > 0 else None
+    tmax = max((r.get(ms_key) or 0.0) for r in per_rank)
+    total = sum(r[bytes_key_in] for r in per_rank)
+    agg = total / (tmax * 1e-3) / 1e9 if tmax > 0 else None
+    peak = world * links * XGMI_LINK_GBPS
+    return {"bytes_all_ranks": total, "max_exchange_ms": tmax, "GBps": agg, "peak_GBps": peak,
+            "frac": agg / peak if agg else None,
+            "peak_note": "N (N - 1) x %g GB/s: every rank on its N - 1 peer links, one "
+                         "direction each (task brief's per-link figure)" % XGMI_LINK_GBPS}
 
 
 # Exit status of a run whose headline line was printed but one of its side lines

@@ -1469,8 +1469,10 @@ int64_t DGLMIEdgeSoftmaxWorkspaceBytes(const DGLMICsr* in_csr, int64_t values_pe
   const int64_t K = softmax_chunk_edges(in_csr->nnz, values_per_edge);
   const int64_t chunks = (in_csr->nnz + K - 1) / K;
   const int64_t stats = ((2 * in_csr->num_rows * values_per_edge * 4) + 255) & ~int64_t(255);
-  // carries, then one segmented-fixup counter per chunk
-  return stats + ((chunks * 2 * values_per_edge * 4 + 15) & ~int64_t(15)) + chunks * 4;
+  // carries, then one segmented-fixup counter per chunk (the row-owned walk's carries
+  // fit in the same room)
+  const int64_t chunked = ((chunks * 2 * values_per_edge * 4 + 15) & ~int64_t(15)) + chunks * 4;
+  return stats + std::max(chunked, softmax_owned_carry_bytes(in_csr->nnz, values_per_edge));
 }
 
 namespace {
@@ -1488,7 +1490,12 @@ int64_t softmax_setup(const DGLMIGraph* g, const DGLMIArray* x, const char* name
   std::memset(&a, 0, sizeof(a));
   a.indptr = idx(g, in.indptr);
   a.rows = in.rows;
-  a.eids = idx(g, in.data);
+  // identity edge ids (a position view; a graph whose edges came sorted by destination):
+  // the row-owned walk, which reads no edge ids (DGLMI_SOFTMAX_OWNED=0: the chunked
+  // row pass + edge pass, for A/B)
+  const char* owned = std::getenv("DGLMI_SOFTMAX_OWNED");
+  const bool ident = (g->eid_identity & 1) != 0 && !(owned != nullptr && owned[0] == '0');
+  a.eids = ident ? IdxPtr{nullptr, wide(g) ? 1 : 0} : idx(g, in.data);
   a.coo_dst = (g->coo_src && g->coo_dst) ? g->coo_dst : nullptr;
   a.nnz = in.nnz;
   a.num_rows = in.num_rows;

@@ -262,6 +262,9 @@ struct SoftmaxArgs {
 };
 bool softmax_supported(int64_t H);
 int64_t softmax_chunk_edges(int64_t nnz, int64_t H);
+// eids NULL (identity edge ids): the row-owned walk (one read, one write per value);
+// its carries need this many bytes after the statistics
+int64_t softmax_owned_carry_bytes(int64_t nnz, int64_t H);
 void launch_edge_softmax(const SoftmaxArgs& a, bool backward, hipStream_t s);
 
 // Load-balanced reduce-to-row kernels (kernels_spmm.hip).

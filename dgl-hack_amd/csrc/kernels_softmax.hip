@@ -252,8 +252,385 @@ __global__ void __launch_bounds__(kBlock) k_sm_edges(SoftmaxArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Row-owned walk (identity edge ids: a position view, or a graph whose edges came
+// sorted by destination).  The logits of a row are contiguous, so one wave can own
+// whole rows: it reads them once from HBM, reduces them, and re-reads them from the
+// cache it has just filled to write the output -- one HBM read and one write per value
+// instead of the row pass + edge pass (two HBM reads, plus rows and edge ids).
+//
+// Window w = positions [w W, (w + 1) W) (one wave each).  The wave owns every row that
+// STARTS in its window (ends at most T = 2W positions later), and of rows longer than T
+// ("hub" rows) only the positions inside its window (a "piece").  A piece's partial
+// state goes to carry slot (w, 0) when the hub row started in an earlier window and
+// (w, 1) when it starts in this one (a row longer than W crosses every boundary it
+// meets, so a window meets at most those two); k_sm_hub merges a hub row's pieces in
+// window order (deterministic, no atomics) and writes its positions.  Lane (j, q) holds
+// V = min(H, 4) consecutive values (heads q V ..) of position b + j; L = 64 / (H / V)
+// positions per step.  A step inside the current row needs no row ids and no cross-lane
+// work (every lane keeps its own running max / sum); only a step that crosses a row
+// boundary reads the row ids and reduces across lanes.
+template <int H>
+struct OwnedShape {
+  static constexpr int V = H < 4 ? H : 4;  // values per lane
+  static constexpr int LP = H / V;         // lanes per position
+  static constexpr int L = 64 / LP;        // positions per step
+  static constexpr int U = 16 / V;         // steps whose loads are issued together
+  static constexpr int64_t W = 32 * L;     // window (positions)
+  static constexpr int64_t T = 2 * W;      // longer rows are hub rows
+};
+
+// e^x as one v_exp_f32 (relative error ~|x| 2^-24; x = s - max <= 0 here)
+__device__ __forceinline__ float fexp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
+
+// an agent-coherent load (global_load sc1: past this CU's L1) of a value another lane
+// of the same wave stored earlier in this kernel
+__device__ __forceinline__ float ld_fresh(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int H, int MODE>
+struct OwnedWalk {
+  using S = OwnedShape<H>;
+  static constexpr int V = S::V, LP = S::LP, L = S::L, U = S::U;
+  static constexpr float kId = MODE == SM_STATS ? -INFINITY : 0.0f;  // identity of m
+  const SoftmaxArgs& a;
+  int j, q;  // position in the step, head group
+  float m[V], l[V];  // this lane's running state (MODE DOTSUM: m = sum, l unused)
+
+  __device__ __forceinline__ OwnedWalk(const SoftmaxArgs& args, int lane)
+      : a(args), j(lane / LP), q(lane % LP) { clear(); }
+  __device__ __forceinline__ void clear() {
+#pragma unroll
+    for (int v = 0; v < V; ++v) { m[v] = kId; l[v] = 0.0f; }
+  }
+  __device__ __forceinline__ int64_t off(int64_t p) const { return p * H + q * V; }
+  // the U-step (or 1-step) batch of positions b + u L + j, all in one row
+  template <int N>
+  __device__ __forceinline__ void accumulate(int64_t b, int64_t pend) {
+    float x[N][V], g[MODE == SM_DOTSUM ? N : 1][V];
+#pragma unroll
+    for (int u = 0; u < N; ++u) {
+      const int64_t p = b + u * L + j;
+      if (p < pend) {
+        ldrow<V>(a.s + off(p), x[u]);
+        if constexpr (MODE == SM_DOTSUM) ldrow<V>(a.ga + off(p), g[u]);
+      } else {
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          x[u][v] = kId;
+          if constexpr (MODE == SM_DOTSUM) g[u][v] = 0.0f;
+        }
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      if constexpr (MODE == SM_STATS) {
+        // one rescale per batch: mn = max(m, x_u); l = l e^(m - mn) + sum e^(x_u - mn).
+        // All -inf so far: nothing added (l stays 0); a +inf or NaN logit makes l NaN.
+        float mb = x[0][v];
+#pragma unroll
+        for (int u = 1; u < N; ++u) mb = fmaxf(mb, x[u][v]);
+        const float mn = fmaxf(m[v], mb);
+        float s = l[v] * fexp(m[v] - mn);
+#pragma unroll
+        for (int u = 0; u < N; ++u) s += fexp(x[u][v] - mn);
+        if (mn != -INFINITY) l[v] = s;
+        m[v] = mn;
+      } else {
+#pragma unroll
+        for (int u = 0; u < N; ++u) m[v] += x[u][v] * g[u][v];
+      }
+    }
+  }
+  // fold one value into a lane state
+  __device__ __forceinline__ static void fold(float& m, float& l, float x) {
+    if constexpr (MODE == SM_STATS)
+      merge1(m, l, x, x == INFINITY ? __builtin_nanf("") : (x == -INFINITY ? 0.0f : 1.0f));
+    else
+      m += x;
+  }
+  // every lane of head group q ends with the group's reduction (xor butterfly: both
+  // partners compute the same commutative merge)
+  __device__ __forceinline__ void reduce() {
+#pragma unroll
+    for (int d = LP; d < 64; d <<= 1)
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const float m2 = __shfl_xor(m[v], d);
+        if constexpr (MODE == SM_STATS) {
+          const float l2 = __shfl_xor(l[v], d);
+          merge1(m[v], l[v], m2, l2);
+        } else {
+          m[v] += m2;
+        }
+      }
+  }
+  // a finished row's statistics: forward (max, 1 / sum), backward sum(a ga)
+  __device__ __forceinline__ void put(int row, const float (&pm)[V], const float (&pl)[V]) const {
+    float* s0 = a.stat0 + (int64_t)row * H + q * V;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      s0[v] = pm[v];
+      if constexpr (MODE == SM_STATS) a.stat1[(int64_t)row * H + q * V + v] = 1.0f / pl[v];
+    }
+  }
+  __device__ __forceinline__ void stats_of(int row, float (&sm)[V], float (&si)[V]) const {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      sm[v] = ld_fresh(a.stat0 + (int64_t)row * H + q * V + v);
+      si[v] = MODE == SM_STATS ? ld_fresh(a.stat1 + (int64_t)row * H + q * V + v) : 0.0f;
+    }
+  }
+  // the output of positions b + u L + j < pend with their row's statistics
+  template <int N>
+  __device__ __forceinline__ void emit(int64_t b, int64_t pend, const float (&sm)[V], const float (&si)[V]) const {
+    float x[N][V], g[MODE == SM_DOTSUM ? N : 1][V];
+#pragma unroll
+    for (int u = 0; u < N; ++u) {
+      const int64_t p = b + u * L + j;
+      if (p < pend) {
+        ldrow<V>(a.s + off(p), x[u]);
+        if constexpr (MODE == SM_DOTSUM) ldrow<V>(a.ga + off(p), g[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < N; ++u) {
+      const int64_t p = b + u * L + j;
+      if (p >= pend) continue;
+      float o[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        if constexpr (MODE == SM_STATS) o[v] = fexp(x[u][v] - sm[v]) * si[v];
+        else o[v] = x[u][v] * g[u][v] - x[u][v] * sm[v];  // softmax.py:103-112's order
+      }
+      strow<V>(a.out + off(p), o);
+    }
+  }
+
+  // rows [s0, s1) complete: statistics, then outputs
+  __device__ void span(int64_t s0, int64_t s1) {
+    const int jl_full = L - 1;
+    int cur = a.rows[s0];
+    int64_t cur_end = a.indptr[cur + 1];
+    bool open = true;
+    clear();
+    for (int64_t b = s0; b < s1;) {
+      if (cur_end - b >= U * L) { accumulate<U>(b, s1); b += U * L; continue; }
+      if (cur_end - b >= L) { accumulate<1>(b, s1); b += L; continue; }
+      // a step that crosses a row boundary (cur ends at or before b + L)
+      const int64_t p = b + j;
+      const bool valid = p < s1, in_cur = p < cur_end;
+      float x[V], g[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) { x[v] = kId; g[v] = 0.0f; }
+      if (valid) {
+        ldrow<V>(a.s + off(p), x);
+        if constexpr (MODE == SM_DOTSUM) ldrow<V>(a.ga + off(p), g);
+      }
+      if constexpr (MODE == SM_DOTSUM) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) x[v] *= g[v];
+      }
+      const int rr = in_cur ? cur : (valid ? a.rows[p] : INT_MAX);
+      if (in_cur) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) fold(m[v], l[v], x[v]);
+      }
+      reduce();
+      if (j == 0) put(cur, m, l);
+      const int jl = s1 - b < L ? static_cast<int>(s1 - b) - 1 : jl_full;  // last valid j
+      // cur ends at b + jl + 1 only in the span's last step (in a full step that is a
+      // step inside cur): the span is done
+      if (cur_end > b + jl) {
+        open = false;
+        b += L;
+        continue;
+      }
+      const int rl = __shfl(rr, jl * LP + q);
+      const bool mine = valid && !in_cur;
+      if (__ballot(mine && rr != rl) == 0) {
+        // one new row from cur_end on: each lane starts its own state
+        clear();
+        if (mine) {
+#pragma unroll
+          for (int v = 0; v < V; ++v) fold(m[v], l[v], x[v]);
+        }
+      } else {
+        // rows that start and end inside the step: segmented inclusive scan over j
+        float sm[V], sl[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          sm[v] = kId;
+          sl[v] = 0.0f;
+          if (mine) fold(sm[v], sl[v], x[v]);
+        }
+        const int rs = in_cur ? -1 : rr;
+#pragma unroll
+        for (int d = 1; d < L; d <<= 1) {
+          const int r2 = __shfl_up(rs, d * LP);
+#pragma unroll
+          for (int v = 0; v < V; ++v) {
+            const float m2 = __shfl_up(sm[v], d * LP);
+            const float l2 = MODE == SM_STATS ? __shfl_up(sl[v], d * LP) : 0.0f;
+            if (j >= d && r2 == rs) {
+              if constexpr (MODE == SM_STATS) merge1(sm[v], sl[v], m2, l2);
+              else sm[v] += m2;
+            }
+          }
+        }
+        const int rn = __shfl_down(rs, LP);
+        const bool seg_end = mine && (j == jl || rn != rs);
+        if (seg_end && rs != rl) put(rs, sm, sl);
+        clear();
+        if (j == jl) {
+#pragma unroll
+          for (int v = 0; v < V; ++v) { m[v] = sm[v]; l[v] = sl[v]; }
+        }
+      }
+      cur = rl;
+      cur_end = a.indptr[cur + 1];
+      b += L;
+    }
+    if (open) {
+      reduce();
+      if (j == 0) put(cur, m, l);
+    }
+    // this wave's row statistics, stored above by the j == 0 lanes, before any lane
+    // reads them back (ld_fresh: L2, the point of coherence)
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_s_waitcnt(0);  // every store of this wave performed at L2
+    __builtin_amdgcn_wave_barrier();
+    cur = a.rows[s0];
+    cur_end = a.indptr[cur + 1];
+    float cm[V], ci[V];
+    stats_of(cur, cm, ci);
+    for (int64_t b = s0; b < s1;) {
+      if (cur_end - b >= U * L) { emit<U>(b, s1, cm, ci); b += U * L; continue; }
+      if (cur_end - b >= L) { emit<1>(b, s1, cm, ci); b += L; continue; }
+      const int64_t p = b + j;
+      const bool valid = p < s1, in_cur = p < cur_end;
+      const int rr = in_cur ? cur : (valid ? a.rows[p] : cur);
+      float rm[V], ri[V];
+      if (in_cur) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) { rm[v] = cm[v]; ri[v] = ci[v]; }
+      } else {
+        stats_of(rr, rm, ri);
+      }
+      emit<1>(b, s1, rm, ri);
+      const int jl = s1 - b < L ? static_cast<int>(s1 - b) - 1 : jl_full;
+      if (cur_end <= b + jl) {
+        cur = __shfl(rr, jl * LP + q);
+        cur_end = a.indptr[cur + 1];
+        stats_of(cur, cm, ci);
+      }
+      b += L;
+    }
+  }
+  // partial state of hub row positions [pa, pb) -> carry slot
+  __device__ void piece(int64_t pa, int64_t pb, float* slot) {
+    clear();
+    for (int64_t b = pa; b < pb; b += U * L) accumulate<U>(b, pb);
+    reduce();
+    if (j == 0) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        slot[q * V + v] = m[v];
+        if constexpr (MODE == SM_STATS) slot[H + q * V + v] = l[v];
+      }
+    }
+  }
+};
+
+template <int H, int MODE>
+__global__ void __launch_bounds__(kBlock) k_sm_owned(SoftmaxArgs a) {
+  using S = OwnedShape<H>;
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+  const int64_t lo = w * S::W;
+  if (lo >= a.nnz) return;
+  const int64_t hi = lo + S::W < a.nnz ? lo + S::W : a.nnz;
+  OwnedWalk<H, MODE> walk(a, lane);
+  const int r0 = a.rows[lo];
+  const int64_t st0 = a.indptr[r0], en0 = a.indptr[r0 + 1];
+  int64_t s0 = lo;
+  if (st0 < lo) {  // a row that started in an earlier window
+    if (en0 - st0 > S::T) walk.piece(lo, en0 < hi ? en0 : hi, a.carry + (2 * w) * 2 * H);
+    s0 = en0;  // a shorter one belongs to the window it started in
+  }
+  if (s0 >= hi) return;
+  const int r1 = a.rows[hi - 1];
+  const int64_t st1 = a.indptr[r1], en1 = a.indptr[r1 + 1];
+  int64_t s1 = en1;
+  if (en1 - st1 > S::T) {  // a hub row starting in this window: its first piece
+    walk.piece(st1, hi, a.carry + (2 * w + 1) * 2 * H);
+    s1 = st1;
+  }
+  if (s1 > s0) walk.span(s0, s1);
+}
+
+// hub rows: merge the row's pieces in window order, then write this window's piece
+template <int H, int MODE>
+__global__ void __launch_bounds__(kBlock) k_sm_hub(SoftmaxArgs a) {
+  using S = OwnedShape<H>;
+  constexpr int V = S::V;
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+  const int64_t lo = w * S::W;
+  if (lo >= a.nnz) return;
+  const int64_t hi = lo + S::W < a.nnz ? lo + S::W : a.nnz;
+  OwnedWalk<H, MODE> walk(a, lane);
+  auto finish = [&](int64_t st, int64_t en, int64_t pa, int64_t pb) {
+    const int64_t wf = st / S::W, wl = (en - 1) / S::W;
+    float m[V], l[V];
+    const float* c = a.carry + (2 * wf + 1) * 2 * H + walk.q * V;  // the first piece
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      m[v] = c[v];
+      l[v] = MODE == SM_STATS ? c[H + v] : 0.0f;
+    }
+    for (int64_t w2 = wf + 1; w2 <= wl; ++w2) {
+      const float* c2 = a.carry + (2 * w2) * 2 * H + walk.q * V;
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        if constexpr (MODE == SM_STATS) merge(m[v], l[v], c2[v], c2[H + v]);
+        else m[v] += c2[v];
+      }
+    }
+    if constexpr (MODE == SM_STATS) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) l[v] = 1.0f / l[v];
+    }
+    for (int64_t b = pa; b < pb; b += S::U * S::L) walk.template emit<S::U>(b, pb, m, l);
+  };
+  const int r0 = a.rows[lo];
+  const int64_t st0 = a.indptr[r0], en0 = a.indptr[r0 + 1];
+  if (st0 < lo && en0 - st0 > S::T) finish(st0, en0, lo, en0 < hi ? en0 : hi);
+  const int r1 = a.rows[hi - 1];
+  const int64_t st1 = a.indptr[r1], en1 = a.indptr[r1 + 1];
+  if (st1 >= lo && en1 - st1 > S::T) finish(st1, en1, st1, hi);
+}
+
+template <int H>
+void run_owned(const SoftmaxArgs& a, bool backward, hipStream_t st) {
+  const int64_t windows = (a.nnz + OwnedShape<H>::W - 1) / OwnedShape<H>::W;
+  const dim3 grid(static_cast<unsigned>((windows + kBlock / 64 - 1) / (kBlock / 64))), blk(kBlock);
+  if (!backward) {
+    hipLaunchKernelGGL((k_sm_owned<H, SM_STATS>), grid, blk, 0, st, a);
+    hipLaunchKernelGGL((k_sm_hub<H, SM_STATS>), grid, blk, 0, st, a);
+  } else {
+    hipLaunchKernelGGL((k_sm_owned<H, SM_DOTSUM>), grid, blk, 0, st, a);
+    hipLaunchKernelGGL((k_sm_hub<H, SM_DOTSUM>), grid, blk, 0, st, a);
+  }
+}
+
 template <int H>
 void run(const SoftmaxArgs& a, bool backward, hipStream_t st) {
+  if (!a.eids) {
+    run_owned<H>(a, backward, st);
+    return;
+  }
   const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
   const dim3 rb(static_cast<unsigned>((chunks + kBlock - 1) / kBlock)), blk(kBlock);
   // k_sm_rows: one wave per chunk
@@ -282,6 +659,19 @@ int64_t softmax_chunk_edges(int64_t nnz, int64_t H) {
   int64_t steps = 16;
   while (steps > 1 && nnz / (L * steps) < 2048) steps >>= 1;
   return L * steps;
+}
+
+// the row-owned walk's carries: two slots of 2H floats per window
+int64_t softmax_owned_carry_bytes(int64_t nnz, int64_t H) {
+  int64_t W = 0;
+  switch (H) {
+    case 1: W = OwnedShape<1>::W; break;
+    case 2: W = OwnedShape<2>::W; break;
+    case 4: W = OwnedShape<4>::W; break;
+    case 8: W = OwnedShape<8>::W; break;
+    default: W = OwnedShape<16>::W; break;
+  }
+  return ((nnz + W - 1) / W) * 2 * 2 * H * 4;
 }
 
 void launch_edge_softmax(const SoftmaxArgs& a, bool backward, hipStream_t s) {

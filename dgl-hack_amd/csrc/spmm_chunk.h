@@ -146,6 +146,11 @@ __device__ __forceinline__ typename VecT<VW>::T edge_value(const FastArgs& a, in
     const int64_t c = a.x_map ? a.x_map[col] : col;
     const int64_t e = a.w_map ? a.w_map[eid] : eid;
     return vmul(vld<VW>(a.x + c * a.F + VW * fv), vld<VW>(a.w + e * a.F + VW * fv));
+  } else if constexpr (KIND == FAST_COL_MUL_POS) {
+    // the position's weight is staged with the walk (s_w) and applied by the caller;
+    // there is no edge id to index the weight by
+    const int64_t c = a.x_map ? a.x_map[col] : col;
+    return vld<VW>(a.x + c * a.F + VW * fv);
   } else {
     const int64_t c = a.x_map ? a.x_map[col] : col;
     const int64_t e = a.w_map ? a.w_map[eid] : eid;
@@ -337,8 +342,10 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, IdxPtr indp
             val[u][v] = (ok && f4 < F4) ? (nt ? vld_nt<VW>(px) : vld<VW>(px)) : I;
           } else {
             val[u][v] = (ok && f4 < F4) ? edge_value<KIND, VW>(a, col, eid, f4, hsel[v], wn, s_row[g][ub + u]) : I;
-            // (mapped mul kinds: the product is already in val)
-            if constexpr (kMulScl) wsc[u][kMulScl ? v : 0] = 1.0f;
+            // (mapped mul kinds: the product is already in val, except the staged
+            // per-position weight)
+            if constexpr (kScalarW) wsc[u][kMulScl ? v : 0] = s_w[kScalarW ? g : 0][kScalarW ? ub + u : 0];
+            else if constexpr (kMulScl) wsc[u][kMulScl ? v : 0] = 1.0f;
             if constexpr (kMulVec) wv[kTwo ? u : 0][kTwo ? v : 0] = vone<VW>();
           }
         }

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Fused edge softmax on the C3 graph (232,965 nodes / 114.6 M edges), H = 8 and
-H = 1: forward and backward HIP-event medians on the graph and on its in-CSR position
-view, plus a digest of every output (run against two builds of the library to
+H = 1: forward and backward HIP-event medians on the graph, on its in-CSR position
+view with the chunked row + edge passes, and on the view with the row-owned walk, plus a digest of every output (run against two builds of the library to
 show bit-identity)."""
 import hashlib
 import json
@@ -40,12 +40,19 @@ def main():
         gen = th.Generator(device=dev).manual_seed(H)
         s = th.randn(gidx.number_of_edges(), H, 1, device=dev, generator=gen) * 3
         ga = th.randn(s.shape, device=dev, generator=gen)
-        for name, gi in (("graph", gidx), ("view", gidx.position_view("in"))):
+        view = gidx.position_view("in")
+        for name, gi, owned in (("graph", gidx, "1"), ("view_chunked", view, "0"), ("view", view, "1")):
+            os.environ["DGLMI_SOFTMAX_OWNED"] = owned  # 0: the chunked row + edge passes
             out, gs = th.empty_like(s), th.empty_like(s)
             res["H%d_%s_fwd_ms" % (H, name)] = ktime(lambda: K.edge_softmax_forward(gi, s, out))
             res["H%d_%s_bwd_ms" % (H, name)] = ktime(lambda: K.edge_softmax_backward(gi, out, ga, gs))
             for t in (out, gs):
                 dig.update(t.cpu().numpy().tobytes())
+            # operand bytes: forward reads the logits and writes the softmax, backward
+            # reads the softmax and its gradient and writes the logits' gradient
+            nb = s.numel() * 4
+            res["H%d_%s_fwd_TBps" % (H, name)] = 2 * nb / res["H%d_%s_fwd_ms" % (H, name)] / 1e9
+            res["H%d_%s_bwd_TBps" % (H, name)] = 3 * nb / res["H%d_%s_bwd_ms" % (H, name)] / 1e9
     res["digest"] = dig.hexdigest()
     print(json.dumps(res), flush=True)
 

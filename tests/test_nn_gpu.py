@@ -340,12 +340,17 @@ def test_graph_conv_fused_epilogue_matches_reference_steps(norm, fin, fout, bloc
             assert th.equal(res[0][0], res[1][0])
 
 
+@pytest.mark.parametrize("owned", ["0", "1"])
 @pytest.mark.parametrize("H,D", [(8, 8), (3, 5), (1, 16)])
-def test_gat_composition_position_space_bit_identical(H, D, monkeypatch):
+def test_gat_composition_position_space_bit_identical(H, D, owned, monkeypatch):
     """GATConv's unfused composition run on the in-CSR position view (logits and
     attention in walk order, GATConv._position_space) gives the same bits as the
-    edge-id composition: output and every gradient.  (3 heads: the edge softmax's
-    decomposition rather than its fused kernel.)"""
+    edge-id composition: output and every gradient, when the view's edge softmax runs
+    the same chunked kernels (DGLMI_SOFTMAX_OWNED=0).  With the row-owned softmax the
+    view's (the default since round 5: one read per logit, another summation order) the
+    results agree within fp32 tolerance.  (3 heads: the edge softmax's decomposition
+    rather than its fused kernel.)"""
+    monkeypatch.setenv("DGLMI_SOFTMAX_OWNED", owned)
     from dgl.nn.pytorch.conv import gatconv
     from graphs import powerlaw
     src, dst, n = powerlaw(20000, 300000, seed=21)
@@ -370,7 +375,11 @@ def test_gat_composition_position_space_bit_identical(H, D, monkeypatch):
         assert bool(calls) == pos
         res.append([out.detach().clone(), x.grad.clone()] + [p.grad.clone() for p in gat.parameters()])
     for a, b in zip(*res):
-        assert th.equal(a, b), float((a - b).abs().max())
+        if owned == "0" or H == 3:
+            assert th.equal(a, b), float((a - b).abs().max())
+        else:
+            assert th.allclose(a, b, rtol=1e-4, atol=1e-5 * float(b.abs().max())), \
+                float((a - b).abs().max())
     # attention dropout in training keeps the edge-id order (nn.Dropout's draws)
     gd = nn.GATConv(32, D, H, attn_drop=0.5).to(DEV)
     gd.use_fused = False

@@ -1,0 +1,155 @@
+"""The row-owned edge softmax (kernels_softmax.hip k_sm_owned / k_sm_hub), taken when
+the in-CSR's edge ids are its positions (a position view, a destination-sorted graph):
+forward and backward against an fp64 softmax per destination and against the chunked
+row pass + edge pass (DGLMI_SOFTMAX_OWNED=0), on degree sequences that put row ends on
+every boundary the walk has -- a step (L positions), a window (W), the hub threshold
+(T = 2W) -- plus rows of 0-3 edges (several rows inside one step), hub rows many windows
+long, and masked / NaN / +inf logits.  Reference: python/dgl/nn/pytorch/softmax.py:33-114."""
+import numpy as np
+import pytest
+import torch as th
+
+import dgl
+from dgl import kernel as K
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _shape(H):
+    V = min(H, 4)
+    L = 64 // (H // V)
+    W = 32 * L
+    return L, W, 2 * W
+
+
+def _degrees(H, seed):
+    L, W, T = _shape(H)
+    rs = np.random.RandomState(seed)
+    edge = [0, 1, 2, 3, L - 1, L, L + 1, W - 1, W, W + 1, T - 1, T, T + 1, 3 * W + 5, 11 * W + 3]
+    tiny = list(rs.randint(0, 4, 3000))
+    mid = list(rs.randint(1, 3 * L, 400))
+    big = list(rs.randint(W // 2, T + 1, 60))
+    deg = edge + tiny + mid + big + edge[::-1]
+    rs.shuffle(deg)
+    return np.array(deg, dtype=np.int64)
+
+
+def _graph(deg, seed):
+    n = len(deg)
+    rs = np.random.RandomState(seed)
+    dst = np.repeat(np.arange(n), deg)
+    src = rs.randint(0, n, len(dst))
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    return g._graph.get_immutable_gidx(DEV)
+
+
+def _fp64(rows, s, n):
+    s64 = s.double()
+    mx = th.full((n,) + s.shape[1:], -float("inf"), dtype=th.float64, device=DEV)
+    mx = mx.index_reduce(0, rows, s64, "amax")
+    ex = th.exp(s64 - mx[rows])
+    den = th.zeros_like(mx).index_add_(0, rows, ex)
+    return ex / den[rows]
+
+
+@pytest.mark.parametrize("H", [1, 2, 4, 8, 16])
+def test_owned_softmax_fp64_and_chunked(H, monkeypatch):
+    deg = _degrees(H, H)
+    gidx = _graph(deg, H + 1)
+    view = gidx.position_view("in")
+    m = int(deg.sum())
+    rows = view.in_csr.rows.long()
+    gen = th.Generator(device=DEV).manual_seed(H)
+    s = th.randn(m, H, device=DEV, generator=gen) * 3
+    ga = th.randn(m, H, device=DEV, generator=gen)
+    res = {}
+    for owned in ("1", "0"):
+        monkeypatch.setenv("DGLMI_SOFTMAX_OWNED", owned)
+        out, gs = th.empty_like(s), th.empty_like(s)
+        K.edge_softmax_forward(view, s, out)
+        K.edge_softmax_backward(view, out, ga, gs)
+        res[owned] = (out, gs)
+    (a1, g1), (a0, g0) = res["1"], res["0"]
+    ref = _fp64(rows, s, len(deg))
+    assert th.allclose(a1.double(), ref, rtol=1e-5, atol=1e-7)
+    assert th.allclose(a1, a0, rtol=1e-5, atol=1e-7)
+    # backward: a ga - a sum(a ga), fp64 from the fp32 forward output
+    a64, g64 = a1.double(), ga.double()
+    S = th.zeros((len(deg), H), dtype=th.float64, device=DEV).index_add_(0, rows, a64 * g64)
+    gref = a64 * g64 - a64 * S[rows]
+    assert th.allclose(g1.double(), gref, rtol=1e-4, atol=1e-6)
+    assert th.allclose(g1, g0, rtol=1e-4, atol=1e-6)
+
+
+def test_owned_softmax_deterministic(monkeypatch):
+    monkeypatch.setenv("DGLMI_SOFTMAX_OWNED", "1")
+    deg = _degrees(8, 3)
+    view = _graph(deg, 4).position_view("in")
+    s = th.randn(int(deg.sum()), 8, device=DEV)
+    a = th.empty_like(s)
+    b = th.empty_like(s)
+    K.edge_softmax_forward(view, s, a)
+    K.edge_softmax_forward(view, s, b)
+    assert th.equal(a, b)
+
+
+@pytest.mark.parametrize("H", [1, 8])
+def test_owned_softmax_special_values(H, monkeypatch):
+    """-inf logits get 0, an all -inf row NaN, a +inf or NaN logit makes its row NaN
+    (exp(s - max) / sum, as the decomposition) -- in short rows, in rows cut by steps
+    and in hub rows cut into pieces."""
+    L, W, T = _shape(H)
+    deg = np.array([3, L + 2, 2, 5, W + 7, T + 9, 4, 3 * W, 1, 6], dtype=np.int64)
+    view = _graph(deg, 7).position_view("in")
+    rows = view.in_csr.rows.long()
+    m = int(deg.sum())
+    s = th.randn(m, H, device=DEV)
+    starts = np.concatenate([[0], np.cumsum(deg)[:-1]])
+    s[int(starts[0]) + 1, 0] = -float("inf")          # one masked logit
+    s[int(starts[2]):int(starts[2]) + 2] = -float("inf")  # an all-masked row
+    s[int(starts[3]) + 4, 0] = float("nan")           # NaN in a short row
+    s[int(starts[4]) + W, 0] = float("inf")           # +inf in a row cut by a window
+    s[int(starts[5]) + 2 * W + 3, 0] = -float("inf")   # masked inside a hub row
+    s[int(starts[7]) + W + 1, 0] = float("nan")       # NaN in a hub row
+    out = {}
+    for owned in ("1", "0"):
+        monkeypatch.setenv("DGLMI_SOFTMAX_OWNED", owned)
+        o = th.empty_like(s)
+        K.edge_softmax_forward(view, s, o)
+        out[owned] = o
+    a, b = out["1"], out["0"]
+    assert th.equal(th.isnan(a), th.isnan(b))
+    fin = ~th.isnan(b)
+    assert th.allclose(a[fin], b[fin], rtol=1e-5, atol=1e-7)
+    assert a[int(starts[0]) + 1, 0].item() == 0.0
+    assert bool(th.isnan(a[int(starts[2]):int(starts[2]) + 2]).all())
+    ref = _fp64(rows, s, len(deg))
+    assert th.equal(th.isnan(a), th.isnan(ref))
+    assert th.allclose(a[fin].double(), ref[fin], rtol=1e-5, atol=1e-7)
+
+
+def test_dst_sorted_graph_takes_owned_route(monkeypatch):
+    """A whole graph whose edges came sorted by destination (in-CSR edge ids = positions)
+    runs the row-owned walk through nn.edge_softmax, with the same values as the
+    chunked route."""
+    from dgl.nn.pytorch import edge_softmax
+    from graphs import powerlaw
+    src, dst, n = powerlaw(20_000, 400_000, seed=31)
+    order = np.lexsort((src, dst))
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src[order], dst[order])
+    assert g._graph.get_immutable_gidx(DEV).eid_identity_bits() & 1
+    s = th.randn(len(src), 4, 1, device=DEV)
+    res = {}
+    for owned in ("1", "0"):
+        monkeypatch.setenv("DGLMI_SOFTMAX_OWNED", owned)
+        x = s.clone().requires_grad_()
+        a = edge_softmax(g, x)
+        a.backward(th.ones_like(a) * th.arange(a.shape[0], device=DEV).reshape(-1, 1, 1) % 7)
+        res[owned] = (a.detach(), x.grad)
+    assert th.allclose(res["1"][0], res["0"][0], rtol=1e-5, atol=1e-7)
+    assert th.allclose(res["1"][1], res["0"][1], rtol=1e-4, atol=1e-6)

@@ -156,3 +156,45 @@ def test_dst_sorted_graph_reads_edge_operands_at_positions(msg, order_by, monkey
         outs.append((out.detach(),) + tuple(grads))
     for a, b in zip(*outs):
         assert th.equal(a, b)
+
+
+@pytest.mark.parametrize("route", ["dst_sorted", "position_view"])
+def test_mapped_u_mul_e_on_identity_edge_ids(route, monkeypatch):
+    """A node mapping (lhs_map) on a walk whose edge ids are its positions: the
+    per-position weight must be read at each position, not at position 0
+    (the identity-id switch to the staged-weight kernel took the mapped
+    gather path, which read w[0] for every edge).  Compared with the edge-id walk."""
+    import numpy as np
+    from dgl import kernel as K
+    src, dst, n = powerlaw(40_000, 300_000, seed=13)
+    order = np.lexsort((src, dst))
+    src, dst = src[order], dst[order]
+    m = len(src)
+    gen = th.Generator(device=DEV).manual_seed(17)
+    D = 16  # D % 4 == 0 and D >= 16: the float4 staged-weight kernel
+    x = th.randn(n + 7, D, device=DEV, generator=gen)
+    lhs_map = th.randperm(n + 7, device=DEV, generator=gen)[:n].to(th.int32)
+    w = th.rand(m, 1, device=DEV, generator=gen) + 0.5
+    monkeypatch.setenv("DGLMI_EID_IDENTITY", "0")
+    g0 = dgl.DGLGraph()
+    g0.add_nodes(n)
+    g0.add_edges(src, dst)
+    ref = th.zeros(n, D, device=DEV)
+    K.binary_op_reduce("sum", "mul", g0._graph.get_immutable_gidx(DEV), "src", "edge", x, w, ref,
+                       lhs_map=lhs_map)
+    exact = (x[lhs_map.long()][th.as_tensor(src).long().to(DEV)] * w)
+    exact = th.zeros(n, D, device=DEV).index_add_(0, th.as_tensor(dst).long().to(DEV), exact)
+    assert th.allclose(ref, exact, rtol=1e-4, atol=1e-4)
+    if route == "dst_sorted":
+        monkeypatch.setenv("DGLMI_EID_IDENTITY", "1")
+        g1 = dgl.DGLGraph()
+        g1.add_nodes(n)
+        g1.add_edges(src, dst)
+        gidx = g1._graph.get_immutable_gidx(DEV)
+        assert gidx.eid_identity_bits() & 1
+        wv = w
+    else:
+        gidx, wv = g0._graph.get_immutable_gidx(DEV).position_operand(w, "in")
+    out = th.zeros(n, D, device=DEV)
+    K.binary_op_reduce("sum", "mul", gidx, "src", "edge", x, wv.contiguous(), out, lhs_map=lhs_map)
+    assert th.equal(out, ref)
