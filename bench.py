@@ -1466,7 +1466,18 @@ def main():
             pmc = None
     # per-rank launch record: kernel time, edges and the fabric bytes of this rank's
     # own launch pair (its PMC passes) -> its roofline fraction
+    # Bytes models per launch of THIS rank's row block, DESIGN.md §6:
+    #  * algorithmic (SURVEY §8d): indptr + indices + one gathered 4F-byte source row
+    #    per edge + one 4F-byte output row per destination -- counts the re-reads
+    #    that L2 serves, so its rate exceeds HBM peak on skewed graphs;
+    #  * compulsory: every source row once (the bytes no cache can avoid);
+    #  * traffic: what the PMC counters saw leave L2 for the fabric (Infinity
+    #    Cache + HBM), measured by this run's own rocprofv3 passes -- the bytes the
+    #    kernel is actually bound by.  roofline.achieved = traffic / kernel time.
+    alg_rank = 4 * (n_dst + 1) + 4 * m_local + 4 * FEAT * m_local + 4 * FEAT * n_dst
+    comp_rank = 4 * (n_dst + 1) + 4 * m_local + 4 * FEAT * n + 4 * FEAT * n_dst
     per_rank = [{"rank": rank, "kernel_ms": kernel_ms, "edges": int(m_local), "n_dst": int(n_dst),
+                 "alg_bytes": int(alg_rank), "compulsory_bytes": int(comp_rank),
                  "traffic": pmc["bytes_per_launch"] if pmc else None,
                  "l2_hit_rate": pmc.get("l2_hit_rate") if pmc else None}]
     if dist is not None:
@@ -1492,41 +1503,38 @@ def main():
     if upd is not None:
         upd_res = measure_update_all(upd, x, out, args)
         del upd
-    # Bytes models per launch (per rank), DESIGN.md §6:
-    #  * algorithmic (SURVEY §8d): indptr + indices + one gathered 4F-byte source row
-    #    per edge + one 4F-byte output row per destination -- counts the re-reads
-    #    that L2 serves, so its rate exceeds HBM peak on skewed graphs;
-    #  * compulsory: every source row once (the bytes no cache can avoid);
-    #  * traffic: what the PMC counters saw leave L2 for the fabric (Infinity
-    #    Cache + HBM), measured by this run's own rocprofv3 passes -- the bytes the
-    #    kernel is actually bound by.  roofline.achieved = traffic / kernel time.
-    alg_bytes = 4 * (n_dst + 1) + 4 * m_local + 4 * FEAT * m_local + 4 * FEAT * n_dst
-    compulsory = 4 * (n_dst + 1) + 4 * m_local + 4 * FEAT * n + 4 * FEAT * n_dst
-    alg_gbps = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    comp_gbps = compulsory / (kernel_ms * 1e-3) / 1e9
-    # the line's roofline: at N = 1 the launch's own; at N > 1 the rank with the
-    # highest fraction (per_rank lists every rank's, frac_min the lowest)
-    fr = [r for r in per_rank if r["frac"] is not None]
-    best = max(fr, key=lambda r: r["frac"]) if fr else None
-    traffic = best["traffic"] if best else None
-    achieved = best["achieved_GBps"] if best else None
-    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": best["frac"] if best else None, "traffic": traffic,
+    # The line's roofline is the JOB's: the bytes of every rank's launch over the
+    # slowest rank's kernel time, against N x the HBM peak (N = 1: the launch's own).
+    # per_rank keeps each rank's own fraction beside it, frac_min the lowest.
+    kmax = max(r["kernel_ms"] for r in per_rank)
+    peak = HBM_PEAK_GBPS * world
+    alg_bytes = sum(r["alg_bytes"] for r in per_rank)
+    compulsory = sum(r["compulsory_bytes"] for r in per_rank)
+    alg_gbps = alg_bytes / (kmax * 1e-3) / 1e9
+    comp_gbps = compulsory / (kmax * 1e-3) / 1e9
+    have = all(r["traffic"] for r in per_rank)
+    traffic = sum(r["traffic"] for r in per_rank) if have else None
+    achieved = traffic / (kmax * 1e-3) / 1e9 if have else None
+    roof = {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
+            "frac": achieved / peak if have else None, "traffic": traffic,
             "kernel": "k_chunk_reduce + k_chunk_fixup (one copy_u_sum launch pair)",
-            "kernel_ms": kernel_ms,
+            "kernel_ms": kmax,
             "achieved_from": ("fabric bytes per launch (rocprofv3 PMC, this run%s) / HIP-event "
                               "kernel time" % ("" if world == 1 else
-                                               ", each rank on its own GPU; the rank with the "
-                                               "highest fraction")) if traffic else
-                             "no counters this run",
+                                               ", each rank on its own GPU; summed over the "
+                                               "ranks, over the slowest rank's kernel time, "
+                                               "against %d x %g GB/s" % (world, HBM_PEAK_GBPS)))
+                             if have else "no counters this run",
             "alg_bytes_per_launch": alg_bytes, "alg_GBps": alg_gbps,
             "alg_note": "SURVEY §8d model: counts L2-served re-reads of hub rows, above peak",
             "compulsory_bytes_per_launch": compulsory, "compulsory_GBps": comp_gbps,
-            "compulsory_frac": comp_gbps / HBM_PEAK_GBPS}
+            "compulsory_frac": comp_gbps / peak}
     if world > 1:
+        fr = [r for r in per_rank if r["frac"] is not None]
         roof["per_rank"] = per_rank
         roof["frac_min"] = min(r["frac"] for r in fr) if fr else None
-        roof["alg_note"] += "; per rank: this rank's row block of the world-size graph"
+        roof["alg_note"] += ("; per rank: that rank's row block of the world-size graph, "
+                             "summed over the ranks")
     if pmc:
         roof["pmc"] = pmc if world == 1 else {k: v for k, v in pmc.items()
                                               if k in ("method", "passes", "fetch_scale")}

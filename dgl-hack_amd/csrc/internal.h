@@ -361,16 +361,19 @@ struct GatArgs {
   float* lf;
   float* ls;
   // attention dropout (DGLMIFusedGatDropout*): edge e, head h keeps its weight, scaled by
-  // 1 / (1 - p), when gat_drop_hash(seed, eid * H + h) >= drop_thresh; the walk's edge
-  // ids in `eids` (its CSR's data).  drop = 0: off.
+  // 1 / (1 - p), when gat_head_keep(gat_edge_key(seed, eid), h, drop_thresh) (16-bit
+  // threshold, round(p 2^16)); the walk's edge ids in `eids` (its CSR's data).  drop = 0: off.
   int drop;
   uint32_t drop_thresh;
   float drop_scale;
   uint64_t drop_seed;
   const int32_t* eids;
 };
-// the dropout mask's hash (two rounds of a 32-bit avalanche mix keyed by the seed's
-// halves; mirrored in numpy by dgl.kernel.gat_dropout_keep for the tests)
+// The dropout mask's hash (mirrored in numpy by dgl.kernel.gat_dropout_keep for the
+// tests): one key per edge -- two rounds of a 32-bit avalanche mix of the edge id keyed
+// by the seed's halves -- then one more round per PAIR of heads, whose low / high 16
+// bits decide heads 2j / 2j + 1 (kept when >= the 16-bit threshold).  H / 2 + 2 mixes
+// per edge instead of 2 H, and no eid * H product (it wrapped at 2^32 edge-heads).
 __host__ __device__ __forceinline__ uint32_t gat_mix32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x7feb352du;
@@ -379,8 +382,14 @@ __host__ __device__ __forceinline__ uint32_t gat_mix32(uint32_t x) {
   x ^= x >> 16;
   return x;
 }
-__host__ __device__ __forceinline__ uint32_t gat_drop_hash(uint64_t seed, uint32_t key) {
-  return gat_mix32(gat_mix32(key ^ static_cast<uint32_t>(seed)) ^ static_cast<uint32_t>(seed >> 32));
+__host__ __device__ __forceinline__ uint32_t gat_edge_key(uint64_t seed, uint32_t eid) {
+  return gat_mix32(gat_mix32(eid ^ static_cast<uint32_t>(seed)) ^ static_cast<uint32_t>(seed >> 32));
+}
+__host__ __device__ __forceinline__ uint32_t gat_pair_bits(uint32_t key, int pair) {
+  return gat_mix32(key + static_cast<uint32_t>(pair + 1) * 0x9e3779b9u);
+}
+__host__ __device__ __forceinline__ bool gat_head_keep(uint32_t key, int h, uint32_t thresh16) {
+  return ((gat_pair_bits(key, h >> 1) >> (16 * (h & 1))) & 0xffffu) >= thresh16;
 }
 bool gat_supported(int64_t H, int64_t D);
 int64_t gat_chunk_edges(int64_t nnz);

@@ -87,22 +87,23 @@ __device__ __forceinline__ float head_sum(float x, int d4) {
 }
 
 // Attention dropout, staged per position: the H keep bits of the position's edge (one
-// hash per edge and head, computed by the one lane that stages the position, instead of
-// by every lane of the head in the edge loop: 16 lanes per row at 8 x 8), or the edge
-// id itself for more than 32 heads (hashed per lane then).
+// key per edge, one hash per pair of heads, computed by the one lane that stages the
+// position instead of by every lane of the head in the edge loop: 16 lanes per row at
+// 8 x 8), or the edge's key itself for more than 32 heads (each lane hashes its head's
+// pair then).
 __device__ __forceinline__ uint32_t gat_stage_keep(const GatArgs& a, int64_t p) {
-  const uint32_t e = static_cast<uint32_t>(a.eids[p]);
-  if (a.H > 32) return e;
+  const uint32_t key = gat_edge_key(a.drop_seed, static_cast<uint32_t>(a.eids[p]));
+  if (a.H > 32) return key;
   uint32_t kb = 0;
-  for (int h = 0; h < a.H; ++h)
-    kb |= (gat_drop_hash(a.drop_seed, e * static_cast<uint32_t>(a.H) + static_cast<uint32_t>(h)) >=
-           a.drop_thresh ? 1u : 0u) << h;
-  return kb;
+  for (int j = 0; 2 * j < a.H; ++j) {
+    const uint32_t r = gat_pair_bits(key, j);
+    kb |= ((r & 0xffffu) >= a.drop_thresh ? 1u : 0u) << (2 * j);
+    kb |= ((r >> 16) >= a.drop_thresh ? 1u : 0u) << (2 * j + 1);
+  }
+  return a.H == 32 ? kb : kb & ((1u << a.H) - 1u);
 }
 __device__ __forceinline__ bool gat_kept(const GatArgs& a, uint32_t staged, int h) {
-  if (a.H > 32)
-    return gat_drop_hash(a.drop_seed, staged * static_cast<uint32_t>(a.H) + static_cast<uint32_t>(h)) >=
-           a.drop_thresh;
+  if (a.H > 32) return gat_head_keep(staged, h, a.drop_thresh);
   return (staged >> h) & 1u;
 }
 

@@ -17,6 +17,7 @@
 // order by the fixup -- deterministic, no atomics.
 #include "internal.h"
 
+#include <algorithm>
 #include <climits>
 
 namespace dglmi {
@@ -270,14 +271,21 @@ __global__ void __launch_bounds__(kBlock) k_sm_edges(SoftmaxArgs a) {
 // positions per step.  A step inside the current row needs no row ids and no cross-lane
 // work (every lane keeps its own running max / sum); only a step that crosses a row
 // boundary reads the row ids and reduces across lanes.
-template <int H>
+#ifndef DGLMI_SM_WSTEPS
+#define DGLMI_SM_WSTEPS 32  // steps per window (probe builds vary it)
+#endif
+// (An LDS-staged form of this walk -- each wave's chunk of whole rows loaded once into
+// 36 KiB of LDS by buffer_load ... lds and both sweeps read from there -- holds one
+// block of four waves per CU and measured slower: C3 view H = 8 fwd 3.67 / bwd 4.28 ms
+// against 2.17 / 3.61 here; profiles/r05_edge_softmax_variants.json)
+template <int H, int MODE>
 struct OwnedShape {
   static constexpr int V = H < 4 ? H : 4;  // values per lane
   static constexpr int LP = H / V;         // lanes per position
   static constexpr int L = 64 / LP;        // positions per step
   static constexpr int U = 16 / V;         // steps whose loads are issued together
-  static constexpr int64_t W = 32 * L;     // window (positions)
-  static constexpr int64_t T = 2 * W;      // longer rows are hub rows
+  static constexpr int64_t W = DGLMI_SM_WSTEPS * L;  // window (positions)
+  static constexpr int64_t T = 2 * W;                // longer rows are hub rows
 };
 
 // e^x as one v_exp_f32 (relative error ~|x| 2^-24; x = s - max <= 0 here)
@@ -291,7 +299,7 @@ __device__ __forceinline__ float ld_fresh(const float* p) {
 
 template <int H, int MODE>
 struct OwnedWalk {
-  using S = OwnedShape<H>;
+  using S = OwnedShape<H, MODE>;
   static constexpr int V = S::V, LP = S::LP, L = S::L, U = S::U;
   static constexpr float kId = MODE == SM_STATS ? -INFINITY : 0.0f;  // identity of m
   const SoftmaxArgs& a;
@@ -305,7 +313,6 @@ struct OwnedWalk {
     for (int v = 0; v < V; ++v) { m[v] = kId; l[v] = 0.0f; }
   }
   __device__ __forceinline__ int64_t off(int64_t p) const { return p * H + q * V; }
-  // the U-step (or 1-step) batch of positions b + u L + j, all in one row
   template <int N>
   __device__ __forceinline__ void accumulate(int64_t b, int64_t pend) {
     float x[N][V], g[MODE == SM_DOTSUM ? N : 1][V];
@@ -545,7 +552,7 @@ struct OwnedWalk {
 
 template <int H, int MODE>
 __global__ void __launch_bounds__(kBlock) k_sm_owned(SoftmaxArgs a) {
-  using S = OwnedShape<H>;
+  using S = OwnedShape<H, MODE>;
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
   const int64_t lo = w * S::W;
@@ -573,7 +580,7 @@ __global__ void __launch_bounds__(kBlock) k_sm_owned(SoftmaxArgs a) {
 // hub rows: merge the row's pieces in window order, then write this window's piece
 template <int H, int MODE>
 __global__ void __launch_bounds__(kBlock) k_sm_hub(SoftmaxArgs a) {
-  using S = OwnedShape<H>;
+  using S = OwnedShape<H, MODE>;
   constexpr int V = S::V;
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
@@ -614,14 +621,19 @@ __global__ void __launch_bounds__(kBlock) k_sm_hub(SoftmaxArgs a) {
 
 template <int H>
 void run_owned(const SoftmaxArgs& a, bool backward, hipStream_t st) {
-  const int64_t windows = (a.nnz + OwnedShape<H>::W - 1) / OwnedShape<H>::W;
-  const dim3 grid(static_cast<unsigned>((windows + kBlock / 64 - 1) / (kBlock / 64))), blk(kBlock);
+  auto grid = [&](int64_t W) {
+    const int64_t windows = (a.nnz + W - 1) / W;
+    return dim3(static_cast<unsigned>((windows + kBlock / 64 - 1) / (kBlock / 64)));
+  };
+  const dim3 blk(kBlock);
   if (!backward) {
-    hipLaunchKernelGGL((k_sm_owned<H, SM_STATS>), grid, blk, 0, st, a);
-    hipLaunchKernelGGL((k_sm_hub<H, SM_STATS>), grid, blk, 0, st, a);
+    const dim3 g = grid(OwnedShape<H, SM_STATS>::W);
+    hipLaunchKernelGGL((k_sm_owned<H, SM_STATS>), g, blk, 0, st, a);
+    hipLaunchKernelGGL((k_sm_hub<H, SM_STATS>), g, blk, 0, st, a);
   } else {
-    hipLaunchKernelGGL((k_sm_owned<H, SM_DOTSUM>), grid, blk, 0, st, a);
-    hipLaunchKernelGGL((k_sm_hub<H, SM_DOTSUM>), grid, blk, 0, st, a);
+    const dim3 g = grid(OwnedShape<H, SM_DOTSUM>::W);
+    hipLaunchKernelGGL((k_sm_owned<H, SM_DOTSUM>), g, blk, 0, st, a);
+    hipLaunchKernelGGL((k_sm_hub<H, SM_DOTSUM>), g, blk, 0, st, a);
   }
 }
 
@@ -663,13 +675,13 @@ int64_t softmax_chunk_edges(int64_t nnz, int64_t H) {
 
 // the row-owned walk's carries: two slots of 2H floats per window
 int64_t softmax_owned_carry_bytes(int64_t nnz, int64_t H) {
-  int64_t W = 0;
+  int64_t W = 0;  // the smaller window of the two passes
   switch (H) {
-    case 1: W = OwnedShape<1>::W; break;
-    case 2: W = OwnedShape<2>::W; break;
-    case 4: W = OwnedShape<4>::W; break;
-    case 8: W = OwnedShape<8>::W; break;
-    default: W = OwnedShape<16>::W; break;
+    case 1: W = std::min(OwnedShape<1, SM_STATS>::W, OwnedShape<1, SM_DOTSUM>::W); break;
+    case 2: W = std::min(OwnedShape<2, SM_STATS>::W, OwnedShape<2, SM_DOTSUM>::W); break;
+    case 4: W = std::min(OwnedShape<4, SM_STATS>::W, OwnedShape<4, SM_DOTSUM>::W); break;
+    case 8: W = std::min(OwnedShape<8, SM_STATS>::W, OwnedShape<8, SM_DOTSUM>::W); break;
+    default: W = std::min(OwnedShape<16, SM_STATS>::W, OwnedShape<16, SM_DOTSUM>::W); break;
   }
   return ((nnz + W - 1) / W) * 2 * 2 * H * 4;
 }

@@ -18,6 +18,7 @@ and its PyTorch implementation (``backend/pytorch/tensor.py:291-381,
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch as th
 
@@ -656,7 +657,25 @@ def rgcn_fused_route(graph, x, weight_shape, norm, etypes, self_loop=False):
         # the cache holds the caller's etypes, so its address stays theirs
         hit = (key, gidx, et32, etypes)
         gi.__dict__["_rgcn_fused"] = hit
-    return hit[1], hit[2], norm.reshape(-1).contiguous()
+    return hit[1], hit[2], _flat_norm(gi, norm)
+
+
+def _flat_norm(gi, norm):
+    """``norm`` as one contiguous float per edge.  A contiguous norm is viewed (same
+    storage: the prepared state's pointer / version check sees the caller's tensor); a
+    non-contiguous one is copied ONCE per (tensor, version) and the copy reused, so
+    RgcnState.sync_norm does not re-gather the state's norm copies on every call.  The
+    cache holds the source only by a weak reference (dropped with it)."""
+    flat = norm.reshape(-1)
+    if flat.is_contiguous():
+        return flat
+    key = (norm.data_ptr(), norm._version, tuple(norm.shape), tuple(norm.stride()))
+    hit = gi.__dict__.get("_rgcn_norm_flat")
+    if hit is not None and hit[0] == key and hit[1]() is norm:
+        return hit[2]
+    copy = flat.contiguous()
+    gi.__dict__["_rgcn_norm_flat"] = (key, weakref.ref(norm), copy)
+    return copy
 
 
 def rgcn_fused_layer1(route, x, weight, loop_weight=None, bias=None):

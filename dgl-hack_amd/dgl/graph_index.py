@@ -212,14 +212,29 @@ class ImmutableGraphIndex:
         ic, oc = self.in_csr, self.out_csr
         view = self.position_view(direction)
         walk = ic if direction == "in" else oc
-        # the cache holds `w` itself: while it is alive no other tensor can take its
-        # address, so (address, version counter, layout) identifies its contents
+        # (address, version counter, layout) identifies `w`'s contents while `w` is
+        # alive; the cache holds `w` only by a weak reference whose callback drops the
+        # entry (and the permuted copy) the moment `w` is freed, so a dropped operand
+        # costs no memory and its address cannot be mistaken for a later tensor's
         key = self._operand_key(w)
         cached = self._pos_operands.get(direction)
-        if cached is None or cached[0] != key:
-            cached = (key, w, w[walk.data.long()].contiguous())
+        if cached is None or cached[0] != key or cached[1]() is not w:
+            ops = self._pos_operands
+
+            def drop(ref, direction=direction):
+                ent = ops.get(direction)
+                if ent is not None and ent[1] is ref:
+                    del ops[direction]
+            cached = (key, weakref.ref(w, drop), w[walk.data.long()].contiguous())
             self._pos_operands[direction] = cached
         return view, cached[2]
+
+    def clear_operand_cache(self):
+        """Drop the cached position-ordered operand copies (position_operand) and the
+        last-seen operand record (reused_operand)."""
+        if getattr(self, "_pos_operands", None) is not None:
+            self._pos_operands.clear()
+        self._operand_seen = None
 
     @staticmethod
     def _operand_key(w):
@@ -234,7 +249,7 @@ class ImmutableGraphIndex:
         if getattr(self, "_pos_views", None) is None:
             self._pos_views, self._pos_operands = {}, {}
         cached = self._pos_operands.get("in")
-        if cached is not None and cached[0] == key:
+        if cached is not None and cached[0] == key and cached[1]() is w:
             return True
         # the same tensor OBJECT (a weak reference: the caching allocator hands a
         # fresh tensor of the same size the same address, so the key alone would

@@ -321,9 +321,10 @@ int DGLMIFusedGatBackwardEx(const DGLMIGraph* graph, const DGLMIArray* feat_src,
 
 /* Fused GAT with attention dropout (GATConv's attn_drop in training, gatconv.py:154:
  * dropout on the softmax weights, per edge and head).  Edge e, head h keeps its weight,
- * scaled by 1 / (1 - attn_drop), when a counter hash of (seed, e * H + h) clears the
- * threshold attn_drop * 2^32 -- a mask no buffer holds: the backward recomputes it from
- * the same seed and the walks' edge ids.  The softmax denominator (sum_out) is the plain
+ * scaled by 1 / (1 - attn_drop), when a counter hash of (seed, e) -- one key per edge,
+ * one more mix per pair of heads, 16 bits per head -- clears the threshold
+ * round(attn_drop * 2^16) -- a mask no buffer holds: the backward recomputes it from the
+ * same seed and the walks' edge ids.  The softmax denominator (sum_out) is the plain
  * one; out and slope_feat carry the kept, rescaled weights.  The backward needs the
  * forward's slope aggregates.  attn_drop = 0 equals DGLMIFusedGatForwardEx /
  * BackwardEx bit for bit.  Extension: the reference has no fused dropout (its

@@ -242,3 +242,36 @@ def test_relgraphconv_fused_first_layer_param_grads():
     grads2 = th.autograd.grad(conv(g, x, etypes, norm), list(conv.parameters()), go)
     for a, b in zip(grads, grads2):
         assert (a - b).abs().max().item() <= 1e-3 + 1e-4 * b.abs().max().item()
+
+
+def test_relgraphconv_fused_noncontiguous_norm_refreshes_once(monkeypatch):
+    """A non-contiguous norm (a column of a wider tensor) is flattened once per (tensor,
+    version) and the copy reused (dgl.backend._flat_norm), so the prepared state's norm
+    copies are re-gathered (DGLMIRgcnRefreshNorm) once, not on every call; an in-place
+    update still refreshes them."""
+    from dgl import _ffi
+    g, src, dst, et, n = typed_graph(seed=9)
+    R = 4
+    th.manual_seed(4)
+    conv = RelGraphConv(64, 64, R, "basis").to(DEV)
+    x = th.randn(n, 64, device=DEV)
+    etypes = th.from_numpy(et).to(DEV)
+    wide = th.rand(len(src), 3, device=DEV)
+    norm = wide[:, 1:2]  # (E, 1), stride 3: not contiguous
+    assert not norm.is_contiguous()
+    lib = _ffi.lib()
+    orig = lib.DGLMIRgcnRefreshNorm
+    calls = []
+    monkeypatch.setattr(lib, "DGLMIRgcnRefreshNorm", lambda *a: calls.append(1) or orig(*a))
+    with th.no_grad():
+        a = conv(g, x, etypes, norm)
+        first = len(calls)
+        for _ in range(3):
+            b = conv(g, x, etypes, norm)
+        assert len(calls) == first  # no re-gather for the same tensor and version
+        assert th.equal(a, b)
+        wide.mul_(2.0)  # the same view, a new version
+        c = conv(g, x, etypes, norm)
+        assert len(calls) == first + 1
+    ref = conv(g, x, etypes, norm.contiguous())
+    assert th.allclose(c, ref, rtol=1e-5, atol=1e-5)

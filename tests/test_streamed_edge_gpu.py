@@ -198,3 +198,26 @@ def test_mapped_u_mul_e_on_identity_edge_ids(route, monkeypatch):
     out = th.zeros(n, D, device=DEV)
     K.binary_op_reduce("sum", "mul", gidx, "src", "edge", x, wv.contiguous(), out, lhs_map=lhs_map)
     assert th.equal(out, ref)
+
+
+def test_position_operand_cache_drops_with_the_tensor():
+    """The position-ordered copy of a constant edge operand is cached by weak reference:
+    freeing the operand frees the copy, and clear_operand_cache drops it."""
+    import gc
+    src, dst, n = powerlaw(30_000, 200_000, seed=3)
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    gidx = g._graph.get_immutable_gidx(DEV)
+    w = th.rand(len(src), 1, device=DEV)
+    view, wp = gidx.position_operand(w, "in")
+    assert gidx._pos_operands.get("in") is not None
+    view2, wp2 = gidx.position_operand(w, "in")
+    assert wp2 is wp  # cached
+    del w, wp, wp2
+    gc.collect()
+    assert gidx._pos_operands.get("in") is None
+    w = th.rand(len(src), 1, device=DEV)
+    gidx.position_operand(w, "out")
+    gidx.clear_operand_cache()
+    assert not gidx._pos_operands
