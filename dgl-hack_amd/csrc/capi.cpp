@@ -1003,6 +1003,7 @@ void gat_set_dropout(GatArgs& a, float p, uint64_t seed) {
   a.drop = p > 0.0f ? 1 : 0;
   if (!a.drop) return;
   DGLMI_CHECK(a.o32, "attention dropout needs gathered tables below 2^31 elements");
+  DGLMI_CHECK(a.H <= 32, "attention dropout in the fused kernels takes at most 32 heads");
   // 16-bit uniforms per edge and head (internal.h gat_head_keep): p resolved to 2^-16
   a.drop_thresh = static_cast<uint32_t>(std::min(65535.0, std::floor(static_cast<double>(p) * 65536.0 + 0.5)));
   a.drop_scale = 1.0f / (1.0f - p);

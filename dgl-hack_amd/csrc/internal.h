@@ -370,10 +370,12 @@ struct GatArgs {
   const int32_t* eids;
 };
 // The dropout mask's hash (mirrored in numpy by dgl.kernel.gat_dropout_keep for the
-// tests): one key per edge -- two rounds of a 32-bit avalanche mix of the edge id keyed
-// by the seed's halves -- then one more round per PAIR of heads, whose low / high 16
-// bits decide heads 2j / 2j + 1 (kept when >= the 16-bit threshold).  H / 2 + 2 mixes
-// per edge instead of 2 H, and no eid * H product (it wrapped at 2^32 edge-heads).
+// tests): one key per edge -- a 32-bit avalanche mix of the edge id keyed by the seed's
+// low half, xor the high half -- then, per PAIR of heads, a one-multiply finish of
+// key + (pair + 1) * golden ratio whose low / high 16 bits decide heads 2j / 2j + 1
+// (kept when >= the 16-bit threshold).  Two multiplies per edge plus one per pair of
+// heads (the staging lane's VALU is what the dropout walks pay for), and no eid * H
+// product (it wrapped at 2^32 edge-heads).
 __host__ __device__ __forceinline__ uint32_t gat_mix32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x7feb352du;
@@ -383,10 +385,14 @@ __host__ __device__ __forceinline__ uint32_t gat_mix32(uint32_t x) {
   return x;
 }
 __host__ __device__ __forceinline__ uint32_t gat_edge_key(uint64_t seed, uint32_t eid) {
-  return gat_mix32(gat_mix32(eid ^ static_cast<uint32_t>(seed)) ^ static_cast<uint32_t>(seed >> 32));
+  return gat_mix32(eid ^ static_cast<uint32_t>(seed)) ^ static_cast<uint32_t>(seed >> 32);
 }
 __host__ __device__ __forceinline__ uint32_t gat_pair_bits(uint32_t key, int pair) {
-  return gat_mix32(key + static_cast<uint32_t>(pair + 1) * 0x9e3779b9u);
+  uint32_t x = key + static_cast<uint32_t>(pair + 1) * 0x9e3779b9u;
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  return x;
 }
 __host__ __device__ __forceinline__ bool gat_head_keep(uint32_t key, int h, uint32_t thresh16) {
   return ((gat_pair_bits(key, h >> 1) >> (16 * (h & 1))) & 0xffffu) >= thresh16;

@@ -86,26 +86,23 @@ __device__ __forceinline__ float head_sum(float x, int d4) {
   return x;
 }
 
-// Attention dropout, staged per position: the H keep bits of the position's edge (one
-// key per edge, one hash per pair of heads, computed by the one lane that stages the
-// position instead of by every lane of the head in the edge loop: 16 lanes per row at
-// 8 x 8), or the edge's key itself for more than 32 heads (each lane hashes its head's
-// pair then).
-__device__ __forceinline__ uint32_t gat_stage_keep(const GatArgs& a, int64_t p) {
-  const uint32_t key = gat_edge_key(a.drop_seed, static_cast<uint32_t>(a.eids[p]));
-  if (a.H > 32) return key;
+// Attention dropout, staged per position: the H <= 32 keep bits of the position's edge
+// (one key per edge, one hash per pair of heads), computed by the one lane that stages
+// the position instead of by every lane of the head in the edge loop (16 lanes per row
+// at 8 x 8).  The edge loop only tests a bit: a hash there (round 4 kept one for
+// H > 32, which the compiler evaluated for every edge and selected away) cost ~24 VALU
+// instructions per edge and lane.  The C entry takes H <= 32 (gat_set_dropout).
+__device__ __forceinline__ uint32_t gat_stage_keep(const GatArgs& a, int32_t eid) {
+  const uint32_t key = gat_edge_key(a.drop_seed, static_cast<uint32_t>(eid));
   uint32_t kb = 0;
   for (int j = 0; 2 * j < a.H; ++j) {
     const uint32_t r = gat_pair_bits(key, j);
     kb |= ((r & 0xffffu) >= a.drop_thresh ? 1u : 0u) << (2 * j);
     kb |= ((r >> 16) >= a.drop_thresh ? 1u : 0u) << (2 * j + 1);
   }
-  return a.H == 32 ? kb : kb & ((1u << a.H) - 1u);
+  return kb;  // bits past H unused
 }
-__device__ __forceinline__ bool gat_kept(const GatArgs& a, uint32_t staged, int h) {
-  if (a.H > 32) return gat_head_keep(staged, h, a.drop_thresh);
-  return (staged >> h) & 1u;
-}
+__device__ __forceinline__ bool gat_kept(uint32_t staged, int h) { return (staged >> h) & 1u; }
 
 // ---------------------------------------------------------------------------
 // forward
@@ -203,17 +200,35 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
       }
     }
   };
-  for (int64_t base = p0; base < p1; base += B) {
-    for (int q = lane; q < B; q += L) {
-      const int64_t p = base + q;
+  // the batch's row / column (and, with dropout, edge) ids are loaded one batch ahead,
+  // into registers, while this batch's gathers are in flight (round 5): the staging
+  // loads, and the edge-id load the keep-bit hash waits for, are off the critical path
+  constexpr int SQ = B / L;  // positions each lane stages per batch
+  int32_t nr[SQ], nc[SQ], ne[drop ? SQ : 1];
+  auto fetch = [&](int64_t nb) {
+#pragma unroll
+    for (int i = 0; i < SQ; ++i) {
+      const int64_t p = nb + lane + i * L;
       const bool ok = p < p1;
-      s_row[g][q] = ok ? a.rows[p] : INT_MAX;
-      s_col[g][q] = ok ? a.indices[p] : 0;
-      if constexpr (drop) s_keep[drop ? g : 0][drop ? q : 0] = ok ? gat_stage_keep(a, p) : 0u;
+      nr[i] = ok ? a.rows[p] : INT_MAX;
+      nc[i] = ok ? a.indices[p] : 0;
+      if constexpr (drop) ne[drop ? i : 0] = ok ? a.eids[p] : 0;
+    }
+  };
+  fetch(p0);
+  for (int64_t base = p0; base < p1; base += B) {
+#pragma unroll
+    for (int i = 0; i < SQ; ++i) {
+      const int q = lane + i * L;
+      s_row[g][q] = nr[i];
+      s_col[g][q] = nc[i];
+      if constexpr (drop)
+        s_keep[drop ? g : 0][drop ? q : 0] = nr[i] != INT_MAX ? gat_stage_keep(a, ne[drop ? i : 0]) : 0u;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (base + B < p1) fetch(base + B);
 #pragma unroll
     for (int ub = 0; ub < B; ub += U) {
       float4 val[U][NV];
@@ -266,7 +281,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
           // denominator and ls the plain one
           float pk = pe;
           if constexpr (drop)
-            pk = gat_kept(a, s_keep[drop ? g : 0][drop ? ub + u : 0], hd[v]) ? pe * a.drop_scale : 0.0f;
+            pk = gat_kept(s_keep[drop ? g : 0][drop ? ub + u : 0], hd[v]) ? pe * a.drop_scale : 0.0f;
           const float4 x = val[u][v];
           acc[v] = make_float4(acc[v].x + pk * x.x, acc[v].y + pk * x.y, acc[v].z + pk * x.z,
                                acc[v].w + pk * x.w);
@@ -508,8 +523,8 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_dst(GatArgs a) {
 // ---------------------------------------------------------------------------
 // backward, source side (out-CSR): grad_ft, grad_el
 // ---------------------------------------------------------------------------
-template <int L, int NV, bool O32, bool DROP = false>
-__global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
+template <int L, int NV, bool O32, bool DROP>
+__device__ __forceinline__ void gat_bwd_src_body(const GatArgs& a) {
   static_assert(L >= 1 && L <= 64, "a lane group must fit in one wavefront");
   constexpr int G = kBlock / L;
   constexpr int B = L > 16 ? L : 16;
@@ -582,17 +597,35 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
   int64_t cur = a.rows[p0];
   bool cont = p0 > 0 && a.rows[p0 - 1] == cur;
   load_row(cur);
-  for (int64_t base = p0; base < p1; base += B) {
-    for (int q = lane; q < B; q += L) {
-      const int64_t p = base + q;
+  // the batch's row / column (and, with dropout, edge) ids are loaded one batch ahead,
+  // into registers, while this batch's gathers are in flight (round 5): the staging
+  // loads, and the edge-id load the keep-bit hash waits for, are off the critical path
+  constexpr int SQ = B / L;  // positions each lane stages per batch
+  int32_t nr[SQ], nc[SQ], ne[drop ? SQ : 1];
+  auto fetch = [&](int64_t nb) {
+#pragma unroll
+    for (int i = 0; i < SQ; ++i) {
+      const int64_t p = nb + lane + i * L;
       const bool ok = p < p1;
-      s_row[g][q] = ok ? a.rows[p] : INT_MAX;
-      s_col[g][q] = ok ? a.indices[p] : 0;
-      if constexpr (drop) s_keep[drop ? g : 0][drop ? q : 0] = ok ? gat_stage_keep(a, p) : 0u;
+      nr[i] = ok ? a.rows[p] : INT_MAX;
+      nc[i] = ok ? a.indices[p] : 0;
+      if constexpr (drop) ne[drop ? i : 0] = ok ? a.eids[p] : 0;
+    }
+  };
+  fetch(p0);
+  for (int64_t base = p0; base < p1; base += B) {
+#pragma unroll
+    for (int i = 0; i < SQ; ++i) {
+      const int q = lane + i * L;
+      s_row[g][q] = nr[i];
+      s_col[g][q] = nc[i];
+      if constexpr (drop)
+        s_keep[drop ? g : 0][drop ? q : 0] = nr[i] != INT_MAX ? gat_stage_keep(a, ne[drop ? i : 0]) : 0u;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (base + B < p1) fetch(base + B);
 #pragma unroll
     for (int ub = 0; ub < B; ub += U) {
       float4 gov[U][NV], st[U][NV];
@@ -626,7 +659,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
           // softmax (grad of the logit: att (d <grad_out, ft> - delta) lrelu')
           float dk = 1.0f;
           if constexpr (drop)
-            dk = gat_kept(a, s_keep[drop ? g : 0][drop ? ub + u : 0], hd[v]) ? a.drop_scale : 0.0f;
+            dk = gat_kept(s_keep[drop ? g : 0][drop ? ub + u : 0], hd[v]) ? a.drop_scale : 0.0f;
           const float te = att * (dk * ge - sv.w) * dleaky(pre, a.slope);
           acce[v] += te;
           // the edge's grad_er term, in this walk's position order (edge-position
@@ -643,6 +676,14 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
   flush(cur, cont);
   fill_empty_rows(a.indptr, a.num_rows, chunk, (a.nnz + K - 1) / K, L, lane, zero_row);
 }
+
+template <int L, int NV, bool O32, bool DROP = false>
+__global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
+  gat_bwd_src_body<L, NV, O32, DROP>(a);
+}
+// (The dropout instance takes 129 VGPRs and three waves per SIMD; held to four by
+// amdgpu_waves_per_eu(4) it spilled two registers and ran no faster: 632 vs 627 us per
+// C3 block launch, profiles/r05_c3_and_dropout.json.)
 
 // carries of the backward walks: plain sums (W floats per chunk record, the first
 // `wf` of them are per-float4 slots, the rest per head)

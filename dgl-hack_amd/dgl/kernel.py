@@ -319,8 +319,8 @@ def gat_dropout_keep(seed, eids, num_heads, p):
     """The fused GAT's attention-dropout mask (DGLMIFusedGatDropout*; internal.h
     gat_edge_key / gat_pair_bits / gat_head_keep) on the host, for tests: a
     (len(eids), num_heads) bool array, True where edge eids[i], head h keeps its weight.
-    One key per edge, one hash per pair of heads whose low / high 16 bits decide the two
-    heads against round(p 2^16).  numpy uint32 arithmetic wraps like the kernel's."""
+    One key per edge (a mix of the edge id and the seed), one multiply-xorshift per pair
+    of heads whose low / high 16 bits decide the two heads against round(p 2^16).  numpy uint32 arithmetic wraps like the kernel's."""
     seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     lo, hi = np.uint32(seed & 0xFFFFFFFF), np.uint32(seed >> 32)
 
@@ -330,12 +330,16 @@ def gat_dropout_keep(seed, eids, num_heads, p):
         x = x ^ (x >> np.uint32(15))
         x = x * np.uint32(0x846CA68B)
         return x ^ (x >> np.uint32(16))
+    def finish(x):  # gat_pair_bits: one multiply
+        x = x ^ (x >> np.uint32(16))
+        x = x * np.uint32(0x7FEB352D)
+        return x ^ (x >> np.uint32(15))
     e = np.asarray(eids, dtype=np.int64).astype(np.uint32)
     pairs = (num_heads + 1) // 2
     with np.errstate(over="ignore"):
-        key = mix(mix(e ^ lo) ^ hi)
+        key = mix(e ^ lo) ^ hi
         off = (np.arange(pairs, dtype=np.uint32) + np.uint32(1)) * np.uint32(0x9E3779B9)
-        r = mix(key[:, None] + off[None, :])                      # (E, pairs)
+        r = finish(key[:, None] + off[None, :])                   # (E, pairs)
     u16 = np.stack([r & np.uint32(0xFFFF), r >> np.uint32(16)], 2).reshape(len(e), 2 * pairs)
     thresh = min(65535, int(np.floor(float(np.float32(p)) * 65536.0 + 0.5)))  # the C entry's
     return u16[:, :num_heads] >= np.uint32(thresh)

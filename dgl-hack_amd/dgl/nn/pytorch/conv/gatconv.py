@@ -77,8 +77,9 @@ class GATConv(nn.Module):
         """Whether this call takes the fused kernels: the head size suits them, the
         graph has 32-bit device indices (a 2^31+-edge graph takes the composition,
         whose kernels have 64-bit offsets) and, with attention dropout in training,
-        the gathered tables stay below 2^31 elements (the dropout walks are built with
-        32-bit offsets only; ``capi.cpp`` gat_set_dropout).  ``graph``: a DGLGraph or
+        the gathered tables stay below 2^31 elements and there are at most 32 heads (the
+        dropout walks are built with 32-bit offsets and stage 32 keep bits per edge;
+        ``capi.cpp`` gat_set_dropout).  ``graph``: a DGLGraph or
         an ImmutableGraphIndex; ``n_rows``: the larger of its source / destination
         row counts."""
         if not self._fused_ok():
@@ -89,7 +90,9 @@ class GATConv(nn.Module):
         elif getattr(graph._graph, "device_bits", lambda: 32)() != 32:
             return False
         if self.training and self.attn_drop.p > 0:
-            return n_rows * self._num_heads * self._fused_dim() < (1 << 31)
+            # the dropout walks stage <= 32 keep bits per edge (capi.cpp gat_set_dropout)
+            return (self._num_heads <= 32
+                    and n_rows * self._num_heads * self._fused_dim() < (1 << 31))
         return True
 
     def _position_space(self, graph, feat_src):

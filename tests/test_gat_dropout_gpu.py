@@ -31,9 +31,9 @@ def dense_gat_dropout(src, dst, n, ft, el, er, slope, keep, p):
 
 
 @pytest.mark.parametrize("nb,p,H,D", [(1, 0.5, 8, 8), (1, 0.1, 8, 8), (4, 0.6, 8, 8),
-                                      (8, 0.3, 8, 8), (1, 0.5, 64, 4), (2, 0.4, 3, 16)])
+                                      (8, 0.3, 8, 8), (1, 0.5, 32, 4), (2, 0.4, 3, 16)])
 def test_fused_gat_dropout_vs_dense(nb, p, H, D, monkeypatch):
-    """(more than 32 heads: the mask is hashed per lane instead of staged as bits)"""
+    """(32 heads: every bit of the staged keep mask in use)"""
     monkeypatch.setenv("DGLMI_GAT_BLOCKS", str(nb))
     src, dst, n = powerlaw(20000, 300000, seed=13)
     g = dgl.DGLGraph()
@@ -94,3 +94,21 @@ def test_gatconv_training_dropout_runs_fused(monkeypatch):
     with th.no_grad():
         e1, e2 = conv(g, x), conv(g, x)
     assert calls == [0.0, 0.0] and th.equal(e1, e2)
+
+
+def test_dropout_over_32_heads_takes_the_composition():
+    """The dropout walks stage 32 keep bits per edge: more heads raise in the C entry,
+    and GATConv routes such a layer to the composition (nn.Dropout on edge_softmax)."""
+    from dgl._ffi import DGLError
+    src, dst, n = powerlaw(3000, 30000, seed=4)
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    ft = th.randn(n, 64, 4, device=DEV)
+    el, er = th.randn(n, 64, 1, device=DEV), th.randn(n, 64, 1, device=DEV)
+    with pytest.raises(DGLError, match="32 heads"):
+        B.fused_gat(g, ft, el, er, 0.2, attn_drop=0.5, seed=1)
+    conv = GATConv(16, 4, 64, attn_drop=0.5).to(DEV).train()
+    assert not conv._fused_route(g, n)
+    y = conv(g, th.randn(n, 16, device=DEV))
+    assert y.shape == (n, 64, 4) and th.isfinite(y).all()
