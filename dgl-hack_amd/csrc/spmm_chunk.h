@@ -245,21 +245,40 @@ __global__ void __launch_bounds__(kBlock) k_chunk_reduce(FastArgs a, IdxPtr indp
 #pragma unroll
   for (int v = 0; v < NV; ++v) acc[v] = I;
 
-  for (int64_t base = p0; base < p1; base += B) {
-    // stage B positions through LDS (coalesced, one row/col/eid per lane slot)
-    for (int q = lane; q < B; q += L) {
-      const int64_t p = base + q;
+  // B positions per batch staged through LDS (coalesced, one row/col/eid per lane slot);
+  // each batch's ids are loaded into registers one batch ahead, while the previous
+  // batch's gathers are in flight, and written to LDS at the batch's start
+  constexpr int SQ = B / L;  // positions each lane stages per batch
+  constexpr bool kEid = needs_eid<KIND>();
+  int32_t nr[SQ], nc[SQ];
+  [[maybe_unused]] int64_t ne[kEid ? SQ : 1];
+  [[maybe_unused]] float nw[kScalarW ? SQ : 1];
+  auto fetch = [&](int64_t nb) {
+#pragma unroll
+    for (int i = 0; i < SQ; ++i) {
+      const int64_t p = nb + lane + i * L;
       const bool ok = p < p1;
-      s_row[g][q] = ok ? ld_stream<VAR>(a.rows + p) : INT_MAX;
-      s_col[g][q] = ok ? ld_stream<VAR>(a.indices + p) : 0;
+      nr[i] = ok ? ld_stream<VAR>(a.rows + p) : INT_MAX;
+      nc[i] = ok ? ld_stream<VAR>(a.indices + p) : 0;
       // identity edge ids (a position view's walk, a.eids null): no `data` stream
-      if constexpr (needs_eid<KIND>())
-        s_eid[needs_eid<KIND>() ? g : 0][q] = ok ? (a.eids ? ld_stream<VAR>(a.eids, p) : p) : 0;
-      if constexpr (kScalarW) s_w[kScalarW ? g : 0][kScalarW ? q : 0] = ok ? ld_stream_f<VAR>(a.w + p) : 0.0f;
+      if constexpr (kEid) ne[kEid ? i : 0] = ok ? (a.eids ? ld_stream<VAR>(a.eids, p) : p) : 0;
+      if constexpr (kScalarW) nw[kScalarW ? i : 0] = ok ? ld_stream_f<VAR>(a.w + p) : 0.0f;
+    }
+  };
+  fetch(p0);
+  for (int64_t base = p0; base < p1; base += B) {
+#pragma unroll
+    for (int i = 0; i < SQ; ++i) {
+      const int q = lane + i * L;
+      s_row[g][q] = nr[i];
+      s_col[g][q] = nc[i];
+      if constexpr (kEid) s_eid[kEid ? g : 0][q] = ne[kEid ? i : 0];
+      if constexpr (kScalarW) s_w[kScalarW ? g : 0][kScalarW ? q : 0] = nw[kScalarW ? i : 0];
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (base + B < p1) fetch(base + B);
     // the mul kinds load both operands in the gather loop and multiply in the
     // accumulation loop: a product inside the bounds-checked gather made the compiler
     // wait for each gather before issuing the next (s_waitcnt vmcnt(0) per edge)
