@@ -1277,6 +1277,44 @@ def measure_configs(device, steps=5, warmup=2, budgets=(("c2", 120), ("c3", 300)
     return out
 
 
+def job_roofline(per_rank, world):
+    """The headline line's roofline is the JOB's: the bytes of every rank's launch over
+    the slowest rank's kernel time, against N x the HBM peak (N = 1: the launch's own).
+    ``per_rank``: one record per rank with kernel_ms, alg_bytes, compulsory_bytes,
+    traffic (fabric bytes from its PMC passes, or None) and frac.  Returns (roofline
+    dict, achieved GB/s or None); per_rank and frac_min ride along at N > 1."""
+    kmax = max(r["kernel_ms"] for r in per_rank)
+    peak = HBM_PEAK_GBPS * world
+    alg_bytes = sum(r["alg_bytes"] for r in per_rank)
+    compulsory = sum(r["compulsory_bytes"] for r in per_rank)
+    alg_gbps = alg_bytes / (kmax * 1e-3) / 1e9
+    comp_gbps = compulsory / (kmax * 1e-3) / 1e9
+    have = all(r["traffic"] for r in per_rank)
+    traffic = sum(r["traffic"] for r in per_rank) if have else None
+    achieved = traffic / (kmax * 1e-3) / 1e9 if have else None
+    roof = {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
+            "frac": achieved / peak if have else None, "traffic": traffic,
+            "kernel": "k_chunk_reduce + k_chunk_fixup (one copy_u_sum launch pair)",
+            "kernel_ms": kmax,
+            "achieved_from": ("fabric bytes per launch (rocprofv3 PMC, this run%s) / HIP-event "
+                              "kernel time" % ("" if world == 1 else
+                                               ", each rank on its own GPU; summed over the "
+                                               "ranks, over the slowest rank's kernel time, "
+                                               "against %d x %g GB/s" % (world, HBM_PEAK_GBPS)))
+                             if have else "no counters this run",
+            "alg_bytes_per_launch": alg_bytes, "alg_GBps": alg_gbps,
+            "alg_note": "SURVEY §8d model: counts L2-served re-reads of hub rows, above peak",
+            "compulsory_bytes_per_launch": compulsory, "compulsory_GBps": comp_gbps,
+            "compulsory_frac": comp_gbps / peak}
+    if world > 1:
+        fr = [r for r in per_rank if r["frac"] is not None]
+        roof["per_rank"] = per_rank
+        roof["frac_min"] = min(r["frac"] for r in fr) if fr else None
+        roof["alg_note"] += ("; per rank: that rank's row block of the world-size graph, "
+                             "summed over the ranks")
+    return roof, achieved
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1503,38 +1541,7 @@ def main():
     if upd is not None:
         upd_res = measure_update_all(upd, x, out, args)
         del upd
-    # The line's roofline is the JOB's: the bytes of every rank's launch over the
-    # slowest rank's kernel time, against N x the HBM peak (N = 1: the launch's own).
-    # per_rank keeps each rank's own fraction beside it, frac_min the lowest.
-    kmax = max(r["kernel_ms"] for r in per_rank)
-    peak = HBM_PEAK_GBPS * world
-    alg_bytes = sum(r["alg_bytes"] for r in per_rank)
-    compulsory = sum(r["compulsory_bytes"] for r in per_rank)
-    alg_gbps = alg_bytes / (kmax * 1e-3) / 1e9
-    comp_gbps = compulsory / (kmax * 1e-3) / 1e9
-    have = all(r["traffic"] for r in per_rank)
-    traffic = sum(r["traffic"] for r in per_rank) if have else None
-    achieved = traffic / (kmax * 1e-3) / 1e9 if have else None
-    roof = {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
-            "frac": achieved / peak if have else None, "traffic": traffic,
-            "kernel": "k_chunk_reduce + k_chunk_fixup (one copy_u_sum launch pair)",
-            "kernel_ms": kmax,
-            "achieved_from": ("fabric bytes per launch (rocprofv3 PMC, this run%s) / HIP-event "
-                              "kernel time" % ("" if world == 1 else
-                                               ", each rank on its own GPU; summed over the "
-                                               "ranks, over the slowest rank's kernel time, "
-                                               "against %d x %g GB/s" % (world, HBM_PEAK_GBPS)))
-                             if have else "no counters this run",
-            "alg_bytes_per_launch": alg_bytes, "alg_GBps": alg_gbps,
-            "alg_note": "SURVEY §8d model: counts L2-served re-reads of hub rows, above peak",
-            "compulsory_bytes_per_launch": compulsory, "compulsory_GBps": comp_gbps,
-            "compulsory_frac": comp_gbps / peak}
-    if world > 1:
-        fr = [r for r in per_rank if r["frac"] is not None]
-        roof["per_rank"] = per_rank
-        roof["frac_min"] = min(r["frac"] for r in fr) if fr else None
-        roof["alg_note"] += ("; per rank: that rank's row block of the world-size graph, "
-                             "summed over the ranks")
+    roof, achieved = job_roofline(per_rank, world)
     if pmc:
         roof["pmc"] = pmc if world == 1 else {k: v for k, v in pmc.items()
                                               if k in ("method", "passes", "fetch_scale")}
