@@ -153,3 +153,29 @@ def test_dst_sorted_graph_takes_owned_route(monkeypatch):
         res[owned] = (a.detach(), x.grad)
     assert th.allclose(res["1"][0], res["0"][0], rtol=1e-5, atol=1e-7)
     assert th.allclose(res["1"][1], res["0"][1], rtol=1e-4, atol=1e-6)
+
+
+def test_owned_softmax_64bit_offsets_bit_identical(monkeypatch):
+    """The row-owned walk on a graph in the 64-bit layout (int64 offsets: IdxPtr wide)
+    gives the 32-bit layout's bits, hub rows included."""
+    monkeypatch.setenv("DGLMI_SOFTMAX_OWNED", "1")
+    deg = _degrees(8, 5)
+    n = len(deg)
+    rs = np.random.RandomState(6)
+    dst = np.repeat(np.arange(n), deg)
+    src = rs.randint(0, n, len(dst))
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    g64 = dgl.DGLGraph(g._graph.asbits(64))
+    s = th.randn(len(dst), 8, device=DEV)
+    ga = th.randn(len(dst), 8, device=DEV)
+    res = []
+    for gg in (g, g64):
+        view = gg._graph.get_immutable_gidx(DEV).position_view("in")
+        out, gs = th.empty_like(s), th.empty_like(s)
+        K.edge_softmax_forward(view, s, out)
+        K.edge_softmax_backward(view, out, ga, gs)
+        res.append((out, gs))
+    assert g64._graph.get_immutable_gidx(DEV).num_bits == 64
+    assert th.equal(res[0][0], res[1][0]) and th.equal(res[0][1], res[1][1])
