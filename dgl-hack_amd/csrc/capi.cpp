@@ -1907,30 +1907,6 @@ int rgcn_layer1_backward_impl(const DGLMIGraph* graph,
       launch_gemm(hidden->data, 1, K, grad_out->data, X, 1, grad_loop->data, K, X, N, lsplits,
                   static_cast<float*>(parts.ptr), s);
   };
-  const char* fold_env = std::getenv("DGLMI_RGCN_FOLD");
-  if (fused && fold_env != nullptr && fold_env[0] == '1' && K == 64 && X == 64 &&
-      aligned16(hidden->data)) {
-    // the weight gradient folded into the walk: no gy, no hidden^T . gy GEMM
-    const int32_t* eids = nullptr;
-    const float* w = nullptr;
-    rgcn_fused_walk(fs, fs->out_typed[0], fs->out_norm[0], norm->data, &eids, &w);
-    const int64_t mats = R + (loop != nullptr);
-    Scratch fparts(&z, rgcn_fold_parts_bytes(mats), s), dw(&z, mats * K * X * 4, s);
-    float* d = static_cast<float*>(dw.ptr);
-    if (launch_rgcn_bwd_fold(fs->out_typed[0].indptr, fs->out_typed[0].indices, fs->out_typed[0].rows,
-                             eids, w, grad_out->data, weight->data, K * X, 1, X,
-                             grad_hidden ? grad_hidden->data : nullptr, hidden->data,
-                             static_cast<float*>(fparts.ptr), d, N, R, loop ? loop->data : nullptr,
-                             graph->in_csr.num_rows, s)) {
-      check_hip(hipMemcpyAsync(grad_weight->data, d, R * K * X * 4, hipMemcpyDeviceToDevice, s),
-                "copy grad_weight");
-      if (grad_loop)
-        check_hip(hipMemcpyAsync(grad_loop->data, d + R * K * X, K * X * 4, hipMemcpyDeviceToDevice, s),
-                  "copy grad_loop_weight");
-      check_hip(hipGetLastError(), "rgcn folded layer1 backward launch");
-      return 0;
-    }
-  }
   if (fused) {
     // fused: gy rows and grad_hidden = sum_t G_t . W_t^T in one walk of the
     // relation-major out-CSR; the weight gradient from gy below

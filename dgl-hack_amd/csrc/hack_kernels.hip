@@ -782,231 +782,6 @@ __global__ void __launch_bounds__(kR16Threads) k_rgcn_fused16(
   }
 }
 
-// ---------------------------------------------------------------------------
-// Layer-1 backward with the weight gradient folded into the walk (round 5,
-// DGLMI_RGCN_FOLD=1; the verdict's item 3).  k_rgcn_fused16<true> stores every tile's
-// G_t = sum_{u->v, type t} norm_e grad_out[v] (and the self-loop block) to gy for
-// k_gemm_tn's hidden^T . gy: 6.4 GB written and 7.7 GB read back on C5.  Here each wave
-// also multiplies the tile's own hidden rows (16 x 64, staged in LDS) by its G_t slot
-// into 64 x 64 accumulators per matrix, dW_t += h_tile^T . G_t (v_mfma_f32_16x16x4_f32,
-// 64 per tile and matrix), and nothing is stored but grad_hidden and one partial per
-// wave.  The RL x 64 x 64 accumulators (4 relations + self-loop: 320 floats per lane)
-// need the whole register file, so the kernel runs ONE wave per SIMD (a 4-wave block
-// per CU, amdgpu_waves_per_eu(1, 1)) with 8 row gathers in flight per lane.  Tiles are
-// static contiguous ranges per wave (deterministic: the partials are summed in wave
-// order by k_sum_splits); relations a tile has no edge of are skipped.
-constexpr int kFoldThreads = 256;
-constexpr int kFoldGU = 8;
-
-template <int R_, bool LOOP>
-__global__ void __launch_bounds__(kFoldThreads) __attribute__((amdgpu_waves_per_eu(1, 1)))
-k_rgcn_bwd_fold(const int32_t* __restrict__ ptr, const int32_t* __restrict__ cols,
-                const int32_t* __restrict__ rows, const int32_t* __restrict__ eids,
-                const float* __restrict__ w, const float* __restrict__ T, const float* __restrict__ W,
-                int64_t ws_t, int64_t ws_k, int64_t ws_n, float* __restrict__ out,
-                const float* __restrict__ Hd, float* __restrict__ parts, int64_t num_rows,
-                const float* __restrict__ Lw, int64_t tiles_per_wave) {
-  using f32x4 = __attribute__((ext_vector_type(4))) float;
-  constexpr int RL = R_ + (LOOP ? 1 : 0);
-  constexpr int SW = kFusedW;  // 64 output columns (grad_hidden width)
-  constexpr int NB16 = SW / 16;
-  __shared__ float Ws[RL * kFusedW * SW];
-  __shared__ float slots[kFoldThreads / 64][16 * kFusedW];
-  __shared__ float hslot[kFoldThreads / 64][16 * kFusedW];
-  __shared__ float carries[kFoldThreads / 64][3][kFusedW];
-  for (int i = threadIdx.x; i < RL * kFusedW * SW; i += kFoldThreads) {
-    const int t = i / (kFusedW * SW), k = (i / SW) % kFusedW, n = i % SW;
-    const float v = t < R_ ? W[t * ws_t + k * ws_k + n * ws_n] : Lw[k * ws_k + n * ws_n];
-    Ws[t * kFusedW * SW + n * kFusedW + swz(n & 15, k)] = v;
-  }
-  __syncthreads();  // the only block barrier
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int m = lane & 15, kq = lane >> 4;
-  const int g = lane >> 4, q = lane & 15;
-  float* slot = slots[wv];
-  float* hs = hslot[wv];
-  float* carry = carries[wv][0];
-  const __amdgpu_buffer_rsrc_t trs =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(T), 0, -1, 0x00020000);
-  const int64_t tiles = (num_rows + 15) / 16;
-  const int64_t wg = static_cast<int64_t>(blockIdx.x) * (kFoldThreads / 64) + wv;
-  const int64_t t0 = wg * tiles_per_wave;
-  const int64_t t1 = t0 + tiles_per_wave < tiles ? t0 + tiles_per_wave : tiles;
-  f32x4 aw[RL][4][4];
-#pragma unroll
-  for (int t = 0; t < RL; ++t)
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) aw[t][a][b] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  for (int64_t tile = t0; tile < t1; ++tile) {
-    const int64_t v0 = tile * 16;
-    const int tile_rows = num_rows - v0 < 16 ? static_cast<int>(num_rows - v0) : 16;
-    f32x4 acc[NB16];
-#pragma unroll
-    for (int nb = 0; nb < NB16; ++nb) acc[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    // the tile's own hidden rows (the weight gradient's left operand), 4 rows per group
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = 4 * g + i;
-      const int64_t v = v0 + row;
-      const float4 a = v < num_rows ? *reinterpret_cast<const float4*>(Hd + v * kFusedW + 4 * q)
-                                    : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      *reinterpret_cast<float4*>(hs + row * kFusedW + swz(row, 4 * q)) = a;
-    }
-    // the matrix loop stays rolled (one copy of the gather code); only the fold into
-    // the statically indexed accumulators is unrolled over the matrices
-#pragma unroll 1
-    for (int t = 0; t < RL; ++t) {
-      if (LOOP && t == R_) {
-        // self-loop: the tile's own rows of grad_out
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = 4 * g + i;
-          const int64_t v = v0 + row;
-          const float4 a = v < num_rows ? *reinterpret_cast<const float4*>(T + v * kFusedW + 4 * q)
-                                        : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-          *reinterpret_cast<float4*>(slot + row * kFusedW + swz(row, 4 * q)) = a;
-        }
-      } else {
-        const int64_t base = static_cast<int64_t>(t) * num_rows + v0;
-        const int64_t pb = ptr[base], pe = ptr[base + tile_rows];
-        if (pb == pe) continue;  // G_t = 0 on this tile: nothing to add anywhere
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = 4 * g + i;
-          *reinterpret_cast<float4*>(slot + row * kFusedW + swz(row, 4 * q)) =
-              make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        }
-        const int64_t share = (pe - pb + 3) / 4;
-        const int64_t gb = pb + g * share < pe ? pb + g * share : pe;
-        const int64_t ge = gb + share < pe ? gb + share : pe;
-        const bool cont = gb < ge && gb > pb && rows[gb - 1] == rows[gb];
-        bool first = true;
-        int crow = -1;
-        float4 a4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        int cur = -1;
-        auto flush = [&]() {
-          float* d = (first && cont) ? carry + (g - 1) * kFusedW + 4 * q
-                                     : slot + cur * kFusedW + swz(cur, 4 * q);
-          if (first && cont) crow = cur;
-          *reinterpret_cast<float4*>(d) = a4;
-          first = false;
-        };
-        for (int64_t p = gb; p < ge; p += 16) {
-          const int n = ge - p < 16 ? static_cast<int>(ge - p) : 16;
-          int my_col = 0, my_row = -1;
-          float my_w = 0.0f;
-          if (q < n) {
-            my_col = cols[p + q];
-            my_row = static_cast<int>(rows[p + q] - base);
-            my_w = w[eids ? eids[p + q] : p + q];
-          }
-#pragma unroll
-          for (int j0 = 0; j0 < 16; j0 += kFoldGU) {
-            float4 x[kFoldGU];
-            float wj[kFoldGU];
-            int rj[kFoldGU];
-#pragma unroll
-            for (int u = 0; u < kFoldGU; ++u) {
-              const int c = row_bcast16(my_col, j0 + u);
-              rj[u] = row_bcast16(my_row, j0 + u);
-              wj[u] = __int_as_float(row_bcast16(__float_as_int(my_w), j0 + u));
-              const uint32_t off = (static_cast<uint32_t>(c) * kFusedW + 4u * q) * 4u;
-              typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
-              const u32x4v r4 = __builtin_amdgcn_raw_buffer_load_b128(trs, static_cast<int>(off), 0, 0);
-              x[u] = make_float4(__uint_as_float(r4.x), __uint_as_float(r4.y), __uint_as_float(r4.z),
-                                 __uint_as_float(r4.w));
-            }
-#pragma unroll
-            for (int u = 0; u < kFoldGU; ++u) {
-              if (rj[u] < 0) break;  // past the batch (group-uniform)
-              if (rj[u] != cur) {
-                if (cur >= 0) flush();
-                a4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                cur = rj[u];
-              }
-              a4.x += wj[u] * x[u].x;
-              a4.y += wj[u] * x[u].y;
-              a4.z += wj[u] * x[u].z;
-              a4.w += wj[u] * x[u].w;
-            }
-          }
-        }
-        if (cur >= 0) flush();
-        wave_lds_sync();
-#pragma unroll
-        for (int gg = 1; gg < 4; ++gg) {
-          const int cr = __builtin_amdgcn_readlane(crow, gg * 16);
-          if (cr >= 0) slot[cr * kFusedW + swz(cr, lane)] += carry[(gg - 1) * kFusedW + lane];
-        }
-      }
-      wave_lds_sync();
-      if (out != nullptr) {
-        // grad_hidden tile += G_t (16 x 64) . W_t^T (as k_rgcn_fused16)
-        const float* wt = Ws + t * kFusedW * SW;
-#pragma unroll 1
-        for (int s4 = 0; s4 < 4; ++s4) {
-          const int c = 16 * kq + 4 * s4;
-          const float4 a = *reinterpret_cast<const float4*>(slot + m * kFusedW + swz(m, c));
-#pragma unroll
-          for (int nb = 0; nb < NB16; ++nb) {
-            const int n = nb * 16 + m;
-            const float4 b = *reinterpret_cast<const float4*>(wt + n * kFusedW + swz(m, c));
-            acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc[nb], 0, 0, 0);
-            acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc[nb], 0, 0, 0);
-            acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc[nb], 0, 0, 0);
-            acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc[nb], 0, 0, 0);
-          }
-        }
-      }
-      // dW_t[k][n] += sum_u h[u][k] G_t[u][n]: A[i][kk] = h[4 s + kk][16 mb + i],
-      // B[kk][j] = G_t[4 s + kk][16 nb + j] (lane: i, j = m; kk = kq)
-#pragma unroll
-      for (int tt = 0; tt < RL; ++tt) {
-        if (tt != t) continue;  // wave-uniform: one matrix's accumulators per pass
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-          const int u = 4 * s4 + kq;
-          float ha[4], gb4[4];
-#pragma unroll
-          for (int mb = 0; mb < 4; ++mb) ha[mb] = hs[u * kFusedW + swz(u, 16 * mb + m)];
-#pragma unroll
-          for (int nb = 0; nb < 4; ++nb) gb4[nb] = slot[u * kFusedW + swz(u, 16 * nb + m)];
-#pragma unroll
-          for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-            for (int nb = 0; nb < 4; ++nb)
-              aw[tt][mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[mb], gb4[nb], aw[tt][mb][nb], 0, 0, 0);
-        }
-      }
-      wave_lds_sync();  // the slot is read; the next matrix may overwrite it
-    }
-    if (out != nullptr) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t mrow = v0 + 4 * kq + i;
-        if (mrow >= num_rows) continue;
-#pragma unroll
-        for (int nb = 0; nb < NB16; ++nb)
-          __builtin_nontemporal_store(acc[nb][i], out + mrow * SW + nb * 16 + m);
-      }
-    }
-    wave_lds_sync();  // hs is read; the next tile overwrites it
-  }
-  // this wave's partial: parts[wg][t][k][n], C[4 kq + r][m] of block (mb, nb)
-  float* pw = parts + wg * (static_cast<int64_t>(RL) * kFusedW * kFusedW);
-#pragma unroll
-  for (int t = 0; t < RL; ++t)
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          pw[t * kFusedW * kFusedW + (16 * mb + 4 * kq + r) * kFusedW + 16 * nb + m] = aw[t][mb][nb][r];
-}
-
 // out[i] = sum over z (in order) of parts[z * n + i]
 __global__ void k_sum_splits(const float* __restrict__ parts, int splits, int64_t n,
                              float* __restrict__ out) {
@@ -1232,53 +1007,6 @@ void launch_gemm(const float* A, int64_t a_rs, int64_t a_cs, const float* B, int
                      K, k_split);
   hipLaunchKernelGGL(k_sum_splits, dim3(grid1(M * N)), dim3(kBlock), 0, s, partials,
                      static_cast<int>(used), M * N, C);
-}
-
-// The folded backward (k_rgcn_bwd_fold): grad_hidden and dW = [dW_0 .. dW_{R-1} | dLw]
-// ([mats][64][64], summed over the waves in wave order); false when the shape is not one
-// it takes (64-wide rows both ways, R + loop <= 5, tables under 4 GiB).
-int64_t rgcn_fold_waves() { return 256 * (kFoldThreads / 64); }
-int64_t rgcn_fold_parts_bytes(int64_t mats) {
-  return rgcn_fold_waves() * mats * kFusedW * kFusedW * 4;
-}
-bool launch_rgcn_bwd_fold(const int32_t* ptr, const int32_t* cols, const int32_t* rows,
-                          const int32_t* eids, const float* w, const float* grad_out,
-                          const float* W, int64_t ws_t, int64_t ws_k, int64_t ws_n,
-                          float* grad_hidden, const float* hidden, float* parts, float* dW,
-                          int64_t num_rows, int64_t R, const float* loop_w, int64_t t_rows,
-                          hipStream_t s) {
-  if (num_rows <= 0 || R < 1 || R > 4 + (loop_w == nullptr ? 1 : 0)) return false;
-  if ((num_rows + 1) * kFusedW * 4 >= (int64_t(1) << 32) || t_rows * kFusedW * 4 >= (int64_t(1) << 32))
-    return false;
-  const int64_t nw = rgcn_fold_waves();
-  const int64_t tiles = (num_rows + 15) / 16;
-  const int64_t per = (tiles + nw - 1) / nw;
-  const dim3 grid(static_cast<unsigned>(nw / (kFoldThreads / 64))), block(kFoldThreads);
-  const int mats = static_cast<int>(R) + (loop_w != nullptr);
-#define DGLMI_FOLD(R__, L__)                                                                    \
-  hipLaunchKernelGGL((k_rgcn_bwd_fold<R__, L__>), grid, block, 0, s, ptr, cols, rows, eids, w,  \
-                     grad_out, W, ws_t, ws_k, ws_n, grad_hidden, hidden, parts, num_rows, loop_w, \
-                     per)
-  if (loop_w != nullptr) {
-    switch (R) {
-      case 1: DGLMI_FOLD(1, true); break;
-      case 2: DGLMI_FOLD(2, true); break;
-      case 3: DGLMI_FOLD(3, true); break;
-      default: DGLMI_FOLD(4, true); break;
-    }
-  } else {
-    switch (R) {
-      case 1: DGLMI_FOLD(1, false); break;
-      case 2: DGLMI_FOLD(2, false); break;
-      case 3: DGLMI_FOLD(3, false); break;
-      case 4: DGLMI_FOLD(4, false); break;
-      default: DGLMI_FOLD(5, false); break;
-    }
-  }
-#undef DGLMI_FOLD
-  const int64_t n = static_cast<int64_t>(mats) * kFusedW * kFusedW;
-  hipLaunchKernelGGL(k_sum_splits, dim3(grid1(n)), dim3(kBlock), 0, s, parts, static_cast<int>(nw), n, dW);
-  return true;
 }
 
 }  // namespace dglmi

@@ -432,16 +432,6 @@ void launch_permute_rkx(const float* w, int64_t R, int64_t K, int64_t X, bool to
 // to the tile's own rows of T (RelGraphConv's self-loop; square graphs).
 // rgcn_fused_ok: the shapes it takes (R counts the self-loop matrix too).
 bool rgcn_fused_ok(int64_t gathered_w, int64_t out_w, int64_t R);
-// layer-1 backward with the weight gradient folded into the walk (hack_kernels.hip
-// k_rgcn_bwd_fold; DGLMI_RGCN_FOLD=1): grad_hidden and dW = [mats][64][64]; `parts`
-// holds rgcn_fold_parts_bytes(mats); false when the shape is not one it takes
-int64_t rgcn_fold_parts_bytes(int64_t mats);
-bool launch_rgcn_bwd_fold(const int32_t* ptr, const int32_t* cols, const int32_t* rows,
-                          const int32_t* eids, const float* w, const float* grad_out,
-                          const float* W, int64_t ws_t, int64_t ws_k, int64_t ws_n,
-                          float* grad_hidden, const float* hidden, float* parts, float* dW,
-                          int64_t num_rows, int64_t R, const float* loop_w, int64_t t_rows,
-                          hipStream_t s);
 void launch_rgcn_fused(bool bwd, const int32_t* ptr, const int32_t* cols, const int32_t* rows,
                        const int32_t* eids, const float* w, const float* T, const float* W,
                        int64_t ws_t, int64_t ws_k, int64_t ws_n, float* out, float* gy,
