@@ -6,15 +6,17 @@
 // and two torch ops per forward (copy_e max, e_sub_v, exp, copy_e sum,
 // e_div_v) and four per backward, each one a pass over the edges with a
 // random gather by edge id.  Here:
-//   forward  = k_sm_rows<STATS>  (per destination: running max m and sum of
+//   forward  = k_sm_rows_v<STATS>  (per destination: running max m and sum of
 //              exp(s - m), merged online -- one gather of the logits) + its
 //              fixup, then k_sm_edges<NORMALIZE> (a[e] = exp(s[e] - m[v]) / l[v],
 //              edge-id order: sequential logits in, sequential a out);
-//   backward = k_sm_rows<DOTSUM> (S[v] = sum_e a[e] * ga[e]) + fixup, then
+//   backward = k_sm_rows_v<DOTSUM> (S[v] = sum_e a[e] * ga[e]) + fixup, then
 //              k_sm_edges<GRAD> (gs[e] = a[e] ga[e] - a[e] S[v], the
 //              reference's order of operations, softmax.py:103-112).
-// Row work is cut into fixed chunks of CSR positions (one wave per chunk), rows cut by a chunk boundary are merged in chunk
-// order by the fixup -- deterministic, no atomics.
+// Row work is cut into fixed chunks of CSR positions (one wave per chunk), rows cut by a
+// chunk boundary are merged in chunk order by the fixup -- deterministic, no atomics.
+// On identity-id walks (position views, destination-sorted graphs) the row-owned walk
+// (k_sm_owned + k_sm_hub, below) replaces all three.
 #include "internal.h"
 
 #include <algorithm>
@@ -57,121 +59,26 @@ __device__ __forceinline__ void strow(float* __restrict__ p, const float (&v)[H]
   }
 }
 
-// (m, l) <- merge of two partial softmax states
+// (m, l) <- merge of two partial softmax states.  Both maxima -inf: the sums add
+// (0 + 0, or NaN when either saw a NaN logit), so a NaN is never dropped.
 __device__ __forceinline__ void merge(float& m, float& l, float m2, float l2) {
   const float mn = m > m2 ? m : m2;
-  if (mn == -INFINITY) return;  // both empty / all -inf
-  l = l * expf(m - mn) + l2 * expf(m2 - mn);
+  const float ms = mn == -INFINITY ? 0.0f : mn;
+  l = l * expf(m - ms) + l2 * expf(m2 - ms);
   m = mn;
 }
 
 // merge() with one exponential: the larger maximum's own factor is exp(0) = 1.  The
 // same (m, l) for finite values; a NaN or +inf anywhere leaves l NaN (so the row's
 // softmax is NaN, as with the reference's exp(score - max)); two empty states
-// (m = -inf, l = 0) stay empty.
+// (m = -inf, l = 0) stay empty, and one -inf state with l NaN (a NaN seen while the
+// maximum was -inf) keeps its NaN.
 __device__ __forceinline__ void merge1(float& m, float& l, float m2, float l2) {
   const bool ge = m >= m2;
   const float hi = ge ? m : m2, lo = ge ? m2 : m;
   const float lhi = ge ? l : l2, llo = ge ? l2 : l;
-  if (hi == -INFINITY) return;
-  l = lhi + llo * expf(lo - hi);
+  l = lhi + llo * expf(lo - (hi == -INFINITY ? 0.0f : hi));
   m = hi;
-}
-
-// One wave per chunk of K CSR positions, walked L = 64 / H positions at a time with
-// lane (j, h) on position base + j and head h: every load instruction reads L
-// consecutive positions' row ids and edge ids and, when the edge ids are the
-// positions (a position view), one contiguous 256-byte run of logits.  (A lane per
-// chunk walking its own positions -- the round-1 form -- kept 64 streams per wave
-// whose lines left L2 before the lane came back: 6 ms for 1.4 GB at H = 1.)  The
-// positions of one step are reduced by a segmented inclusive scan over j (rows are
-// sorted, so equal row ids are one segment); each finished segment is written out,
-// the step's last one carries into the next step.  Outputs per chunk as before: a row
-// continued from the previous chunk goes to the chunk's carry, every other row to
-// the row statistics, and k_sm_fixup merges the carries in chunk order --
-// deterministic, no atomics.
-template <int H, int MODE>
-__global__ void __launch_bounds__(kBlock) k_sm_rows(SoftmaxArgs a) {
-  constexpr int L = 64 / H;      // positions per step
-  constexpr int U = L >= 16 ? 2 : 4;  // steps whose loads are issued together
-  const int lane = threadIdx.x & 63, j = lane / H, h = lane % H;
-  const int64_t chunk = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
-  const int64_t K = a.chunk;
-  const int64_t p0 = chunk * K;
-  if (p0 >= a.nnz) return;
-  const int64_t p1 = p0 + K < a.nnz ? p0 + K : a.nnz;
-  if (a.seg_cnt != nullptr && lane == 0) a.seg_cnt[chunk] = 0;  // k_sm_fixup's counters
-  const int first_row = a.rows[p0];
-  const bool cont = p0 > 0 && a.rows[p0 - 1] == first_row;
-  auto put = [&](int row, float m, float l) {
-    const bool carry = cont && row == first_row;
-    float* pm = carry ? a.carry + chunk * 2 * H : a.stat0 + (int64_t)row * H;
-    pm[h] = m;
-    if constexpr (MODE == SM_STATS) (carry ? pm + H : a.stat1 + (int64_t)row * H)[h] = l;
-  };
-  int run_row = -1;  // the row the previous step ended in, and its partial state
-  float run_m = MODE == SM_STATS ? -INFINITY : 0.0f, run_l = 0.0f;
-  for (int64_t base = p0; base < p1; base += U * L) {
-    int r[U];
-    float x[U], g[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t p = base + u * L + j;
-      r[u] = -1;
-      x[u] = MODE == SM_STATS ? -INFINITY : 0.0f;
-      g[u] = 0.0f;
-      if (p < p1) {
-        r[u] = a.rows[p];
-        const int64_t e = a.eids[p];
-        x[u] = a.s[e * H + h];
-        if constexpr (MODE == SM_DOTSUM) g[u] = a.ga[e * H + h];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t sb = base + u * L;
-      if (sb >= p1) break;  // wave-uniform
-      const int jl = p1 - sb < L ? static_cast<int>(p1 - sb) - 1 : L - 1;  // last valid j
-      float m, l;
-      if constexpr (MODE == SM_STATS) {
-        m = x[u];
-        l = x[u] == INFINITY ? __builtin_nanf("") : (x[u] == -INFINITY ? 0.0f : 1.0f);
-      } else {
-        m = x[u] * g[u];
-        l = 0.0f;
-      }
-      // the previous step's last row: continued by this step's first segment, or done
-      const int r0 = __shfl(r[u], h);
-      if (run_row >= 0) {
-        if (r0 == run_row) {
-          if (j == 0) {
-            if constexpr (MODE == SM_STATS) merge1(m, l, run_m, run_l);
-            else m += run_m;
-          }
-        } else if (j == 0) {
-          put(run_row, run_m, run_l);
-        }
-      }
-#pragma unroll
-      for (int d = 1; d < L; d <<= 1) {
-        const float m2 = __shfl_up(m, d * H);
-        const float l2 = MODE == SM_STATS ? __shfl_up(l, d * H) : 0.0f;
-        const int r2 = __shfl_up(r[u], d * H);
-        if (j >= d && r2 == r[u]) {
-          if constexpr (MODE == SM_STATS) merge1(m, l, m2, l2);
-          else m += m2;
-        }
-      }
-      const int rn = __shfl_down(r[u], H);
-      const int rl = __shfl(r[u], jl * H + h);
-      const bool seg_end = j <= jl && (j == jl || rn != r[u]);
-      if (seg_end && r[u] != rl) put(r[u], m, l);
-      run_row = rl;
-      run_m = __shfl(m, jl * H + h);
-      run_l = MODE == SM_STATS ? __shfl(l, jl * H + h) : 0.0f;
-    }
-  }
-  if (j == 0) put(run_row, run_m, run_l);
 }
 
 template <int H, int MODE>
@@ -297,7 +204,11 @@ __device__ __forceinline__ float ld_fresh(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int H, int MODE>
+// CHUNK: the statistics sweep of the chunked row pass on an edge-id walk (k_sm_rows):
+// values gathered through the walk's edge ids, (max, sum) stored as they are (the edge
+// pass divides), and the chunk's first row, when it continues from the previous chunk,
+// stored to the chunk's carry for k_sm_fixup.
+template <int H, int MODE, bool CHUNK = false>
 struct OwnedWalk {
   using S = OwnedShape<H, MODE>;
   static constexpr int V = S::V, LP = S::LP, L = S::L, U = S::U;
@@ -305,6 +216,8 @@ struct OwnedWalk {
   const SoftmaxArgs& a;
   int j, q;  // position in the step, head group
   float m[V], l[V];  // this lane's running state (MODE DOTSUM: m = sum, l unused)
+  int carry_row = -1;      // CHUNK: the row continued from the previous chunk
+  float* carry = nullptr;  // CHUNK: its partial state (2H floats)
 
   __device__ __forceinline__ OwnedWalk(const SoftmaxArgs& args, int lane)
       : a(args), j(lane / LP), q(lane % LP) { clear(); }
@@ -313,6 +226,11 @@ struct OwnedWalk {
     for (int v = 0; v < V; ++v) { m[v] = kId; l[v] = 0.0f; }
   }
   __device__ __forceinline__ int64_t off(int64_t p) const { return p * H + q * V; }
+  // where position p's values sit in s / ga (the edge id's row on an edge-id walk)
+  __device__ __forceinline__ int64_t voff(int64_t p) const {
+    if constexpr (CHUNK) return a.eids[p] * H + q * V;
+    else return p * H + q * V;
+  }
   template <int N>
   __device__ __forceinline__ void accumulate(int64_t b, int64_t pend) {
     float x[N][V], g[MODE == SM_DOTSUM ? N : 1][V];
@@ -320,8 +238,8 @@ struct OwnedWalk {
     for (int u = 0; u < N; ++u) {
       const int64_t p = b + u * L + j;
       if (p < pend) {
-        ldrow<V>(a.s + off(p), x[u]);
-        if constexpr (MODE == SM_DOTSUM) ldrow<V>(a.ga + off(p), g[u]);
+        ldrow<V>(a.s + voff(p), x[u]);
+        if constexpr (MODE == SM_DOTSUM) ldrow<V>(a.ga + voff(p), g[u]);
       } else {
 #pragma unroll
         for (int v = 0; v < V; ++v) {
@@ -338,11 +256,13 @@ struct OwnedWalk {
         float mb = x[0][v];
 #pragma unroll
         for (int u = 1; u < N; ++u) mb = fmaxf(mb, x[u][v]);
+        // (fmaxf skips NaN: with mn = -inf every term is exp(-inf) = 0 except a NaN's)
         const float mn = fmaxf(m[v], mb);
-        float s = l[v] * fexp(m[v] - mn);
+        const float ms = mn == -INFINITY ? 0.0f : mn;
+        float s = l[v] * fexp(m[v] - ms);
 #pragma unroll
-        for (int u = 0; u < N; ++u) s += fexp(x[u][v] - mn);
-        if (mn != -INFINITY) l[v] = s;
+        for (int u = 0; u < N; ++u) s += fexp(x[u][v] - ms);
+        l[v] = s;
         m[v] = mn;
       } else {
 #pragma unroll
@@ -375,11 +295,22 @@ struct OwnedWalk {
   }
   // a finished row's statistics: forward (max, 1 / sum), backward sum(a ga)
   __device__ __forceinline__ void put(int row, const float (&pm)[V], const float (&pl)[V]) const {
-    float* s0 = a.stat0 + (int64_t)row * H + q * V;
+    if constexpr (CHUNK) {
+      const bool c = row == carry_row;
+      float* s0 = c ? carry + q * V : a.stat0 + (int64_t)row * H + q * V;
+      float* s1 = c ? carry + H + q * V : a.stat1 + (int64_t)row * H + q * V;
 #pragma unroll
-    for (int v = 0; v < V; ++v) {
-      s0[v] = pm[v];
-      if constexpr (MODE == SM_STATS) a.stat1[(int64_t)row * H + q * V + v] = 1.0f / pl[v];
+      for (int v = 0; v < V; ++v) {
+        s0[v] = pm[v];
+        if constexpr (MODE == SM_STATS) s1[v] = pl[v];
+      }
+    } else {
+      float* s0 = a.stat0 + (int64_t)row * H + q * V;
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        s0[v] = pm[v];
+        if constexpr (MODE == SM_STATS) a.stat1[(int64_t)row * H + q * V + v] = 1.0f / pl[v];
+      }
     }
   }
   __device__ __forceinline__ void stats_of(int row, float (&sm)[V], float (&si)[V]) const {
@@ -417,6 +348,11 @@ struct OwnedWalk {
 
   // rows [s0, s1) complete: statistics, then outputs
   __device__ void span(int64_t s0, int64_t s1) {
+    sweep_stats(s0, s1);
+    sweep_out(s0, s1);
+  }
+  // statistics of the rows of [s0, s1) (rows cut by s0 / s1: their partial states)
+  __device__ void sweep_stats(int64_t s0, int64_t s1) {
     const int jl_full = L - 1;
     int cur = a.rows[s0];
     int64_t cur_end = a.indptr[cur + 1];
@@ -432,8 +368,8 @@ struct OwnedWalk {
 #pragma unroll
       for (int v = 0; v < V; ++v) { x[v] = kId; g[v] = 0.0f; }
       if (valid) {
-        ldrow<V>(a.s + off(p), x);
-        if constexpr (MODE == SM_DOTSUM) ldrow<V>(a.ga + off(p), g);
+        ldrow<V>(a.s + voff(p), x);
+        if constexpr (MODE == SM_DOTSUM) ldrow<V>(a.ga + voff(p), g);
       }
       if constexpr (MODE == SM_DOTSUM) {
 #pragma unroll
@@ -503,13 +439,17 @@ struct OwnedWalk {
       reduce();
       if (j == 0) put(cur, m, l);
     }
-    // this wave's row statistics, stored above by the j == 0 lanes, before any lane
+  }
+  // the outputs of the complete rows [s0, s1) from their statistics
+  __device__ void sweep_out(int64_t s0, int64_t s1) {
+    const int jl_full = L - 1;
+    // this wave's row statistics, stored by sweep_stats's j == 0 lanes, before any lane
     // reads them back (ld_fresh: L2, the point of coherence)
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     __builtin_amdgcn_s_waitcnt(0);  // every store of this wave performed at L2
     __builtin_amdgcn_wave_barrier();
-    cur = a.rows[s0];
-    cur_end = a.indptr[cur + 1];
+    int cur = a.rows[s0];
+    int64_t cur_end = a.indptr[cur + 1];
     float cm[V], ci[V];
     stats_of(cur, cm, ci);
     for (int64_t b = s0; b < s1;) {
@@ -619,6 +559,32 @@ __global__ void __launch_bounds__(kBlock) k_sm_hub(SoftmaxArgs a) {
   if (st1 >= lo && en1 - st1 > S::T) finish(st1, en1, st1, hi);
 }
 
+// The chunked row pass of an edge-id walk (round 5): a wave per chunk of K positions,
+// walked like the row-owned walk's statistics sweep -- V heads per lane, every lane
+// keeping its own running state inside a row, the cross-lane reduction and the
+// segmented scan only on steps that cross a row end -- with the logits gathered through
+// the edge ids.  (Round 4's k_sm_rows ran the segmented scan on every step: 1.85e9 VALU
+// instructions per C3 H = 8 launch, VALU-bound.)  Outputs as before: the chunk's first
+// row, when it continues from the previous chunk, to the chunk's carry; every other row
+// to the statistics (max, sum); k_sm_fixup merges in chunk order.
+template <int H, int MODE>
+__global__ void __launch_bounds__(kBlock) k_sm_rows_v(SoftmaxArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t chunk = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+  const int64_t K = a.chunk;
+  const int64_t p0 = chunk * K;
+  if (p0 >= a.nnz) return;
+  const int64_t p1 = p0 + K < a.nnz ? p0 + K : a.nnz;
+  if (a.seg_cnt != nullptr && lane == 0) a.seg_cnt[chunk] = 0;  // k_sm_fixup's counters
+  OwnedWalk<H, MODE, true> walk(a, lane);
+  const int first_row = a.rows[p0];
+  if (p0 > 0 && a.rows[p0 - 1] == first_row) {
+    walk.carry_row = first_row;
+    walk.carry = a.carry + chunk * 2 * H;
+  }
+  walk.sweep_stats(p0, p1);
+}
+
 template <int H>
 void run_owned(const SoftmaxArgs& a, bool backward, hipStream_t st) {
   auto grid = [&](int64_t W) {
@@ -650,11 +616,11 @@ void run(const SoftmaxArgs& a, bool backward, hipStream_t st) {
   const int64_t eb = (a.nnz + kBlock - 1) / kBlock;
   const dim3 ebl(static_cast<unsigned>(eb < 256 * 64 ? eb : 256 * 64));
   if (!backward) {
-    hipLaunchKernelGGL((k_sm_rows<H, SM_STATS>), rrb, blk, 0, st, a);
+    hipLaunchKernelGGL((k_sm_rows_v<H, SM_STATS>), rrb, blk, 0, st, a);
     if (chunks > 1) hipLaunchKernelGGL((k_sm_fixup<H, SM_STATS>), rb, blk, 0, st, a);
     hipLaunchKernelGGL((k_sm_edges<H, SM_NORMALIZE>), ebl, blk, 0, st, a);
   } else {
-    hipLaunchKernelGGL((k_sm_rows<H, SM_DOTSUM>), rrb, blk, 0, st, a);
+    hipLaunchKernelGGL((k_sm_rows_v<H, SM_DOTSUM>), rrb, blk, 0, st, a);
     if (chunks > 1) hipLaunchKernelGGL((k_sm_fixup<H, SM_DOTSUM>), rb, blk, 0, st, a);
     hipLaunchKernelGGL((k_sm_edges<H, SM_GRAD>), ebl, blk, 0, st, a);
   }
@@ -664,10 +630,11 @@ void run(const SoftmaxArgs& a, bool backward, hipStream_t st) {
 
 bool softmax_supported(int64_t H) { return H == 1 || H == 2 || H == 4 || H == 8 || H == 16; }
 
-// positions per chunk (one wave each): 16 steps of 64 / H positions, fewer while the
-// graph would give fewer than 2048 waves
+// positions per chunk (one wave each): 16 steps of the walk's L positions (64 / (H / V),
+// V = min(H, 4) heads per lane), fewer while the graph would give fewer than 2048 waves
 int64_t softmax_chunk_edges(int64_t nnz, int64_t H) {
-  const int64_t L = H >= 1 && H <= 64 ? 64 / H : 1;
+  const int64_t V = H < 4 ? H : 4;
+  const int64_t L = H >= 1 && H <= 64 ? 64 / (H / V) : 1;
   int64_t steps = 16;
   while (steps > 1 && nnz / (L * steps) < 2048) steps >>= 1;
   return L * steps;

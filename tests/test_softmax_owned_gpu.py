@@ -102,7 +102,7 @@ def test_owned_softmax_special_values(H, monkeypatch):
     (exp(s - max) / sum, as the decomposition) -- in short rows, in rows cut by steps
     and in hub rows cut into pieces."""
     L, W, T = _shape(H)
-    deg = np.array([3, L + 2, 2, 5, W + 7, T + 9, 4, 3 * W, 1, 6], dtype=np.int64)
+    deg = np.array([3, L + 2, 2, 5, W + 7, T + 9, 4, 3 * W, 1, 6, T + 5, 3, L * 3], dtype=np.int64)
     view = _graph(deg, 7).position_view("in")
     rows = view.in_csr.rows.long()
     m = int(deg.sum())
@@ -114,6 +114,11 @@ def test_owned_softmax_special_values(H, monkeypatch):
     s[int(starts[4]) + W, 0] = float("inf")           # +inf in a row cut by a window
     s[int(starts[5]) + 2 * W + 3, 0] = -float("inf")   # masked inside a hub row
     s[int(starts[7]) + W + 1, 0] = float("nan")       # NaN in a hub row
+    # rows masked everywhere but one NaN (a NaN met while the running maximum is -inf):
+    # a hub row, a short row, a row a few steps long
+    for r, k in ((10, 2 * W + 17), (11, 1), (12, 2 * L + 5)):
+        s[int(starts[r]):int(starts[r]) + int(deg[r])] = -float("inf")
+        s[int(starts[r]) + k, 0] = float("nan")
     out = {}
     for owned in ("1", "0"):
         monkeypatch.setenv("DGLMI_SOFTMAX_OWNED", owned)
@@ -126,6 +131,8 @@ def test_owned_softmax_special_values(H, monkeypatch):
     assert th.allclose(a[fin], b[fin], rtol=1e-5, atol=1e-7)
     assert a[int(starts[0]) + 1, 0].item() == 0.0
     assert bool(th.isnan(a[int(starts[2]):int(starts[2]) + 2]).all())
+    for r in (10, 11, 12):
+        assert bool(th.isnan(a[int(starts[r]):int(starts[r]) + int(deg[r]), 0]).all())
     ref = _fp64(rows, s, len(deg))
     assert th.equal(th.isnan(a), th.isnan(ref))
     assert th.allclose(a[fin].double(), ref[fin], rtol=1e-5, atol=1e-7)
