@@ -156,84 +156,106 @@ __global__ void __launch_bounds__(kBlock) k_sddmm_lane(SddmmArgs a) {
 }
 
 // ---- a group of L lanes per edge, float4 slices (NF % 4 == 0, NF >= 16) -----
+// A group takes U consecutive items per iteration: their ids, then every operand load,
+// then the outputs, so U edges' gathers are in flight per group (one edge at a time:
+// C3 u_dot_v(ft, grad) for the GAT composition's attention gradient, 16 lanes per edge,
+// 6.69 ms).
+template <int NV>
+struct GroupUnroll {
+  static constexpr int U = NV == 1 ? 4 : (NV == 2 ? 2 : 1);
+};
+
 template <int OP, bool BWD, int L, int NV>
 __global__ void __launch_bounds__(kBlock) k_sddmm_group(SddmmArgs a) {
   constexpr int G = kBlock / L;
+  constexpr int U = GroupUnroll<NV>::U;
   const int lane = threadIdx.x % L;
   const int64_t NF = a.D * a.len;
   const int NF4 = static_cast<int>(NF / 4);
   const int64_t len = a.len;
   const int S = static_cast<int>(len / 4);  // float4 per dot segment (pow2)
-  const int64_t stride = (int64_t)gridDim.x * G;
-  for (int64_t p = (int64_t)blockIdx.x * G + threadIdx.x / L; p < a.nnz; p += stride) {
-    int64_t row, col, eid;
-    item(a, p, row, col, eid);
-    const bool need_l = !BWD || bwd_needs_lhs<OP>(a.want);
-    const bool need_r = OP != OP_USE_LHS && (!BWD || bwd_needs_rhs<OP>(a.want));
-    const float* lp = a.lhs + pick(a.lhs_role, row, col, eid) * NF;
-    const float* rp = need_r ? a.rhs + pick(a.rhs_role, row, col, eid) * NF : nullptr;
-    float4 l4[NV], r4[NV];
+  const int64_t stride = (int64_t)gridDim.x * G * U;
+  const bool need_l = !BWD || bwd_needs_lhs<OP>(a.want);
+  const bool need_r = OP != OP_USE_LHS && (!BWD || bwd_needs_rhs<OP>(a.want));
+  for (int64_t p0 = ((int64_t)blockIdx.x * G + threadIdx.x / L) * U; p0 < a.nnz; p0 += stride) {
+    int64_t row[U], col[U], eid[U];
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int f4 = lane + v * L;
-      const bool ok = f4 < NF4;
-      l4[v] = (ok && need_l) ? ld4(lp + 4 * f4) : make_float4(0.f, 0.f, 0.f, 0.f);
-      r4[v] = (ok && need_r) ? ld4(rp + 4 * f4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u = 0; u < U; ++u) {
+      const int64_t p = p0 + u < a.nnz ? p0 + u : a.nnz - 1;
+      item(a, p, row[u], col[u], eid[u]);
     }
-    if constexpr (!BWD) {
-      if constexpr (OP == OP_DOT) {
-        float part[NV];
+    float4 l4[U][NV], r4[U][NV];
 #pragma unroll
-        for (int v = 0; v < NV; ++v)
-          part[v] = ((l4[v].x * r4[v].x + l4[v].y * r4[v].y) + l4[v].z * r4[v].z) + l4[v].w * r4[v].w;
-        const int span = S < L ? S : L;
-        for (int o = 1; o < span; o <<= 1) {
-#pragma unroll
-          for (int v = 0; v < NV; ++v) part[v] += __shfl_xor(part[v], o, L);
-        }
-        float* out = a.out + eid * a.D;
-        if (S <= L) {
-#pragma unroll
-          for (int v = 0; v < NV; ++v) {
-            const int f4 = lane + v * L;
-            if (f4 < NF4 && (lane & (S - 1)) == 0) out[f4 / S] = part[v];
-          }
-        } else if (lane == 0) {
-          const int R = S / L;  // consecutive slots of one segment
-          for (int v0 = 0; v0 < NV; v0 += R) {
-            float acc = 0.0f;
-            for (int v = v0; v < v0 + R && v < NV; ++v) acc += part[v];
-            if (v0 * L < NF4) out[(v0 * L) / S] = acc;
-          }
-        }
-      } else {
-        float* out = a.out + eid * NF;
-#pragma unroll
-        for (int v = 0; v < NV; ++v) {
-          const int f4 = lane + v * L;
-          if (f4 < NF4)
-            st4(out + 4 * f4, make_float4(op1<OP>(l4[v].x, r4[v].x), op1<OP>(l4[v].y, r4[v].y),
-                                          op1<OP>(l4[v].z, r4[v].z), op1<OP>(l4[v].w, r4[v].w)));
-        }
-      }
-    } else {
-      const float* go = a.go + pick(a.go_role, row, col, eid) * a.D;
-      float* out = a.out + eid * NF;
+    for (int u = 0; u < U; ++u) {
+      const float* lp = a.lhs + pick(a.lhs_role, row[u], col[u], eid[u]) * NF;
+      const float* rp = need_r ? a.rhs + pick(a.rhs_role, row[u], col[u], eid[u]) * NF : nullptr;
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
         const int f4 = lane + v * L;
-        if (f4 >= NF4) continue;
-        float4 g4;
-        if (OP == OP_DOT && len > 1) {
-          const float ge = go[(4 * f4) / len];
-          g4 = make_float4(ge, ge, ge, ge);
+        const bool ok = f4 < NF4 && p0 + u < a.nnz;
+        l4[u][v] = (ok && need_l) ? ld4(lp + 4 * f4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        r4[u][v] = (ok && need_r) ? ld4(rp + 4 * f4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (p0 + u >= a.nnz) break;
+      if constexpr (!BWD) {
+        if constexpr (OP == OP_DOT) {
+          float part[NV];
+#pragma unroll
+          for (int v = 0; v < NV; ++v)
+            part[v] = ((l4[u][v].x * r4[u][v].x + l4[u][v].y * r4[u][v].y) + l4[u][v].z * r4[u][v].z) +
+                      l4[u][v].w * r4[u][v].w;
+          const int span = S < L ? S : L;
+          for (int o = 1; o < span; o <<= 1) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v) part[v] += __shfl_xor(part[v], o, L);
+          }
+          float* out = a.out + eid[u] * a.D;
+          if (S <= L) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+              const int f4 = lane + v * L;
+              if (f4 < NF4 && (lane & (S - 1)) == 0) out[f4 / S] = part[v];
+            }
+          } else if (lane == 0) {
+            const int R = S / L;  // consecutive slots of one segment
+            for (int v0 = 0; v0 < NV; v0 += R) {
+              float acc = 0.0f;
+              for (int v = v0; v < v0 + R && v < NV; ++v) acc += part[v];
+              if (v0 * L < NF4) out[(v0 * L) / S] = acc;
+            }
+          }
         } else {
-          g4 = ld4(go + 4 * f4);
+          float* out = a.out + eid[u] * NF;
+#pragma unroll
+          for (int v = 0; v < NV; ++v) {
+            const int f4 = lane + v * L;
+            if (f4 < NF4)
+              st4(out + 4 * f4, make_float4(op1<OP>(l4[u][v].x, r4[u][v].x), op1<OP>(l4[u][v].y, r4[u][v].y),
+                                            op1<OP>(l4[u][v].z, r4[u][v].z), op1<OP>(l4[u][v].w, r4[u][v].w)));
+          }
         }
-        st4(out + 4 * f4, make_float4(bwd1<OP>(g4.x, l4[v].x, r4[v].x, a.want),
-                                      bwd1<OP>(g4.y, l4[v].y, r4[v].y, a.want),
-                                      bwd1<OP>(g4.z, l4[v].z, r4[v].z, a.want),
-                                      bwd1<OP>(g4.w, l4[v].w, r4[v].w, a.want)));
+      } else {
+        const float* go = a.go + pick(a.go_role, row[u], col[u], eid[u]) * a.D;
+        float* out = a.out + eid[u] * NF;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          const int f4 = lane + v * L;
+          if (f4 >= NF4) continue;
+          float4 g4;
+          if (OP == OP_DOT && len > 1) {
+            const float ge = go[(4 * f4) / len];
+            g4 = make_float4(ge, ge, ge, ge);
+          } else {
+            g4 = ld4(go + 4 * f4);
+          }
+          st4(out + 4 * f4, make_float4(bwd1<OP>(g4.x, l4[u][v].x, r4[u][v].x, a.want),
+                                        bwd1<OP>(g4.y, l4[u][v].y, r4[u][v].y, a.want),
+                                        bwd1<OP>(g4.z, l4[u][v].z, r4[u][v].z, a.want),
+                                        bwd1<OP>(g4.w, l4[u][v].w, r4[u][v].w, a.want)));
+        }
       }
     }
   }
@@ -260,7 +282,8 @@ void run_lane(const SddmmArgs& a, int64_t NF, hipStream_t s) {
 
 template <int OP, bool BWD, int L, int NV>
 void run_group_cfg(const SddmmArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((k_sddmm_group<OP, BWD, L, NV>), dim3(grid_for(a.nnz, kBlock / L)),
+  constexpr int U = GroupUnroll<NV>::U;
+  hipLaunchKernelGGL((k_sddmm_group<OP, BWD, L, NV>), dim3(grid_for((a.nnz + U - 1) / U, kBlock / L)),
                      dim3(kBlock), 0, s, a);
 }
 
