@@ -1521,11 +1521,14 @@ int64_t softmax_setup(const DGLMIGraph* g, const DGLMIArray* x, const char* name
 }
 }  // namespace
 
-int DGLMIEdgeSoftmaxForward(const DGLMIGraph* graph, const DGLMIArray* logits, DGLMIArray* out,
-                            void* stream) {
+namespace {
+int softmax_forward(const DGLMIGraph* graph, const DGLMIArray* logits, DGLMIArray* out, int act,
+                    float slope, void* stream) {
   API_BEGIN();
   dglmi::SoftmaxArgs a;
   const int64_t H = softmax_setup(graph, logits, "logits", a);
+  a.act = act;
+  a.act_slope = slope;
   check_array(out, "out");
   DGLMI_CHECK(feat_numel(out) == H && out->shape[0] == logits->shape[0], "out shape");
   DGLMI_CHECK(aligned16(out->data), "out must be 16-byte aligned");
@@ -1547,11 +1550,19 @@ int DGLMIEdgeSoftmaxForward(const DGLMIGraph* graph, const DGLMIArray* logits, D
   API_END();
 }
 
-int DGLMIEdgeSoftmaxBackward(const DGLMIGraph* graph, const DGLMIArray* out,
-                             const DGLMIArray* grad_out, DGLMIArray* grad_logits, void* stream) {
+int softmax_backward(const DGLMIGraph* graph, const DGLMIArray* out, const DGLMIArray* grad_out,
+                     const DGLMIArray* logits, float slope, DGLMIArray* grad_logits, void* stream) {
   API_BEGIN();
   dglmi::SoftmaxArgs a;
   const int64_t H = softmax_setup(graph, out, "out", a);
+  if (logits != nullptr) {
+    check_array(logits, "logits");
+    DGLMI_CHECK(feat_numel(logits) == H && logits->shape[0] == out->shape[0], "logits shape");
+    DGLMI_CHECK(aligned16(logits->data), "logits must be 16-byte aligned");
+    a.act = 1;
+    a.act_x = logits->data;
+    a.act_slope = slope;
+  }
   check_array(grad_out, "grad_out");
   check_array(grad_logits, "grad_logits");
   DGLMI_CHECK(feat_numel(grad_out) == H && feat_numel(grad_logits) == H &&
@@ -1575,6 +1586,32 @@ int DGLMIEdgeSoftmaxBackward(const DGLMIGraph* graph, const DGLMIArray* out,
   launch_edge_softmax(a, true, s);
   check_hip(hipGetLastError(), "edge softmax backward launch");
   API_END();
+}
+}  // namespace
+
+int DGLMIEdgeSoftmaxForward(const DGLMIGraph* graph, const DGLMIArray* logits, DGLMIArray* out,
+                            void* stream) {
+  return softmax_forward(graph, logits, out, 0, 0.0f, stream);
+}
+
+int DGLMIEdgeSoftmaxBackward(const DGLMIGraph* graph, const DGLMIArray* out,
+                             const DGLMIArray* grad_out, DGLMIArray* grad_logits, void* stream) {
+  return softmax_backward(graph, out, grad_out, nullptr, 0.0f, grad_logits, stream);
+}
+
+int DGLMIEdgeSoftmaxLeakyForward(const DGLMIGraph* graph, const DGLMIArray* logits,
+                                 float negative_slope, DGLMIArray* out, void* stream) {
+  return softmax_forward(graph, logits, out, 1, negative_slope, stream);
+}
+
+int DGLMIEdgeSoftmaxLeakyBackward(const DGLMIGraph* graph, const DGLMIArray* out,
+                                  const DGLMIArray* grad_out, const DGLMIArray* logits,
+                                  float negative_slope, DGLMIArray* grad_logits, void* stream) {
+  if (logits == nullptr) {
+    g_last_error = "logits (the pre-activation input) is required";
+    return -1;
+  }
+  return softmax_backward(graph, out, grad_out, logits, negative_slope, grad_logits, stream);
 }
 
 }  // extern "C"

@@ -259,6 +259,13 @@ struct SoftmaxArgs {
   float* carry;            // num_chunks x 2H
   int64_t chunk;
   int32_t* seg_cnt;        // num_chunks counters after the carries (segmented fixup), or null
+  // GATConv's leaky_relu -> edge_softmax pair in one pass (act != 0): the forward reads the
+  // pre-activation logits x and takes the softmax of leaky(x) = x > 0 ? x : x * slope; the
+  // backward multiplies its gradient by leaky'(x) = x > 0 ? 1 : slope, x read from act_x
+  // (torch's leaky_relu / leaky_relu_backward, the same operations in the same order)
+  const float* act_x;
+  float act_slope;
+  int act;
 };
 bool softmax_supported(int64_t H);
 int64_t softmax_chunk_edges(int64_t nnz, int64_t H);

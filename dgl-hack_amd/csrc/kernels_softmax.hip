@@ -59,6 +59,20 @@ __device__ __forceinline__ void strow(float* __restrict__ p, const float (&v)[H]
   }
 }
 
+// the fused leaky_relu (SoftmaxArgs.act): forward on loaded logits, backward on a gradient
+template <int N>
+__device__ __forceinline__ void act_fwd(const SoftmaxArgs& a, float (&x)[N]) {
+  if (a.act) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) x[i] = x[i] > 0.0f ? x[i] : x[i] * a.act_slope;
+  }
+}
+template <int N>
+__device__ __forceinline__ void act_bwd(const SoftmaxArgs& a, const float (&x)[N], float (&g)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) g[i] = x[i] > 0.0f ? g[i] : g[i] * a.act_slope;
+}
+
 // (m, l) <- merge of two partial softmax states.  Both maxima -inf: the sums add
 // (0 + 0, or NaN when either saw a NaN logit), so a NaN is never dropped.
 __device__ __forceinline__ void merge(float& m, float& l, float m2, float l2) {
@@ -148,13 +162,16 @@ __global__ void __launch_bounds__(kBlock) k_sm_edges(SoftmaxArgs a) {
     if constexpr (MODE == SM_NORMALIZE) {
       float l[H];
       ldrow<H>(a.stat1 + v * H, l);
+      act_fwd<H>(a, s);
 #pragma unroll
       for (int h = 0; h < H; ++h) o[h] = expf(s[h] - x[h]) / l[h];
     } else {
-      float g[H];
+      float g[H], ax[H];
       ldrow<H>(a.ga + e * H, g);
+      if (a.act) ldrow<H>(a.act_x + e * H, ax);
 #pragma unroll
       for (int h = 0; h < H; ++h) o[h] = s[h] * g[h] - s[h] * x[h];
+      if (a.act) act_bwd<H>(a, ax, o);
     }
     strow<H>(a.out + e * H, o);
   }
@@ -240,6 +257,7 @@ struct OwnedWalk {
       if (p < pend) {
         ldrow<V>(a.s + voff(p), x[u]);
         if constexpr (MODE == SM_DOTSUM) ldrow<V>(a.ga + voff(p), g[u]);
+        else act_fwd<V>(a, x[u]);
       } else {
 #pragma unroll
         for (int v = 0; v < V; ++v) {
@@ -323,13 +341,16 @@ struct OwnedWalk {
   // the output of positions b + u L + j < pend with their row's statistics
   template <int N>
   __device__ __forceinline__ void emit(int64_t b, int64_t pend, const float (&sm)[V], const float (&si)[V]) const {
-    float x[N][V], g[MODE == SM_DOTSUM ? N : 1][V];
+    float x[N][V], g[MODE == SM_DOTSUM ? N : 1][V], ax[MODE == SM_DOTSUM ? N : 1][V];
 #pragma unroll
     for (int u = 0; u < N; ++u) {
       const int64_t p = b + u * L + j;
       if (p < pend) {
         ldrow<V>(a.s + off(p), x[u]);
-        if constexpr (MODE == SM_DOTSUM) ldrow<V>(a.ga + off(p), g[u]);
+        if constexpr (MODE == SM_DOTSUM) {
+          ldrow<V>(a.ga + off(p), g[u]);
+          if (a.act) ldrow<V>(a.act_x + off(p), ax[u]);
+        }
       }
     }
 #pragma unroll
@@ -337,10 +358,14 @@ struct OwnedWalk {
       const int64_t p = b + u * L + j;
       if (p >= pend) continue;
       float o[V];
+      if constexpr (MODE == SM_STATS) act_fwd<V>(a, x[u]);
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         if constexpr (MODE == SM_STATS) o[v] = fexp(x[u][v] - sm[v]) * si[v];
         else o[v] = x[u][v] * g[u][v] - x[u][v] * sm[v];  // softmax.py:103-112's order
+      }
+      if constexpr (MODE == SM_DOTSUM) {
+        if (a.act) act_bwd<V>(a, ax[u], o);
       }
       strow<V>(a.out + off(p), o);
     }
@@ -370,6 +395,7 @@ struct OwnedWalk {
       if (valid) {
         ldrow<V>(a.s + voff(p), x);
         if constexpr (MODE == SM_DOTSUM) ldrow<V>(a.ga + voff(p), g);
+        else act_fwd<V>(a, x);
       }
       if constexpr (MODE == SM_DOTSUM) {
 #pragma unroll

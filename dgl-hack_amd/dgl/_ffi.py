@@ -213,6 +213,12 @@ _SIGS = {
     "DGLMIEdgeSoftmaxBackward": (ctypes.c_int, [
         ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.c_void_p]),
+    "DGLMIEdgeSoftmaxLeakyForward": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.c_float, ctypes.POINTER(Array),
+        ctypes.c_void_p]),
+    "DGLMIEdgeSoftmaxLeakyBackward": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_float, ctypes.POINTER(Array), ctypes.c_void_p]),
     "DGLMIPartitionLDG": (ctypes.c_int, [
         ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_double,
         ctypes.c_void_p]),

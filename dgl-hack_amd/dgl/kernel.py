@@ -463,6 +463,29 @@ def edge_softmax_backward(graph, out, grad_out, grad_logits):
     return grad_logits
 
 
+def edge_softmax_leaky_forward(graph, logits, negative_slope, out):
+    """edge_softmax(leaky_relu(logits)) in the softmax's passes (GATConv's pair,
+    gatconv.py:160-161) -> DGLMIEdgeSoftmaxLeakyForward; ``logits`` pre-activation."""
+    _check_ctx(graph, [("logits", logits), ("out", out)])
+    g = graph.cstruct(_softmax_ws(graph, _feat_len(logits), logits.device), coo=True)
+    check_call(_ffi.lib().DGLMIEdgeSoftmaxLeakyForward(ctypes.byref(g), _arr(logits, "logits"),
+                                                       ctypes.c_float(negative_slope),
+                                                       _arr(out, "out"), _stream(out)))
+    return out
+
+
+def edge_softmax_leaky_backward(graph, out, grad_out, logits, negative_slope, grad_logits):
+    """The gradient wrt the pre-activation logits of edge_softmax_leaky_forward ->
+    DGLMIEdgeSoftmaxLeakyBackward."""
+    _check_ctx(graph, [("out", out), ("grad_out", grad_out), ("logits", logits),
+                       ("grad_logits", grad_logits)])
+    g = graph.cstruct(_softmax_ws(graph, _feat_len(out), out.device), coo=True)
+    check_call(_ffi.lib().DGLMIEdgeSoftmaxLeakyBackward(
+        ctypes.byref(g), _arr(out, "out"), _arr(grad_out, "grad_out"), _arr(logits, "logits"),
+        ctypes.c_float(negative_slope), _arr(grad_logits, "grad_logits"), _stream(out)))
+    return grad_logits
+
+
 # --------------------------------------------------------------------------- #
 # the hack's extra kernels (kernel.py:156-169 of the reference)
 # --------------------------------------------------------------------------- #

@@ -22,10 +22,13 @@ from .... import function as fn
 from .... import kernel as K
 from ..softmax import edge_softmax
 from ..softmax import _apply as _edge_softmax_on
+from ..softmax import _apply_leaky as _leaky_edge_softmax_on
 
 # run the unfused composition in in-CSR position order (GATConv._position_space);
 # False: edge-id order throughout, as the reference
 POSITION_SPACE = True
+# the composition's leaky_relu -> edge_softmax pair as one fused softmax call (False: two)
+FUSED_LEAKY = True
 
 
 def expand_as_pair(x):
@@ -119,7 +122,12 @@ class GATConv(nn.Module):
         view = gidx.position_view("in")
         n_dst, m = view.num_dst, view.number_of_edges()
         e = B.binary_reduce("none", "add", view, B.SRC, B.DST, el, er, m)
-        a = self.attn_drop(_edge_softmax_on(view, self.leaky_relu(e), n_dst))
+        if type(self.leaky_relu) is nn.LeakyReLU and FUSED_LEAKY:
+            # the activation inside the softmax's passes (bit-identical to the two steps)
+            a = _leaky_edge_softmax_on(view, e, n_dst, self.leaky_relu.negative_slope)
+        else:
+            a = _edge_softmax_on(view, self.leaky_relu(e), n_dst)
+        a = self.attn_drop(a)
         return B.binary_reduce("sum", "mul", view, B.SRC, B.EDGE, feat_src, a, n_dst)
 
     def _fused_dim(self):
@@ -169,8 +177,15 @@ class GATConv(nn.Module):
             graph.srcdata.update({"ft": feat_src, "el": el})
             graph.dstdata.update({"er": er})
             graph.apply_edges(fn.u_add_v("el", "er", "e"))
-            e = self.leaky_relu(graph.edata.pop("e"))
-            graph.edata["a"] = self.attn_drop(edge_softmax(graph, e))
+            e = graph.edata.pop("e")
+            if type(self.leaky_relu) is nn.LeakyReLU and FUSED_LEAKY and e.is_cuda and \
+                    hasattr(graph._graph, "get_immutable_gidx"):
+                gidx = graph._graph.get_immutable_gidx(e.device)
+                a = _leaky_edge_softmax_on(gidx, e, graph.number_of_nodes(),
+                                           self.leaky_relu.negative_slope)
+            else:
+                a = edge_softmax(graph, self.leaky_relu(e))
+            graph.edata["a"] = self.attn_drop(a)
             graph.update_all(fn.u_mul_e("ft", "a", "m"), fn.sum("m", "ft"))
             rst = graph.dstdata["ft"]
         if self.res_fc is not None:

@@ -44,12 +44,46 @@ class FusedEdgeSoftmax(th.autograd.Function):
         return None, grad
 
 
-def _apply(gidx, logits, n_nodes):
+class FusedLeakyEdgeSoftmax(th.autograd.Function):
+    """edge_softmax(leaky_relu(x)) with the activation inside the softmax's passes: the
+    activated logits are never written, and the backward multiplies by leaky_relu'(x)
+    where it writes the gradient (torch's operations: bit-identical to the two steps)."""
+
+    @staticmethod
+    def forward(ctx, gidx, x, slope):
+        x = x.contiguous()
+        out = th.empty_like(x)
+        K.edge_softmax_leaky_forward(gidx, x, slope, out)
+        ctx.gidx, ctx.slope = gidx, slope
+        ctx.save_for_backward(out, x)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        out, x = ctx.saved_tensors
+        grad = th.empty_like(out)
+        K.edge_softmax_leaky_backward(ctx.gidx, out, grad_out.contiguous(), x, ctx.slope, grad)
+        return None, grad, None
+
+
+def _fusable(gidx, logits):
     h = 1
     for d in logits.shape[1:]:
         h *= d
-    if FUSED and logits.dtype == th.float32 and K.edge_softmax_supported(h) and \
-            logits.shape[0] == gidx.number_of_edges() and logits.is_cuda:
+    return (FUSED and logits.dtype == th.float32 and K.edge_softmax_supported(h) and
+            logits.shape[0] == gidx.number_of_edges() and logits.is_cuda)
+
+
+def _apply_leaky(gidx, x, n_nodes, slope):
+    """edge_softmax(leaky_relu(x, slope)) -- one fused pair where the softmax is fused,
+    else the two steps."""
+    if _fusable(gidx, x):
+        return FusedLeakyEdgeSoftmax.apply(gidx, x, float(slope))
+    return _apply(gidx, th.nn.functional.leaky_relu(x, slope), n_nodes)
+
+
+def _apply(gidx, logits, n_nodes):
+    if _fusable(gidx, logits):
         return FusedEdgeSoftmax.apply(gidx, logits)
     return EdgeSoftmax.apply(gidx, logits, n_nodes)
 

@@ -383,6 +383,18 @@ int DGLMIEdgeSoftmaxForward(const DGLMIGraph* graph, const DGLMIArray* logits, D
 /* grad_logits = out * grad_out - out * sum_{in-edges}(out * grad_out) (softmax.py:86-114). */
 int DGLMIEdgeSoftmaxBackward(const DGLMIGraph* graph, const DGLMIArray* out,
                              const DGLMIArray* grad_out, DGLMIArray* grad_logits, void* stream);
+/* GATConv's leaky_relu -> edge_softmax pair (gatconv.py:160-161) in the same passes
+ * (extension): out = edge_softmax(leaky_relu(logits, negative_slope)), and
+ * grad_logits = leaky_relu'(logits) * (the softmax backward of out, grad_out) with
+ * leaky_relu'(x) = x > 0 ? 1 : negative_slope -- torch's leaky_relu /
+ * leaky_relu_backward operations, so the results are those of the two-step form bit for
+ * bit.  `logits` is the pre-activation input in both calls; the activated logits are
+ * never written. */
+int DGLMIEdgeSoftmaxLeakyForward(const DGLMIGraph* graph, const DGLMIArray* logits,
+                                 float negative_slope, DGLMIArray* out, void* stream);
+int DGLMIEdgeSoftmaxLeakyBackward(const DGLMIGraph* graph, const DGLMIArray* out,
+                                  const DGLMIArray* grad_out, const DGLMIArray* logits,
+                                  float negative_slope, DGLMIArray* grad_logits, void* stream);
 
 /* ---- the hack's R-GCN layer kernels and neighbour-access benchmark -------------
  * (_CAPI_DGLRgcnLayer0 / 0Backward / 1 / 1Backward / _CAPI_DGLNbAccess,

@@ -8,8 +8,8 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 T=${TAG:-r05_comp2}
 timeout -k 10 700 python -u -m pytest -x -q -p no:cacheprovider --timeout 120 --timeout-method thread \
-  tests/test_kernels_gpu.py tests/test_nn_gpu.py tests/test_generic_gpu.py tests/test_empty_rows_gpu.py \
-  tests/test_int64_gpu.py tests/test_message_api_gpu.py tests/test_specialization_gpu.py > gpurun_out/${T}_tests.log 2>&1
+  ${TESTS:-tests/test_kernels_gpu.py tests/test_nn_gpu.py tests/test_generic_gpu.py tests/test_empty_rows_gpu.py \
+  tests/test_int64_gpu.py tests/test_message_api_gpu.py tests/test_specialization_gpu.py} > gpurun_out/${T}_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/${T}_tests.log
 [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" gpurun_out/${T}_tests.log | head -30; exit $rc; }
 timeout -k 10 300 python -u scripts/gat_unfused_probe.py > gpurun_out/${T}_probe.json 2> gpurun_out/${T}_probe.err

@@ -385,3 +385,35 @@ def test_gat_composition_position_space_bit_identical(H, D, owned, monkeypatch):
     gd.use_fused = False
     monkeypatch.setattr(gatconv, "POSITION_SPACE", True)
     assert not gd._position_space(g, x) and gd.eval()._position_space(g, x)
+
+
+@pytest.mark.parametrize("pos", [True, False])
+@pytest.mark.parametrize("owned", ["0", "1"])
+def test_gat_composition_fused_leaky_bit_identical(pos, owned, monkeypatch):
+    """The composition's leaky_relu -> edge_softmax pair as one fused softmax call
+    (gatconv.FUSED_LEAKY, DGLMIEdgeSoftmaxLeaky*) gives the two-step form's bits: output
+    and every gradient, on the position view and in edge-id order, with either softmax
+    route."""
+    monkeypatch.setenv("DGLMI_SOFTMAX_OWNED", owned)
+    from dgl.nn.pytorch.conv import gatconv
+    from graphs import powerlaw
+    monkeypatch.setattr(gatconv, "POSITION_SPACE", pos)
+    src, dst, n = powerlaw(20000, 300000, seed=22)
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    th.manual_seed(4)
+    gat = nn.GATConv(32, 8, 8, negative_slope=0.15).to(DEV)
+    gat.use_fused = False
+    x = th.randn(n, 32, device=DEV, requires_grad=True)
+    go = th.randn(n, 8, 8, device=DEV)
+    res = []
+    for fused in (True, False):
+        monkeypatch.setattr(gatconv, "FUSED_LEAKY", fused)
+        gat.zero_grad()
+        x.grad = None
+        out = gat(g, x)
+        out.backward(go)
+        res.append([out.detach().clone(), x.grad.clone()] + [p.grad.clone() for p in gat.parameters()])
+    for a, b in zip(*res):
+        assert th.equal(a, b), float((a - b).abs().max())

@@ -186,3 +186,45 @@ def test_owned_softmax_64bit_offsets_bit_identical(monkeypatch):
         res.append((out, gs))
     assert g64._graph.get_immutable_gidx(DEV).num_bits == 64
     assert th.equal(res[0][0], res[1][0]) and th.equal(res[0][1], res[1][1])
+
+
+@pytest.mark.parametrize("route", ["view_owned", "view_chunked", "graph"])
+@pytest.mark.parametrize("H", [1, 8, 16])
+def test_leaky_softmax_bit_identical(route, H, monkeypatch):
+    """DGLMIEdgeSoftmaxLeakyForward / Backward (leaky_relu inside the softmax's passes)
+    against torch's leaky_relu + the plain softmax entries on the same route: the same
+    bits forward and backward, masked / NaN / +inf / zero logits included."""
+    monkeypatch.setenv("DGLMI_SOFTMAX_OWNED", "0" if route == "view_chunked" else "1")
+    deg = _degrees(H, 40 + H)
+    if route == "graph":  # edges in shuffled order: the edge-id walk (chunked row pass)
+        n = len(deg)
+        rs = np.random.RandomState(41 + H)
+        dst = np.repeat(np.arange(n), deg)
+        src = rs.randint(0, n, len(dst))
+        perm = rs.permutation(len(dst))
+        gg = dgl.DGLGraph()
+        gg.add_nodes(n)
+        gg.add_edges(src[perm], dst[perm])
+        g = gg._graph.get_immutable_gidx(DEV)
+        assert not (g.eid_identity_bits() & 1)
+    else:
+        g = _graph(deg, 41 + H).position_view("in")
+    m = int(deg.sum())
+    gen = th.Generator(device=DEV).manual_seed(H + 7)
+    x = th.randn(m, H, device=DEV, generator=gen) * 3
+    x[5, 0] = -float("inf")
+    x[17, 0] = 0.0
+    x[m // 2, 0] = float("nan")
+    x[m // 3, 0] = float("inf")
+    ga = th.randn(m, H, device=DEV, generator=gen)
+    slope = 0.2
+    a1, g1 = th.empty_like(x), th.empty_like(x)
+    K.edge_softmax_leaky_forward(g, x, slope, a1)
+    K.edge_softmax_leaky_backward(g, a1, ga, x, slope, g1)
+    y = th.nn.functional.leaky_relu(x, slope)
+    a0, gy = th.empty_like(x), th.empty_like(x)
+    K.edge_softmax_forward(g, y, a0)
+    K.edge_softmax_backward(g, a0, ga, gy)
+    g0 = th.ops.aten.leaky_relu_backward(gy, x, slope, False)
+    assert th.equal(th.isnan(a1), th.isnan(a0)) and th.equal(a1[~th.isnan(a0)], a0[~th.isnan(a0)])
+    assert th.equal(th.isnan(g1), th.isnan(g0)) and th.equal(g1[~th.isnan(g0)], g0[~th.isnan(g0)])
