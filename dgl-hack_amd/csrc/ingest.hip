@@ -229,6 +229,46 @@ Ws64 ws64_layout(int64_t n, int64_t nnz) {
 
 thread_local std::string g_ingest_error;
 
+// rows of R = 4 << SH floats: 1 << SH lanes per row, one float4 each, so one load
+// instruction reads 64 / (1 << SH) whole rows (one cache-line request per row, not one
+// per float4); two float4 in flight per lane
+template <int SH>
+__global__ void __launch_bounds__(256) k_gather_rows_v4(const float4* __restrict__ src,
+                                                        const int32_t* __restrict__ i32,
+                                                        const int64_t* __restrict__ i64,
+                                                        int64_t n, float4* __restrict__ out) {
+  const int64_t total = n << SH;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += 2 * stride) {
+    const int64_t q2 = q + stride;
+    const int64_t i = q >> SH, i2 = q2 >> SH;
+    const int64_t j = i32 != nullptr ? static_cast<int64_t>(i32[i]) : i64[i];
+    const int64_t c = q & ((1 << SH) - 1);
+    const float4 v = src[(j << SH) + c];
+    float4 v2;
+    if (q2 < total) {
+      const int64_t j2 = i32 != nullptr ? static_cast<int64_t>(i32[i2]) : i64[i2];
+      v2 = src[(j2 << SH) + (q2 & ((1 << SH) - 1))];
+    }
+    out[q] = v;
+    if (q2 < total) out[q2] = v2;
+  }
+}
+
+// any other row width: one lane per row
+__global__ void __launch_bounds__(256) k_gather_rows(const float* __restrict__ src, int64_t R,
+                                                     const int32_t* __restrict__ i32,
+                                                     const int64_t* __restrict__ i64, int64_t n,
+                                                     float* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t j = i32 != nullptr ? static_cast<int64_t>(i32[i]) : i64[i];
+    const float* s = src + j * R;
+    float* o = out + i * R;
+    for (int64_t c = 0; c < R; ++c) o[c] = s[c];
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -385,6 +425,46 @@ int DGLMICSRExpandRows(const int32_t* indptr, int64_t num_rows, int64_t nnz, int
                                                          static_cast<int>(nnz), s);
   (void)hipFreeAsync(temp, s);
   if (e != hipSuccess) return -1;
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// out[i, :] = src[index[i], :], rows of R floats: a per-edge operand put into a walk's
+// position order.  Rows of 4, 8, .. 256 floats: float4 slices, a row's slices on
+// adjacent lanes (k_gather_rows_v4); other widths one lane per row.  torch's
+// index_select on a (114.6 M, 8, 1) tensor took 12 ms.
+int DGLMIGatherRows(const float* src, int64_t row_floats, const void* index, int index_bits,
+                    int64_t n, float* out, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (n == 0 || row_floats == 0) return 0;
+  if (src == nullptr || index == nullptr || out == nullptr || row_floats < 0 || n < 0 ||
+      (index_bits != 32 && index_bits != 64))
+    return -1;
+  const int32_t* i32 = index_bits == 32 ? static_cast<const int32_t*>(index) : nullptr;
+  const int64_t* i64 = index_bits == 64 ? static_cast<const int64_t*>(index) : nullptr;
+  int sh = -1;  // row_floats = 4 << sh, sh <= 6
+  for (int k = 0; k <= 6; ++k)
+    if (row_floats == (int64_t{4} << k)) sh = k;
+  const bool v4 = sh >= 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0 &&
+                  (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+  auto grid_of_items = [](int64_t items) {
+    return dim3(static_cast<unsigned>(std::min<int64_t>((items + 255) / 256, 65536)));
+  };
+  const float4* s4 = reinterpret_cast<const float4*>(src);
+  float4* o4 = reinterpret_cast<float4*>(out);
+  const dim3 g4 = grid_of_items(((n << (sh < 0 ? 0 : sh)) + 1) / 2), blk(256);
+  if (!v4) {
+    hipLaunchKernelGGL(k_gather_rows, grid_of_items(n), blk, 0, s, src, row_floats, i32, i64, n, out);
+  } else {
+    switch (sh) {
+      case 0: hipLaunchKernelGGL(k_gather_rows_v4<0>, g4, blk, 0, s, s4, i32, i64, n, o4); break;
+      case 1: hipLaunchKernelGGL(k_gather_rows_v4<1>, g4, blk, 0, s, s4, i32, i64, n, o4); break;
+      case 2: hipLaunchKernelGGL(k_gather_rows_v4<2>, g4, blk, 0, s, s4, i32, i64, n, o4); break;
+      case 3: hipLaunchKernelGGL(k_gather_rows_v4<3>, g4, blk, 0, s, s4, i32, i64, n, o4); break;
+      case 4: hipLaunchKernelGGL(k_gather_rows_v4<4>, g4, blk, 0, s, s4, i32, i64, n, o4); break;
+      case 5: hipLaunchKernelGGL(k_gather_rows_v4<5>, g4, blk, 0, s, s4, i32, i64, n, o4); break;
+      default: hipLaunchKernelGGL(k_gather_rows_v4<6>, g4, blk, 0, s, s4, i32, i64, n, o4); break;
+    }
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

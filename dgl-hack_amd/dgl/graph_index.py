@@ -225,7 +225,8 @@ class ImmutableGraphIndex:
                 ent = ops.get(direction)
                 if ent is not None and ent[1] is ref:
                     del ops[direction]
-            cached = (key, weakref.ref(w, drop), w[walk.data.long()].contiguous())
+            from . import kernel as K
+            cached = (key, weakref.ref(w, drop), K.gather_rows(w, walk.data))
             self._pos_operands[direction] = cached
         return view, cached[2]
 

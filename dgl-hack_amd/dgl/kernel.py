@@ -463,6 +463,27 @@ def edge_softmax_backward(graph, out, grad_out, grad_logits):
     return grad_logits
 
 
+def gather_rows(src, index):
+    """src[index] for a contiguous fp32 device tensor and an int32 / int64 index on its
+    device -> DGLMIGatherRows (one random row read per output row, rows written in
+    order); other dtypes take torch's indexing."""
+    if src.dtype != th.float32 or index.dtype not in (th.int32, th.int64):
+        return src[index.long()]
+    if not src.is_cuda or index.device != src.device:
+        raise DGLError("gather_rows: src and index must be on one ROCm device")
+    src = src.contiguous()
+    index = index.contiguous()
+    out = src.new_empty((index.shape[0],) + tuple(src.shape[1:]))
+    row = 1
+    for d in src.shape[1:]:
+        row *= d
+    check_call(_ffi.lib().DGLMIGatherRows(
+        ctypes.c_void_p(src.data_ptr()), ctypes.c_int64(row), ctypes.c_void_p(index.data_ptr()),
+        32 if index.dtype == th.int32 else 64, ctypes.c_int64(index.shape[0]),
+        ctypes.c_void_p(out.data_ptr()), _stream(out)))
+    return out
+
+
 def edge_softmax_leaky_forward(graph, logits, negative_slope, out):
     """edge_softmax(leaky_relu(logits)) in the softmax's passes (GATConv's pair,
     gatconv.py:160-161) -> DGLMIEdgeSoftmaxLeakyForward; ``logits`` pre-activation."""

@@ -103,10 +103,15 @@ class GATConv(nn.Module):
         and attention are internal to this call (the reference sets them on a
         ``local_var`` graph), so they can live in the walk's order instead of edge-id
         order -- every per-edge read and write streams instead of landing on a random
-        line per edge.  Whole graphs only (edge ids a permutation), and not while
-        attention dropout is active (``nn.Dropout`` then draws its mask in edge-id
-        order, as the reference's composition does)."""
-        if not POSITION_SPACE or not feat_src.is_cuda or (self.training and self.attn_drop.p > 0):
+        line per edge.  Whole graphs only (edge ids a permutation).  Attention dropout
+        in training keeps ``nn.Dropout``'s draws in edge-id order (the reference's
+        composition): the module draws a mask of ones in edge-id order, gathered into
+        walk order (``_composed_in_positions``); another dropout module keeps the
+        edge-id composition."""
+        if not POSITION_SPACE or not feat_src.is_cuda:
+            return False
+        if self.training and self.attn_drop.p > 0 and \
+                (type(self.attn_drop) is not nn.Dropout or self.attn_drop.inplace):
             return False
         if not hasattr(getattr(graph, "_graph", None), "get_immutable_gidx"):
             return False
@@ -127,7 +132,12 @@ class GATConv(nn.Module):
             a = _leaky_edge_softmax_on(view, e, n_dst, self.leaky_relu.negative_slope)
         else:
             a = _edge_softmax_on(view, self.leaky_relu(e), n_dst)
-        a = self.attn_drop(a)
+        if self.training and self.attn_drop.p > 0:
+            # nn.Dropout's draws in edge-id order, as dropout(a) in the edge-id
+            # composition: (1 * keep) * scale per edge, gathered into walk order; a times
+            # it is dropout's (a * keep) * scale bit for bit, and so is the gradient
+            scale = self.attn_drop(a.new_ones(a.shape))
+            a = a * K.gather_rows(scale, gidx.in_csr.data)
         return B.binary_reduce("sum", "mul", view, B.SRC, B.EDGE, feat_src, a, n_dst)
 
     def _fused_dim(self):

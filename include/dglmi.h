@@ -390,6 +390,12 @@ int DGLMIEdgeSoftmaxBackward(const DGLMIGraph* graph, const DGLMIArray* out,
  * leaky_relu_backward operations, so the results are those of the two-step form bit for
  * bit.  `logits` is the pre-activation input in both calls; the activated logits are
  * never written. */
+/* out[i, :] = src[index[i], :] for i < n, rows of row_floats floats; index int32
+ * (index_bits 32) or int64 (64), device pointers.  A per-edge operand put into a walk's
+ * position order (the position views' operands, GATConv's dropout scale in position
+ * space; extension). */
+int DGLMIGatherRows(const float* src, int64_t row_floats, const void* index, int index_bits,
+                    int64_t n, float* out, void* stream);
 int DGLMIEdgeSoftmaxLeakyForward(const DGLMIGraph* graph, const DGLMIArray* logits,
                                  float negative_slope, DGLMIArray* out, void* stream);
 int DGLMIEdgeSoftmaxLeakyBackward(const DGLMIGraph* graph, const DGLMIArray* out,

@@ -39,6 +39,7 @@ def main():
     gat.use_fused = False
     res = {"config": "C3 232965 nodes / 114.6 M edges, GATConv 602 -> 8 x 8, composition"}
     if "--module-only" in sys.argv:  # only module forward + backward steps (kernel stats)
+        gat.attn_drop.p = float(os.environ.get("GAT_ATTN_DROP", "0"))
         for _ in range(4):
             gat(g, x).sum().backward()
         th.cuda.synchronize()
@@ -87,6 +88,14 @@ def main():
         res["edge_id_order_module_fwd_ms"] = ktime(fwd)
     res["edge_id_order_module_fwd_bwd_ms"] = ktime(fwd_bwd)
     gatconv.POSITION_SPACE = True
+    # attention dropout 0.6 in training (nn.Dropout's edge-id draws; position space since
+    # round 5), then the same in edge-id order
+    gat.attn_drop.p = 0.6
+    res["drop0.6_module_fwd_bwd_ms"] = ktime(fwd_bwd)
+    gatconv.POSITION_SPACE = False
+    res["drop0.6_edge_id_order_module_fwd_bwd_ms"] = ktime(fwd_bwd)
+    gatconv.POSITION_SPACE = True
+    gat.attn_drop.p = 0.0
     if "--kernels" in sys.argv:  # a few module steps for rocprofv3 kernel statistics
         for _ in range(3):
             fwd_bwd()

@@ -380,11 +380,32 @@ def test_gat_composition_position_space_bit_identical(H, D, owned, monkeypatch):
         else:
             assert th.allclose(a, b, rtol=1e-4, atol=1e-5 * float(b.abs().max())), \
                 float((a - b).abs().max())
-    # attention dropout in training keeps the edge-id order (nn.Dropout's draws)
+    # attention dropout in training: nn.Dropout's edge-id-order draws gathered into
+    # walk order (the same kept edges, the same bits with the same softmax kernels)
     gd = nn.GATConv(32, D, H, attn_drop=0.5).to(DEV)
     gd.use_fused = False
     monkeypatch.setattr(gatconv, "POSITION_SPACE", True)
-    assert not gd._position_space(g, x) and gd.eval()._position_space(g, x)
+    assert gd._position_space(g, x) and gd.eval()._position_space(g, x)
+    gd.train()
+    gd.attn_drop.inplace = True  # a dropout that writes its input keeps the edge-id route
+    assert not gd._position_space(g, x)
+    gd.attn_drop.inplace = False
+    res = []
+    for pos in (True, False):
+        monkeypatch.setattr(gatconv, "POSITION_SPACE", pos)
+        gd.zero_grad()
+        x.grad = None
+        th.manual_seed(11)
+        out = gd(g, x)
+        out.backward(go)
+        res.append([out.detach().clone(), x.grad.clone()] + [p.grad.clone() for p in gd.parameters()])
+    assert float((res[0][0] == 0).float().mean()) < 0.9  # dropout did not zero everything
+    for a, b in zip(*res):
+        if owned == "0" or H == 3:
+            assert th.equal(a, b), float((a - b).abs().max())
+        else:
+            assert th.allclose(a, b, rtol=1e-4, atol=1e-5 * float(b.abs().max())), \
+                float((a - b).abs().max())
 
 
 @pytest.mark.parametrize("pos", [True, False])

@@ -11,6 +11,7 @@ import torch as th
 import dgl
 import dgl.function as fn
 from dgl import backend as B
+from dgl import kernel as K
 from graphs import powerlaw
 
 pytestmark = pytest.mark.gpu
@@ -221,3 +222,15 @@ def test_position_operand_cache_drops_with_the_tensor():
     gidx.position_operand(w, "out")
     gidx.clear_operand_cache()
     assert not gidx._pos_operands
+
+
+@pytest.mark.parametrize("shape", [(1000,), (1000, 3), (1000, 2, 2), (1000, 8, 1), (1000, 4, 16), (1000, 256)])
+@pytest.mark.parametrize("idt", [th.int32, th.int64])
+def test_gather_rows_matches_indexing(shape, idt):
+    """DGLMIGatherRows (the position-order copy of a per-edge operand) equals torch's
+    src[index], float4 rows and scalar rows, int32 and int64 indices, repeated and
+    out-of-order rows."""
+    src = th.randn(*shape, device=DEV)
+    idx = th.randint(0, shape[0], (4321,), device=DEV, dtype=idt)
+    assert th.equal(K.gather_rows(src, idx), src[idx.long()])
+    assert K.gather_rows(src, idx[:0]).shape == (0,) + tuple(shape[1:])
