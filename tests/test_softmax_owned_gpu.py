@@ -189,7 +189,7 @@ def test_owned_softmax_64bit_offsets_bit_identical(monkeypatch):
 
 
 @pytest.mark.parametrize("route", ["view_owned", "view_chunked", "graph"])
-@pytest.mark.parametrize("H", [1, 8, 16])
+@pytest.mark.parametrize("H", [1, 2, 4, 8, 16])
 def test_leaky_softmax_bit_identical(route, H, monkeypatch):
     """DGLMIEdgeSoftmaxLeakyForward / Backward (leaky_relu inside the softmax's passes)
     against torch's leaky_relu + the plain softmax entries on the same route: the same
