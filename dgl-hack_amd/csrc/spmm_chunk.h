@@ -606,6 +606,15 @@ void run(const FastArgs& a, IdxPtr indptr, hipStream_t s) {
       case 27: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 27>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
       default: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
     }
+  } else if constexpr (KIND == FAST_COL_MUL_EDGE_BCAST && RED == RED_SUM && L == 16 && NV == 1 &&
+                       VW == 4) {
+    // the same variants for u_mul_e_sum with a per-head edge weight (GAT composition)
+    switch (spmm_variant()) {
+      case 0: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 0>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
+      case 1: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 1>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
+      case 7: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV, 7>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
+      default: hipLaunchKernelGGL((k_chunk_reduce<KIND, RED, L, NV>), dim3(blocks), dim3(kBlock), 0, s, a, indptr); break;
+    }
   } else
 #endif
   {
