@@ -15,4 +15,7 @@ rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/${T}_tests.log
 timeout -k 10 300 python -u scripts/gat_unfused_probe.py > gpurun_out/${T}_probe.json 2> gpurun_out/${T}_probe.err
 rc=$?; echo "probe rc=$rc"; cat gpurun_out/${T}_probe.json; [ $rc -eq 0 ] || { tail -20 gpurun_out/${T}_probe.err; exit $rc; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}prof -o run --output-format csv -- python3 scripts/gat_unfused_probe.py --module-only > gpurun_out/${T}prof.log 2>&1
-rc=$?; echo "rocprof rc=$rc"; exit $rc
+rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
+# the same module steps with attention dropout 0.6 (position space)
+GAT_ATTN_DROP=0.6 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}dropprof -o run --output-format csv -- python3 scripts/gat_unfused_probe.py --module-only > gpurun_out/${T}dropprof.log 2>&1
+rc=$?; echo "rocprof (dropout) rc=$rc"; exit $rc
