@@ -166,6 +166,7 @@ def c3(dev, steps, warmup):
         fgat(g, x).sum().backward()
     ms_ff = timeit(ffwd, steps, warmup)
     ms_ffb = timeit(ffwd_bwd, steps, warmup)
+    check = verify_gat_fused(gat, fgat, g, x)
     # training with the reference GAT example's attention dropout (train.py --attn-drop
     # 0.6): the composition applies nn.Dropout to the softmax; GATConv now keeps it in
     # the fused kernels
@@ -182,7 +183,33 @@ def c3(dev, steps, warmup):
             "unfused_fwd_ms": ms_f, "unfused_fwd_bwd_ms": ms_fb,
             "fused_fwd_ms": ms_ff, "fused_fwd_bwd_ms": ms_ffb,
             "fused_fwd_Gedges_s": m / ms_ff / 1e6, "fused_fwd_bwd_Gedges_s": m / ms_ffb / 1e6,
-            "attn_drop_0.6_fused_fwd_bwd_ms": ms_dfb, "attn_drop_0.6_unfused_fwd_bwd_ms": ms_dufb}
+            "attn_drop_0.6_fused_fwd_bwd_ms": ms_dfb, "attn_drop_0.6_unfused_fwd_bwd_ms": ms_dufb,
+            "check": check}
+
+
+def verify_gat_fused(gat, fgat, g, x):
+    """The fused kernels (FusedGATConv) against the unfused composition (GATConv with
+    use_fused = False, same weights) on the timed C3 graph: output, input gradient and
+    every parameter gradient under one random output gradient.  Raises on a mismatch."""
+    xr = x.detach().clone().requires_grad_()
+    go = th.randn(x.shape[0], 8, 8, device=x.device)
+    res = []
+    for mod in (gat, fgat):
+        mod.zero_grad()
+        xr.grad = None
+        out = mod(g, xr)
+        out.backward(go)
+        res.append([out.detach(), xr.grad.clone()] + [p.grad.clone() for p in mod.parameters()])
+    worst = 0.0
+    for a, b in zip(*res):
+        err = float((a - b).abs().max())
+        bound = 1e-4 + 1e-4 * float(b.abs().max())
+        worst = max(worst, err / bound)
+        if err > bound:
+            raise AssertionError("C3: fused differs from the composition by %.3g (bound %.3g)"
+                                 % (err, bound))
+    return {"fused_vs_unfused_checked": True, "worst_err_over_bound": worst,
+            "compared": "output, x.grad and parameter grads; bound 1e-4 + 1e-4 max|composition|"}
 
 
 def verify_rgcn_fused(conv, g, x, et, norm):
