@@ -1604,6 +1604,85 @@ int DGLMIEdgeSoftmaxLeakyForward(const DGLMIGraph* graph, const DGLMIArray* logi
   return softmax_forward(graph, logits, out, 1, negative_slope, stream);
 }
 
+namespace {
+// el / er of the node-logit entries: H values per row, one row per source / destination
+void node_logit_args(const DGLMIGraph* g, const DGLMIArray* el, const DGLMIArray* er, int64_t H,
+                     float slope, dglmi::SoftmaxArgs& a) {
+  check_array(el, "el");
+  check_array(er, "er");
+  DGLMI_CHECK(feat_numel(el) == H && feat_numel(er) == H, "el / er must have H values per node");
+  DGLMI_CHECK(el->shape[0] >= g->in_csr.num_cols && er->shape[0] >= g->in_csr.num_rows,
+              "el has a row per source node, er a row per destination node");
+  DGLMI_CHECK(aligned16(el->data) && aligned16(er->data), "el / er must be 16-byte aligned");
+  DGLMI_CHECK(g->in_csr.indices != nullptr, "in_csr.indices is required");
+  a.node_l = el->data;
+  a.node_r = er->data;
+  a.cols = g->in_csr.indices;
+  a.coo_src = a.coo_dst ? g->coo_src : nullptr;
+  a.act = 1;
+  a.act_slope = slope;
+}
+}  // namespace
+
+int DGLMIEdgeSoftmaxNodeLogitsForward(const DGLMIGraph* graph, const DGLMIArray* el,
+                                      const DGLMIArray* er, float negative_slope, DGLMIArray* out,
+                                      void* stream) {
+  API_BEGIN();
+  dglmi::SoftmaxArgs a;
+  const int64_t H = softmax_setup(graph, out, "out", a);
+  node_logit_args(graph, el, er, H, negative_slope, a);
+  DGLMI_CHECK(aligned16(out->data), "out must be 16-byte aligned");
+  DeviceGuard guard(graph->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (a.nnz == 0) return 0;
+  Scratch ws(graph, DGLMIEdgeSoftmaxWorkspaceBytes(&graph->in_csr, H), s);
+  const int64_t stats = ((2 * a.num_rows * H * 4) + 255) & ~int64_t(255);
+  a.stat0 = static_cast<float*>(ws.ptr);
+  a.stat1 = a.stat0 + a.num_rows * H;
+  a.carry = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + stats);
+  a.seg_cnt = reinterpret_cast<int32_t*>(
+      reinterpret_cast<char*>(a.carry) +
+      ((((a.nnz + a.chunk - 1) / a.chunk) * 2 * H * 4 + 15) & ~int64_t(15)));
+  a.s = nullptr;
+  a.out = out->data;
+  launch_edge_softmax(a, false, s);
+  check_hip(hipGetLastError(), "edge softmax (node logits) forward launch");
+  API_END();
+}
+
+int DGLMIEdgeSoftmaxNodeLogitsBackward(const DGLMIGraph* graph, const DGLMIArray* out,
+                                       const DGLMIArray* grad_out, const DGLMIArray* el,
+                                       const DGLMIArray* er, float negative_slope,
+                                       DGLMIArray* grad_logits, void* stream) {
+  API_BEGIN();
+  dglmi::SoftmaxArgs a;
+  const int64_t H = softmax_setup(graph, out, "out", a);
+  node_logit_args(graph, el, er, H, negative_slope, a);
+  check_array(grad_out, "grad_out");
+  check_array(grad_logits, "grad_logits");
+  DGLMI_CHECK(feat_numel(grad_out) == H && feat_numel(grad_logits) == H &&
+                  grad_out->shape[0] == out->shape[0] && grad_logits->shape[0] == out->shape[0],
+              "grad shapes");
+  DGLMI_CHECK(aligned16(grad_out->data) && aligned16(grad_logits->data),
+              "grads must be 16-byte aligned");
+  DeviceGuard guard(graph->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (a.nnz == 0) return 0;
+  Scratch ws(graph, DGLMIEdgeSoftmaxWorkspaceBytes(&graph->in_csr, H), s);
+  const int64_t stats = ((2 * a.num_rows * H * 4) + 255) & ~int64_t(255);
+  a.stat0 = static_cast<float*>(ws.ptr);
+  a.carry = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + stats);
+  a.seg_cnt = reinterpret_cast<int32_t*>(
+      reinterpret_cast<char*>(a.carry) +
+      ((((a.nnz + a.chunk - 1) / a.chunk) * 2 * H * 4 + 15) & ~int64_t(15)));
+  a.s = out->data;
+  a.ga = grad_out->data;
+  a.out = grad_logits->data;
+  launch_edge_softmax(a, true, s);
+  check_hip(hipGetLastError(), "edge softmax (node logits) backward launch");
+  API_END();
+}
+
 int DGLMIEdgeSoftmaxLeakyBackward(const DGLMIGraph* graph, const DGLMIArray* out,
                                   const DGLMIArray* grad_out, const DGLMIArray* logits,
                                   float negative_slope, DGLMIArray* grad_logits, void* stream) {

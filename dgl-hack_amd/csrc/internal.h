@@ -266,6 +266,14 @@ struct SoftmaxArgs {
   const float* act_x;
   float act_slope;
   int act;
+  // GATConv's u_add_v -> leaky_relu -> edge_softmax (node_l != null): the logit of the
+  // edge at in-CSR position p is node_l[cols[p]] + node_r[rows[p]] (H values each; the
+  // SDDMM's lhs + rhs), computed where the softmax reads it -- forward, and the backward's
+  // leaky_relu mask -- so the per-edge logits are never stored
+  const float* node_l;
+  const float* node_r;
+  const int32_t* cols;     // in-CSR indices (node_l mode)
+  const int32_t* coo_src;  // with coo_dst: the edge-id-order pass's source per edge
 };
 bool softmax_supported(int64_t H);
 int64_t softmax_chunk_edges(int64_t nnz, int64_t H);

@@ -157,7 +157,17 @@ __global__ void __launch_bounds__(kBlock) k_sm_edges(SoftmaxArgs a) {
       v = a.rows[p];
     }
     float s[H], x[H], o[H];
-    ldrow<H>(a.s + e * H, s);
+    // node logits: the source of this item (edge-id order: coo_src; CSR order: cols)
+    auto node_logits = [&](float (&y)[H]) {
+      const int64_t u = a.coo_dst ? a.coo_src[p] : a.cols[p];
+      float l[H], r[H];
+      ldrow<H>(a.node_l + u * H, l);
+      ldrow<H>(a.node_r + v * H, r);
+#pragma unroll
+      for (int h = 0; h < H; ++h) y[h] = l[h] + r[h];
+    };
+    if (MODE == SM_NORMALIZE && a.node_l != nullptr) node_logits(s);
+    else ldrow<H>(a.s + e * H, s);
     ldrow<H>(a.stat0 + v * H, x);
     if constexpr (MODE == SM_NORMALIZE) {
       float l[H];
@@ -168,7 +178,10 @@ __global__ void __launch_bounds__(kBlock) k_sm_edges(SoftmaxArgs a) {
     } else {
       float g[H], ax[H];
       ldrow<H>(a.ga + e * H, g);
-      if (a.act) ldrow<H>(a.act_x + e * H, ax);
+      if (a.act) {
+        if (a.node_l != nullptr) node_logits(ax);
+        else ldrow<H>(a.act_x + e * H, ax);
+      }
 #pragma unroll
       for (int h = 0; h < H; ++h) o[h] = s[h] * g[h] - s[h] * x[h];
       if (a.act) act_bwd<H>(a, ax, o);
@@ -248,16 +261,39 @@ struct OwnedWalk {
     if constexpr (CHUNK) return a.eids[p] * H + q * V;
     else return p * H + q * V;
   }
+  // the logits of position p in row `row`: stored (a.s), or from the nodes (a.node_l:
+  // lhs + rhs as the u_add_v SDDMM adds them)
+  __device__ __forceinline__ void logits(int64_t p, int row, float (&x)[V]) const {
+    if (a.node_l != nullptr) {
+      float l[V], r[V];
+      ldrow<V>(a.node_l + (int64_t)a.cols[p] * H + q * V, l);
+      ldrow<V>(a.node_r + (int64_t)row * H + q * V, r);
+#pragma unroll
+      for (int v = 0; v < V; ++v) x[v] = l[v] + r[v];
+    } else {
+      ldrow<V>(a.s + voff(p), x);
+    }
+  }
+  // the backward's leaky_relu input at position p (row `row`)
+  __device__ __forceinline__ void act_input(int64_t p, int row, float (&x)[V]) const {
+    if (a.node_l != nullptr) logits(p, row, x);
+    else ldrow<V>(a.act_x + off(p), x);
+  }
+  // positions b + u L + j < pend, all in row `row`
   template <int N>
-  __device__ __forceinline__ void accumulate(int64_t b, int64_t pend) {
+  __device__ __forceinline__ void accumulate(int64_t b, int64_t pend, int row) {
     float x[N][V], g[MODE == SM_DOTSUM ? N : 1][V];
 #pragma unroll
     for (int u = 0; u < N; ++u) {
       const int64_t p = b + u * L + j;
       if (p < pend) {
-        ldrow<V>(a.s + voff(p), x[u]);
-        if constexpr (MODE == SM_DOTSUM) ldrow<V>(a.ga + voff(p), g[u]);
-        else act_fwd<V>(a, x[u]);
+        if constexpr (MODE == SM_DOTSUM) {
+          ldrow<V>(a.s + voff(p), x[u]);
+          ldrow<V>(a.ga + voff(p), g[u]);
+        } else {
+          logits(p, row, x[u]);
+          act_fwd<V>(a, x[u]);
+        }
       } else {
 #pragma unroll
         for (int v = 0; v < V; ++v) {
@@ -340,16 +376,19 @@ struct OwnedWalk {
   }
   // the output of positions b + u L + j < pend with their row's statistics
   template <int N>
-  __device__ __forceinline__ void emit(int64_t b, int64_t pend, const float (&sm)[V], const float (&si)[V]) const {
+  __device__ __forceinline__ void emit(int64_t b, int64_t pend, const float (&sm)[V], const float (&si)[V],
+                                       int row) const {
     float x[N][V], g[MODE == SM_DOTSUM ? N : 1][V], ax[MODE == SM_DOTSUM ? N : 1][V];
 #pragma unroll
     for (int u = 0; u < N; ++u) {
       const int64_t p = b + u * L + j;
       if (p < pend) {
-        ldrow<V>(a.s + off(p), x[u]);
         if constexpr (MODE == SM_DOTSUM) {
+          ldrow<V>(a.s + off(p), x[u]);
           ldrow<V>(a.ga + off(p), g[u]);
-          if (a.act) ldrow<V>(a.act_x + off(p), ax[u]);
+          if (a.act) act_input(p, row, ax[u]);
+        } else {
+          logits(p, row, x[u]);
         }
       }
     }
@@ -384,24 +423,28 @@ struct OwnedWalk {
     bool open = true;
     clear();
     for (int64_t b = s0; b < s1;) {
-      if (cur_end - b >= U * L) { accumulate<U>(b, s1); b += U * L; continue; }
-      if (cur_end - b >= L) { accumulate<1>(b, s1); b += L; continue; }
+      if (cur_end - b >= U * L) { accumulate<U>(b, s1, cur); b += U * L; continue; }
+      if (cur_end - b >= L) { accumulate<1>(b, s1, cur); b += L; continue; }
       // a step that crosses a row boundary (cur ends at or before b + L)
       const int64_t p = b + j;
       const bool valid = p < s1, in_cur = p < cur_end;
       float x[V], g[V];
 #pragma unroll
       for (int v = 0; v < V; ++v) { x[v] = kId; g[v] = 0.0f; }
+      const int rr = in_cur ? cur : (valid ? a.rows[p] : INT_MAX);
       if (valid) {
-        ldrow<V>(a.s + voff(p), x);
-        if constexpr (MODE == SM_DOTSUM) ldrow<V>(a.ga + voff(p), g);
-        else act_fwd<V>(a, x);
+        if constexpr (MODE == SM_DOTSUM) {
+          ldrow<V>(a.s + voff(p), x);
+          ldrow<V>(a.ga + voff(p), g);
+        } else {
+          logits(p, rr, x);
+          act_fwd<V>(a, x);
+        }
       }
       if constexpr (MODE == SM_DOTSUM) {
 #pragma unroll
         for (int v = 0; v < V; ++v) x[v] *= g[v];
       }
-      const int rr = in_cur ? cur : (valid ? a.rows[p] : INT_MAX);
       if (in_cur) {
 #pragma unroll
         for (int v = 0; v < V; ++v) fold(m[v], l[v], x[v]);
@@ -479,8 +522,8 @@ struct OwnedWalk {
     float cm[V], ci[V];
     stats_of(cur, cm, ci);
     for (int64_t b = s0; b < s1;) {
-      if (cur_end - b >= U * L) { emit<U>(b, s1, cm, ci); b += U * L; continue; }
-      if (cur_end - b >= L) { emit<1>(b, s1, cm, ci); b += L; continue; }
+      if (cur_end - b >= U * L) { emit<U>(b, s1, cm, ci, cur); b += U * L; continue; }
+      if (cur_end - b >= L) { emit<1>(b, s1, cm, ci, cur); b += L; continue; }
       const int64_t p = b + j;
       const bool valid = p < s1, in_cur = p < cur_end;
       const int rr = in_cur ? cur : (valid ? a.rows[p] : cur);
@@ -491,7 +534,7 @@ struct OwnedWalk {
       } else {
         stats_of(rr, rm, ri);
       }
-      emit<1>(b, s1, rm, ri);
+      emit<1>(b, s1, rm, ri, rr);
       const int jl = s1 - b < L ? static_cast<int>(s1 - b) - 1 : jl_full;
       if (cur_end <= b + jl) {
         cur = __shfl(rr, jl * LP + q);
@@ -502,9 +545,9 @@ struct OwnedWalk {
     }
   }
   // partial state of hub row positions [pa, pb) -> carry slot
-  __device__ void piece(int64_t pa, int64_t pb, float* slot) {
+  __device__ void piece(int64_t pa, int64_t pb, float* slot, int row) {
     clear();
-    for (int64_t b = pa; b < pb; b += U * L) accumulate<U>(b, pb);
+    for (int64_t b = pa; b < pb; b += U * L) accumulate<U>(b, pb, row);
     reduce();
     if (j == 0) {
 #pragma unroll
@@ -529,7 +572,7 @@ __global__ void __launch_bounds__(kBlock) k_sm_owned(SoftmaxArgs a) {
   const int64_t st0 = a.indptr[r0], en0 = a.indptr[r0 + 1];
   int64_t s0 = lo;
   if (st0 < lo) {  // a row that started in an earlier window
-    if (en0 - st0 > S::T) walk.piece(lo, en0 < hi ? en0 : hi, a.carry + (2 * w) * 2 * H);
+    if (en0 - st0 > S::T) walk.piece(lo, en0 < hi ? en0 : hi, a.carry + (2 * w) * 2 * H, r0);
     s0 = en0;  // a shorter one belongs to the window it started in
   }
   if (s0 >= hi) return;
@@ -537,7 +580,7 @@ __global__ void __launch_bounds__(kBlock) k_sm_owned(SoftmaxArgs a) {
   const int64_t st1 = a.indptr[r1], en1 = a.indptr[r1 + 1];
   int64_t s1 = en1;
   if (en1 - st1 > S::T) {  // a hub row starting in this window: its first piece
-    walk.piece(st1, hi, a.carry + (2 * w + 1) * 2 * H);
+    walk.piece(st1, hi, a.carry + (2 * w + 1) * 2 * H, r1);
     s1 = st1;
   }
   if (s1 > s0) walk.span(s0, s1);
@@ -554,7 +597,7 @@ __global__ void __launch_bounds__(kBlock) k_sm_hub(SoftmaxArgs a) {
   if (lo >= a.nnz) return;
   const int64_t hi = lo + S::W < a.nnz ? lo + S::W : a.nnz;
   OwnedWalk<H, MODE> walk(a, lane);
-  auto finish = [&](int64_t st, int64_t en, int64_t pa, int64_t pb) {
+  auto finish = [&](int64_t st, int64_t en, int64_t pa, int64_t pb, int row) {
     const int64_t wf = st / S::W, wl = (en - 1) / S::W;
     float m[V], l[V];
     const float* c = a.carry + (2 * wf + 1) * 2 * H + walk.q * V;  // the first piece
@@ -575,14 +618,14 @@ __global__ void __launch_bounds__(kBlock) k_sm_hub(SoftmaxArgs a) {
 #pragma unroll
       for (int v = 0; v < V; ++v) l[v] = 1.0f / l[v];
     }
-    for (int64_t b = pa; b < pb; b += S::U * S::L) walk.template emit<S::U>(b, pb, m, l);
+    for (int64_t b = pa; b < pb; b += S::U * S::L) walk.template emit<S::U>(b, pb, m, l, row);
   };
   const int r0 = a.rows[lo];
   const int64_t st0 = a.indptr[r0], en0 = a.indptr[r0 + 1];
-  if (st0 < lo && en0 - st0 > S::T) finish(st0, en0, lo, en0 < hi ? en0 : hi);
+  if (st0 < lo && en0 - st0 > S::T) finish(st0, en0, lo, en0 < hi ? en0 : hi, r0);
   const int r1 = a.rows[hi - 1];
   const int64_t st1 = a.indptr[r1], en1 = a.indptr[r1 + 1];
-  if (st1 >= lo && en1 - st1 > S::T) finish(st1, en1, st1, hi);
+  if (st1 >= lo && en1 - st1 > S::T) finish(st1, en1, st1, hi, r1);
 }
 
 // The chunked row pass of an edge-id walk (round 5): a wave per chunk of K positions,

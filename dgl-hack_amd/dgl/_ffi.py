@@ -213,6 +213,12 @@ _SIGS = {
     "DGLMIEdgeSoftmaxBackward": (ctypes.c_int, [
         ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.c_void_p]),
+    "DGLMIEdgeSoftmaxNodeLogitsForward": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.c_float,
+        ctypes.POINTER(Array), ctypes.c_void_p]),
+    "DGLMIEdgeSoftmaxNodeLogitsBackward": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.c_float, ctypes.POINTER(Array), ctypes.c_void_p]),
     "DGLMIGatherRows": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64,
         ctypes.c_void_p, ctypes.c_void_p]),

@@ -484,6 +484,30 @@ def gather_rows(src, index):
     return out
 
 
+def edge_softmax_node_logits_forward(graph, el, er, negative_slope, out):
+    """edge_softmax(leaky_relu(el[u] + er[v])) without stored logits (GATConv's u_add_v,
+    leaky_relu, edge_softmax) -> DGLMIEdgeSoftmaxNodeLogitsForward."""
+    _check_ctx(graph, [("el", el), ("er", er), ("out", out)])
+    g = graph.cstruct(_softmax_ws(graph, _feat_len(out), out.device), coo=True)
+    check_call(_ffi.lib().DGLMIEdgeSoftmaxNodeLogitsForward(
+        ctypes.byref(g), _arr(el, "el"), _arr(er, "er"), ctypes.c_float(negative_slope),
+        _arr(out, "out"), _stream(out)))
+    return out
+
+
+def edge_softmax_node_logits_backward(graph, out, grad_out, el, er, negative_slope, grad_logits):
+    """The gradient wrt the logits el[u] + er[v] (before leaky_relu) of
+    edge_softmax_node_logits_forward -> DGLMIEdgeSoftmaxNodeLogitsBackward."""
+    _check_ctx(graph, [("out", out), ("grad_out", grad_out), ("el", el), ("er", er),
+                       ("grad_logits", grad_logits)])
+    g = graph.cstruct(_softmax_ws(graph, _feat_len(out), out.device), coo=True)
+    check_call(_ffi.lib().DGLMIEdgeSoftmaxNodeLogitsBackward(
+        ctypes.byref(g), _arr(out, "out"), _arr(grad_out, "grad_out"), _arr(el, "el"),
+        _arr(er, "er"), ctypes.c_float(negative_slope), _arr(grad_logits, "grad_logits"),
+        _stream(out)))
+    return grad_logits
+
+
 def edge_softmax_leaky_forward(graph, logits, negative_slope, out):
     """edge_softmax(leaky_relu(logits)) in the softmax's passes (GATConv's pair,
     gatconv.py:160-161) -> DGLMIEdgeSoftmaxLeakyForward; ``logits`` pre-activation."""

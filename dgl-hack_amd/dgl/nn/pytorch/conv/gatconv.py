@@ -23,6 +23,7 @@ from .... import kernel as K
 from ..softmax import edge_softmax
 from ..softmax import _apply as _edge_softmax_on
 from ..softmax import _apply_leaky as _leaky_edge_softmax_on
+from ..softmax import _apply_node_logits as _node_logit_edge_softmax_on
 
 # run the unfused composition in in-CSR position order (GATConv._position_space);
 # False: edge-id order throughout, as the reference
@@ -126,11 +127,12 @@ class GATConv(nn.Module):
         gidx = graph._graph.get_immutable_gidx(feat_src.device)
         view = gidx.position_view("in")
         n_dst, m = view.num_dst, view.number_of_edges()
-        e = B.binary_reduce("none", "add", view, B.SRC, B.DST, el, er, m)
         if type(self.leaky_relu) is nn.LeakyReLU and FUSED_LEAKY:
-            # the activation inside the softmax's passes (bit-identical to the two steps)
-            a = _leaky_edge_softmax_on(view, e, n_dst, self.leaky_relu.negative_slope)
+            # u_add_v and the activation inside the softmax's passes: the logits are
+            # computed where they are read, never stored (bit-identical to the three steps)
+            a = _node_logit_edge_softmax_on(view, el, er, n_dst, self.leaky_relu.negative_slope)
         else:
+            e = B.binary_reduce("none", "add", view, B.SRC, B.DST, el, er, m)
             a = _edge_softmax_on(view, self.leaky_relu(e), n_dst)
         if self.training and self.attn_drop.p > 0:
             # nn.Dropout's draws in edge-id order, as dropout(a) in the edge-id

@@ -66,12 +66,61 @@ class FusedLeakyEdgeSoftmax(th.autograd.Function):
         return None, grad, None
 
 
-def _fusable(gidx, logits):
+class FusedNodeLogitEdgeSoftmax(th.autograd.Function):
+    """edge_softmax(leaky_relu(u_add_v(el, er))) with the logits computed where the
+    softmax reads them (never stored); the backward writes their gradient and hands it to
+    u_add_v's own gradient kernels (BinaryReduce.backward's calls) -- the three-step
+    composition's bits."""
+
+    @staticmethod
+    def forward(ctx, gidx, el, er, slope):
+        el, er = el.contiguous(), er.contiguous()
+        out = el.new_empty((gidx.number_of_edges(),) + tuple(el.shape[1:]))
+        K.edge_softmax_node_logits_forward(gidx, el, er, slope, out)
+        ctx.gidx, ctx.slope = gidx, slope
+        ctx.save_for_backward(out, el, er)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        out, el, er = ctx.saved_tensors
+        gidx = ctx.gidx
+        gs = th.empty_like(out)
+        K.edge_softmax_node_logits_backward(gidx, out, grad_out.contiguous(), el, er, ctx.slope, gs)
+        g_el = g_er = None
+        if ctx.needs_input_grad[1]:
+            g_el = th.empty_like(el)
+            K.backward_lhs_binary_op_reduce("none", "add", gidx, TargetCode.SRC, TargetCode.DST,
+                                            el, er, gs, gs, g_el)
+        if ctx.needs_input_grad[2]:
+            g_er = th.empty_like(er)
+            K.backward_rhs_binary_op_reduce("none", "add", gidx, TargetCode.SRC, TargetCode.DST,
+                                            el, er, gs, gs, g_er)
+        return None, g_el, g_er, None
+
+
+def _apply_node_logits(gidx, el, er, n_nodes, slope):
+    """edge_softmax(leaky_relu(u_add_v(el, er))) -- one fused pair without stored
+    logits where the softmax is fused and el / er have the same per-node shape, else the
+    three steps."""
+    m = gidx.number_of_edges()
+    if (el.shape[1:] == er.shape[1:] and er.dtype == el.dtype and er.is_cuda and
+            _fusable_as(gidx, (m,) + tuple(el.shape[1:]), el.dtype, el.is_cuda)):
+        return FusedNodeLogitEdgeSoftmax.apply(gidx, el, er, float(slope))
+    e = F.binary_reduce("none", "add", gidx, TargetCode.SRC, TargetCode.DST, el, er, m)
+    return _apply_leaky(gidx, e, n_nodes, slope)
+
+
+def _fusable_as(gidx, shape, dtype, is_cuda):
     h = 1
-    for d in logits.shape[1:]:
+    for d in shape[1:]:
         h *= d
-    return (FUSED and logits.dtype == th.float32 and K.edge_softmax_supported(h) and
-            logits.shape[0] == gidx.number_of_edges() and logits.is_cuda)
+    return (FUSED and dtype == th.float32 and K.edge_softmax_supported(h) and
+            shape[0] == gidx.number_of_edges() and is_cuda)
+
+
+def _fusable(gidx, logits):
+    return _fusable_as(gidx, logits.shape, logits.dtype, logits.is_cuda)
 
 
 def _apply_leaky(gidx, x, n_nodes, slope):

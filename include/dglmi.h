@@ -390,6 +390,19 @@ int DGLMIEdgeSoftmaxBackward(const DGLMIGraph* graph, const DGLMIArray* out,
  * leaky_relu_backward operations, so the results are those of the two-step form bit for
  * bit.  `logits` is the pre-activation input in both calls; the activated logits are
  * never written. */
+/* GATConv's u_add_v -> leaky_relu -> edge_softmax chain (gatconv.py:158-161) with the
+ * logits never stored (extension): the logit of edge (u -> v) is el[u] + er[v] (H values,
+ * added as the u_add_v SDDMM adds them), computed where the softmax reads it; out =
+ * edge_softmax(leaky_relu(el[u] + er[v])), and the backward writes the gradient wrt the
+ * logits (before leaky_relu), the two-step forms' bits.  el: one row per source
+ * (in_csr.num_cols), er: one row per destination; `out` / grads by edge id. */
+int DGLMIEdgeSoftmaxNodeLogitsForward(const DGLMIGraph* graph, const DGLMIArray* el,
+                                      const DGLMIArray* er, float negative_slope, DGLMIArray* out,
+                                      void* stream);
+int DGLMIEdgeSoftmaxNodeLogitsBackward(const DGLMIGraph* graph, const DGLMIArray* out,
+                                       const DGLMIArray* grad_out, const DGLMIArray* el,
+                                       const DGLMIArray* er, float negative_slope,
+                                       DGLMIArray* grad_logits, void* stream);
 /* out[i, :] = src[index[i], :] for i < n, rows of row_floats floats; index int32
  * (index_bits 32) or int64 (64), device pointers.  A per-edge operand put into a walk's
  * position order (the position views' operands, GATConv's dropout scale in position

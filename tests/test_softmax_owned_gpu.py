@@ -228,3 +228,49 @@ def test_leaky_softmax_bit_identical(route, H, monkeypatch):
     g0 = th.ops.aten.leaky_relu_backward(gy, x, slope, False)
     assert th.equal(th.isnan(a1), th.isnan(a0)) and th.equal(a1[~th.isnan(a0)], a0[~th.isnan(a0)])
     assert th.equal(th.isnan(g1), th.isnan(g0)) and th.equal(g1[~th.isnan(g0)], g0[~th.isnan(g0)])
+
+
+@pytest.mark.parametrize("route", ["view_owned", "view_chunked", "graph"])
+@pytest.mark.parametrize("H", [1, 2, 4, 8, 16])
+def test_node_logit_softmax_bit_identical(route, H, monkeypatch):
+    """DGLMIEdgeSoftmaxNodeLogits{Forward,Backward} (the logit el[u] + er[v] computed
+    where the softmax reads it) against the stored-logit chain on the same route -- the
+    u_add_v SDDMM, then the leaky softmax entries: the same bits forward and backward,
+    masked / NaN / +inf node logits included; the edge-id-order pass (graph route) reads
+    the sources from the COO."""
+    from dgl import backend as B
+    monkeypatch.setenv("DGLMI_SOFTMAX_OWNED", "0" if route == "view_chunked" else "1")
+    deg = _degrees(H, 60 + H)
+    n = len(deg)
+    rs = np.random.RandomState(61 + H)
+    dst = np.repeat(np.arange(n), deg)
+    src = rs.randint(0, n, len(dst))
+    gg = dgl.DGLGraph()
+    gg.add_nodes(n)
+    if route == "graph":
+        perm = rs.permutation(len(dst))
+        gg.add_edges(src[perm], dst[perm])
+        g = gg._graph.get_immutable_gidx(DEV)
+        assert not (g.eid_identity_bits() & 1)
+    else:
+        gg.add_edges(src, dst)
+        g = gg._graph.get_immutable_gidx(DEV).position_view("in")
+    m = int(deg.sum())
+    gen = th.Generator(device=DEV).manual_seed(H + 9)
+    el = th.randn(n, H, 1, device=DEV, generator=gen) * 2
+    er = th.randn(n, H, 1, device=DEV, generator=gen) * 2
+    el[3, 0, 0] = -float("inf")
+    er[7, 0, 0] = float("nan")
+    el[11, 0, 0] = float("inf")
+    ga = th.randn(m, H, 1, device=DEV, generator=gen)
+    slope = 0.2
+    a1, g1 = th.empty(m, H, 1, device=DEV), th.empty(m, H, 1, device=DEV)
+    K.edge_softmax_node_logits_forward(g, el, er, slope, a1)
+    K.edge_softmax_node_logits_backward(g, a1, ga, el, er, slope, g1)
+    e = th.empty(m, H, 1, device=DEV)
+    K.binary_op_reduce("none", "add", g, B.SRC, B.DST, el, er, e)
+    a0, g0 = th.empty_like(e), th.empty_like(e)
+    K.edge_softmax_leaky_forward(g, e, slope, a0)
+    K.edge_softmax_leaky_backward(g, a0, ga, e, slope, g0)
+    for x, y in ((a1, a0), (g1, g0)):
+        assert th.equal(th.isnan(x), th.isnan(y)) and th.equal(x[~th.isnan(y)], y[~th.isnan(y)])
