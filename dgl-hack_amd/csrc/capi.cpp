@@ -1614,7 +1614,7 @@ void node_logit_args(const DGLMIGraph* g, const DGLMIArray* el, const DGLMIArray
   DGLMI_CHECK(el->shape[0] >= g->in_csr.num_cols && er->shape[0] >= g->in_csr.num_rows,
               "el has a row per source node, er a row per destination node");
   DGLMI_CHECK(aligned16(el->data) && aligned16(er->data), "el / er must be 16-byte aligned");
-  DGLMI_CHECK(g->in_csr.indices != nullptr, "in_csr.indices is required");
+  DGLMI_CHECK(g->in_csr.nnz == 0 || g->in_csr.indices != nullptr, "in_csr.indices is required");
   a.node_l = el->data;
   a.node_r = er->data;
   a.cols = g->in_csr.indices;

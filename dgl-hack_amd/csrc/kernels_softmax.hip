@@ -16,7 +16,10 @@
 // Row work is cut into fixed chunks of CSR positions (one wave per chunk), rows cut by a
 // chunk boundary are merged in chunk order by the fixup -- deterministic, no atomics.
 // On identity-id walks (position views, destination-sorted graphs) the row-owned walk
-// (k_sm_owned + k_sm_hub, below) replaces all three.
+// (k_sm_owned + k_sm_hub, below) replaces all three.  Two fused modes serve GATConv's
+// composition: SoftmaxArgs.act applies leaky_relu where the logits are read (and its
+// derivative where the gradient is written), and SoftmaxArgs.node_l computes each logit
+// as el[u] + er[v] where it is read, so the per-edge logits are never stored.
 #include "internal.h"
 
 #include <algorithm>

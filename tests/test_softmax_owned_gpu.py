@@ -274,3 +274,36 @@ def test_node_logit_softmax_bit_identical(route, H, monkeypatch):
     K.edge_softmax_leaky_backward(g, a0, ga, e, slope, g0)
     for x, y in ((a1, a0), (g1, g0)):
         assert th.equal(th.isnan(x), th.isnan(y)) and th.equal(x[~th.isnan(y)], y[~th.isnan(y)])
+
+
+def test_node_logit_softmax_64bit_and_empty():
+    """The node-logit entries on a graph in the 64-bit layout give the 32-bit layout's
+    bits (position view, hub rows included), and on an edgeless graph they return
+    without touching their outputs."""
+    deg = _degrees(8, 70)
+    n = len(deg)
+    rs = np.random.RandomState(71)
+    dst = np.repeat(np.arange(n), deg)
+    src = rs.randint(0, n, len(dst))
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    g64 = dgl.DGLGraph(g._graph.asbits(64))
+    el = th.randn(n, 8, 1, device=DEV)
+    er = th.randn(n, 8, 1, device=DEV)
+    ga = th.randn(len(dst), 8, 1, device=DEV)
+    res = []
+    for gg in (g, g64):
+        view = gg._graph.get_immutable_gidx(DEV).position_view("in")
+        a, gs = th.empty_like(ga), th.empty_like(ga)
+        K.edge_softmax_node_logits_forward(view, el, er, 0.2, a)
+        K.edge_softmax_node_logits_backward(view, a, ga, el, er, 0.2, gs)
+        res.append((a, gs))
+    assert g64._graph.get_immutable_gidx(DEV).num_bits == 64
+    assert th.equal(res[0][0], res[1][0]) and th.equal(res[0][1], res[1][1])
+    e0 = dgl.DGLGraph()
+    e0.add_nodes(5)
+    gi = e0._graph.get_immutable_gidx(DEV)
+    out = th.full((0, 8, 1), 7.0, device=DEV)
+    K.edge_softmax_node_logits_forward(gi, el[:5], er[:5], 0.2, out)
+    K.edge_softmax_node_logits_backward(gi, out, out, el[:5], er[:5], 0.2, out)
