@@ -1683,6 +1683,23 @@ int DGLMIEdgeSoftmaxNodeLogitsBackward(const DGLMIGraph* graph, const DGLMIArray
   API_END();
 }
 
+int DGLMIProjectSupported(int64_t k, int64_t n) { return dglmi::project_supported(k, n) ? 1 : 0; }
+
+int DGLMIProject(const float* x, int64_t m, int64_t k, const float* w, int64_t w_stride_k,
+                 int64_t w_stride_n, int64_t n, const float* bias, float* y, int device, void* stream) {
+  API_BEGIN();
+  DGLMI_CHECK(dglmi::project_supported(k, n), "DGLMIProject: unsupported (k, n) = (" +
+                                                  std::to_string(k) + ", " + std::to_string(n) + ")");
+  DGLMI_CHECK(m >= 0 && x != nullptr && w != nullptr && y != nullptr, "DGLMIProject: null operand");
+  DGLMI_CHECK(aligned16(x) && aligned16(y) && (bias == nullptr || aligned16(bias)),
+              "DGLMIProject: x, y and bias must be 16-byte aligned");
+  DGLMI_CHECK(w_stride_k >= 1 && w_stride_n >= 1, "DGLMIProject: bad weight strides");
+  DeviceGuard guard(device);
+  dglmi::launch_project(x, m, k, w, w_stride_k, w_stride_n, n, bias, y, static_cast<hipStream_t>(stream));
+  check_hip(hipGetLastError(), "projection launch");
+  API_END();
+}
+
 int DGLMIEdgeSoftmaxLeakyBackward(const DGLMIGraph* graph, const DGLMIArray* out,
                                   const DGLMIArray* grad_out, const DGLMIArray* logits,
                                   float negative_slope, DGLMIArray* grad_logits, void* stream) {

@@ -276,6 +276,12 @@ struct SoftmaxArgs {
   const int32_t* coo_src;  // with coo_dst: the edge-id-order pass's source per edge
 };
 bool softmax_supported(int64_t H);
+
+// Tall-skinny projection Y = X W (+ bias) on MFMA (kernels_project.hip): X (M, K)
+// row-major, W (K, N) with strides (swk, swn), Y (M, N) row-major.
+bool project_supported(int64_t K, int64_t N);
+void launch_project(const float* X, int64_t M, int64_t K, const float* W, int64_t swk, int64_t swn,
+                    int64_t N, const float* bias, float* Y, hipStream_t s);
 int64_t softmax_chunk_edges(int64_t nnz, int64_t H);
 // eids NULL (identity edge ids): the row-owned walk (one read, one write per value);
 // its carries need this many bytes after the statistics

@@ -219,6 +219,11 @@ _SIGS = {
     "DGLMIEdgeSoftmaxNodeLogitsBackward": (ctypes.c_int, [
         ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.c_float, ctypes.POINTER(Array), ctypes.c_void_p]),
+    "DGLMIProjectSupported": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64]),
+    "DGLMIProject": (ctypes.c_int, [
+        ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+        ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+        ctypes.c_void_p]),
     "DGLMIGatherRows": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64,
         ctypes.c_void_p, ctypes.c_void_p]),

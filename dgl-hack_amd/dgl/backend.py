@@ -343,10 +343,14 @@ class _Project(th.autograd.Function):
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
+        x2 = x.reshape(-1, x.shape[-1])
+        if K.project_mfma_ok(x2, w) and (b is None or (b.dim() == 1 and b.dtype == th.float32)):
+            # tall-skinny: the MFMA kernel with W in registers (kernels_project.hip)
+            return K.project_mfma(x2, w, b).view(x.shape[:-1] + (w.shape[1],))
         if b is None:
             return th.matmul(x, w)
         # bias in the GEMM epilogue (hipBLASLt addmm), not a separate pass
-        return th.addmm(b, x.reshape(-1, x.shape[-1]), w).view(x.shape[:-1] + (w.shape[1],))
+        return th.addmm(b, x2, w).view(x.shape[:-1] + (w.shape[1],))
 
     @staticmethod
     def backward(ctx, gy):
@@ -357,7 +361,12 @@ class _Project(th.autograd.Function):
         gy = gy.contiguous()
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            gx = th.matmul(gy, w.t())
+            gy2 = gy.reshape(-1, gy.shape[-1])
+            wt = w.t()
+            if K.project_mfma_ok(gy2, wt):
+                gx = K.project_mfma(gy2, wt).view(gy.shape[:-1] + (w.shape[0],))
+            else:
+                gx = th.matmul(gy, wt)
         if ctx.needs_input_grad[1]:
             gw = weight_grad(x, gy)
         if ctx.has_bias and ctx.needs_input_grad[2]:

@@ -463,6 +463,35 @@ def edge_softmax_backward(graph, out, grad_out, grad_logits):
     return grad_logits
 
 
+# projections on the MFMA kernel from this many rows (fewer: torch.matmul, launch-bound)
+PROJECT_MIN_ROWS = 1 << 14
+
+
+def project_mfma_ok(x2, w):
+    """Whether Y = x2 @ w runs on DGLMIProject: fp32 ROCm tensors on one device, x2 a
+    contiguous (M, K) matrix with M >= PROJECT_MIN_ROWS, (K, N) supported."""
+    return (x2.is_cuda and x2.dtype == th.float32 and w.dtype == th.float32 and w.dim() == 2
+            and x2.dim() == 2 and w.device == x2.device and x2.is_contiguous()
+            and x2.shape[0] >= PROJECT_MIN_ROWS and x2.data_ptr() % 16 == 0
+            and bool(_ffi.lib().DGLMIProjectSupported(int(w.shape[0]), int(w.shape[1]))))
+
+
+def project_mfma(x2, w, bias=None):
+    """x2 @ w (+ bias) on the MFMA projection kernel -> DGLMIProject (w may be a
+    transposed view; its strides are passed)."""
+    m, k = x2.shape
+    n = int(w.shape[1])
+    y = x2.new_empty((m, n))
+    if bias is not None:
+        bias = bias.contiguous()
+    check_call(_ffi.lib().DGLMIProject(
+        ctypes.c_void_p(x2.data_ptr()), ctypes.c_int64(m), ctypes.c_int64(k),
+        ctypes.c_void_p(w.data_ptr()), ctypes.c_int64(w.stride(0)), ctypes.c_int64(w.stride(1)),
+        ctypes.c_int64(n), ctypes.c_void_p(bias.data_ptr() if bias is not None else None),
+        ctypes.c_void_p(y.data_ptr()), int(x2.device.index or 0), _stream(y)))
+    return y
+
+
 def gather_rows(src, index):
     """src[index] for a contiguous fp32 device tensor and an int32 / int64 index on its
     device -> DGLMIGatherRows (one random row read per output row, rows written in

@@ -403,6 +403,15 @@ int DGLMIEdgeSoftmaxNodeLogitsBackward(const DGLMIGraph* graph, const DGLMIArray
                                        const DGLMIArray* grad_out, const DGLMIArray* el,
                                        const DGLMIArray* er, float negative_slope,
                                        DGLMIArray* grad_logits, void* stream);
+/* The bracketing projection Y = X W (+ bias) of GraphConv / GATConv / RelGraphConv
+ * (torch.matmul in the reference, graphconv.py:146-170) on MFMA, for tall-skinny shapes:
+ * x (m, k) row-major, w (k, n) element (i, j) at w[i * w_stride_k + j * w_stride_n] (a
+ * transposed nn.Linear weight is strides (1, k)), bias (n) or NULL, y (m, n) row-major;
+ * device pointers on `device`, x / y / bias 16-byte aligned.  DGLMIProjectSupported(k, n):
+ * k in {16, 32, 64, 128}, n a multiple of 64 up to 4096 (extension). */
+int DGLMIProjectSupported(int64_t k, int64_t n);
+int DGLMIProject(const float* x, int64_t m, int64_t k, const float* w, int64_t w_stride_k,
+                 int64_t w_stride_n, int64_t n, const float* bias, float* y, int device, void* stream);
 /* out[i, :] = src[index[i], :] for i < n, rows of row_floats floats; index int32
  * (index_bits 32) or int64 (64), device pointers.  A per-edge operand put into a walk's
  * position order (the position views' operands, GATConv's dropout scale in position

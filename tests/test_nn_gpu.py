@@ -186,6 +186,35 @@ def test_project_split_k_weight_grad(m, k, n):
     assert th.allclose(x.grad.double(), ref_x, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("k,n", [(16, 64), (32, 128), (64, 256), (128, 128), (128, 192)])
+@pytest.mark.parametrize("wt", [False, True])
+def test_project_mfma_kernel(k, n, wt):
+    """DGLMIProject (the tall-skinny MFMA projection) against fp64: a plain and a
+    transposed weight view (nn.Linear's weight.t()), with and without bias, a row count
+    that is not a multiple of the 16-row tile; and B.project's forward / dX take it."""
+    from dgl import backend as B
+    from dgl import kernel as K
+    g = th.Generator(device=DEV).manual_seed(k + n)
+    m = K.PROJECT_MIN_ROWS + 37
+    x = th.randn(m, k, device=DEV, generator=g)
+    w = th.randn(n, k, device=DEV, generator=g).t() if wt else th.randn(k, n, device=DEV, generator=g)
+    b = th.randn(n, device=DEV, generator=g)
+    assert K.project_mfma_ok(x, w)
+    ref = x.double() @ w.double()
+    mag = x.double().abs() @ w.double().abs()
+    for bias in (None, b):
+        y = K.project_mfma(x, w, bias)
+        r = ref if bias is None else ref + bias.double()
+        assert bool(((y.double() - r).abs() <= 2e-6 * mag + 1e-6).all())
+    xr = x.clone().requires_grad_()
+    wr = w.detach().clone().requires_grad_()
+    gy = th.randn(m, n, device=DEV, generator=g)
+    B.project(xr, wr).backward(gy)
+    gref = gy.double() @ wr.detach().double().t()
+    gmag = gy.double().abs() @ wr.detach().double().abs().t()
+    assert bool(((xr.grad.double() - gref).abs() <= 2e-6 * gmag + 1e-6).all())
+
+
 def test_nb_access_bench():
     """The hack's neighbour-access benchmark entry point returns feat and a time."""
     from dgl import backend as B
