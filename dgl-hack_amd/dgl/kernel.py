@@ -473,6 +473,7 @@ def project_mfma_ok(x2, w):
     return (x2.is_cuda and x2.dtype == th.float32 and w.dtype == th.float32 and w.dim() == 2
             and x2.dim() == 2 and w.device == x2.device and x2.is_contiguous()
             and x2.shape[0] >= PROJECT_MIN_ROWS and x2.data_ptr() % 16 == 0
+            and w.stride(0) >= 1 and w.stride(1) >= 1
             and bool(_ffi.lib().DGLMIProjectSupported(int(w.shape[0]), int(w.shape[1]))))
 
 
