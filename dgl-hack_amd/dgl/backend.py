@@ -344,7 +344,9 @@ class _Project(th.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
         x2 = x.reshape(-1, x.shape[-1])
-        if K.project_mfma_ok(x2, w) and (b is None or (b.dim() == 1 and b.dtype == th.float32)):
+        if K.project_mfma_ok(x2, w) and (b is None or (
+                b.dim() == 1 and b.dtype == th.float32 and b.shape[0] == w.shape[1]
+                and b.device == x2.device)):
             # tall-skinny: the MFMA kernel with W in registers (kernels_project.hip)
             return K.project_mfma(x2, w, b).view(x.shape[:-1] + (w.shape[1],))
         if b is None:
