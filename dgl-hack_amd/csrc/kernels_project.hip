@@ -96,8 +96,10 @@ __global__ void __launch_bounds__(64 * kWaves) k_project(const float* __restrict
 
 }  // namespace
 
+// N <= 128: X is read once per 64-column slice, so wider outputs re-read it (5 M x 64 ->
+// 256: 2.28 ms here against 2.13 ms on hipBLASLt, profiles/r05_mfma_util.json) and stay there
 bool project_supported(int64_t K, int64_t N) {
-  return (K == 16 || K == 32 || K == 64 || K == 128) && N >= kNW && N % kNW == 0 && N <= 4096;
+  return (K == 16 || K == 32 || K == 64 || K == 128) && (N == 64 || N == 128);
 }
 
 void launch_project(const float* X, int64_t M, int64_t K, const float* W, int64_t swk, int64_t swn,

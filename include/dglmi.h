@@ -408,7 +408,7 @@ int DGLMIEdgeSoftmaxNodeLogitsBackward(const DGLMIGraph* graph, const DGLMIArray
  * x (m, k) row-major, w (k, n) element (i, j) at w[i * w_stride_k + j * w_stride_n] (a
  * transposed nn.Linear weight is strides (1, k)), bias (n) or NULL, y (m, n) row-major;
  * device pointers on `device`, x / y / bias 16-byte aligned.  DGLMIProjectSupported(k, n):
- * k in {16, 32, 64, 128}, n a multiple of 64 up to 4096 (extension). */
+ * k in {16, 32, 64, 128}, n 64 or 128 (extension). */
 int DGLMIProjectSupported(int64_t k, int64_t n);
 int DGLMIProject(const float* x, int64_t m, int64_t k, const float* w, int64_t w_stride_k,
                  int64_t w_stride_n, int64_t n, const float* bias, float* y, int device, void* stream);

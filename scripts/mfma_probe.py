@@ -36,8 +36,13 @@ def main():
     w = th.randn(k, n, device=dev)
     gy = th.randn(m, n, device=dev)
     th.cuda.synchronize()
-    ops = [("fwd", lambda: x @ w), ("grad_x", lambda: gy @ w.t()),
-           ("grad_w", lambda: B.weight_grad(x, gy))]
+    from dgl import kernel as K
+    # the route B.project takes: the MFMA projection kernel where it applies (round 5),
+    # hipBLASLt otherwise
+    fwd = (lambda: K.project_mfma(x, w)) if K.project_mfma_ok(x, w) else (lambda: x @ w)
+    wt = w.t()
+    gx = (lambda: K.project_mfma(gy, wt)) if K.project_mfma_ok(gy, wt) else (lambda: gy @ wt)
+    ops = [("fwd", fwd), ("grad_x", gx), ("grad_w", lambda: B.weight_grad(x, gy))]
     for _, fn in ops:
         for _ in range(args.reps):
             fn()
