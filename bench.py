@@ -1103,10 +1103,12 @@ def launch_ranks(nproc, argv, grace_s=60.0):
 def launcher_stub(mode, world, rank):
     """Worker body of the launcher's CPU test (``--launcher-stub MODE``): no GPU;
     gloo collectives over the ranks the launcher started, then the same
-    side-line / print path as the real run.  MODE: ok | crash1 (rank 1 exits 7
-    before joining) | side1 (rank 1 raises inside a side line)."""
+    side-line / print path as the real run.  MODE: ok | crash<r> (rank r exits 7
+    before joining) | side<r> (rank r raises inside a side line)."""
     import torch.distributed as dist
-    if mode == "crash1" and rank == 1:
+    crash = int(mode[5:]) if mode.startswith("crash") else -1
+    side = int(mode[4:]) if mode.startswith("side") else -1
+    if rank == crash:
         sys.exit(7)
     if world > 1:
         dist.init_process_group("gloo", timeout=__import__("datetime").timedelta(seconds=60))
@@ -1120,7 +1122,7 @@ def launcher_stub(mode, world, rank):
     lines = SideLines(dist if world > 1 else None, rank, res, budget_s=60.0)
 
     def c4():
-        if mode == "side1" and rank == 1:
+        if rank == side:
             raise RuntimeError("injected side-line failure")
         t = th.ones(1)
         if world > 1:

@@ -1011,29 +1011,47 @@ void gat_check_ls(const GatArgs& a, const DGLMIArray* lf, const DGLMIArray* ls) 
   DGLMI_CHECK(aligned16(lf->data), "slope_feat must be 16-byte aligned");
 }
 
-// attention dropout parameters of the GatArgs (p = 0: off)
-void gat_set_dropout(GatArgs& a, float p, uint64_t seed) {
-  DGLMI_CHECK(p >= 0.0f && p < 1.0f, "attn_drop must be in [0, 1)");
-  a.drop = p > 0.0f ? 1 : 0;
-  if (!a.drop) return;
+// attention dropout parameters of the GatArgs (p = 0 and no keep words: off).  Hashed
+// mask: 16-bit uniforms per edge and head (internal.h gat_head_keep), p resolved to
+// 2^-16 as t = round(p 2^16); a weight is kept when its uniform is >= t, so the keep
+// probability is (2^16 - t) / 2^16 and the scale its inverse (the rescaled expectation
+// stays unbiased); t = 2^16 (p >= 1 - 2^-17, p = 1 included) keeps nothing, scale 0.
+// Caller's mask (`keep`, one uint32 word per edge id, bit h = head h kept): the kernels
+// read it through the walk's edge ids and scale kept weights by `keep_scale`.
+void gat_set_dropout(GatArgs& a, float p, uint64_t seed, const DGLMIArray* keep = nullptr,
+                     float keep_scale = 0.0f, int64_t num_edges = 0) {
+  if (keep != nullptr) {
+    check_array(keep, "keep");
+    DGLMI_CHECK(keep->shape[0] == num_edges && feat_numel(keep) == 1,
+                "keep must hold one word per edge (E,)");
+    DGLMI_CHECK(std::isfinite(keep_scale) && keep_scale >= 0.0f, "keep_scale must be finite and >= 0");
+    a.drop = 2;
+    a.drop_bits = reinterpret_cast<const uint32_t*>(keep->data);
+    a.drop_scale = keep_scale;
+  } else {
+    DGLMI_CHECK(p >= 0.0f && p <= 1.0f, "attn_drop must be in [0, 1]");
+    a.drop = p > 0.0f ? 1 : 0;
+    if (!a.drop) return;
+    const double t = std::min(65536.0, std::floor(static_cast<double>(p) * 65536.0 + 0.5));
+    a.drop_thresh = static_cast<uint32_t>(t);
+    a.drop_scale = t < 65536.0 ? static_cast<float>(65536.0 / (65536.0 - t)) : 0.0f;
+    a.drop_seed = seed;
+  }
   DGLMI_CHECK(a.o32, "attention dropout needs gathered tables below 2^31 elements");
   DGLMI_CHECK(a.H <= 32, "attention dropout in the fused kernels takes at most 32 heads");
-  // 16-bit uniforms per edge and head (internal.h gat_head_keep): p resolved to 2^-16
-  a.drop_thresh = static_cast<uint32_t>(std::min(65535.0, std::floor(static_cast<double>(p) * 65536.0 + 0.5)));
-  a.drop_scale = 1.0f / (1.0f - p);
-  a.drop_seed = seed;
 }
 
 int gat_forward_impl(const DGLMIGraph* graph, const DGLMIArray* feat_src, const DGLMIArray* el,
                      const DGLMIArray* er, float negative_slope, DGLMIArray* out,
                      DGLMIArray* max_out, DGLMIArray* sum_out, DGLMIArray* lf, DGLMIArray* ls,
-                     void* stream, float attn_drop = 0.0f, uint64_t seed = 0) {
+                     void* stream, float attn_drop = 0.0f, uint64_t seed = 0,
+                     const DGLMIArray* keep = nullptr, float keep_scale = 0.0f) {
   API_BEGIN();
   check_graph32(graph, "fused GAT");
   DeviceGuard guard(graph->device);
   GatArgs a = gat_args(graph, feat_src, el, er, negative_slope, out, max_out, sum_out);
   gat_check_ls(a, lf, ls);
-  gat_set_dropout(a, attn_drop, seed);
+  gat_set_dropout(a, attn_drop, seed, keep, keep_scale, graph->in_csr.nnz);
   a.eids = graph->in_csr.data;
   a.lf = lf ? lf->data : nullptr;
   a.ls = ls ? ls->data : nullptr;
@@ -1136,13 +1154,13 @@ int gat_backward_impl(const DGLMIGraph* graph, const DGLMIArray* feat_src, const
                       const DGLMIArray* max_in, const DGLMIArray* sum_in, const DGLMIArray* lf_in,
                       const DGLMIArray* ls_in, const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
                       DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream, float attn_drop = 0.0f,
-                      uint64_t seed = 0) {
+                      uint64_t seed = 0, const DGLMIArray* keep = nullptr, float keep_scale = 0.0f) {
   API_BEGIN();
   check_graph32(graph, "fused GAT");
   DeviceGuard guard(graph->device);
   GatArgs a = gat_args(graph, feat_src, el, er, negative_slope, const_cast<DGLMIArray*>(out),
                        const_cast<DGLMIArray*>(max_in), const_cast<DGLMIArray*>(sum_in));
-  gat_set_dropout(a, attn_drop, seed);
+  gat_set_dropout(a, attn_drop, seed, keep, keep_scale, graph->in_csr.nnz);
   // with dropout only the slope-aggregate backward (no destination-side walk) applies
   DGLMI_CHECK(!a.drop || lf_in != nullptr,
               "attention dropout needs the forward's slope aggregates (slope_feat / slope_sum)");
@@ -1336,6 +1354,44 @@ int DGLMIFusedGatDropoutBackward(const DGLMIGraph* graph, const DGLMIArray* feat
   return gat_backward_impl(graph, feat_src, el, er, negative_slope, out, max_in, sum_in, slope_feat,
                            slope_sum, grad_out, grad_feat_src, grad_el, grad_er, stream, attn_drop,
                            seed);
+}
+
+int DGLMIFusedGatKeepForward(const DGLMIGraph* graph, const DGLMIArray* feat_src,
+                             const DGLMIArray* el, const DGLMIArray* er, float negative_slope,
+                             const DGLMIArray* keep, float keep_scale, DGLMIArray* out,
+                             DGLMIArray* max_out, DGLMIArray* sum_out, DGLMIArray* slope_feat,
+                             DGLMIArray* slope_sum, void* stream) {
+  if (keep == nullptr) {
+    g_last_error = "keep (one word per edge) is required";
+    return -1;
+  }
+  return gat_forward_impl(graph, feat_src, el, er, negative_slope, out, max_out, sum_out, slope_feat,
+                          slope_sum, stream, 0.0f, 0, keep, keep_scale);
+}
+
+int DGLMIFusedGatKeepBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src,
+                              const DGLMIArray* el, const DGLMIArray* er, float negative_slope,
+                              const DGLMIArray* keep, float keep_scale, const DGLMIArray* out,
+                              const DGLMIArray* max_in, const DGLMIArray* sum_in,
+                              const DGLMIArray* slope_feat, const DGLMIArray* slope_sum,
+                              const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
+                              DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream) {
+  if (keep == nullptr) {
+    g_last_error = "keep (one word per edge) is required";
+    return -1;
+  }
+  return gat_backward_impl(graph, feat_src, el, er, negative_slope, out, max_in, sum_in, slope_feat,
+                           slope_sum, grad_out, grad_feat_src, grad_el, grad_er, stream, 0.0f, 0,
+                           keep, keep_scale);
+}
+
+int DGLMIGatKeepBits(const float* table, int64_t num_edges, int heads, uint32_t* bits, void* stream) {
+  API_BEGIN();
+  DGLMI_CHECK(num_edges >= 0 && heads >= 1 && heads <= 32, "DGLMIGatKeepBits: 1 <= heads <= 32");
+  DGLMI_CHECK(num_edges == 0 || (table != nullptr && bits != nullptr), "DGLMIGatKeepBits: null operand");
+  launch_gat_keep_bits(table, num_edges, heads, bits, static_cast<hipStream_t>(stream));
+  check_hip(hipGetLastError(), "keep bits launch");
+  API_END();
 }
 
 // The reference's argument order (_CAPI_DGLFusedGatKernel /
@@ -1685,9 +1741,12 @@ int DGLMIEdgeSoftmaxNodeLogitsBackward(const DGLMIGraph* graph, const DGLMIArray
 
 int DGLMIProjectSupported(int64_t k, int64_t n) { return dglmi::project_supported(k, n) ? 1 : 0; }
 
-int DGLMIProject(const float* x, int64_t m, int64_t k, const float* w, int64_t w_stride_k,
-                 int64_t w_stride_n, int64_t n, const float* bias, float* y, int device, void* stream) {
+int DGLMIProject(const float* x, int64_t m, int64_t k, const float* w, int64_t w_rows,
+                 int64_t w_stride_k, int64_t w_stride_n, int64_t n, const float* bias, float* y, int device,
+                 void* stream) {
   API_BEGIN();
+  DGLMI_CHECK(w_rows == k, "DGLMIProject: x has " + std::to_string(k) + " columns but w has " +
+                               std::to_string(w_rows) + " rows");
   DGLMI_CHECK(dglmi::project_supported(k, n), "DGLMIProject: unsupported (k, n) = (" +
                                                   std::to_string(k) + ", " + std::to_string(n) + ")");
   DGLMI_CHECK(m >= 0 && x != nullptr && w != nullptr && y != nullptr, "DGLMIProject: null operand");

@@ -381,13 +381,17 @@ struct GatArgs {
   // and no destination-side walk runs.  NULL = not kept.
   float* lf;
   float* ls;
-  // attention dropout (DGLMIFusedGatDropout*): edge e, head h keeps its weight, scaled by
-  // 1 / (1 - p), when gat_head_keep(gat_edge_key(seed, eid), h, drop_thresh) (16-bit
-  // threshold, round(p 2^16)); the walk's edge ids in `eids` (its CSR's data).  drop = 0: off.
+  // attention dropout.  drop = 0: off.  drop = 1 (DGLMIFusedGatDropout*, hashed): edge e,
+  // head h keeps its weight, scaled by drop_scale, when gat_head_keep(gat_edge_key(seed,
+  // eid), h, drop_thresh) (16-bit threshold, round(p 2^16)).  drop = 2 (DGLMIFusedGatKeep*,
+  // the caller's mask): bit h of drop_bits[eid] -- one word per edge id, drawn by the
+  // caller (GATConv: its nn.Dropout) -- scaled by drop_scale.  The walk's edge ids in
+  // `eids` (its CSR's data).
   int drop;
   uint32_t drop_thresh;
   float drop_scale;
   uint64_t drop_seed;
+  const uint32_t* drop_bits;
   const int32_t* eids;
 };
 // The dropout mask's hash (mirrored in numpy by dgl.kernel.gat_dropout_keep for the
@@ -419,6 +423,9 @@ __host__ __device__ __forceinline__ bool gat_head_keep(uint32_t key, int h, uint
   return ((gat_pair_bits(key, h >> 1) >> (16 * (h & 1))) & 0xffffu) >= thresh16;
 }
 bool gat_supported(int64_t H, int64_t D);
+// bits[e] = OR over h < H of (table[e * H + h] != 0) << h, e < n (H <= 32): a dropout
+// output table (E, H) in edge-id order packed to one keep word per edge (drop = 2)
+void launch_gat_keep_bits(const float* table, int64_t n, int H, uint32_t* bits, hipStream_t s);
 int64_t gat_chunk_edges(int64_t nnz);
 void launch_gat_forward(const GatArgs& a, hipStream_t s);
 void launch_gat_backward_dst(const GatArgs& a, hipStream_t s);

@@ -108,8 +108,9 @@ __device__ __forceinline__ bool gat_kept(uint32_t staged, int h) { return (stage
 // forward
 // ---------------------------------------------------------------------------
 // LS: also the slope aggregates lf / ls (carry record [acc F][m H][l H][lf F][ls H])
-// DROP: attention dropout (a separate instance, so the plain walk's code is untouched)
-template <int L, int NV, bool O32, bool LS, bool DROP = false>
+// DROP: attention dropout (a separate instance, so the plain walk's code is untouched):
+// 1 the hashed mask, 2 the caller's keep words (GatArgs.drop_bits)
+template <int L, int NV, bool O32, bool LS, int DROP = 0>
 __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
   static_assert(L >= 1 && L <= 64, "a lane group must fit in one wavefront");
   constexpr int G = kBlock / L;
@@ -129,7 +130,8 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
   const int F4 = static_cast<int>(a.F / 4);
   const int H = a.H, D = a.D;
   const int64_t CW = LS ? 2 * a.F + 3 * H : a.F + 2 * H;  // carry record, see above
-  constexpr bool drop = DROP;
+  constexpr bool drop = DROP != 0;
+  constexpr bool table = DROP == 2;  // the caller's keep words, else the hash
   int hd[NV], fl[NV];
   bool ok4[NV], lead[NV];
 #pragma unroll
@@ -205,6 +207,9 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
   // loads, and the edge-id load the keep-bit hash waits for, are off the critical path
   constexpr int SQ = B / L;  // positions each lane stages per batch
   int32_t nr[SQ], nc[SQ], ne[drop ? SQ : 1];
+  uint32_t nk[table ? SQ : 1];
+  // caller's mask (DROP 2): a batch's keep words are loaded with its row / column ids,
+  // from edge ids loaded one batch earlier still, so the dependent load never waits
   auto fetch = [&](int64_t nb) {
 #pragma unroll
     for (int i = 0; i < SQ; ++i) {
@@ -212,9 +217,21 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
       const bool ok = p < p1;
       nr[i] = ok ? a.rows[p] : INT_MAX;
       nc[i] = ok ? a.indices[p] : 0;
-      if constexpr (drop) ne[drop ? i : 0] = ok ? a.eids[p] : 0;
+      if constexpr (table) {
+        nk[table ? i : 0] = ok ? a.drop_bits[ne[table ? i : 0]] : 0u;
+        ne[table ? i : 0] = p + B < p1 ? a.eids[p + B] : 0;
+      } else if constexpr (drop) {
+        ne[drop ? i : 0] = ok ? a.eids[p] : 0;
+      }
     }
   };
+  if constexpr (table) {
+#pragma unroll
+    for (int i = 0; i < SQ; ++i) {
+      const int64_t p = p0 + lane + i * L;
+      ne[table ? i : 0] = p < p1 ? a.eids[p] : 0;
+    }
+  }
   fetch(p0);
   for (int64_t base = p0; base < p1; base += B) {
 #pragma unroll
@@ -223,7 +240,8 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
       s_row[g][q] = nr[i];
       s_col[g][q] = nc[i];
       if constexpr (drop)
-        s_keep[drop ? g : 0][drop ? q : 0] = nr[i] != INT_MAX ? gat_stage_keep(a, ne[drop ? i : 0]) : 0u;
+        s_keep[drop ? g : 0][drop ? q : 0] =
+            nr[i] == INT_MAX ? 0u : table ? nk[table ? i : 0] : gat_stage_keep(a, ne[drop ? i : 0]);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -523,7 +541,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_dst(GatArgs a) {
 // ---------------------------------------------------------------------------
 // backward, source side (out-CSR): grad_ft, grad_el
 // ---------------------------------------------------------------------------
-template <int L, int NV, bool O32, bool DROP>
+template <int L, int NV, bool O32, int DROP>
 __device__ __forceinline__ void gat_bwd_src_body(const GatArgs& a) {
   static_assert(L >= 1 && L <= 64, "a lane group must fit in one wavefront");
   constexpr int G = kBlock / L;
@@ -532,7 +550,8 @@ __device__ __forceinline__ void gat_bwd_src_body(const GatArgs& a) {
   __shared__ int32_t s_row[G][B];
   __shared__ int32_t s_col[G][B];
   __shared__ uint32_t s_keep[DROP ? G : 1][DROP ? B : 1];  // dropout keep bits (gat_stage_keep)
-  constexpr bool drop = DROP;
+  constexpr bool drop = DROP != 0;
+  constexpr bool table = DROP == 2;  // the caller's keep words, else the hash
   const int g = threadIdx.x / L;
   const int lane = threadIdx.x % L;
   const int64_t chunk = (int64_t)blockIdx.x * G + g;
@@ -602,6 +621,9 @@ __device__ __forceinline__ void gat_bwd_src_body(const GatArgs& a) {
   // loads, and the edge-id load the keep-bit hash waits for, are off the critical path
   constexpr int SQ = B / L;  // positions each lane stages per batch
   int32_t nr[SQ], nc[SQ], ne[drop ? SQ : 1];
+  uint32_t nk[table ? SQ : 1];
+  // caller's mask (DROP 2): a batch's keep words are loaded with its row / column ids,
+  // from edge ids loaded one batch earlier still, so the dependent load never waits
   auto fetch = [&](int64_t nb) {
 #pragma unroll
     for (int i = 0; i < SQ; ++i) {
@@ -609,9 +631,21 @@ __device__ __forceinline__ void gat_bwd_src_body(const GatArgs& a) {
       const bool ok = p < p1;
       nr[i] = ok ? a.rows[p] : INT_MAX;
       nc[i] = ok ? a.indices[p] : 0;
-      if constexpr (drop) ne[drop ? i : 0] = ok ? a.eids[p] : 0;
+      if constexpr (table) {
+        nk[table ? i : 0] = ok ? a.drop_bits[ne[table ? i : 0]] : 0u;
+        ne[table ? i : 0] = p + B < p1 ? a.eids[p + B] : 0;
+      } else if constexpr (drop) {
+        ne[drop ? i : 0] = ok ? a.eids[p] : 0;
+      }
     }
   };
+  if constexpr (table) {
+#pragma unroll
+    for (int i = 0; i < SQ; ++i) {
+      const int64_t p = p0 + lane + i * L;
+      ne[table ? i : 0] = p < p1 ? a.eids[p] : 0;
+    }
+  }
   fetch(p0);
   for (int64_t base = p0; base < p1; base += B) {
 #pragma unroll
@@ -620,7 +654,8 @@ __device__ __forceinline__ void gat_bwd_src_body(const GatArgs& a) {
       s_row[g][q] = nr[i];
       s_col[g][q] = nc[i];
       if constexpr (drop)
-        s_keep[drop ? g : 0][drop ? q : 0] = nr[i] != INT_MAX ? gat_stage_keep(a, ne[drop ? i : 0]) : 0u;
+        s_keep[drop ? g : 0][drop ? q : 0] =
+            nr[i] == INT_MAX ? 0u : table ? nk[table ? i : 0] : gat_stage_keep(a, ne[drop ? i : 0]);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -677,7 +712,7 @@ __device__ __forceinline__ void gat_bwd_src_body(const GatArgs& a) {
   fill_empty_rows(a.indptr, a.num_rows, chunk, (a.nnz + K - 1) / K, L, lane, zero_row);
 }
 
-template <int L, int NV, bool O32, bool DROP = false>
+template <int L, int NV, bool O32, int DROP = 0>
 __global__ void __launch_bounds__(kBlock) k_gat_bwd_src(GatArgs a) {
   gat_bwd_src_body<L, NV, O32, DROP>(a);
 }
@@ -861,9 +896,12 @@ void fwd_cfg(const GatArgs& a, hipStream_t s) {
   const bool ls = a.lf != nullptr;
 #define DGLMI_GAT_FWD(O_, LS_) \
   hipLaunchKernelGGL((k_gat_fwd<L, NV, O_, LS_>), dim3(blocks), dim3(kBlock), 0, s, a)
-  if (a.drop) {  // dropout instances for 32-bit offsets only (checked by the C entry)
-    if (ls) hipLaunchKernelGGL((k_gat_fwd<L, NV, true, true, true>), dim3(blocks), dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL((k_gat_fwd<L, NV, true, false, true>), dim3(blocks), dim3(kBlock), 0, s, a);
+  if (a.drop == 2) {  // dropout instances for 32-bit offsets only (checked by the C entry)
+    if (ls) hipLaunchKernelGGL((k_gat_fwd<L, NV, true, true, 2>), dim3(blocks), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((k_gat_fwd<L, NV, true, false, 2>), dim3(blocks), dim3(kBlock), 0, s, a);
+  } else if (a.drop) {
+    if (ls) hipLaunchKernelGGL((k_gat_fwd<L, NV, true, true, 1>), dim3(blocks), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((k_gat_fwd<L, NV, true, false, 1>), dim3(blocks), dim3(kBlock), 0, s, a);
   } else if (a.o32) {
     if (ls) DGLMI_GAT_FWD(true, true); else DGLMI_GAT_FWD(true, false);
   } else {
@@ -895,8 +933,10 @@ void bwd_src_cfg(const GatArgs& a, hipStream_t s) {
   constexpr int G = kBlock / L;
   const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
   const unsigned blocks = static_cast<unsigned>((chunks + G - 1) / G);
-  if (a.drop)  // dropout instances for 32-bit offsets only (checked by the C entry)
-    hipLaunchKernelGGL((k_gat_bwd_src<L, NV, true, true>), dim3(blocks), dim3(kBlock), 0, s, a);
+  if (a.drop == 2)  // dropout instances for 32-bit offsets only (checked by the C entry)
+    hipLaunchKernelGGL((k_gat_bwd_src<L, NV, true, 2>), dim3(blocks), dim3(kBlock), 0, s, a);
+  else if (a.drop)
+    hipLaunchKernelGGL((k_gat_bwd_src<L, NV, true, 1>), dim3(blocks), dim3(kBlock), 0, s, a);
   else if (a.o32)
     hipLaunchKernelGGL((k_gat_bwd_src<L, NV, true>), dim3(blocks), dim3(kBlock), 0, s, a);
   else
@@ -957,6 +997,23 @@ void launch_gat_fold_lse(const float* m, float* l, int64_t n, hipStream_t s) {
   const int64_t want = (n + kBlock - 1) / kBlock;
   const unsigned blocks = static_cast<unsigned>(want < 65536 ? want : 65536);
   hipLaunchKernelGGL(k_gat_fold_lse, dim3(blocks), dim3(kBlock), 0, s, m, l, n);
+}
+// One keep word per edge from a dropout output (E, H) in edge-id order: the lanes of a
+// wave read 64 consecutive rows, every byte of the span used over the H loads.
+__global__ void k_gat_keep_bits(const float* __restrict__ table, int64_t n, int H,
+                                uint32_t* __restrict__ bits) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < n; e += stride) {
+    uint32_t w = 0;
+    for (int h = 0; h < H; ++h) w |= (table[e * H + h] != 0.0f ? 1u : 0u) << h;
+    bits[e] = w;
+  }
+}
+void launch_gat_keep_bits(const float* table, int64_t n, int H, uint32_t* bits, hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t want = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_gat_keep_bits, dim3(static_cast<unsigned>(want < 65536 ? want : 65536)),
+                     dim3(kBlock), 0, s, table, n, H, bits);
 }
 void launch_gat_backward_dst(const GatArgs& a, hipStream_t s) { DGLMI_GAT_DISPATCH(bwd_dst_cfg, a, s); }
 void launch_gat_backward_src(const GatArgs& a, hipStream_t s) { DGLMI_GAT_DISPATCH(bwd_src_cfg, a, s); }

@@ -197,6 +197,19 @@ _SIGS = {
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.c_void_p]),
+    "DGLMIFusedGatKeepForward": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_float, ctypes.POINTER(Array), ctypes.c_float, ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_void_p]),
+    "DGLMIFusedGatKeepBackward": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_float, ctypes.POINTER(Array), ctypes.c_float, ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_void_p]),
+    "DGLMIGatKeepBits": (ctypes.c_int, [
+        ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     "DGLMIFusedGatKernel": (ctypes.c_int, [
         ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.c_float,
@@ -222,8 +235,8 @@ _SIGS = {
     "DGLMIProjectSupported": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64]),
     "DGLMIProject": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
-        ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
-        ctypes.c_void_p]),
+        ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_int, ctypes.c_void_p]),
     "DGLMIGatherRows": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64,
         ctypes.c_void_p, ctypes.c_void_p]),

@@ -344,9 +344,7 @@ class _Project(th.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
         x2 = x.reshape(-1, x.shape[-1])
-        if K.project_mfma_ok(x2, w) and (b is None or (
-                b.dim() == 1 and b.dtype == th.float32 and b.shape[0] == w.shape[1]
-                and b.device == x2.device)):
+        if K.project_mfma_ok(x2, w) and (b is None or K.project_bias_ok(b, w.shape[1], x2.device)):
             # tall-skinny: the MFMA kernel with W in registers (kernels_project.hip)
             return K.project_mfma(x2, w, b).view(x.shape[:-1] + (w.shape[1],))
         if b is None:
@@ -481,10 +479,13 @@ class FusedGat(th.autograd.Function):
     DGLMI_GAT_SLOPES=0 keeps the round-3 backward (destination walk / edge positions).
     ``attn_drop`` > 0: GATConv's attention dropout (gatconv.py:154) inside the same
     kernels, the mask a hash of ``seed`` and the edge id, recomputed by the backward
-    (DGLMIFusedGatDropout*; always with the slope aggregates)."""
+    (DGLMIFusedGatDropout*; always with the slope aggregates).  ``keep`` (E,) int32 keep
+    words with ``keep_scale`` instead: the caller's mask (DGLMIFusedGatKeep*; GATConv's
+    own nn.Dropout draws)."""
 
     @staticmethod
-    def forward(ctx, gidx, feat_src, el, er, slope, attn_drop=0.0, seed=0):
+    def forward(ctx, gidx, feat_src, el, er, slope, attn_drop=0.0, seed=0, keep=None,
+                keep_scale=None):
         feat_src, el, er = feat_src.contiguous(), el.contiguous(), er.contiguous()
         n_dst = er.shape[0]
         H, D = feat_src.shape[1], feat_src.shape[2]
@@ -493,13 +494,15 @@ class FusedGat(th.autograd.Function):
         sm = feat_src.new_empty((n_dst, H))
         lf = ls = None
         if any(ctx.needs_input_grad[1:4]) and (
-                attn_drop > 0.0 or os.environ.get("DGLMI_GAT_SLOPES", "1") != "0"):
+                attn_drop > 0.0 or keep is not None
+                or os.environ.get("DGLMI_GAT_SLOPES", "1") != "0"):
             lf = feat_src.new_empty((n_dst, H, D))
             ls = feat_src.new_empty((n_dst, H))
         K.fused_gat_forward(gidx, feat_src, el, er, slope, out, mx, sm, lf, ls,
-                            attn_drop=attn_drop, seed=seed)
+                            attn_drop=attn_drop, seed=seed, keep=keep, keep_scale=keep_scale)
         ctx.gidx, ctx.slope = gidx, slope
         ctx.attn_drop, ctx.seed = attn_drop, seed
+        ctx.keep, ctx.keep_scale = keep, keep_scale
         ctx.slopes = lf is not None
         if lf is not None:
             ctx.save_for_backward(feat_src, el, er, out, mx, sm, lf, ls)
@@ -517,19 +520,31 @@ class FusedGat(th.autograd.Function):
         g_el = th.empty_like(el)
         g_er = th.empty_like(er)
         K.fused_gat_backward(ctx.gidx, feat_src, el, er, ctx.slope, out, mx, sm, grad_out, g_ft,
-                             g_el, g_er, lf, ls, attn_drop=ctx.attn_drop, seed=ctx.seed)
-        return None, g_ft, g_el, g_er, None, None, None
+                             g_el, g_er, lf, ls, attn_drop=ctx.attn_drop, seed=ctx.seed,
+                             keep=ctx.keep, keep_scale=ctx.keep_scale)
+        return None, g_ft, g_el, g_er, None, None, None, None, None
 
 
-def fused_gat(graph, feat_src, el, er, slope, attn_drop=0.0, seed=None):
+def fused_gat(graph, feat_src, el, er, slope, attn_drop=0.0, seed=None, keep=None,
+              keep_scale=None):
     """backend.py:1235 / tensor.py:415-420: softmax attention + aggregation in one kernel.
 
     ``graph`` is a DGLGraph (or an ImmutableGraphIndex); feat_src (N, H, D), el / er
-    (N, H, 1).  Returns (N, H, D).  ``attn_drop``: dropout on the attention weights
-    (GATConv in training); ``seed`` (default: drawn from torch's default generator, so
-    ``torch.manual_seed`` reproduces the mask) keys the mask."""
+    (N, H, 1).  Returns (N, H, D).  Attention dropout, two forms:
+
+    * ``keep`` (E,) int32 keep words in edge-id order (:func:`dgl.kernel.gat_keep_bits` of
+      a dropout output (E, H, 1)) with ``keep_scale`` (the dropout's 1 / (1 - p)): the
+      caller's mask -- GATConv passes its own ``nn.Dropout``'s draws, the reference's;
+    * ``attn_drop`` > 0: a hashed mask keyed by ``seed`` (default: drawn from torch's
+      default generator, so ``torch.manual_seed`` reproduces it) -- no (E, H) buffer, not
+      torch's draws."""
     gidx = graph if hasattr(graph, "in_csr") else graph._graph.get_immutable_gidx(feat_src.device)
     attn_drop = float(attn_drop)
+    if keep is not None:
+        if keep_scale is None:
+            raise DGLError("fused_gat: keep needs keep_scale")
+        return FusedGat.apply(gidx, feat_src, el, er, float(slope), 0.0, 0, keep,
+                              float(keep_scale))
     if attn_drop > 0.0 and seed is None:
         seed = int(th.randint(0, 2 ** 62, (1,)).item())
     return FusedGat.apply(gidx, feat_src, el, er, float(slope), attn_drop, int(seed or 0))

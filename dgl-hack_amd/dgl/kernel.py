@@ -43,6 +43,19 @@ def _arr(t, name):
     return ctypes.byref(a)
 
 
+def _arr_words(t, name):
+    """An int32 (uint32 bit-word) device array for the entries that take one."""
+    if not isinstance(t, th.Tensor) or t.device.type != "cuda" or t.dtype != th.int32 \
+            or not t.is_contiguous() or t.dim() != 1:
+        raise DGLError("%s must be a contiguous 1-D int32 ROCm tensor" % name)
+    a = _ffi.Array()
+    a.data = t.data_ptr() if t.numel() else None
+    a.ndim = 1
+    a.shape[0] = t.shape[0]
+    a._keep = t
+    return ctypes.byref(a)
+
+
 def _map(m, name):
     if m is None:
         return None
@@ -341,19 +354,57 @@ def gat_dropout_keep(seed, eids, num_heads, p):
         off = (np.arange(pairs, dtype=np.uint32) + np.uint32(1)) * np.uint32(0x9E3779B9)
         r = finish(key[:, None] + off[None, :])                   # (E, pairs)
     u16 = np.stack([r & np.uint32(0xFFFF), r >> np.uint32(16)], 2).reshape(len(e), 2 * pairs)
-    thresh = min(65535, int(np.floor(float(np.float32(p)) * 65536.0 + 0.5)))  # the C entry's
-    return u16[:, :num_heads] >= np.uint32(thresh)
+    return u16[:, :num_heads].astype(np.int64) >= _gat_drop_thresh(p)
+
+
+def _gat_drop_thresh(p):
+    """The C entry's 16-bit threshold round(p 2^16), capped at 2^16 (keeps nothing)."""
+    return min(65536, int(np.floor(float(np.float32(p)) * 65536.0 + 0.5)))
+
+
+def gat_dropout_scale(p):
+    """The hashed mask's scale for kept weights (capi.cpp gat_set_dropout): the inverse of
+    the quantised keep probability (2^16 - t) / 2^16, so E[dropout(a)] = a exactly; 0
+    when nothing is kept."""
+    t = _gat_drop_thresh(p)
+    return float(np.float32(65536.0 / (65536.0 - t))) if t < 65536 else 0.0
+
+
+def gat_keep_bits(table):
+    """One int32 keep word per edge from a dropout output ``table`` (E, H[, 1]) in edge-id
+    order: bit h set where head h was kept (non-zero) -> DGLMIGatKeepBits (H <= 32)."""
+    t = table.reshape(table.shape[0], -1)
+    if t.dtype != th.float32 or not t.is_cuda:
+        raise DGLError("gat_keep_bits: a float32 ROCm table")
+    t = t.contiguous()
+    h = int(t.shape[1])
+    if not 1 <= h <= 32:
+        raise DGLError("gat_keep_bits: 1 <= heads <= 32")
+    bits = th.empty(t.shape[0], dtype=th.int32, device=t.device)
+    check_call(_ffi.lib().DGLMIGatKeepBits(
+        ctypes.c_void_p(t.data_ptr()), ctypes.c_int64(t.shape[0]), h,
+        ctypes.c_void_p(bits.data_ptr()), _stream(bits)))
+    return bits
 
 
 def fused_gat_forward(graph, feat_src, el, er, slope, out, max_out, sum_out, slope_feat=None,
-                      slope_sum=None, attn_drop=0.0, seed=0):
+                      slope_sum=None, attn_drop=0.0, seed=0, keep=None, keep_scale=None):
     """_CAPI_DGLFusedGatKernel (binary_reduce.cc:380-396) -> DGLMIFusedGatForward, or
     with ``slope_feat`` (N, H, D) / ``slope_sum`` (N, H) DGLMIFusedGatForwardEx: the
     forward also keeps the attention's slope aggregates, so the backward needs no
     destination-side walk.  ``attn_drop`` > 0: DGLMIFusedGatDropoutForward (GATConv's
-    attention dropout in the same pass, the mask a hash of ``seed`` and the edge id)."""
+    attention dropout in the same pass, the mask a hash of ``seed`` and the edge id).
+    ``keep`` (E,) int32 words (:func:`gat_keep_bits`) with ``keep_scale``:
+    DGLMIFusedGatKeepForward, the caller's mask."""
     _check_ctx(graph, [("feat_src", feat_src), ("el", el), ("er", er), ("out", out)])
     g = graph.cstruct(None, col_blocks=gat_col_blocks(graph, feat_src))
+    if keep is not None:
+        check_call(_ffi.lib().DGLMIFusedGatKeepForward(
+            ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"),
+            float(slope), _arr_words(keep, "keep"), float(keep_scale), _arr(out, "out"),
+            _arr(max_out, "max_out"), _arr(sum_out, "sum_out"), _arr(slope_feat, "slope_feat"),
+            _arr(slope_sum, "slope_sum"), _stream(out)))
+        return out
     if attn_drop > 0.0:
         check_call(_ffi.lib().DGLMIFusedGatDropoutForward(
             ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"),
@@ -373,11 +424,24 @@ def fused_gat_forward(graph, feat_src, el, er, slope, out, max_out, sum_out, slo
 
 def fused_gat_backward(graph, feat_src, el, er, slope, out, max_in, sum_in, grad_out,
                        grad_feat_src, grad_el, grad_er, slope_feat=None, slope_sum=None,
-                       attn_drop=0.0, seed=0):
+                       attn_drop=0.0, seed=0, keep=None, keep_scale=None):
     """_CAPI_DGLKernelBackwardFusedGat (binary_reduce.cc:529-549) -> DGLMIFusedGatBackward
     (or DGLMIFusedGatBackwardEx with the forward's slope aggregates; with ``attn_drop`` > 0
-    DGLMIFusedGatDropoutBackward, the forward's seed)."""
+    DGLMIFusedGatDropoutBackward, the forward's seed; with ``keep``
+    DGLMIFusedGatKeepBackward, the forward's mask)."""
     _check_ctx(graph, [("feat_src", feat_src), ("grad_out", grad_out)])
+    if keep is not None:
+        if slope_feat is None:
+            raise DGLError("fused GAT dropout backward needs the forward's slope aggregates")
+        g = graph.cstruct(None, col_blocks=gat_col_blocks(graph, feat_src, backward=True))
+        check_call(_ffi.lib().DGLMIFusedGatKeepBackward(
+            ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"),
+            float(slope), _arr_words(keep, "keep"), float(keep_scale), _arr(out, "out"),
+            _arr(max_in, "max_in"), _arr(sum_in, "sum_in"), _arr(slope_feat, "slope_feat"),
+            _arr(slope_sum, "slope_sum"), _arr(grad_out, "grad_out"),
+            _arr(grad_feat_src, "grad_feat_src"), _arr(grad_el, "grad_el"),
+            _arr(grad_er, "grad_er"), _stream(grad_out)))
+        return
     if attn_drop > 0.0:
         if slope_feat is None:
             raise DGLError("fused GAT dropout backward needs the forward's slope aggregates")
@@ -469,17 +533,29 @@ PROJECT_MIN_ROWS = 1 << 14
 
 def project_mfma_ok(x2, w):
     """Whether Y = x2 @ w runs on DGLMIProject: fp32 ROCm tensors on one device, x2 a
-    contiguous (M, K) matrix with M >= PROJECT_MIN_ROWS, (K, N) supported."""
+    contiguous (M, K) matrix with M >= PROJECT_MIN_ROWS whose K equals w's row count
+    (a mismatch stays on torch.matmul, which raises), (K, N) supported."""
     return (x2.is_cuda and x2.dtype == th.float32 and w.dtype == th.float32 and w.dim() == 2
             and x2.dim() == 2 and w.device == x2.device and x2.is_contiguous()
+            and x2.shape[1] == w.shape[0]
             and x2.shape[0] >= PROJECT_MIN_ROWS and x2.data_ptr() % 16 == 0
             and w.stride(0) >= 1 and w.stride(1) >= 1
             and bool(_ffi.lib().DGLMIProjectSupported(int(w.shape[0]), int(w.shape[1]))))
 
 
+def project_bias_ok(b, n, device):
+    """Whether ``b`` can ride in DGLMIProject's epilogue: an fp32 vector of the output
+    width on the device whose contiguous form is 16-byte aligned (a slice of a flat
+    parameter buffer may not be; it then takes torch.addmm)."""
+    if not (b.dim() == 1 and b.dtype == th.float32 and b.shape[0] == n and b.device == device):
+        return False
+    return b.contiguous().data_ptr() % 16 == 0
+
+
 def project_mfma(x2, w, bias=None):
     """x2 @ w (+ bias) on the MFMA projection kernel -> DGLMIProject (w may be a
-    transposed view; its strides are passed)."""
+    transposed view; its strides are passed; its row count is checked against x2's
+    columns in C)."""
     m, k = x2.shape
     n = int(w.shape[1])
     y = x2.new_empty((m, n))
@@ -487,8 +563,9 @@ def project_mfma(x2, w, bias=None):
         bias = bias.contiguous()
     check_call(_ffi.lib().DGLMIProject(
         ctypes.c_void_p(x2.data_ptr()), ctypes.c_int64(m), ctypes.c_int64(k),
-        ctypes.c_void_p(w.data_ptr()), ctypes.c_int64(w.stride(0)), ctypes.c_int64(w.stride(1)),
-        ctypes.c_int64(n), ctypes.c_void_p(bias.data_ptr() if bias is not None else None),
+        ctypes.c_void_p(w.data_ptr()), ctypes.c_int64(w.shape[0]), ctypes.c_int64(w.stride(0)),
+        ctypes.c_int64(w.stride(1)), ctypes.c_int64(n),
+        ctypes.c_void_p(bias.data_ptr() if bias is not None else None),
         ctypes.c_void_p(y.data_ptr()), int(x2.device.index or 0), _stream(y)))
     return y
 

@@ -6,14 +6,18 @@ max-stabilised ``edge_softmax`` and ``u_mul_e_sum`` with the attention
 broadcast over the head dimension (the load-balanced HIP kernel).  When the
 head size suits the fused kernel, the middle of that chain (u_add_v ..
 u_mul_e_sum) runs as ONE fused HIP kernel (``dgl.backend.fused_gat``; same math,
-max-stabilised in both forms), attention dropout in training included (its mask
-drawn inside the kernel from a per-call seed: the same Bernoulli(1 - p) per edge
-and head, scaled by 1 / (1 - p), as ``nn.Dropout`` on the softmax output, not the
-same draws) -- set ``use_fused = False`` on the module to force the unfused
-composition.
+max-stabilised in both forms), attention dropout in training included: by default
+the module's own ``nn.Dropout`` draws the mask on an (E, H, 1) tensor of ones in
+edge-id order -- the draws the reference's ``self.attn_drop(edge_softmax(...))``
+(gatconv.py:154) makes under the same seed -- packed to one keep word per edge that
+the fused kernels read (``attn_drop_mask = "module"``); ``attn_drop_mask =
+"hashed"`` opts into a mask hashed inside the kernels from a per-call seed (the same
+Bernoulli(1 - p) per edge and head, not torch's draws; no (E, H) tensors).  Set
+``use_fused = False`` on the module to force the unfused composition.
 The reference's unconditional ``th.cuda.synchronize()`` + timing prints
 (:146-170) are not reproduced.
 """
+import numpy as np
 import torch as th
 from torch import nn
 
@@ -69,10 +73,18 @@ class GATConv(nn.Module):
         self.activation = activation
         self.negative_slope = negative_slope
         self.use_fused = True
+        # "module": attention dropout with this module's nn.Dropout draws (the
+        # reference's); "hashed": the fused kernels' own hashed mask (faster, other draws)
+        self.attn_drop_mask = "module"
+
+    # FusedGATConv builds attn_drop but never applies it (fusedGatConv.py:80,152)
+    _applies_attn_drop = True
+
+    def _attn_drop_active(self):
+        return self._applies_attn_drop and self.training and self.attn_drop.p > 0
 
     def _fused_ok(self):
-        # attention dropout in training runs inside the fused kernels (the mask a hash
-        # of a per-call seed and the edge id; dgl.backend.fused_gat)
+        # attention dropout in training runs inside the fused kernels (dgl.backend.fused_gat)
         if not self.use_fused:
             return False
         return self._fused_dim() is not None
@@ -93,7 +105,20 @@ class GATConv(nn.Module):
                 return False
         elif getattr(graph._graph, "device_bits", lambda: 32)() != 32:
             return False
-        if self.training and self.attn_drop.p > 0:
+        if self._attn_drop_active():
+            if self.attn_drop.p >= 1.0:
+                return False  # nn.Dropout(1) zeroes every weight: the composition
+            if self.attn_drop_mask == "module":
+                # the module's draws: a plain nn.Dropout (scale 1 / (1 - p)) over the
+                # graph's own edge ids (keep words indexed by edge id)
+                if type(self.attn_drop) is not nn.Dropout or self.attn_drop.inplace:
+                    return False
+                gidx = graph if hasattr(graph, "in_csr") else \
+                    graph._graph.get_immutable_gidx(self.attn_l.device)
+                if not gidx.eid_perm:
+                    return False
+            elif self.attn_drop_mask != "hashed":
+                raise ValueError("attn_drop_mask must be 'module' or 'hashed'")
             # the dropout walks stage <= 32 keep bits per edge (capi.cpp gat_set_dropout)
             return (self._num_heads <= 32
                     and n_rows * self._num_heads * self._fused_dim() < (1 << 31))
@@ -111,7 +136,7 @@ class GATConv(nn.Module):
         edge-id composition."""
         if not POSITION_SPACE or not feat_src.is_cuda:
             return False
-        if self.training and self.attn_drop.p > 0 and \
+        if self._attn_drop_active() and \
                 (type(self.attn_drop) is not nn.Dropout or self.attn_drop.inplace):
             return False
         if not hasattr(getattr(graph, "_graph", None), "get_immutable_gidx"):
@@ -134,7 +159,7 @@ class GATConv(nn.Module):
         else:
             e = B.binary_reduce("none", "add", view, B.SRC, B.DST, el, er, m)
             a = _edge_softmax_on(view, self.leaky_relu(e), n_dst)
-        if self.training and self.attn_drop.p > 0:
+        if self._attn_drop_active():
             # nn.Dropout's draws in edge-id order, as dropout(a) in the edge-id
             # composition: (1 * keep) * scale per edge, gathered into walk order; a times
             # it is dropout's (a * keep) * scale bit for bit, and so is the gradient
@@ -151,11 +176,26 @@ class GATConv(nn.Module):
 
     def _fused(self, graph, feat_src, el, er):
         d = self._fused_dim()
-        p = self.attn_drop.p if self.training else 0.0
+        kw = {}
+        if self._attn_drop_active():
+            p = float(self.attn_drop.p)
+            if self.attn_drop_mask == "hashed":
+                kw = {"attn_drop": p}
+            else:
+                # this module's nn.Dropout on (E, H, 1) ones in edge-id order: the RNG
+                # draws of the reference's attn_drop(a) (same shape, same layout), packed
+                # to one keep word per edge; kept weights take torch's scale
+                # float(1 / float(1 - p)) (its fused dropout kernel's)
+                gidx = graph if hasattr(graph, "in_csr") else \
+                    graph._graph.get_immutable_gidx(feat_src.device)
+                ones = feat_src.new_ones((gidx.in_csr.nnz, self._num_heads, 1))
+                kw = {"keep": K.gat_keep_bits(self.attn_drop(ones)),
+                      "keep_scale": float(np.float32(1.0 / float(np.float32(1.0 - p))))}
+                del ones
         if d == self._out_feats:
-            return B.fused_gat(graph, feat_src, el, er, self.negative_slope, attn_drop=p)
+            return B.fused_gat(graph, feat_src, el, er, self.negative_slope, **kw)
         ft = th.nn.functional.pad(feat_src, (0, d - self._out_feats))
-        return B.fused_gat(graph, ft, el, er, self.negative_slope, attn_drop=p)[..., :self._out_feats]
+        return B.fused_gat(graph, ft, el, er, self.negative_slope, **kw)[..., :self._out_feats]
 
     def reset_parameters(self):
         gain = nn.init.calculate_gain("relu")
@@ -197,7 +237,7 @@ class GATConv(nn.Module):
                                            self.leaky_relu.negative_slope)
             else:
                 a = edge_softmax(graph, self.leaky_relu(e))
-            graph.edata["a"] = self.attn_drop(a)
+            graph.edata["a"] = self.attn_drop(a) if self._applies_attn_drop else a
             graph.update_all(fn.u_mul_e("ft", "a", "m"), fn.sum("m", "ft"))
             rst = graph.dstdata["ft"]
         if self.res_fc is not None:

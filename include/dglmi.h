@@ -321,10 +321,12 @@ int DGLMIFusedGatBackwardEx(const DGLMIGraph* graph, const DGLMIArray* feat_src,
 
 /* Fused GAT with attention dropout (GATConv's attn_drop in training, gatconv.py:154:
  * dropout on the softmax weights, per edge and head).  Edge e, head h keeps its weight,
- * scaled by 1 / (1 - attn_drop), when a counter hash of (seed, e) -- one key per edge,
- * one more mix per pair of heads, 16 bits per head -- clears the threshold
- * round(attn_drop * 2^16) -- a mask no buffer holds: the backward recomputes it from the
- * same seed and the walks' edge ids.  The softmax denominator (sum_out) is the plain
+ * when a counter hash of (seed, e) -- one key per edge, one more mix per pair of heads,
+ * 16 bits per head -- clears the threshold t = round(attn_drop * 2^16) -- a mask no buffer
+ * holds: the backward recomputes it from the same seed and the walks' edge ids.  Kept
+ * weights are scaled by 2^16 / (2^16 - t), the inverse of the quantised keep probability
+ * (within 2^-17 of 1 / (1 - attn_drop)); attn_drop in [0, 1], and t = 2^16 (attn_drop >=
+ * 1 - 2^-17) drops every weight.  The softmax denominator (sum_out) is the plain
  * one; out and slope_feat carry the kept, rescaled weights.  The backward needs the
  * forward's slope aggregates.  attn_drop = 0 equals DGLMIFusedGatForwardEx /
  * BackwardEx bit for bit.  Extension: the reference has no fused dropout (its
@@ -342,6 +344,30 @@ int DGLMIFusedGatDropoutBackward(const DGLMIGraph* graph, const DGLMIArray* feat
                                  const DGLMIArray* slope_feat, const DGLMIArray* slope_sum,
                                  const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
                                  DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream);
+/* Fused GAT with the CALLER's attention-dropout mask: keep (E,) holds one uint32 word per
+ * edge id, bit h set when head h keeps its weight (H <= 32), and kept weights are scaled
+ * by keep_scale.  GATConv draws the mask with its own nn.Dropout on an (E, H, 1) tensor
+ * of ones in edge-id order -- the draws the reference's dropout(edge_softmax(...)) makes
+ * under the same seed (gatconv.py:154) -- packs it with DGLMIGatKeepBits and passes
+ * keep_scale = the dropout's 1 / (1 - p).  The kernels read each edge's word through the
+ * walks' edge ids (column blocks included); otherwise as DGLMIFusedGatDropout*.
+ * Extension. */
+int DGLMIFusedGatKeepForward(const DGLMIGraph* graph, const DGLMIArray* feat_src,
+                             const DGLMIArray* el, const DGLMIArray* er, float negative_slope,
+                             const DGLMIArray* keep, float keep_scale, DGLMIArray* out,
+                             DGLMIArray* max_out, DGLMIArray* sum_out, DGLMIArray* slope_feat,
+                             DGLMIArray* slope_sum, void* stream);
+int DGLMIFusedGatKeepBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src,
+                              const DGLMIArray* el, const DGLMIArray* er, float negative_slope,
+                              const DGLMIArray* keep, float keep_scale, const DGLMIArray* out,
+                              const DGLMIArray* max_in, const DGLMIArray* sum_in,
+                              const DGLMIArray* slope_feat, const DGLMIArray* slope_sum,
+                              const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
+                              DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream);
+/* bits[e] = OR over h < heads of (table[e * heads + h] != 0) << h for e < num_edges
+ * (1 <= heads <= 32): a dropout output (E, H) packed to the keep words above.  Device
+ * pointers.  Extension. */
+int DGLMIGatKeepBits(const float* table, int64_t num_edges, int heads, uint32_t* bits, void* stream);
 /* The same two kernels in the reference's argument order, for a binding of the hack's
  * PackedFuncs that keeps its Python caller unchanged (tensor.py:383-420):
  *   _CAPI_DGLFusedGatKernel(G, feat_src, el, er, sum, exp, ret, slope)
@@ -404,14 +430,16 @@ int DGLMIEdgeSoftmaxNodeLogitsBackward(const DGLMIGraph* graph, const DGLMIArray
                                        const DGLMIArray* er, float negative_slope,
                                        DGLMIArray* grad_logits, void* stream);
 /* The bracketing projection Y = X W (+ bias) of GraphConv / GATConv / RelGraphConv
- * (torch.matmul in the reference, graphconv.py:146-170) on MFMA, for tall-skinny shapes:
- * x (m, k) row-major, w (k, n) element (i, j) at w[i * w_stride_k + j * w_stride_n] (a
- * transposed nn.Linear weight is strides (1, k)), bias (n) or NULL, y (m, n) row-major;
- * device pointers on `device`, x / y / bias 16-byte aligned.  DGLMIProjectSupported(k, n):
- * k in {16, 32, 64, 128}, n 64 or 128 (extension). */
+ * (torch.matmul in the reference, graphconv.py:146-170, gatconv.py:127-132) on MFMA, for
+ * tall-skinny shapes: x (m, k) row-major, w (w_rows, n) element (i, j) at w[i *
+ * w_stride_k + j * w_stride_n] (a transposed nn.Linear weight is strides (1, k)), bias
+ * (n) or NULL, y (m, n) row-major; device pointers on `device`, x / y / bias 16-byte
+ * aligned.  w_rows must equal k (a mismatch is an error, as torch.matmul's).
+ * DGLMIProjectSupported(k, n): 1 <= k <= 640, 1 <= n <= 2^20 (extension). */
 int DGLMIProjectSupported(int64_t k, int64_t n);
-int DGLMIProject(const float* x, int64_t m, int64_t k, const float* w, int64_t w_stride_k,
-                 int64_t w_stride_n, int64_t n, const float* bias, float* y, int device, void* stream);
+int DGLMIProject(const float* x, int64_t m, int64_t k, const float* w, int64_t w_rows,
+                 int64_t w_stride_k, int64_t w_stride_n, int64_t n, const float* bias, float* y,
+                 int device, void* stream);
 /* out[i, :] = src[index[i], :] for i < n, rows of row_floats floats; index int32
  * (index_bits 32) or int64 (64), device pointers.  A per-edge operand put into a walk's
  * position order (the position views' operands, GATConv's dropout scale in position

@@ -24,6 +24,8 @@ def main():
             raise RuntimeError("injected failure")
         if mode == "raise0" and rank == 0:
             raise RuntimeError("injected failure on rank 0")
+        if mode == "raiselast" and rank == dist.get_world_size() - 1:
+            raise RuntimeError("injected failure on the last rank")
         if mode == "stall" and rank == 1:
             time.sleep(600)
         t = th.ones(1)

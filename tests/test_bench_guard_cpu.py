@@ -19,10 +19,10 @@ def _free_port():
     return port
 
 
-def _run(mode, budget=300):
+def _run(mode, budget=300, nproc=2):
     env = dict(os.environ, BUDGET=str(budget), OMP_NUM_THREADS="1")
     env.pop("RANK", None)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % nproc,
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(HERE, "guard_worker.py"), mode]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
@@ -30,9 +30,13 @@ def _run(mode, budget=300):
     return p.returncode, lines, p.stderr
 
 
-@pytest.mark.parametrize("mode", ["ok", "raise", "raise0"])
-def test_side_line_failure_keeps_headline(mode):
-    code, lines, err = _run(mode)
+@pytest.mark.parametrize("mode,nproc", [("ok", 2), ("raise", 2), ("raise0", 2), ("ok", 8),
+                                         ("raise", 8), ("raiselast", 8), ("raise0", 8)])
+def test_side_line_failure_keeps_headline(mode, nproc):
+    """World 2 and the driver's 8 ranks: a raise on rank 1, on the last rank or on rank 0
+    (the watchdog's own rank) leaves one line with the error while the peers wait in an
+    all-reduce."""
+    code, lines, err = _run(mode, nproc=nproc)
     # a failed side line keeps the line but not a zero exit status (torchrun
     # reports the ranks' SIDE_LINE_RC as its own failure)
     assert (code == 0) == (mode == "ok"), err[-2000:]
@@ -40,15 +44,16 @@ def test_side_line_failure_keeps_headline(mode):
     res = json.loads(lines[0])
     assert res["value"] == 1.0
     if mode == "ok":
-        assert res["c4"] == {"value": 2.0}
+        assert res["c4"] == {"value": float(nproc)}
         assert "side_line_errors" not in res
     else:
         assert "injected failure" in res["c4"]["error"]
         assert res["side_line_errors"][0]["line"] == "c4"
 
 
-def test_side_line_stall_hits_budget():
-    code, lines, err = _run("stall", budget=3)
+@pytest.mark.parametrize("nproc", [2, 8])
+def test_side_line_stall_hits_budget(nproc):
+    code, lines, err = _run("stall", budget=3, nproc=nproc)
     assert code != 0
     assert len(lines) == 1, err[-2000:]
     assert "exceeded" in json.loads(lines[0])["c4"]["error"]

@@ -23,16 +23,22 @@ def _run(*argv, env_extra=None, timeout=200):
     return p.returncode, lines, p.stderr
 
 
-def test_launches_n_ranks():
-    code, lines, err = _run("--gpus", "3", "--launcher-stub", "ok")
+import pytest
+
+
+@pytest.mark.parametrize("n", [3, 8])
+def test_launches_n_ranks(n):
+    """N stub ranks (8: the driver's node), one JSON line, LOCAL_RANK = rank, N processes,
+    the side line's all-reduce over all of them."""
+    code, lines, err = _run("--gpus", str(n), "--launcher-stub", "ok")
     assert code == 0, err[-3000:]
     assert len(lines) == 1, (lines, err[-3000:])
     res = json.loads(lines[0])
-    assert res["n_gpus"] == 3
-    assert sorted(r[0] for r in res["ranks"]) == [0, 1, 2]
-    assert [r[1] for r in sorted(res["ranks"])] == [0, 1, 2]  # LOCAL_RANK = rank
-    assert len({r[2] for r in res["ranks"]}) == 3  # three processes
-    assert res["c4"] == {"value": 3.0}
+    assert res["n_gpus"] == n
+    assert sorted(r[0] for r in res["ranks"]) == list(range(n))
+    assert [r[1] for r in sorted(res["ranks"])] == list(range(n))  # LOCAL_RANK = rank
+    assert len({r[2] for r in res["ranks"]}) == n  # n processes
+    assert res["c4"] == {"value": float(n)}
     assert "side_line_errors" not in res
 
 
@@ -66,14 +72,28 @@ def test_rank_crash_propagates_status():
     assert "rank 1 exited with status 7" in err
 
 
-def test_side_line_failure_sets_status_and_list():
-    code, lines, err = _run("--gpus", "2", "--launcher-stub", "side1")
+@pytest.mark.parametrize("n,bad", [(2, 1), (8, 7), (8, 0)])
+def test_side_line_failure_sets_status_and_list(n, bad):
+    """A side line raising on one rank (the last of 8, or rank 0 itself): the headline
+    line still prints once, with the error under the line and in side_line_errors, and
+    the job exits SIDE_LINE_RC."""
+    code, lines, err = _run("--gpus", str(n), "--launcher-stub", "side%d" % bad)
     assert code == 3, err[-3000:]  # bench.SIDE_LINE_RC
     assert len(lines) == 1, (lines, err[-3000:])
     res = json.loads(lines[0])
-    assert res["value"] == 1.0 and res["n_gpus"] == 2
+    assert res["value"] == 1.0 and res["n_gpus"] == n
     assert "injected side-line failure" in res["c4"]["error"]
     assert [e["line"] for e in res["side_line_errors"]] == ["c4"]
+
+
+def test_rank_crash_of_eight_propagates_status():
+    """Rank 5 of 8 exits 7 before joining: the launcher kills the other seven after its
+    grace period and reports rank 5's status."""
+    code, lines, err = _run("--gpus", "8", "--launch-grace", "3", "--launcher-stub", "crash5",
+                            timeout=240)
+    assert code == 7, err[-3000:]
+    assert not lines
+    assert "rank 5 exited with status 7" in err
 
 
 def _bench():

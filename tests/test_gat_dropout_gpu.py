@@ -1,10 +1,16 @@
-"""Attention dropout inside the fused GAT kernels (DGLMIFusedGatDropout*): GATConv in
-training applies ``nn.Dropout`` to the edge softmax (the reference's
-``gatconv.py:154``); here the kernels draw the same Bernoulli(1 - p) mask per edge and
-head from a hash of a seed and the edge id and scale kept weights by 1 / (1 - p).  The
-tests rebuild that mask on the host (``dgl.kernel.gat_dropout_keep``) and check the
-output and every gradient against a dense fp64 restatement that applies it to the
-softmax -- unblocked and column-blocked -- plus the module routing."""
+"""Attention dropout inside the fused GAT kernels.  GATConv in training applies
+``nn.Dropout`` to the edge softmax (the reference's ``gatconv.py:154``).  Two fused forms:
+
+* the module's own draws (default, DGLMIFusedGatKeep*): GATConv's nn.Dropout on (E, H, 1)
+  ones in edge-id order, packed to one keep word per edge -- the fused module must agree
+  with the unfused composition (the reference's shape) under one seed;
+* the hashed mask (opt-in, DGLMIFusedGatDropout*): the same Bernoulli(1 - p) per edge and
+  head from a hash of a seed and the edge id, rebuilt on the host
+  (``dgl.kernel.gat_dropout_keep``) for a dense fp64 restatement that applies it to the
+  softmax -- unblocked and column-blocked.
+
+Plus the module routing, FusedGATConv's reference behaviour (attn_drop built, never
+applied: fusedGatConv.py:80,152) and p = 1."""
 import numpy as np
 import pytest
 import torch as th
@@ -26,7 +32,7 @@ def dense_gat_dropout(src, dst, n, ft, el, er, slope, keep, p):
     emax = th.full((n, H), -1e300, dtype=th.float64, device=DEV).index_reduce(0, d, e.detach(), "amax")
     ex = th.exp(e - emax[d])
     den = th.zeros(n, H, dtype=th.float64, device=DEV).index_add(0, d, ex)
-    a = ex / den[d] * (th.from_numpy(keep).to(DEV).double() / (1.0 - p))
+    a = ex / den[d] * (th.from_numpy(keep).to(DEV).double() * K.gat_dropout_scale(p))
     return th.zeros(n, H, ft.shape[2], dtype=th.float64, device=DEV).index_add(0, d, ft[s] * a[:, :, None])
 
 
@@ -64,13 +70,15 @@ def test_fused_gat_dropout_vs_dense(nb, p, H, D, monkeypatch):
 
 
 def test_gatconv_training_dropout_runs_fused(monkeypatch):
-    """GATConv(attn_drop=0.6) in training takes the fused kernels (no per-edge
-    attention tensor), reproducibly under torch.manual_seed; eval mode has no dropout."""
+    """GATConv(attn_drop=0.6) with the hashed mask in training takes the fused kernels (no
+    per-edge attention tensor), reproducibly under torch.manual_seed; eval mode has no
+    dropout."""
     src, dst, n = powerlaw(5000, 60000, seed=3)
     g = dgl.DGLGraph()
     g.add_nodes(n)
     g.add_edges(src, dst)
     conv = GATConv(32, 8, 4, attn_drop=0.6).to(DEV)
+    conv.attn_drop_mask = "hashed"
     x = th.randn(n, 32, device=DEV)
     calls = []
     orig = B.fused_gat
@@ -112,3 +120,113 @@ def test_dropout_over_32_heads_takes_the_composition():
     assert not conv._fused_route(g, n)
     y = conv(g, th.randn(n, 16, device=DEV))
     assert y.shape == (n, 64, 4) and th.isfinite(y).all()
+
+
+def _graph(n_nodes, n_edges, seed):
+    src, dst, n = powerlaw(n_nodes, n_edges, seed=seed)
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    return g, n
+
+
+@pytest.mark.parametrize("nb,p,H,D", [(1, 0.5, 8, 8), (4, 0.5, 8, 8), (1, 0.3, 3, 16),
+                                      (1, 0.6, 32, 4), (2, 0.5, 4, 8)])
+def test_gatconv_module_dropout_matches_composition(nb, p, H, D, monkeypatch):
+    """The default fused route draws the mask with the module's nn.Dropout: under one
+    torch.manual_seed the fused GATConv and the unfused composition (the reference's
+    dropout(edge_softmax(...)), which draws on the (E, H, 1) attention) agree within fp32
+    tolerance in the output, the input gradient and every parameter gradient -- unblocked
+    and with column blocks (the kernels read the keep words through each block's edge
+    ids); the route really is the fused one with the module's keep words."""
+    monkeypatch.setenv("DGLMI_GAT_BLOCKS", str(nb))
+    g, n = _graph(20000, 300000, 21 + nb)
+    conv = GATConv(24, D, H, attn_drop=p).to(DEV).train()
+    x0 = th.randn(n, 24, device=DEV, generator=th.Generator(device=DEV).manual_seed(2))
+    go = th.randn(n, H, D, device=DEV, generator=th.Generator(device=DEV).manual_seed(3))
+    calls = []
+    orig = B.fused_gat
+
+    def spy(*a, **k):
+        calls.append(sorted(k))
+        return orig(*a, **k)
+    monkeypatch.setattr(B, "fused_gat", spy)
+    res = []
+    for fused in (True, False):
+        conv.use_fused = fused
+        conv.zero_grad()
+        x = x0.clone().requires_grad_()
+        th.manual_seed(11)
+        y = conv(g, x)
+        y.backward(go)
+        res.append((y.detach(), x.grad, conv.fc.weight.grad.clone(), conv.attn_l.grad.clone(),
+                    conv.attn_r.grad.clone()))
+    assert calls == [["keep", "keep_scale"]]
+    (yf, *gf), (yc, *gc) = res
+    assert (yc == 0).any()  # dropout happened
+    assert th.allclose(yf, yc, rtol=1e-4, atol=1e-5), float((yf - yc).abs().max())
+    for a, b, name in zip(gf, gc, ("x", "fc", "attn_l", "attn_r")):
+        tol = 1e-4 * float(b.abs().max()) + 1e-6
+        assert float((a - b).abs().max()) <= tol, (name, float((a - b).abs().max()), tol)
+    # a different seed draws a different mask
+    conv.use_fused = True
+    th.manual_seed(12)
+    assert not th.equal(conv(g, x0), yf)
+
+
+def test_keep_bits_pack():
+    """DGLMIGatKeepBits: one word per edge, bit h = (table[e, h] != 0)."""
+    gen = th.Generator(device=DEV).manual_seed(4)
+    for h in (1, 3, 8, 32):
+        t = (th.rand(1001, h, 1, device=DEV, generator=gen) < 0.5).float() * 2.0
+        bits = K.gat_keep_bits(t).cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+        m = (t.reshape(1001, h).cpu().numpy() != 0).astype(np.int64)
+        want = (m << np.arange(h, dtype=np.int64)[None, :]).sum(1)
+        assert np.array_equal(bits, want)
+
+
+def test_fused_gatconv_ignores_attn_drop(monkeypatch):
+    """The reference's FusedGATConv builds attn_drop but calls fused_gat without it
+    (fusedGatConv.py:80,152): training output == eval output and equals a
+    GATConv without dropout holding the same parameters (eval: bit for bit; training keeps
+    the slope aggregates for the backward, the same sums to fp32 rounding)."""
+    from dgl.nn.pytorch.conv import FusedGATConv
+    g, n = _graph(5000, 60000, 5)
+    conv = FusedGATConv(16, 8, 4, attn_drop=0.6).to(DEV)
+    plain = GATConv(16, 8, 4).to(DEV)
+    plain.load_state_dict(conv.state_dict())
+    x = th.randn(n, 16, device=DEV)
+    conv.train()
+    th.manual_seed(1)
+    yt = conv(g, x)
+    conv.eval()
+    with th.no_grad():
+        ye = conv(g, x)
+        yp = plain.eval()(g, x)
+    assert th.allclose(yt.detach(), ye, rtol=1e-6, atol=1e-7) and th.equal(ye, yp)
+    # the unfused fallback does not apply it either
+    conv.train()
+    conv.use_fused = False
+    plain.use_fused = False
+    th.manual_seed(1)
+    assert th.allclose(conv(g, x), plain.eval()(g, x), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("mask", ["module", "hashed"])
+def test_gatconv_attn_drop_one(mask):
+    """nn.Dropout(1.0) zeroes every attention weight: the output is 0 (no residual) and
+    finite gradients; the hashed kernels at p = 1 keep nothing (threshold 2^16, scale 0)
+    instead of keeping 1 in 2^16 at an infinite scale."""
+    g, n = _graph(3000, 40000, 8)
+    conv = GATConv(16, 8, 4, attn_drop=1.0).to(DEV).train()
+    conv.attn_drop_mask = mask
+    x = th.randn(n, 16, device=DEV, requires_grad=True)
+    y = conv(g, x)
+    assert th.equal(y, th.zeros_like(y))
+    y.sum().backward()
+    assert th.isfinite(x.grad).all() and th.isfinite(conv.attn_l.grad).all()
+    ft = th.randn(n, 4, 8, device=DEV)
+    el, er = th.randn(n, 4, 1, device=DEV), th.randn(n, 4, 1, device=DEV)
+    out = B.fused_gat(g, ft, el, er, 0.2, attn_drop=1.0, seed=3)
+    assert th.equal(out, th.zeros_like(out))
+    assert K.gat_dropout_scale(1.0) == 0.0 and not K.gat_dropout_keep(3, np.arange(100), 4, 1.0).any()

@@ -242,18 +242,35 @@ def test_rgcn_fused_ok_matches_the_kernel_rule():
 def test_gatconv_fused_route_limits():
     """GATConv takes the fused kernels only where they apply: 32-bit device CSRs, and
     with attention dropout in training gathered tables below 2^31 elements (the
-    dropout walks have 32-bit offsets only, capi.cpp gat_set_dropout)."""
+    dropout walks have 32-bit offsets only, capi.cpp gat_set_dropout), a plain
+    nn.Dropout below p = 1 and, for the module's own mask, edge ids that index it."""
     from types import SimpleNamespace
+    import torch
     from dgl.nn.pytorch import GATConv, FusedGATConv
-    g32 = SimpleNamespace(in_csr=SimpleNamespace(bits=32))
-    g64 = SimpleNamespace(in_csr=SimpleNamespace(bits=64))
-    for cls in (GATConv, FusedGATConv):
-        conv = cls(16, 8, 8, attn_drop=0.5)
-        big = (1 << 31) // 64
+    g32 = SimpleNamespace(in_csr=SimpleNamespace(bits=32), eid_perm=True)
+    g64 = SimpleNamespace(in_csr=SimpleNamespace(bits=64), eid_perm=True)
+    gview = SimpleNamespace(in_csr=SimpleNamespace(bits=32), eid_perm=False)
+    big = (1 << 31) // 64
+    for mask in ("module", "hashed"):
+        conv = GATConv(16, 8, 8, attn_drop=0.5)
+        conv.attn_drop_mask = mask
         conv.train()
         assert conv._fused_route(g32, big - 1) and not conv._fused_route(g32, big)
         assert not conv._fused_route(g64, 10)
+        # the module's keep words are indexed by edge id: a view whose CSR data are not
+        # its own edge ids takes the composition; the hashed mask does not care
+        assert conv._fused_route(gview, 10) == (mask == "hashed")
         conv.eval()
         assert conv._fused_route(g32, big)
         conv.use_fused = False
         assert not conv._fused_route(g32, 10)
+    # p = 1 (every weight dropped) and a dropout module of another type: the composition
+    conv = GATConv(16, 8, 8, attn_drop=1.0).train()
+    assert not conv._fused_route(g32, 10)
+    conv = GATConv(16, 8, 8, attn_drop=0.5).train()
+    conv.attn_drop = torch.nn.AlphaDropout(0.5)
+    assert not conv._fused_route(g32, 10)
+    # FusedGATConv never applies attn_drop (fusedGatConv.py:80,152): no dropout limits
+    conv = FusedGATConv(16, 8, 8, attn_drop=0.5).train()
+    assert conv._fused_route(g32, big) and conv._fused_route(gview, 10)
+    assert not conv._fused_route(g64, 10)

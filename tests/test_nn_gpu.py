@@ -215,6 +215,75 @@ def test_project_mfma_kernel(k, n, wt):
     assert bool(((xr.grad.double() - gref).abs() <= 2e-6 * gmag + 1e-6).all())
 
 
+@pytest.mark.parametrize("k,n", [(602, 64), (64, 602), (64, 256), (256, 64), (100, 128), (3, 7),
+                                 (17, 41), (300, 33), (640, 50), (64, 1000), (32, 256), (16, 200),
+                                 (200, 100), (500, 64)])
+@pytest.mark.parametrize("wt", [False, True])
+def test_project_tile_kernel(k, n, wt):
+    """k_project_tile (X tiles staged through LDS, waves split over columns or k): any
+    K <= 640 (GATConv's 602 -> 64 on Reddit and its dX 64 -> 602), wide N (R-GCN's
+    64 -> 256 with one X read), odd widths (per-element LDS staging of a row span that is
+    not float4-aligned; float2 / scalar stores), a row count off the 16-row tile, plain
+    and transposed weights, with and without bias -- against fp64 (every instance of
+    kernels_project.hip's table: 16 / 32 / 64 x 256, 64 x 640, 128 x 128, 256 x 128,
+    256 / 512 / 640 x 64)."""
+    from dgl import kernel as K
+    g = th.Generator(device=DEV).manual_seed(3 * k + n)
+    m = K.PROJECT_MIN_ROWS + 21
+    x = th.randn(m, k, device=DEV, generator=g)
+    w = th.randn(n, k, device=DEV, generator=g).t() if wt else th.randn(k, n, device=DEV, generator=g)
+    b = th.randn(n, device=DEV, generator=g)
+    assert K.project_mfma_ok(x, w)
+    ref = x.double() @ w.double()
+    mag = x.double().abs() @ w.double().abs()
+    for bias in (None, b):
+        y = K.project_mfma(x, w, bias)
+        r = ref if bias is None else ref + bias.double()
+        err = (y.double() - r).abs() - (2e-6 * mag + 1e-6)
+        assert bool((err <= 0).all()), float(err.max())
+
+
+def test_project_k_mismatch_raises():
+    """An (M, 128) X against a (64, 64) W: torch.matmul raises, so B.project does, and
+    the C entry -- handed the weight's row count -- refuses it (DGLError) instead of
+    reading W rows 64..127 out of bounds."""
+    from dgl import backend as B
+    from dgl import kernel as K
+    from dgl._ffi import DGLError
+    x = th.randn(K.PROJECT_MIN_ROWS, 128, device=DEV)
+    w = th.randn(64, 64, device=DEV)
+    assert not K.project_mfma_ok(x, w)
+    with pytest.raises(RuntimeError):
+        B.project(x, w)
+    with pytest.raises(DGLError, match="rows"):
+        K.project_mfma(x, w)
+
+
+def test_project_misaligned_bias_slice():
+    """A bias that is a slice of a flat parameter buffer at an offset of 1 float (not
+    16-byte aligned) takes torch.addmm instead of raising, and matches fp64."""
+    from dgl import backend as B
+    from dgl import kernel as K
+    g = th.Generator(device=DEV).manual_seed(9)
+    m = K.PROJECT_MIN_ROWS + 5
+    x = th.randn(m, 64, device=DEV, generator=g)
+    w = th.randn(64, 64, device=DEV, generator=g)
+    flat = th.randn(65, device=DEV, generator=g)
+    bias = flat[1:]
+    assert bias.data_ptr() % 16 != 0 and not K.project_bias_ok(bias, 64, x.device)
+    y = B.project(x, w, bias)
+    ref = x.double() @ w.double() + bias.double()
+    mag = x.double().abs() @ w.double().abs()
+    assert bool(((y.double() - ref).abs() <= 2e-6 * mag + 1e-5).all())
+    # an aligned slice of the same buffer rides in the kernel's epilogue
+    flat4 = th.randn(68, device=DEV, generator=g)
+    b4 = flat4[4:]
+    assert K.project_bias_ok(b4, 64, x.device)
+    y4 = B.project(x, w, b4)
+    ref4 = x.double() @ w.double() + b4.double()
+    assert bool(((y4.double() - ref4).abs() <= 2e-6 * mag + 1e-5).all())
+
+
 def test_nb_access_bench():
     """The hack's neighbour-access benchmark entry point returns feat and a time."""
     from dgl import backend as B
