@@ -1706,6 +1706,40 @@ int DGLMIEdgeSoftmaxNodeLogitsForward(const DGLMIGraph* graph, const DGLMIArray*
   API_END();
 }
 
+int DGLMIEdgeSoftmaxNodeLogitsForwardEx(const DGLMIGraph* graph, const DGLMIArray* el,
+                                        const DGLMIArray* er, float negative_slope, DGLMIArray* out,
+                                        DGLMIArray* row_max, DGLMIArray* row_sum, void* stream) {
+  API_BEGIN();
+  dglmi::SoftmaxArgs a;
+  const int64_t H = softmax_setup(graph, out, "out", a);
+  node_logit_args(graph, el, er, H, negative_slope, a);
+  DGLMI_CHECK(aligned16(out->data), "out must be 16-byte aligned");
+  check_array(row_max, "row_max");
+  check_array(row_sum, "row_sum");
+  DGLMI_CHECK(row_max->shape[0] == a.num_rows && feat_numel(row_max) == H && row_sum->shape[0] == a.num_rows &&
+                  feat_numel(row_sum) == H,
+              "row_max / row_sum must be (N_dst, H)");
+  DGLMI_CHECK(aligned16(row_max->data) && aligned16(row_sum->data), "row_max / row_sum must be 16-byte aligned");
+  DeviceGuard guard(graph->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (a.nnz == 0) return 0;
+  Scratch ws(graph, DGLMIEdgeSoftmaxWorkspaceBytes(&graph->in_csr, H), s);
+  const int64_t stats = ((2 * a.num_rows * H * 4) + 255) & ~int64_t(255);
+  // the row statistics straight into the caller's buffers
+  a.stat0 = row_max->data;
+  a.stat1 = row_sum->data;
+  a.carry = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + stats);
+  a.seg_cnt = reinterpret_cast<int32_t*>(
+      reinterpret_cast<char*>(a.carry) +
+      ((((a.nnz + a.chunk - 1) / a.chunk) * 2 * H * 4 + 15) & ~int64_t(15)));
+  a.s = nullptr;
+  a.out = out->data;
+  launch_edge_softmax(a, false, s);
+  launch_sm_row_sums(a, s);
+  check_hip(hipGetLastError(), "edge softmax (node logits, row statistics) forward launch");
+  API_END();
+}
+
 int DGLMIEdgeSoftmaxNodeLogitsBackward(const DGLMIGraph* graph, const DGLMIArray* out,
                                        const DGLMIArray* grad_out, const DGLMIArray* el,
                                        const DGLMIArray* er, float negative_slope,
@@ -1750,6 +1784,7 @@ int DGLMIProject(const float* x, int64_t m, int64_t k, const float* w, int64_t w
   DGLMI_CHECK(dglmi::project_supported(k, n), "DGLMIProject: unsupported (k, n) = (" +
                                                   std::to_string(k) + ", " + std::to_string(n) + ")");
   DGLMI_CHECK(m >= 0 && x != nullptr && w != nullptr && y != nullptr, "DGLMIProject: null operand");
+  DGLMI_CHECK(m == 0 || m >= 16, "DGLMIProject: tall-skinny shapes only (m >= 16 rows)");
   DGLMI_CHECK(aligned16(x) && aligned16(y) && (bias == nullptr || aligned16(bias)),
               "DGLMIProject: x, y and bias must be 16-byte aligned");
   DGLMI_CHECK(w_stride_k >= 1 && w_stride_n >= 1, "DGLMIProject: bad weight strides");

@@ -287,6 +287,10 @@ int64_t softmax_chunk_edges(int64_t nnz, int64_t H);
 // its carries need this many bytes after the statistics
 int64_t softmax_owned_carry_bytes(int64_t nnz, int64_t H);
 void launch_edge_softmax(const SoftmaxArgs& a, bool backward, hipStream_t s);
+// after a forward: a.stat0 = each row's max, a.stat1 = its sum of exp(s - max) (the
+// row-owned walk leaves 1 / sum there: inverted in place; rows without edges: 0 and
+// 1 / 0 = inf -- never read by an edge)
+void launch_sm_row_sums(const SoftmaxArgs& a, hipStream_t s);
 
 // Load-balanced reduce-to-row kernels (kernels_spmm.hip).
 enum FastKind : int {

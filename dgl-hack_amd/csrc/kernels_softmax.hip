@@ -620,6 +620,14 @@ __global__ void __launch_bounds__(kBlock) k_sm_hub(SoftmaxArgs a) {
     if constexpr (MODE == SM_STATS) {
 #pragma unroll
       for (int v = 0; v < V; ++v) l[v] = 1.0f / l[v];
+      // the hub row's statistics, like every other row's (the window it starts in)
+      if (pa == st && walk.j == 0) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          a.stat0[(int64_t)row * H + walk.q * V + v] = m[v];
+          a.stat1[(int64_t)row * H + walk.q * V + v] = l[v];
+        }
+      }
     }
     for (int64_t b = pa; b < pb; b += S::U * S::L) walk.template emit<S::U>(b, pb, m, l, row);
   };
@@ -723,6 +731,20 @@ int64_t softmax_owned_carry_bytes(int64_t nnz, int64_t H) {
     default: W = std::min(OwnedShape<16, SM_STATS>::W, OwnedShape<16, SM_DOTSUM>::W); break;
   }
   return ((nnz + W - 1) / W) * 2 * 2 * H * 4;
+}
+
+// the forward's row statistics as (max, sum of exp): the row-owned walk keeps 1 / sum
+__global__ void k_sm_invert(float* __restrict__ p, int64_t n) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+    p[i] = 1.0f / p[i];
+}
+void launch_sm_row_sums(const SoftmaxArgs& a, hipStream_t s) {
+  const int64_t n = a.num_rows * a.H;
+  if (a.eids || n <= 0) return;  // the chunked route stores the sum itself
+  const int64_t want = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_sm_invert, dim3(static_cast<unsigned>(want < 65536 ? want : 65536)), dim3(kBlock), 0,
+                     s, a.stat1, n);
 }
 
 void launch_edge_softmax(const SoftmaxArgs& a, bool backward, hipStream_t s) {

@@ -229,6 +229,9 @@ _SIGS = {
     "DGLMIEdgeSoftmaxNodeLogitsForward": (ctypes.c_int, [
         ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.c_float,
         ctypes.POINTER(Array), ctypes.c_void_p]),
+    "DGLMIEdgeSoftmaxNodeLogitsForwardEx": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.c_float,
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.c_void_p]),
     "DGLMIEdgeSoftmaxNodeLogitsBackward": (ctypes.c_int, [
         ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.c_float, ctypes.POINTER(Array), ctypes.c_void_p]),

@@ -550,6 +550,65 @@ def fused_gat(graph, feat_src, el, er, slope, attn_drop=0.0, seed=None, keep=Non
     return FusedGat.apply(gidx, feat_src, el, er, float(slope), attn_drop, int(seed or 0))
 
 
+class GatComposition(th.autograd.Function):
+    """GATConv's unfused composition (gatconv.py:151-157: u_add_v, leaky_relu, edge_softmax,
+    u_mul_e_sum) on the in-CSR position view, forward step by step -- the node-logit edge
+    softmax, then u_mul_e_sum: the kernels and bits of the separate autograd Functions --
+    and ONE fused backward: the fused GAT backward kernels (DGLMIFusedGatBackward: the
+    destination- and source-side walks, or the edge-position path), fed the softmax's row
+    statistics (DGLMIEdgeSoftmaxNodeLogitsForwardEx) and the output.  The step-by-step
+    backward walks the edges five times (attention-gradient SDDMM, softmax backward, the
+    two u_add_v gradient reductions, the u_mul_e_sum node gradient) and moves the E x H
+    attention gradient and logit gradient through HBM; here the softmax identity
+    sum_e a_e (ft_u . g_v) = g_v . rst_v gives each row's correction densely, the
+    attention is recomputed where it is used, and no per-edge tensor is kept from the
+    forward (the attention, E x H, is freed after u_mul_e_sum).  Equal to the step-by-step
+    gradients within fp32 rounding (tests/test_nn_gpu.py)."""
+
+    @staticmethod
+    def forward(ctx, gidx, view, feat_src, el, er, slope):
+        ft, el, er = feat_src.contiguous(), el.contiguous(), er.contiguous()
+        n_dst = view.num_dst
+        H = el.shape[1]
+        a = el.new_empty((view.number_of_edges(),) + tuple(el.shape[1:]))
+        rmax = el.new_zeros((n_dst, H))
+        rsum = el.new_ones((n_dst, H))
+        K.edge_softmax_node_logits_forward_ex(view, el, er, slope, a, rmax, rsum)
+        rst = ft.new_empty((n_dst,) + tuple(ft.shape[1:]))
+        K.binary_op_reduce("sum", "mul", view, SRC, EDGE, ft, a, rst)
+        del a
+        ctx.gidx, ctx.slope = gidx, slope
+        ctx.save_for_backward(ft, el, er, rst, rmax, rsum)
+        return rst
+
+    @staticmethod
+    def backward(ctx, grad):
+        ft, el, er, rst, rmax, rsum = ctx.saved_tensors
+        g_ft, g_el, g_er = th.empty_like(ft), th.empty_like(el), th.empty_like(er)
+        K.fused_gat_backward(ctx.gidx, ft, el, er, ctx.slope, rst, rmax, rsum, grad.contiguous(),
+                             g_ft, g_el, g_er)
+        return None, None, g_ft, g_el, g_er, None
+
+
+def gat_composition_ok(gidx, feat_src, el, er):
+    """Whether GatComposition applies: 32-bit device CSRs with both directions, fp32 ft
+    (N, H, D) whose head size the fused GAT kernels take, el / er (N, H, 1) with an H the
+    fused edge softmax takes."""
+    if not (feat_src.is_cuda and feat_src.dtype == th.float32 and feat_src.dim() == 3):
+        return False
+    n, h, d = feat_src.shape
+    return (gidx.in_csr.bits == 32 and getattr(gidx, "out_csr", None) is not None
+            and el.shape == (n, h, 1) and er.dim() == 3 and er.shape[1:] == (h, 1)
+            and el.dtype == er.dtype == th.float32
+            and K.fused_gat_supported(h, d) and K.edge_softmax_supported(h))
+
+
+def gat_composition(gidx, view, feat_src, el, er, slope):
+    """rst = u_mul_e_sum(ft, edge_softmax(leaky_relu(u_add_v(el, er)))) with the fused
+    backward (:class:`GatComposition`); ``view`` = gidx.position_view("in")."""
+    return GatComposition.apply(gidx, view, feat_src, el, er, float(slope))
+
+
 # --------------------------------------------------------------------------- #
 # R-GCN (hack: RgcnFirstLayer / RgcnSecondLayer, tensor.py:440-495;
 # kernels binary_reduce_impl.cu:913-1246)
@@ -691,16 +750,24 @@ def _flat_norm(gi, norm):
     storage: the prepared state's pointer / version check sees the caller's tensor); a
     non-contiguous one is copied ONCE per (tensor, version) and the copy reused, so
     RgcnState.sync_norm does not re-gather the state's norm copies on every call.  The
-    cache holds the source only by a weak reference (dropped with it)."""
+    cache holds the source's storage owner only by a weak reference whose callback
+    drops the entry -- and the E-float copy -- the moment the source is freed."""
     flat = norm.reshape(-1)
     if flat.is_contiguous():
         return flat
     key = (norm.data_ptr(), norm._version, tuple(norm.shape), tuple(norm.stride()))
+    owner = norm._base if norm._base is not None else norm
     hit = gi.__dict__.get("_rgcn_norm_flat")
-    if hit is not None and hit[0] == key and hit[1]() is norm:
+    if hit is not None and hit[0] == key and hit[1]() is owner:
         return hit[2]
     copy = flat.contiguous()
-    gi.__dict__["_rgcn_norm_flat"] = (key, weakref.ref(norm), copy)
+    d = gi.__dict__
+
+    def drop(ref):
+        ent = d.get("_rgcn_norm_flat")
+        if ent is not None and ent[1] is ref:
+            del d["_rgcn_norm_flat"]
+    d["_rgcn_norm_flat"] = (key, weakref.ref(owner, drop), copy)
     return copy
 
 

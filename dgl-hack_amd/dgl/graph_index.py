@@ -216,9 +216,13 @@ class ImmutableGraphIndex:
         # alive; the cache holds `w` only by a weak reference whose callback drops the
         # entry (and the permuted copy) the moment `w` is freed, so a dropped operand
         # costs no memory and its address cannot be mistaken for a later tensor's
+        # The weak reference is to the STORAGE OWNER (``w._base`` for a view): a caller
+        # that hands a fresh view of the same tensor each call (_typed_aggregate's
+        # ``norm.reshape(E, 1)``) still hits, and the entry lives as long as the data.
         key = self._operand_key(w)
+        owner = w._base if w._base is not None else w
         cached = self._pos_operands.get(direction)
-        if cached is None or cached[0] != key or cached[1]() is not w:
+        if cached is None or cached[0] != key or cached[1]() is not owner:
             ops = self._pos_operands
 
             def drop(ref, direction=direction):
@@ -226,7 +230,7 @@ class ImmutableGraphIndex:
                 if ent is not None and ent[1] is ref:
                     del ops[direction]
             from . import kernel as K
-            cached = (key, weakref.ref(w, drop), K.gather_rows(w, walk.data))
+            cached = (key, weakref.ref(owner, drop), K.gather_rows(w, walk.data))
             self._pos_operands[direction] = cached
         return view, cached[2]
 
@@ -250,7 +254,8 @@ class ImmutableGraphIndex:
         if getattr(self, "_pos_views", None) is None:
             self._pos_views, self._pos_operands = {}, {}
         cached = self._pos_operands.get("in")
-        if cached is not None and cached[0] == key and cached[1]() is w:
+        owner = w._base if w._base is not None else w
+        if cached is not None and cached[0] == key and cached[1]() is owner:
             return True
         # the same tensor OBJECT (a weak reference: the caching allocator hands a
         # fresh tensor of the same size the same address, so the key alone would

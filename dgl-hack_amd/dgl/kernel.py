@@ -570,14 +570,23 @@ def project_mfma(x2, w, bias=None):
     return y
 
 
-def gather_rows(src, index):
+def gather_rows(src, index, check=False):
     """src[index] for a contiguous fp32 device tensor and an int32 / int64 index on its
     device -> DGLMIGatherRows (one random row read per output row, rows written in
-    order); other dtypes take torch's indexing."""
+    order); other dtypes take torch's indexing.  The kernel does NOT bound-check:
+    every index must lie in [0, src.shape[0]) -- the internal callers pass a CSR's edge
+    ids or positions, in range by construction.  ``check=True`` verifies the range
+    first (one device reduction and a host sync) and raises DGLError as torch's
+    indexing raises IndexError."""
     if src.dtype != th.float32 or index.dtype not in (th.int32, th.int64):
         return src[index.long()]
     if not src.is_cuda or index.device != src.device:
         raise DGLError("gather_rows: src and index must be on one ROCm device")
+    if check and index.numel():
+        lo, hi = int(index.min()), int(index.max())
+        if lo < 0 or hi >= src.shape[0]:
+            raise DGLError("gather_rows: index out of range [%d, %d] for %d rows"
+                           % (lo, hi, src.shape[0]))
     src = src.contiguous()
     index = index.contiguous()
     out = src.new_empty((index.shape[0],) + tuple(src.shape[1:]))
@@ -599,6 +608,18 @@ def edge_softmax_node_logits_forward(graph, el, er, negative_slope, out):
     check_call(_ffi.lib().DGLMIEdgeSoftmaxNodeLogitsForward(
         ctypes.byref(g), _arr(el, "el"), _arr(er, "er"), ctypes.c_float(negative_slope),
         _arr(out, "out"), _stream(out)))
+    return out
+
+
+def edge_softmax_node_logits_forward_ex(graph, el, er, negative_slope, out, row_max, row_sum):
+    """edge_softmax_node_logits_forward, also keeping each destination row's (max, sum of
+    exp) -> DGLMIEdgeSoftmaxNodeLogitsForwardEx (the fused GAT backward's softmax state)."""
+    _check_ctx(graph, [("el", el), ("er", er), ("out", out), ("row_max", row_max),
+                       ("row_sum", row_sum)])
+    g = graph.cstruct(_softmax_ws(graph, _feat_len(out), out.device), coo=True)
+    check_call(_ffi.lib().DGLMIEdgeSoftmaxNodeLogitsForwardEx(
+        ctypes.byref(g), _arr(el, "el"), _arr(er, "er"), ctypes.c_float(negative_slope),
+        _arr(out, "out"), _arr(row_max, "row_max"), _arr(row_sum, "row_sum"), _stream(out)))
     return out
 
 

@@ -34,6 +34,9 @@ from ..softmax import _apply_node_logits as _node_logit_edge_softmax_on
 POSITION_SPACE = True
 # the composition's leaky_relu -> edge_softmax pair as one fused softmax call (False: two)
 FUSED_LEAKY = True
+# the position-space composition's backward as ONE fused pass pair (backend.GatComposition:
+# the forward unchanged, the gradients within fp32 rounding); False: step by step
+FUSED_COMPOSITION_BACKWARD = True
 
 
 def expand_as_pair(x):
@@ -152,6 +155,11 @@ class GATConv(nn.Module):
         gidx = graph._graph.get_immutable_gidx(feat_src.device)
         view = gidx.position_view("in")
         n_dst, m = view.num_dst, view.number_of_edges()
+        if (FUSED_COMPOSITION_BACKWARD and FUSED_LEAKY and type(self.leaky_relu) is nn.LeakyReLU
+                and not self._attn_drop_active()
+                and B.gat_composition_ok(gidx, feat_src, el, er)):
+            # the same forward; the backward as the fused GAT's walks (GatComposition)
+            return B.gat_composition(gidx, view, feat_src, el, er, self.leaky_relu.negative_slope)
         if type(self.leaky_relu) is nn.LeakyReLU and FUSED_LEAKY:
             # u_add_v and the activation inside the softmax's passes: the logits are
             # computed where they are read, never stored (bit-identical to the three steps)

@@ -425,6 +425,14 @@ int DGLMIEdgeSoftmaxBackward(const DGLMIGraph* graph, const DGLMIArray* out,
 int DGLMIEdgeSoftmaxNodeLogitsForward(const DGLMIGraph* graph, const DGLMIArray* el,
                                       const DGLMIArray* er, float negative_slope, DGLMIArray* out,
                                       void* stream);
+/* DGLMIEdgeSoftmaxNodeLogitsForward that also returns each destination row's softmax
+ * statistics: row_max (N_dst, H) the maximum of its (activated) logits, row_sum (N_dst,
+ * H) the sum of exp(logit - max) -- the state the fused GAT backward entries take as
+ * max_in / sum_in, so GATConv's unfused composition can hand its backward to them
+ * (rows without in-edges: left as the caller initialised them).  Extension. */
+int DGLMIEdgeSoftmaxNodeLogitsForwardEx(const DGLMIGraph* graph, const DGLMIArray* el,
+                                        const DGLMIArray* er, float negative_slope, DGLMIArray* out,
+                                        DGLMIArray* row_max, DGLMIArray* row_sum, void* stream);
 int DGLMIEdgeSoftmaxNodeLogitsBackward(const DGLMIGraph* graph, const DGLMIArray* out,
                                        const DGLMIArray* grad_out, const DGLMIArray* el,
                                        const DGLMIArray* er, float negative_slope,
@@ -441,7 +449,9 @@ int DGLMIProject(const float* x, int64_t m, int64_t k, const float* w, int64_t w
                  int64_t w_stride_k, int64_t w_stride_n, int64_t n, const float* bias, float* y,
                  int device, void* stream);
 /* out[i, :] = src[index[i], :] for i < n, rows of row_floats floats; index int32
- * (index_bits 32) or int64 (64), device pointers.  A per-edge operand put into a walk's
+ * (index_bits 32) or int64 (64), device pointers.  Indices are NOT bound-checked: each
+ * must lie in [0, rows of src) (dgl.kernel.gather_rows(check=True) verifies on the host
+ * side first).  A per-edge operand put into a walk's
  * position order (the position views' operands, GATConv's dropout scale in position
  * space; extension). */
 int DGLMIGatherRows(const float* src, int64_t row_floats, const void* index, int index_bits,

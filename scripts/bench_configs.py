@@ -155,6 +155,11 @@ def c3(dev, steps, warmup):
         gat(g, x).sum().backward()
     ms_f = timeit(fwd, steps, warmup)
     ms_fb = timeit(fwd_bwd, steps, warmup)
+    # the composition's step-by-step backward (round 5's) beside the fused one
+    from dgl.nn.pytorch.conv import gatconv as _gatconv
+    _gatconv.FUSED_COMPOSITION_BACKWARD = False
+    ms_fb_step = timeit(fwd_bwd, steps, warmup)
+    _gatconv.FUSED_COMPOSITION_BACKWARD = True
     fgat = FusedGATConv(602, 8, 8).to(dev)
     fgat.load_state_dict(gat.state_dict())
 
@@ -176,14 +181,20 @@ def c3(dev, steps, warmup):
 
     def dfwd_bwd():
         dgat(g, x).sum().backward()
-    ms_dfb = timeit(dfwd_bwd, steps, warmup)
+    ms_dfb = timeit(dfwd_bwd, steps, warmup)       # the module's nn.Dropout draws (default)
+    dgat.attn_drop_mask = "hashed"
+    ms_dfb_hashed = timeit(dfwd_bwd, steps, warmup)  # opt-in hashed mask
+    dgat.attn_drop_mask = "module"
     dgat.use_fused = False
     ms_dufb = timeit(dfwd_bwd, steps, warmup)
     return {"config": "C3 Reddit-size GATConv 602 -> 8x8", "nodes": n, "edges": m,
             "unfused_fwd_ms": ms_f, "unfused_fwd_bwd_ms": ms_fb,
+            "unfused_stepwise_bwd_fwd_bwd_ms": ms_fb_step,
             "fused_fwd_ms": ms_ff, "fused_fwd_bwd_ms": ms_ffb,
             "fused_fwd_Gedges_s": m / ms_ff / 1e6, "fused_fwd_bwd_Gedges_s": m / ms_ffb / 1e6,
-            "attn_drop_0.6_fused_fwd_bwd_ms": ms_dfb, "attn_drop_0.6_unfused_fwd_bwd_ms": ms_dufb,
+            "attn_drop_0.6_fused_fwd_bwd_ms": ms_dfb,
+            "attn_drop_0.6_fused_hashed_mask_fwd_bwd_ms": ms_dfb_hashed,
+            "attn_drop_0.6_unfused_fwd_bwd_ms": ms_dufb,
             "check": check}
 
 

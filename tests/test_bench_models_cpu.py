@@ -67,27 +67,37 @@ def test_exchange_summary_without_time():
 def _rec(rank, ms, alg, traffic):
     r = {"rank": rank, "kernel_ms": ms, "alg_bytes": alg, "compulsory_bytes": alg // 4,
          "traffic": traffic}
-    r["frac"] = traffic / (ms * 1e-3) / 1e9 / bench.HBM_PEAK_GBPS if traffic else None
+    r["frac"] = alg / (ms * 1e-3) / 1e9 / bench.HBM_PEAK_GBPS
     return r
 
 
 def test_job_roofline_one_rank_is_the_launch():
-    roof, achieved = bench.job_roofline([_rec(0, 2.0, 30e9, 16e9)], 1)
-    assert achieved == pytest.approx(8000.0)
-    assert roof["peak"] == bench.HBM_PEAK_GBPS and roof["frac"] == pytest.approx(1.0)
+    """achieved = the contract's algorithmic bytes / kernel time; the counter bytes
+    (L2 egress: HBM + Infinity Cache) and the compulsory bytes bound the HBM fraction."""
+    roof, egress = bench.job_roofline([_rec(0, 2.0, 30e9, 16e9)], 1)
+    assert roof["achieved"] == pytest.approx(15000.0)
+    assert roof["frac"] == pytest.approx(15000.0 / bench.HBM_PEAK_GBPS)
+    assert egress == pytest.approx(8000.0) and roof["l2_egress_GBps"] == pytest.approx(8000.0)
+    assert roof["l2_egress_frac"] == pytest.approx(1.0)
+    assert roof["compulsory_GBps"] == pytest.approx(30e9 // 4 / 2e-3 / 1e9)
+    assert roof["hbm_frac_bounds"] == pytest.approx([roof["compulsory_frac"], 1.0])
+    assert roof["peak"] == bench.HBM_PEAK_GBPS and roof["traffic"] == 16e9
     assert "per_rank" not in roof
 
 
 def test_job_roofline_aggregates_over_the_slowest_rank():
     per = [_rec(0, 2.0, 30e9, 14e9), _rec(1, 2.5, 30e9, 16e9)]
-    roof, achieved = bench.job_roofline(per, 2)
-    # (14 + 16) GB over the slowest 2.5 ms against 2 x 8 TB/s -- not the best rank's 0.875
-    assert achieved == pytest.approx(30e9 / 2.5e-3 / 1e9)
-    assert roof["frac"] == pytest.approx(12000.0 / 16000.0)
+    roof, egress = bench.job_roofline(per, 2)
+    # every rank's bytes over the slowest 2.5 ms against 2 x 8 TB/s -- not the best rank's
+    assert roof["achieved"] == pytest.approx(60e9 / 2.5e-3 / 1e9)
+    assert roof["frac"] == pytest.approx(24000.0 / 16000.0)
+    assert egress == pytest.approx(30e9 / 2.5e-3 / 1e9)
+    assert roof["l2_egress_frac"] == pytest.approx(12000.0 / 16000.0)
     assert roof["peak"] == pytest.approx(2 * bench.HBM_PEAK_GBPS)
     assert roof["frac_min"] == pytest.approx(per[1]["frac"])
     assert roof["alg_bytes_per_launch"] == pytest.approx(60e9)
     assert roof["alg_GBps"] == pytest.approx(60e9 / 2.5e-3 / 1e9)
-    # a rank without counters: no traffic-based figure at all
-    roof2, ach2 = bench.job_roofline([_rec(0, 2.0, 30e9, 14e9), _rec(1, 2.0, 30e9, None)], 2)
-    assert ach2 is None and roof2["frac"] is None and roof2["traffic"] is None
+    # a rank without counters: the algorithmic figure stays, no counter-based one
+    roof2, eg2 = bench.job_roofline([_rec(0, 2.0, 30e9, 14e9), _rec(1, 2.0, 30e9, None)], 2)
+    assert eg2 is None and roof2["traffic"] is None and roof2["hbm_frac_bounds"] is None
+    assert roof2["frac"] == pytest.approx(30000.0 / 16000.0)

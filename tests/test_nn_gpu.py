@@ -217,7 +217,7 @@ def test_project_mfma_kernel(k, n, wt):
 
 @pytest.mark.parametrize("k,n", [(602, 64), (64, 602), (64, 256), (256, 64), (100, 128), (3, 7),
                                  (17, 41), (300, 33), (640, 50), (64, 1000), (32, 256), (16, 200),
-                                 (200, 100), (500, 64)])
+                                 (200, 100), (500, 64), (250, 64), (63, 200), (601, 64)])
 @pytest.mark.parametrize("wt", [False, True])
 def test_project_tile_kernel(k, n, wt):
     """k_project_tile (X tiles staged through LDS, waves split over columns or k): any
@@ -226,7 +226,7 @@ def test_project_tile_kernel(k, n, wt):
     not float4-aligned; float2 / scalar stores), a row count off the 16-row tile, plain
     and transposed weights, with and without bias -- against fp64 (every instance of
     kernels_project.hip's table: 16 / 32 / 64 x 256, 64 x 640, 128 x 128, 256 x 128,
-    256 / 512 / 640 x 64)."""
+    256 / 512 / 640 x 64; each in its K % 4 == 0, K even and K odd LDS image)."""
     from dgl import kernel as K
     g = th.Generator(device=DEV).manual_seed(3 * k + n)
     m = K.PROJECT_MIN_ROWS + 21
@@ -451,6 +451,7 @@ def test_gat_composition_position_space_bit_identical(H, D, owned, monkeypatch):
     monkeypatch.setenv("DGLMI_SOFTMAX_OWNED", owned)
     from dgl.nn.pytorch.conv import gatconv
     from graphs import powerlaw
+    monkeypatch.setattr(gatconv, "FUSED_COMPOSITION_BACKWARD", False)  # step by step
     src, dst, n = powerlaw(20000, 300000, seed=21)
     g = dgl.DGLGraph()
     g.add_nodes(n)
@@ -517,6 +518,7 @@ def test_gat_composition_fused_leaky_bit_identical(pos, owned, monkeypatch):
     from dgl.nn.pytorch.conv import gatconv
     from graphs import powerlaw
     monkeypatch.setattr(gatconv, "POSITION_SPACE", pos)
+    monkeypatch.setattr(gatconv, "FUSED_COMPOSITION_BACKWARD", False)  # step by step
     src, dst, n = powerlaw(20000, 300000, seed=22)
     g = dgl.DGLGraph()
     g.add_nodes(n)
@@ -536,3 +538,46 @@ def test_gat_composition_fused_leaky_bit_identical(pos, owned, monkeypatch):
         res.append([out.detach().clone(), x.grad.clone()] + [p.grad.clone() for p in gat.parameters()])
     for a, b in zip(*res):
         assert th.equal(a, b), float((a - b).abs().max())
+
+
+@pytest.mark.parametrize("owned", ["0", "1"])
+@pytest.mark.parametrize("H,D,blocks", [(8, 8, "1"), (8, 8, "4"), (1, 16, "1"), (4, 32, "1"),
+                                        (16, 4, "2"), (2, 8, "1")])
+def test_gat_composition_fused_backward(H, D, blocks, owned, monkeypatch):
+    """The position-space composition with its backward fused (backend.GatComposition:
+    the softmax's row statistics handed to the fused GAT backward walks) against the
+    step-by-step backward: the forward bit for bit (the same kernels), the input and every
+    parameter gradient within fp32 rounding -- on a power-law graph with hub rows and
+    zero-in-degree rows, both softmax routes (the row-owned walk's hub rows included in
+    the exported statistics), unblocked (the edge-position path) and column-blocked (the
+    destination- and source-side walks).  The fused route is the one taken."""
+    monkeypatch.setenv("DGLMI_SOFTMAX_OWNED", owned)
+    monkeypatch.setenv("DGLMI_GAT_BLOCKS", blocks)
+    from dgl import backend as B
+    from dgl.nn.pytorch.conv import gatconv
+    from graphs import powerlaw
+    src, dst, n = powerlaw(30000, 400000, seed=23 + H)
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    th.manual_seed(5)
+    gat = nn.GATConv(24, D, H, negative_slope=0.2).to(DEV)
+    gat.use_fused = False
+    x = th.randn(n, 24, device=DEV, requires_grad=True)
+    go = th.randn(n, H, D, device=DEV)
+    calls = []
+    orig = B.gat_composition
+    monkeypatch.setattr(B, "gat_composition", lambda *a: calls.append(1) or orig(*a))
+    res = []
+    for fused in (True, False):
+        monkeypatch.setattr(gatconv, "FUSED_COMPOSITION_BACKWARD", fused)
+        gat.zero_grad()
+        x.grad = None
+        out = gat(g, x)
+        out.backward(go)
+        res.append([out.detach().clone(), x.grad.clone()] + [p.grad.clone() for p in gat.parameters()])
+    assert calls == [1]
+    assert th.equal(res[0][0], res[1][0])
+    for a, b in zip(res[0][1:], res[1][1:]):
+        tol = 1e-4 * float(b.abs().max()) + 1e-7
+        assert float((a - b).abs().max()) <= tol, (float((a - b).abs().max()), tol)

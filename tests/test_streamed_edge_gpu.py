@@ -224,6 +224,53 @@ def test_position_operand_cache_drops_with_the_tensor():
     assert not gidx._pos_operands
 
 
+def test_position_operand_cache_hits_fresh_views():
+    """A caller that passes a NEW view of the same constant operand every call
+    (_typed_aggregate's ``norm.reshape(E, 1)``) reuses the cached position-ordered copy --
+    the weak reference is to the storage owner -- in both directions; an in-place update
+    (version bump) misses; freeing the owner drops the entry."""
+    import gc
+    src, dst, n = powerlaw(20_000, 150_000, seed=4)
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    gidx = g._graph.get_immutable_gidx(DEV)
+    norm = th.rand(len(src), device=DEV)
+    _, a = gidx.position_operand(norm.reshape(-1, 1), "in")
+    _, b = gidx.position_operand(norm.reshape(-1, 1), "in")
+    assert b is a
+    _, c = gidx.position_operand(norm.reshape(-1, 1), "out")
+    _, d = gidx.position_operand(norm.reshape(-1, 1), "out")
+    assert d is c
+    assert th.equal(a.flatten(), norm[gidx.in_csr.data.long()])
+    norm.mul_(2.0)
+    _, e = gidx.position_operand(norm.reshape(-1, 1), "in")
+    assert e is not a and th.equal(e.flatten(), norm[gidx.in_csr.data.long()])
+    del norm, a, b, c, d, e
+    gc.collect()
+    assert not gidx._pos_operands
+
+
+def test_rgcn_flat_norm_copy_dropped_with_the_norm():
+    """_flat_norm's contiguous copy of a non-contiguous norm is reused per (tensor,
+    version), and dropped from the graph index when the norm is freed."""
+    import gc
+    from dgl import backend as B
+    src, dst, n = powerlaw(5_000, 40_000, seed=5)
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    gi = g._graph.get_immutable_gidx(DEV)
+    base = th.rand(len(src), 2, device=DEV)
+    norm = base[:, 1]  # non-contiguous view
+    f1 = B._flat_norm(gi, norm)
+    f2 = B._flat_norm(gi, base[:, 1])  # a fresh view of the same storage: reused
+    assert f2 is f1 and th.equal(f1, norm)
+    del norm, base, f1, f2
+    gc.collect()
+    assert "_rgcn_norm_flat" not in gi.__dict__
+
+
 @pytest.mark.parametrize("shape", [(1000,), (1000, 3), (1000, 2, 2), (1000, 8, 1), (1000, 4, 16), (1000, 256)])
 @pytest.mark.parametrize("idt", [th.int32, th.int64])
 def test_gather_rows_matches_indexing(shape, idt):
@@ -233,4 +280,9 @@ def test_gather_rows_matches_indexing(shape, idt):
     src = th.randn(*shape, device=DEV)
     idx = th.randint(0, shape[0], (4321,), device=DEV, dtype=idt)
     assert th.equal(K.gather_rows(src, idx), src[idx.long()])
+    assert th.equal(K.gather_rows(src, idx, check=True), src[idx.long()])
     assert K.gather_rows(src, idx[:0]).shape == (0,) + tuple(shape[1:])
+    from dgl._ffi import DGLError
+    for bad in (shape[0], -1):
+        with pytest.raises(DGLError, match="out of range"):
+            K.gather_rows(src, th.tensor([0, bad], device=DEV, dtype=idt), check=True)
