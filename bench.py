@@ -1100,6 +1100,18 @@ def launch_ranks(nproc, argv, grace_s=60.0):
     return 128 - rc if rc < 0 else rc
 
 
+# the largest per-graph edge count a --same-device rehearsal with N >= 3 may use
+SAME_DEVICE_MAX_EDGES = 4_000_000
+
+
+def same_device_small(args):
+    """Whether a --same-device run is small enough for N >= 3 ranks sharing one GPU:
+    every graph the ranks build (M1 block, C4, C5) at most SAME_DEVICE_MAX_EDGES edges."""
+    return (args.edges_per_gpu * args.gpus <= SAME_DEVICE_MAX_EDGES
+            and (args.no_c4 or args.c4_edges <= SAME_DEVICE_MAX_EDGES)
+            and (args.no_c5 or args.c5_edges <= SAME_DEVICE_MAX_EDGES))
+
+
 def launcher_stub(mode, world, rank):
     """Worker body of the launcher's CPU test (``--launcher-stub MODE``): no GPU;
     gloo collectives over the ranks the launcher started, then the same
@@ -1382,10 +1394,13 @@ def main():
     if args.gpus < 1:
         log("--gpus must be >= 1")
         return 2
-    if args.same_device and args.gpus >= 3:
+    if args.same_device and args.gpus >= 3 and not same_device_small(args):
         # three or more processes on one GPU crawl inside rocPRIM's
-        # decoupled-look-back sorts (partition_stats 180 s per rank at N = 3)
-        log("--same-device is refused for N >= 3 (concurrent look-back sorts stall)")
+        # decoupled-look-back sorts at full size (partition_stats 180 s per rank at
+        # N = 3); a reduced-size rehearsal of the 8-rank topology is allowed
+        log("--same-device is refused for N >= 3 at full size (concurrent look-back sorts "
+            "stall); rehearse with --edges-per-gpu, --c4-edges and --c5-edges <= %d"
+            % SAME_DEVICE_MAX_EDGES)
         return 2
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:

@@ -1018,15 +1018,18 @@ void gat_check_ls(const GatArgs& a, const DGLMIArray* lf, const DGLMIArray* ls) 
 // stays unbiased); t = 2^16 (p >= 1 - 2^-17, p = 1 included) keeps nothing, scale 0.
 // Caller's mask (`keep`, one uint32 word per edge id, bit h = head h kept): the kernels
 // read it through the walk's edge ids and scale kept weights by `keep_scale`.
-void gat_set_dropout(GatArgs& a, float p, uint64_t seed, const DGLMIArray* keep = nullptr,
-                     float keep_scale = 0.0f, int64_t num_edges = 0) {
-  if (keep != nullptr) {
-    check_array(keep, "keep");
-    DGLMI_CHECK(keep->shape[0] == num_edges && feat_numel(keep) == 1,
-                "keep must hold one word per edge (E,)");
+void gat_set_dropout(GatArgs& a, float p, uint64_t seed, const void* keep = nullptr, int keep_bits = 0,
+                     float keep_scale = 0.0f, int64_t num_edges = 0, int keep_pos = 0) {
+  if (keep != nullptr || keep_bits != 0) {
+    a.drop_pos = keep_pos != 0 ? 1 : 0;
+    a.drop_off = 0;
+    DGLMI_CHECK(keep_bits == 8 || keep_bits == 16 || keep_bits == 32, "keep_bits must be 8, 16 or 32");
+    DGLMI_CHECK(a.H <= keep_bits, "keep words narrower than the head count");
+    DGLMI_CHECK(keep != nullptr || num_edges == 0, "keep (one word per edge) is required");
     DGLMI_CHECK(std::isfinite(keep_scale) && keep_scale >= 0.0f, "keep_scale must be finite and >= 0");
     a.drop = 2;
-    a.drop_bits = reinterpret_cast<const uint32_t*>(keep->data);
+    a.drop_bits = keep;
+    a.drop_width = keep_bits;
     a.drop_scale = keep_scale;
   } else {
     DGLMI_CHECK(p >= 0.0f && p <= 1.0f, "attn_drop must be in [0, 1]");
@@ -1045,13 +1048,14 @@ int gat_forward_impl(const DGLMIGraph* graph, const DGLMIArray* feat_src, const 
                      const DGLMIArray* er, float negative_slope, DGLMIArray* out,
                      DGLMIArray* max_out, DGLMIArray* sum_out, DGLMIArray* lf, DGLMIArray* ls,
                      void* stream, float attn_drop = 0.0f, uint64_t seed = 0,
-                     const DGLMIArray* keep = nullptr, float keep_scale = 0.0f) {
+                     const void* keep = nullptr, int keep_bits = 0, float keep_scale = 0.0f,
+                     int keep_pos = 0) {
   API_BEGIN();
   check_graph32(graph, "fused GAT");
   DeviceGuard guard(graph->device);
   GatArgs a = gat_args(graph, feat_src, el, er, negative_slope, out, max_out, sum_out);
   gat_check_ls(a, lf, ls);
-  gat_set_dropout(a, attn_drop, seed, keep, keep_scale, graph->in_csr.nnz);
+  gat_set_dropout(a, attn_drop, seed, keep, keep_bits, keep_scale, graph->in_csr.nnz, keep_pos);
   a.eids = graph->in_csr.data;
   a.lf = lf ? lf->data : nullptr;
   a.ls = ls ? ls->data : nullptr;
@@ -1091,9 +1095,12 @@ int gat_forward_impl(const DGLMIGraph* graph, const DGLMIArray* feat_src, const 
     float* m_part = out_part + nb * N * a.F * (lf ? 2 : 1);
     float* l_part = m_part + nb * N * a.H;
     float* ls_part = lf ? l_part + nb * N * a.H : nullptr;
+    int64_t keep_off = 0;  // position-ordered keep words: the blocks in order
     for (int b = 0; b < nb; ++b) {
       const DGLMICsr& c = graph->in_col_blocks[b];
       GatArgs ab = a;
+      ab.drop_off = keep_off;
+      keep_off += c.nnz;
       ab.indptr = c.indptr;
       ab.rows = c.rows;
       ab.indices = c.indices;
@@ -1154,13 +1161,14 @@ int gat_backward_impl(const DGLMIGraph* graph, const DGLMIArray* feat_src, const
                       const DGLMIArray* max_in, const DGLMIArray* sum_in, const DGLMIArray* lf_in,
                       const DGLMIArray* ls_in, const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
                       DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream, float attn_drop = 0.0f,
-                      uint64_t seed = 0, const DGLMIArray* keep = nullptr, float keep_scale = 0.0f) {
+                      uint64_t seed = 0, const void* keep = nullptr, int keep_bits = 0,
+                      float keep_scale = 0.0f, int keep_pos = 0) {
   API_BEGIN();
   check_graph32(graph, "fused GAT");
   DeviceGuard guard(graph->device);
   GatArgs a = gat_args(graph, feat_src, el, er, negative_slope, const_cast<DGLMIArray*>(out),
                        const_cast<DGLMIArray*>(max_in), const_cast<DGLMIArray*>(sum_in));
-  gat_set_dropout(a, attn_drop, seed, keep, keep_scale, graph->in_csr.nnz);
+  gat_set_dropout(a, attn_drop, seed, keep, keep_bits, keep_scale, graph->in_csr.nnz, keep_pos);
   // with dropout only the slope-aggregate backward (no destination-side walk) applies
   DGLMI_CHECK(!a.drop || lf_in != nullptr,
               "attention dropout needs the forward's slope aggregates (slope_feat / slope_sum)");
@@ -1225,8 +1233,11 @@ int gat_backward_impl(const DGLMIGraph* graph, const DGLMIArray* feat_src, const
     a.ls = ls_in->data;
     launch_gat_stats(a, s);
     a.lf = a.ls = nullptr;
+    int64_t keep_off = 0;  // position-ordered keep words: the out-blocks in order
     auto src_walk = [&](const DGLMICsr& c, bool accumulate) {
       GatArgs b = a;
+      b.drop_off = keep_off;
+      keep_off += c.nnz;
       b.indptr = c.indptr;
       b.rows = c.rows;
       b.indices = c.indices;
@@ -1358,38 +1369,51 @@ int DGLMIFusedGatDropoutBackward(const DGLMIGraph* graph, const DGLMIArray* feat
 
 int DGLMIFusedGatKeepForward(const DGLMIGraph* graph, const DGLMIArray* feat_src,
                              const DGLMIArray* el, const DGLMIArray* er, float negative_slope,
-                             const DGLMIArray* keep, float keep_scale, DGLMIArray* out,
-                             DGLMIArray* max_out, DGLMIArray* sum_out, DGLMIArray* slope_feat,
-                             DGLMIArray* slope_sum, void* stream) {
-  if (keep == nullptr) {
-    g_last_error = "keep (one word per edge) is required";
+                             const void* keep, int keep_bits, int keep_by_position, float keep_scale,
+                             DGLMIArray* out, DGLMIArray* max_out, DGLMIArray* sum_out,
+                             DGLMIArray* slope_feat, DGLMIArray* slope_sum, void* stream) {
+  if (keep_bits == 0) {
+    g_last_error = "keep_bits must be 8, 16 or 32";
     return -1;
   }
   return gat_forward_impl(graph, feat_src, el, er, negative_slope, out, max_out, sum_out, slope_feat,
-                          slope_sum, stream, 0.0f, 0, keep, keep_scale);
+                          slope_sum, stream, 0.0f, 0, keep, keep_bits, keep_scale, keep_by_position);
 }
 
 int DGLMIFusedGatKeepBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src,
                               const DGLMIArray* el, const DGLMIArray* er, float negative_slope,
-                              const DGLMIArray* keep, float keep_scale, const DGLMIArray* out,
-                              const DGLMIArray* max_in, const DGLMIArray* sum_in,
+                              const void* keep, int keep_bits, int keep_by_position, float keep_scale,
+                              const DGLMIArray* out, const DGLMIArray* max_in, const DGLMIArray* sum_in,
                               const DGLMIArray* slope_feat, const DGLMIArray* slope_sum,
                               const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
                               DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream) {
-  if (keep == nullptr) {
-    g_last_error = "keep (one word per edge) is required";
+  if (keep_bits == 0) {
+    g_last_error = "keep_bits must be 8, 16 or 32";
     return -1;
   }
   return gat_backward_impl(graph, feat_src, el, er, negative_slope, out, max_in, sum_in, slope_feat,
                            slope_sum, grad_out, grad_feat_src, grad_el, grad_er, stream, 0.0f, 0,
-                           keep, keep_scale);
+                           keep, keep_bits, keep_scale, keep_by_position);
 }
 
-int DGLMIGatKeepBits(const float* table, int64_t num_edges, int heads, uint32_t* bits, void* stream) {
+int DGLMIGatKeepGather(const void* keep, int keep_bits, const int32_t* index, int64_t n, void* out,
+                       void* stream) {
   API_BEGIN();
-  DGLMI_CHECK(num_edges >= 0 && heads >= 1 && heads <= 32, "DGLMIGatKeepBits: 1 <= heads <= 32");
+  DGLMI_CHECK(keep_bits == 8 || keep_bits == 16 || keep_bits == 32, "DGLMIGatKeepGather: keep_bits 8, 16 or 32");
+  DGLMI_CHECK(n >= 0, "DGLMIGatKeepGather: n >= 0");
+  DGLMI_CHECK(n == 0 || (keep != nullptr && index != nullptr && out != nullptr), "DGLMIGatKeepGather: null operand");
+  launch_gat_keep_gather(keep, keep_bits, index, n, out, static_cast<hipStream_t>(stream));
+  check_hip(hipGetLastError(), "keep gather launch");
+  API_END();
+}
+
+int DGLMIGatKeepBits(const float* table, int64_t num_edges, int heads, void* bits, int keep_bits,
+                     void* stream) {
+  API_BEGIN();
+  DGLMI_CHECK(keep_bits == 8 || keep_bits == 16 || keep_bits == 32, "DGLMIGatKeepBits: keep_bits 8, 16 or 32");
+  DGLMI_CHECK(num_edges >= 0 && heads >= 1 && heads <= keep_bits, "DGLMIGatKeepBits: 1 <= heads <= keep_bits");
   DGLMI_CHECK(num_edges == 0 || (table != nullptr && bits != nullptr), "DGLMIGatKeepBits: null operand");
-  launch_gat_keep_bits(table, num_edges, heads, bits, static_cast<hipStream_t>(stream));
+  launch_gat_keep_bits(table, num_edges, heads, bits, keep_bits, static_cast<hipStream_t>(stream));
   check_hip(hipGetLastError(), "keep bits launch");
   API_END();
 }

@@ -388,14 +388,21 @@ struct GatArgs {
   // attention dropout.  drop = 0: off.  drop = 1 (DGLMIFusedGatDropout*, hashed): edge e,
   // head h keeps its weight, scaled by drop_scale, when gat_head_keep(gat_edge_key(seed,
   // eid), h, drop_thresh) (16-bit threshold, round(p 2^16)).  drop = 2 (DGLMIFusedGatKeep*,
-  // the caller's mask): bit h of drop_bits[eid] -- one word per edge id, drawn by the
-  // caller (GATConv: its nn.Dropout) -- scaled by drop_scale.  The walk's edge ids in
-  // `eids` (its CSR's data).
+  // the caller's mask): bit h of drop_bits[eid] -- one word per edge id of drop_width bits
+  // (8, 16 or 32: the narrowest that holds H, so C3's 114.6 M edges at H = 8 take 115 MB,
+  // Infinity-Cache resident, for the walks' random reads), drawn by the caller (GATConv:
+  // its nn.Dropout) -- scaled by drop_scale.  The walk's edge ids in `eids` (its CSR's data).
   int drop;
   uint32_t drop_thresh;
   float drop_scale;
   uint64_t drop_seed;
-  const uint32_t* drop_bits;
+  const void* drop_bits;
+  int drop_width;
+  // drop_pos: the keep words are in this walk's position order, at drop_bits[drop_off +
+  // position] (coalesced; the caller gathers them once per direction, column blocks
+  // concatenated in block order) instead of at drop_bits[edge id] (a random read per edge)
+  int drop_pos;
+  int64_t drop_off;
   const int32_t* eids;
 };
 // The dropout mask's hash (mirrored in numpy by dgl.kernel.gat_dropout_keep for the
@@ -427,9 +434,14 @@ __host__ __device__ __forceinline__ bool gat_head_keep(uint32_t key, int h, uint
   return ((gat_pair_bits(key, h >> 1) >> (16 * (h & 1))) & 0xffffu) >= thresh16;
 }
 bool gat_supported(int64_t H, int64_t D);
-// bits[e] = OR over h < H of (table[e * H + h] != 0) << h, e < n (H <= 32): a dropout
-// output table (E, H) in edge-id order packed to one keep word per edge (drop = 2)
-void launch_gat_keep_bits(const float* table, int64_t n, int H, uint32_t* bits, hipStream_t s);
+// bits[e] = OR over h < H of (table[e * H + h] != 0) << h, e < n (H <= width <= 32): a
+// dropout output table (E, H) in edge-id order packed to one keep word of `width` bits
+// (8, 16 or 32) per edge (drop = 2)
+void launch_gat_keep_bits(const float* table, int64_t n, int H, void* bits, int width, hipStream_t s);
+// out[i] = keep[index[i]], i < n, words of `width` bits: edge-id keep words into a walk's
+// position order (index = the walk CSR's edge ids)
+void launch_gat_keep_gather(const void* keep, int width, const int32_t* index, int64_t n, void* out,
+                            hipStream_t s);
 int64_t gat_chunk_edges(int64_t nnz);
 void launch_gat_forward(const GatArgs& a, hipStream_t s);
 void launch_gat_backward_dst(const GatArgs& a, hipStream_t s);

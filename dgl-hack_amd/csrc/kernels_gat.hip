@@ -103,6 +103,12 @@ __device__ __forceinline__ uint32_t gat_stage_keep(const GatArgs& a, int32_t eid
   return kb;  // bits past H unused
 }
 __device__ __forceinline__ bool gat_kept(uint32_t staged, int h) { return (staged >> h) & 1u; }
+// the caller's keep word of edge e (drop = 2): 8, 16 or 32 bits (a launch-uniform branch)
+__device__ __forceinline__ uint32_t gat_keep_word(const GatArgs& a, int32_t e) {
+  if (a.drop_width == 8) return static_cast<const uint8_t*>(a.drop_bits)[e];
+  if (a.drop_width == 16) return static_cast<const uint16_t*>(a.drop_bits)[e];
+  return static_cast<const uint32_t*>(a.drop_bits)[e];
+}
 
 // ---------------------------------------------------------------------------
 // forward
@@ -218,18 +224,24 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
       nr[i] = ok ? a.rows[p] : INT_MAX;
       nc[i] = ok ? a.indices[p] : 0;
       if constexpr (table) {
-        nk[table ? i : 0] = ok ? a.drop_bits[ne[table ? i : 0]] : 0u;
-        ne[table ? i : 0] = p + B < p1 ? a.eids[p + B] : 0;
+        if (a.drop_pos) {  // position order: one coalesced byte / word per position
+          nk[table ? i : 0] = ok ? gat_keep_word(a, static_cast<int32_t>(a.drop_off + p)) : 0u;
+        } else {
+          nk[table ? i : 0] = ok ? gat_keep_word(a, ne[table ? i : 0]) : 0u;
+          ne[table ? i : 0] = p + B < p1 ? a.eids[p + B] : 0;
+        }
       } else if constexpr (drop) {
         ne[drop ? i : 0] = ok ? a.eids[p] : 0;
       }
     }
   };
   if constexpr (table) {
+    if (!a.drop_pos) {
 #pragma unroll
-    for (int i = 0; i < SQ; ++i) {
-      const int64_t p = p0 + lane + i * L;
-      ne[table ? i : 0] = p < p1 ? a.eids[p] : 0;
+      for (int i = 0; i < SQ; ++i) {
+        const int64_t p = p0 + lane + i * L;
+        ne[table ? i : 0] = p < p1 ? a.eids[p] : 0;
+      }
     }
   }
   fetch(p0);
@@ -632,18 +644,24 @@ __device__ __forceinline__ void gat_bwd_src_body(const GatArgs& a) {
       nr[i] = ok ? a.rows[p] : INT_MAX;
       nc[i] = ok ? a.indices[p] : 0;
       if constexpr (table) {
-        nk[table ? i : 0] = ok ? a.drop_bits[ne[table ? i : 0]] : 0u;
-        ne[table ? i : 0] = p + B < p1 ? a.eids[p + B] : 0;
+        if (a.drop_pos) {  // position order: one coalesced byte / word per position
+          nk[table ? i : 0] = ok ? gat_keep_word(a, static_cast<int32_t>(a.drop_off + p)) : 0u;
+        } else {
+          nk[table ? i : 0] = ok ? gat_keep_word(a, ne[table ? i : 0]) : 0u;
+          ne[table ? i : 0] = p + B < p1 ? a.eids[p + B] : 0;
+        }
       } else if constexpr (drop) {
         ne[drop ? i : 0] = ok ? a.eids[p] : 0;
       }
     }
   };
   if constexpr (table) {
+    if (!a.drop_pos) {
 #pragma unroll
-    for (int i = 0; i < SQ; ++i) {
-      const int64_t p = p0 + lane + i * L;
-      ne[table ? i : 0] = p < p1 ? a.eids[p] : 0;
+      for (int i = 0; i < SQ; ++i) {
+        const int64_t p = p0 + lane + i * L;
+        ne[table ? i : 0] = p < p1 ? a.eids[p] : 0;
+      }
     }
   }
   fetch(p0);
@@ -1000,20 +1018,47 @@ void launch_gat_fold_lse(const float* m, float* l, int64_t n, hipStream_t s) {
 }
 // One keep word per edge from a dropout output (E, H) in edge-id order: the lanes of a
 // wave read 64 consecutive rows, every byte of the span used over the H loads.
-__global__ void k_gat_keep_bits(const float* __restrict__ table, int64_t n, int H,
-                                uint32_t* __restrict__ bits) {
+template <typename T>
+__global__ void k_gat_keep_bits(const float* __restrict__ table, int64_t n, int H, T* __restrict__ bits) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < n; e += stride) {
     uint32_t w = 0;
     for (int h = 0; h < H; ++h) w |= (table[e * H + h] != 0.0f ? 1u : 0u) << h;
-    bits[e] = w;
+    bits[e] = static_cast<T>(w);
   }
 }
-void launch_gat_keep_bits(const float* table, int64_t n, int H, uint32_t* bits, hipStream_t s) {
+void launch_gat_keep_bits(const float* table, int64_t n, int H, void* bits, int width, hipStream_t s) {
   if (n <= 0) return;
   const int64_t want = (n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(k_gat_keep_bits, dim3(static_cast<unsigned>(want < 65536 ? want : 65536)),
-                     dim3(kBlock), 0, s, table, n, H, bits);
+  const dim3 grid(static_cast<unsigned>(want < 65536 ? want : 65536)), blk(kBlock);
+  if (width == 8)
+    hipLaunchKernelGGL(k_gat_keep_bits<uint8_t>, grid, blk, 0, s, table, n, H, static_cast<uint8_t*>(bits));
+  else if (width == 16)
+    hipLaunchKernelGGL(k_gat_keep_bits<uint16_t>, grid, blk, 0, s, table, n, H, static_cast<uint16_t*>(bits));
+  else
+    hipLaunchKernelGGL(k_gat_keep_bits<uint32_t>, grid, blk, 0, s, table, n, H, static_cast<uint32_t*>(bits));
+}
+template <typename T>
+__global__ void k_gat_keep_gather(const T* __restrict__ keep, const int32_t* __restrict__ index, int64_t n,
+                                  T* __restrict__ out) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+    out[i] = keep[index[i]];
+}
+void launch_gat_keep_gather(const void* keep, int width, const int32_t* index, int64_t n, void* out,
+                            hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t want = (n + kBlock - 1) / kBlock;
+  const dim3 grid(static_cast<unsigned>(want < 65536 ? want : 65536)), blk(kBlock);
+  if (width == 8)
+    hipLaunchKernelGGL(k_gat_keep_gather<uint8_t>, grid, blk, 0, s, static_cast<const uint8_t*>(keep), index, n,
+                       static_cast<uint8_t*>(out));
+  else if (width == 16)
+    hipLaunchKernelGGL(k_gat_keep_gather<uint16_t>, grid, blk, 0, s, static_cast<const uint16_t*>(keep), index,
+                       n, static_cast<uint16_t*>(out));
+  else
+    hipLaunchKernelGGL(k_gat_keep_gather<uint32_t>, grid, blk, 0, s, static_cast<const uint32_t*>(keep), index,
+                       n, static_cast<uint32_t*>(out));
 }
 void launch_gat_backward_dst(const GatArgs& a, hipStream_t s) { DGLMI_GAT_DISPATCH(bwd_dst_cfg, a, s); }
 void launch_gat_backward_src(const GatArgs& a, hipStream_t s) { DGLMI_GAT_DISPATCH(bwd_src_cfg, a, s); }

@@ -504,12 +504,16 @@ constexpr TileCfg kTileCfgs[] = {
     {8, 4, 1},   // K <= 512, N <= 64
     {40, 1, 4},  // K <= 640, N <= 64   (GATConv 602 -> 8 x 8 on Reddit), no k split
     {4, 4, 1},   // K <= 256, N <= 64   (k split; A/B)
-    {10, 4, 1},  // K <= 640, N <= 64   (k split; A/B)
+    {10, 4, 1},  // K <= 640, N <= 64   (k split: GATConv 602 -> 8 x 8, 0.24 vs 0.34 ms)
+    {4, 5, 4},   // K <= 64,  N <= 320  (two column slices of GATConv's dX; A/B)
 };
 constexpr int kNumTileCfgs = sizeof(kTileCfgs) / sizeof(kTileCfgs[0]);
 
 // the instance with the least padded MFMA work for (K, N) (X re-reads of extra column
-// slices priced at 10 % each, a k split's LDS reduction at 5 %); -1: none (K > 640).
+// slices priced at 10 % each, a k split's LDS reduction at 5 %, and a wave that reads a
+// whole tile of more than 256 k from LDS -- four times the LDS reads of the k split -- at
+// 50 %: C3's 602 -> 64 runs 0.34 ms that way against 0.24 ms split, while C5's 256 -> 64
+// runs 1.58 ms unsplit against 1.85 ms split; scripts/project_probe.py); -1: none (K > 640).
 // DGLMI_PROJECT_CFG=i forces instance i where it fits (A/B).
 int pick_tile(int64_t K, int64_t N) {
   if (const char* e = std::getenv("DGLMI_PROJECT_CFG")) {
@@ -523,7 +527,7 @@ int pick_tile(int64_t K, int64_t N) {
     if (K > c.kp()) continue;
     const int64_t slices = (N + c.nsl() - 1) / c.nsl();
     const double cost = static_cast<double>(c.kp()) * slices * c.nsl() * (1.0 + 0.1 * (slices - 1)) *
-                        (c.NS < kWaves ? 1.05 : 1.0);
+                        (c.NS < kWaves ? 1.05 : 1.0) * (c.NS == kWaves && 16 * c.KB > 256 ? 1.5 : 1.0);
     if (best < 0 || cost < best_cost) {
       best = i;
       best_cost = cost;
@@ -537,7 +541,7 @@ void launch_tile_raw(const float* X, int64_t M, int64_t K, const float* W, int64
                      const float* bias, float* Y, hipStream_t s) {
   using S = TileShape<KB, CB, NS>;
   // two workgroups per CU where the W fragment leaves room (<= 256 VGPRs per lane)
-  constexpr int OCC = 4 * KB * CB <= 64 ? 2 : 1;
+  constexpr int OCC = 4 * KB * CB <= 80 ? 2 : 1;
   const int64_t slices = (N + S::NSL - 1) / S::NSL;
   const int64_t rtiles = (M + 15) / 16;
   int64_t groups = std::max<int64_t>(1, 256 * OCC / slices);
@@ -616,6 +620,7 @@ void launch_project(const float* X, int64_t M, int64_t K, const float* W, int64_
     case 8: launch_tile<40, 1, 4>(X, M, K, W, swk, swn, N, bias, Y, s); break;
     case 9: launch_tile<4, 4, 1>(X, M, K, W, swk, swn, N, bias, Y, s); break;
     case 10: launch_tile<10, 4, 1>(X, M, K, W, swk, swn, N, bias, Y, s); break;
+    case 11: launch_tile<4, 5, 4>(X, M, K, W, swk, swn, N, bias, Y, s); break;
     default: break;  // unsupported: the C entry checks project_supported first
   }
 }

@@ -471,6 +471,11 @@ def gcn_norm_aggregate(gidx, x, norm, bias=None, n_dst=None):
     return _GcnNormAggregate.apply(gidx, x.contiguous(), norm, bias, n_dst)
 
 
+# where the fused walks read the caller's dropout mask: "<forward>,<backward>", each "eid"
+# (a random word per edge, in the walk) or "pos" (gathered into walk order first)
+GAT_KEEP_ORDER = "pos,pos"
+
+
 class FusedGat(th.autograd.Function):
     """tensor.py:383-413 (FusedGat), max-stabilised and without per-edge buffers.  When
     a gradient will be wanted, the forward also keeps the attention's slope aggregates
@@ -479,7 +484,7 @@ class FusedGat(th.autograd.Function):
     DGLMI_GAT_SLOPES=0 keeps the round-3 backward (destination walk / edge positions).
     ``attn_drop`` > 0: GATConv's attention dropout (gatconv.py:154) inside the same
     kernels, the mask a hash of ``seed`` and the edge id, recomputed by the backward
-    (DGLMIFusedGatDropout*; always with the slope aggregates).  ``keep`` (E,) int32 keep
+    (DGLMIFusedGatDropout*; always with the slope aggregates).  ``keep`` (E,) keep
     words with ``keep_scale`` instead: the caller's mask (DGLMIFusedGatKeep*; GATConv's
     own nn.Dropout draws)."""
 
@@ -498,11 +503,24 @@ class FusedGat(th.autograd.Function):
                 or os.environ.get("DGLMI_GAT_SLOPES", "1") != "0"):
             lf = feat_src.new_empty((n_dst, H, D))
             ls = feat_src.new_empty((n_dst, H))
+        keep_in = keep_out = None
+        # the caller's mask per direction: by edge id (the walk reads a random word per
+        # edge) or gathered into the walk's position order first (DGLMIGatKeepGather: the
+        # same random reads in a pass of their own, then coalesced reads in the walk);
+        # DGLMI_GAT_KEEP_ORDER = "<fwd>,<bwd>" with each "eid" or "pos" (A/B)
+        order = os.environ.get("DGLMI_GAT_KEEP_ORDER", GAT_KEEP_ORDER).split(",")
+        pos_in, pos_out = order[0] == "pos", order[-1] == "pos"
+        if keep is not None:
+            keep_in = K.gat_keep_walk_order(gidx, keep, feat_src, "in") if pos_in else keep
+            if lf is not None:
+                keep_out = K.gat_keep_walk_order(gidx, keep, feat_src, "out") if pos_out else keep
         K.fused_gat_forward(gidx, feat_src, el, er, slope, out, mx, sm, lf, ls,
-                            attn_drop=attn_drop, seed=seed, keep=keep, keep_scale=keep_scale)
+                            attn_drop=attn_drop, seed=seed, keep=keep_in, keep_scale=keep_scale,
+                            keep_pos=pos_in)
+        del keep_in
         ctx.gidx, ctx.slope = gidx, slope
         ctx.attn_drop, ctx.seed = attn_drop, seed
-        ctx.keep, ctx.keep_scale = keep, keep_scale
+        ctx.keep, ctx.keep_scale, ctx.keep_pos = keep_out, keep_scale, pos_out
         ctx.slopes = lf is not None
         if lf is not None:
             ctx.save_for_backward(feat_src, el, er, out, mx, sm, lf, ls)
@@ -521,7 +539,8 @@ class FusedGat(th.autograd.Function):
         g_er = th.empty_like(er)
         K.fused_gat_backward(ctx.gidx, feat_src, el, er, ctx.slope, out, mx, sm, grad_out, g_ft,
                              g_el, g_er, lf, ls, attn_drop=ctx.attn_drop, seed=ctx.seed,
-                             keep=ctx.keep, keep_scale=ctx.keep_scale)
+                             keep=ctx.keep, keep_scale=ctx.keep_scale,
+                             keep_pos=getattr(ctx, "keep_pos", False))
         return None, g_ft, g_el, g_er, None, None, None, None, None
 
 
@@ -532,8 +551,8 @@ def fused_gat(graph, feat_src, el, er, slope, attn_drop=0.0, seed=None, keep=Non
     ``graph`` is a DGLGraph (or an ImmutableGraphIndex); feat_src (N, H, D), el / er
     (N, H, 1).  Returns (N, H, D).  Attention dropout, two forms:
 
-    * ``keep`` (E,) int32 keep words in edge-id order (:func:`dgl.kernel.gat_keep_bits` of
-      a dropout output (E, H, 1)) with ``keep_scale`` (the dropout's 1 / (1 - p)): the
+    * ``keep`` (E,) keep words in edge-id order (:func:`dgl.kernel.gat_keep_bits` of a
+      dropout output (E, H, 1)) with ``keep_scale`` (the dropout's 1 / (1 - p)): the
       caller's mask -- GATConv passes its own ``nn.Dropout``'s draws, the reference's;
     * ``attn_drop`` > 0: a hashed mask keyed by ``seed`` (default: drawn from torch's
       default generator, so ``torch.manual_seed`` reproduces it) -- no (E, H) buffer, not

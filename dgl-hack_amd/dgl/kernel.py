@@ -43,17 +43,16 @@ def _arr(t, name):
     return ctypes.byref(a)
 
 
-def _arr_words(t, name):
-    """An int32 (uint32 bit-word) device array for the entries that take one."""
-    if not isinstance(t, th.Tensor) or t.device.type != "cuda" or t.dtype != th.int32 \
-            or not t.is_contiguous() or t.dim() != 1:
-        raise DGLError("%s must be a contiguous 1-D int32 ROCm tensor" % name)
-    a = _ffi.Array()
-    a.data = t.data_ptr() if t.numel() else None
-    a.ndim = 1
-    a.shape[0] = t.shape[0]
-    a._keep = t
-    return ctypes.byref(a)
+_KEEP_BITS = {th.uint8: 8, th.int16: 16, th.int32: 32}
+
+
+def _keep_words(t, name, num_edges):
+    """(pointer, bits) of a keep-word tensor: contiguous 1-D uint8 / int16 / int32 on the
+    device, one word per edge."""
+    if not isinstance(t, th.Tensor) or t.device.type != "cuda" or t.dtype not in _KEEP_BITS \
+            or not t.is_contiguous() or t.dim() != 1 or t.shape[0] != num_edges:
+        raise DGLError("%s must be a contiguous (E,) uint8 / int16 / int32 ROCm tensor" % name)
+    return ctypes.c_void_p(t.data_ptr() if t.numel() else None), _KEEP_BITS[t.dtype]
 
 
 def _map(m, name):
@@ -371,8 +370,9 @@ def gat_dropout_scale(p):
 
 
 def gat_keep_bits(table):
-    """One int32 keep word per edge from a dropout output ``table`` (E, H[, 1]) in edge-id
-    order: bit h set where head h was kept (non-zero) -> DGLMIGatKeepBits (H <= 32)."""
+    """One keep word per edge from a dropout output ``table`` (E, H[, 1]) in edge-id order:
+    bit h set where head h was kept (non-zero), in the narrowest word that holds H (uint8
+    for H <= 8, int16 for H <= 16, int32 for H <= 32) -> DGLMIGatKeepBits."""
     t = table.reshape(table.shape[0], -1)
     if t.dtype != th.float32 or not t.is_cuda:
         raise DGLError("gat_keep_bits: a float32 ROCm table")
@@ -380,28 +380,62 @@ def gat_keep_bits(table):
     h = int(t.shape[1])
     if not 1 <= h <= 32:
         raise DGLError("gat_keep_bits: 1 <= heads <= 32")
-    bits = th.empty(t.shape[0], dtype=th.int32, device=t.device)
+    dt, width = (th.uint8, 8) if h <= 8 else (th.int16, 16) if h <= 16 else (th.int32, 32)
+    bits = th.empty(t.shape[0], dtype=dt, device=t.device)
     check_call(_ffi.lib().DGLMIGatKeepBits(
         ctypes.c_void_p(t.data_ptr()), ctypes.c_int64(t.shape[0]), h,
-        ctypes.c_void_p(bits.data_ptr()), _stream(bits)))
+        ctypes.c_void_p(bits.data_ptr()), width, _stream(bits)))
     return bits
 
 
+def gat_keep_walk_order(graph, keep, feat_src, direction):
+    """The keep words (edge-id order) in the position order of the fused GAT's walks over
+    ``graph`` for ``feat_src``: "in" the forward's (the in-CSR, or its column blocks in
+    block order), "out" the backward's (the out-CSR or its blocks) -> DGLMIGatKeepGather
+    per block.  With these the kernels read one coalesced word per position instead of a
+    random one per edge (DGLMIFusedGatKeep*, keep_by_position)."""
+    nb = gat_col_blocks(graph, feat_src)
+    if nb > 1:
+        ib, ob = graph.col_blocks(nb)
+        csrs = ib if direction == "in" else ob
+    else:
+        csrs = [graph.in_csr if direction == "in" else graph.out_csr]
+    out = th.empty_like(keep)
+    kp, kb = _keep_words(keep, "keep", graph.in_csr.nnz)
+    off = 0
+    for c in csrs:
+        n = int(c.nnz)
+        if n:
+            idx = c.data
+            if idx.dtype != th.int32 or not idx.is_contiguous():
+                raise DGLError("gat_keep_walk_order: int32 edge ids expected")
+            check_call(_ffi.lib().DGLMIGatKeepGather(
+                kp, kb, ctypes.c_void_p(idx.data_ptr()), ctypes.c_int64(n),
+                ctypes.c_void_p(out.data_ptr() + off * out.element_size()), _stream(out)))
+        off += n
+    if off != keep.shape[0]:
+        raise DGLError("gat_keep_walk_order: the walk covers %d of %d edges" % (off, keep.shape[0]))
+    return out
+
+
 def fused_gat_forward(graph, feat_src, el, er, slope, out, max_out, sum_out, slope_feat=None,
-                      slope_sum=None, attn_drop=0.0, seed=0, keep=None, keep_scale=None):
+                      slope_sum=None, attn_drop=0.0, seed=0, keep=None, keep_scale=None,
+                      keep_pos=False):
     """_CAPI_DGLFusedGatKernel (binary_reduce.cc:380-396) -> DGLMIFusedGatForward, or
     with ``slope_feat`` (N, H, D) / ``slope_sum`` (N, H) DGLMIFusedGatForwardEx: the
     forward also keeps the attention's slope aggregates, so the backward needs no
     destination-side walk.  ``attn_drop`` > 0: DGLMIFusedGatDropoutForward (GATConv's
     attention dropout in the same pass, the mask a hash of ``seed`` and the edge id).
-    ``keep`` (E,) int32 words (:func:`gat_keep_bits`) with ``keep_scale``:
-    DGLMIFusedGatKeepForward, the caller's mask."""
+    ``keep`` (E,) keep words (:func:`gat_keep_bits`) with ``keep_scale``:
+    DGLMIFusedGatKeepForward, the caller's mask -- by edge id, or with ``keep_pos`` in the
+    forward walk's position order (:func:`gat_keep_walk_order` "in")."""
     _check_ctx(graph, [("feat_src", feat_src), ("el", el), ("er", er), ("out", out)])
     g = graph.cstruct(None, col_blocks=gat_col_blocks(graph, feat_src))
     if keep is not None:
+        kp, kb = _keep_words(keep, "keep", graph.in_csr.nnz)
         check_call(_ffi.lib().DGLMIFusedGatKeepForward(
             ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"),
-            float(slope), _arr_words(keep, "keep"), float(keep_scale), _arr(out, "out"),
+            float(slope), kp, kb, int(bool(keep_pos)), float(keep_scale), _arr(out, "out"),
             _arr(max_out, "max_out"), _arr(sum_out, "sum_out"), _arr(slope_feat, "slope_feat"),
             _arr(slope_sum, "slope_sum"), _stream(out)))
         return out
@@ -424,19 +458,21 @@ def fused_gat_forward(graph, feat_src, el, er, slope, out, max_out, sum_out, slo
 
 def fused_gat_backward(graph, feat_src, el, er, slope, out, max_in, sum_in, grad_out,
                        grad_feat_src, grad_el, grad_er, slope_feat=None, slope_sum=None,
-                       attn_drop=0.0, seed=0, keep=None, keep_scale=None):
+                       attn_drop=0.0, seed=0, keep=None, keep_scale=None, keep_pos=False):
     """_CAPI_DGLKernelBackwardFusedGat (binary_reduce.cc:529-549) -> DGLMIFusedGatBackward
     (or DGLMIFusedGatBackwardEx with the forward's slope aggregates; with ``attn_drop`` > 0
     DGLMIFusedGatDropoutBackward, the forward's seed; with ``keep``
-    DGLMIFusedGatKeepBackward, the forward's mask)."""
+    DGLMIFusedGatKeepBackward, the forward's mask -- by edge id, or with ``keep_pos`` in the
+    backward walk's position order, :func:`gat_keep_walk_order` "out")."""
     _check_ctx(graph, [("feat_src", feat_src), ("grad_out", grad_out)])
     if keep is not None:
         if slope_feat is None:
             raise DGLError("fused GAT dropout backward needs the forward's slope aggregates")
         g = graph.cstruct(None, col_blocks=gat_col_blocks(graph, feat_src, backward=True))
+        kp, kb = _keep_words(keep, "keep", graph.in_csr.nnz)
         check_call(_ffi.lib().DGLMIFusedGatKeepBackward(
             ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"),
-            float(slope), _arr_words(keep, "keep"), float(keep_scale), _arr(out, "out"),
+            float(slope), kp, kb, int(bool(keep_pos)), float(keep_scale), _arr(out, "out"),
             _arr(max_in, "max_in"), _arr(sum_in, "sum_in"), _arr(slope_feat, "slope_feat"),
             _arr(slope_sum, "slope_sum"), _arr(grad_out, "grad_out"),
             _arr(grad_feat_src, "grad_feat_src"), _arr(grad_el, "grad_el"),

@@ -344,30 +344,40 @@ int DGLMIFusedGatDropoutBackward(const DGLMIGraph* graph, const DGLMIArray* feat
                                  const DGLMIArray* slope_feat, const DGLMIArray* slope_sum,
                                  const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
                                  DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream);
-/* Fused GAT with the CALLER's attention-dropout mask: keep (E,) holds one uint32 word per
- * edge id, bit h set when head h keeps its weight (H <= 32), and kept weights are scaled
- * by keep_scale.  GATConv draws the mask with its own nn.Dropout on an (E, H, 1) tensor
- * of ones in edge-id order -- the draws the reference's dropout(edge_softmax(...)) makes
- * under the same seed (gatconv.py:154) -- packs it with DGLMIGatKeepBits and passes
- * keep_scale = the dropout's 1 / (1 - p).  The kernels read each edge's word through the
- * walks' edge ids (column blocks included); otherwise as DGLMIFusedGatDropout*.
- * Extension. */
+/* Fused GAT with the CALLER's attention-dropout mask: keep holds one word of keep_bits
+ * bits (8, 16 or 32; >= H) per edge (E = in_csr.nnz words), bit h set when head h keeps
+ * its weight, and kept weights are scaled by keep_scale.  GATConv draws the mask with its
+ * own nn.Dropout on an (E, H, 1) tensor of ones in edge-id order -- the draws the
+ * reference's dropout(edge_softmax(...)) makes under the same seed (gatconv.py:154) --
+ * packs it with DGLMIGatKeepBits into the narrowest word that holds H and passes
+ * keep_scale = the dropout's 1 / (1 - p).  keep_by_position = 0: words indexed by edge id
+ * (the walks read each through their CSR's edge ids, a random read per edge);
+ * keep_by_position = 1: words in the walks' position order (DGLMIGatKeepGather by the
+ * walk CSR's edge ids, once per direction): the forward's in-CSR (its column blocks
+ * concatenated in block order when the graph carries them), the backward's out-CSR
+ * (likewise) -- every read coalesced.  Otherwise as DGLMIFusedGatDropout*.  Extension. */
 int DGLMIFusedGatKeepForward(const DGLMIGraph* graph, const DGLMIArray* feat_src,
                              const DGLMIArray* el, const DGLMIArray* er, float negative_slope,
-                             const DGLMIArray* keep, float keep_scale, DGLMIArray* out,
-                             DGLMIArray* max_out, DGLMIArray* sum_out, DGLMIArray* slope_feat,
-                             DGLMIArray* slope_sum, void* stream);
+                             const void* keep, int keep_bits, int keep_by_position, float keep_scale,
+                             DGLMIArray* out, DGLMIArray* max_out, DGLMIArray* sum_out,
+                             DGLMIArray* slope_feat, DGLMIArray* slope_sum, void* stream);
 int DGLMIFusedGatKeepBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src,
                               const DGLMIArray* el, const DGLMIArray* er, float negative_slope,
-                              const DGLMIArray* keep, float keep_scale, const DGLMIArray* out,
-                              const DGLMIArray* max_in, const DGLMIArray* sum_in,
+                              const void* keep, int keep_bits, int keep_by_position, float keep_scale,
+                              const DGLMIArray* out, const DGLMIArray* max_in, const DGLMIArray* sum_in,
                               const DGLMIArray* slope_feat, const DGLMIArray* slope_sum,
                               const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
                               DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream);
-/* bits[e] = OR over h < heads of (table[e * heads + h] != 0) << h for e < num_edges
- * (1 <= heads <= 32): a dropout output (E, H) packed to the keep words above.  Device
- * pointers.  Extension. */
-int DGLMIGatKeepBits(const float* table, int64_t num_edges, int heads, uint32_t* bits, void* stream);
+/* out[i] = keep[index[i]] for i < n, words of keep_bits bits (8, 16, 32): keep words in
+ * edge-id order into a walk's position order (index = that CSR's edge ids, int32).
+ * Device pointers; indices must lie in range.  Extension. */
+int DGLMIGatKeepGather(const void* keep, int keep_bits, const int32_t* index, int64_t n, void* out,
+                       void* stream);
+/* bits[e] = OR over h < heads of (table[e * heads + h] != 0) << h for e < num_edges, in
+ * words of keep_bits bits (8, 16 or 32; heads <= keep_bits): a dropout output (E, H)
+ * packed to the keep words above.  Device pointers.  Extension. */
+int DGLMIGatKeepBits(const float* table, int64_t num_edges, int heads, void* bits, int keep_bits,
+                     void* stream);
 /* The same two kernels in the reference's argument order, for a binding of the hack's
  * PackedFuncs that keeps its Python caller unchanged (tensor.py:383-420):
  *   _CAPI_DGLFusedGatKernel(G, feat_src, el, er, sum, exp, ret, slope)

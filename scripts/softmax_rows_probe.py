@@ -36,9 +36,11 @@ def main():
     gidx = g._graph.get_immutable_gidx(dev)
     res = {"lib": os.environ.get("DGL_LIBRARY_PATH", "in-tree")}
     dig = hashlib.sha256()
-    # --pmc: H = 8 on the view only (chunked, then row-owned), for counter passes
+    # --pmc: H = 8 (or with --pmc-h1 H = 1) on the view only (chunked, then row-owned),
+    # for counter passes
     pmc = "--pmc" in sys.argv
-    for H in ((8,) if pmc else (8, 1)):
+    pmc_h = 1 if "--pmc-h1" in sys.argv else 8  # --pmc --pmc-h1: the H = 1 view instead
+    for H in ((pmc_h,) if pmc else (8, 1)):
         gen = th.Generator(device=dev).manual_seed(H)
         s = th.randn(gidx.number_of_edges(), H, 1, device=dev, generator=gen) * 3
         ga = th.randn(s.shape, device=dev, generator=gen)

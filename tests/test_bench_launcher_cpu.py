@@ -58,9 +58,16 @@ def test_world_size_mismatch_is_an_error():
 
 
 def test_same_device_refused_from_three_ranks():
+    """Full-size --same-device runs with N >= 3 are refused (look-back-sort stall); a
+    reduced-size rehearsal of the 8-rank topology is let through to the launcher."""
     code, lines, err = _run("--gpus", "3", "--same-device", "--launcher-stub", "ok")
     assert code == 2 and not lines
     assert "refused" in err
+    code, lines, err = _run("--gpus", "8", "--same-device", "--edges-per-gpu", "250000",
+                            "--c4-edges", "2000000", "--c5-edges", "2000000",
+                            "--launcher-stub", "ok", timeout=240)
+    assert code == 0, err[-3000:]
+    assert json.loads(lines[0])["n_gpus"] == 8
 
 
 def test_rank_crash_propagates_status():

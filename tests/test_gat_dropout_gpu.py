@@ -175,11 +175,14 @@ def test_gatconv_module_dropout_matches_composition(nb, p, H, D, monkeypatch):
 
 
 def test_keep_bits_pack():
-    """DGLMIGatKeepBits: one word per edge, bit h = (table[e, h] != 0)."""
+    """DGLMIGatKeepBits: one word per edge, bit h = (table[e, h] != 0), in the narrowest
+    word that holds H (8 / 16 / 32 bits)."""
     gen = th.Generator(device=DEV).manual_seed(4)
-    for h in (1, 3, 8, 32):
+    for h in (1, 3, 8, 9, 16, 17, 32):
         t = (th.rand(1001, h, 1, device=DEV, generator=gen) < 0.5).float() * 2.0
-        bits = K.gat_keep_bits(t).cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+        kb = K.gat_keep_bits(t)
+        assert kb.dtype == (th.uint8 if h <= 8 else th.int16 if h <= 16 else th.int32)
+        bits = kb.cpu().numpy().astype(np.int64) & ((1 << (8 * kb.element_size())) - 1)
         m = (t.reshape(1001, h).cpu().numpy() != 0).astype(np.int64)
         want = (m << np.arange(h, dtype=np.int64)[None, :]).sum(1)
         assert np.array_equal(bits, want)
@@ -230,3 +233,37 @@ def test_gatconv_attn_drop_one(mask):
     out = B.fused_gat(g, ft, el, er, 0.2, attn_drop=1.0, seed=3)
     assert th.equal(out, th.zeros_like(out))
     assert K.gat_dropout_scale(1.0) == 0.0 and not K.gat_dropout_keep(3, np.arange(100), 4, 1.0).any()
+
+
+@pytest.mark.parametrize("nb", ["1", "4"])
+def test_keep_words_by_edge_id_and_by_position_agree(nb, monkeypatch):
+    """DGLMIFusedGatKeep* with the keep words by edge id (a random read per edge in the
+    walks) and in the walks' position order (dgl.kernel.gat_keep_walk_order, per column
+    block): the same mask, the same kernels -- bit-identical output, slope aggregates and
+    gradients."""
+    monkeypatch.setenv("DGLMI_GAT_BLOCKS", nb)
+    g, n = _graph(20000, 300000, 31)
+    gidx = g._graph.get_immutable_gidx(th.device(DEV))
+    H, D = 8, 8
+    gen = th.Generator(device=DEV).manual_seed(8)
+    ft = th.randn(n, H, D, device=DEV, generator=gen)
+    el = th.randn(n, H, 1, device=DEV, generator=gen)
+    er = th.randn(n, H, 1, device=DEV, generator=gen)
+    go = th.randn(n, H, D, device=DEV, generator=gen)
+    t = th.nn.functional.dropout(th.ones(gidx.in_csr.nnz, H, 1, device=DEV), 0.5, True)
+    keep = K.gat_keep_bits(t)
+    res = []
+    for pos in (False, True):
+        kin = K.gat_keep_walk_order(gidx, keep, ft, "in") if pos else keep
+        kout = K.gat_keep_walk_order(gidx, keep, ft, "out") if pos else keep
+        out, mx, sm = (th.empty(n, H, D, device=DEV), th.empty(n, H, device=DEV),
+                       th.empty(n, H, device=DEV))
+        lf, ls = th.empty(n, H, D, device=DEV), th.empty(n, H, device=DEV)
+        K.fused_gat_forward(gidx, ft, el, er, 0.2, out, mx, sm, lf, ls, keep=kin, keep_scale=2.0,
+                            keep_pos=pos)
+        gf, gl, gr = th.empty_like(ft), th.empty_like(el), th.empty_like(er)
+        K.fused_gat_backward(gidx, ft, el, er, 0.2, out, mx, sm, go, gf, gl, gr, lf, ls,
+                             keep=kout, keep_scale=2.0, keep_pos=pos)
+        res.append((out, lf, ls, gf, gl, gr))
+    for a, b in zip(*res):
+        assert th.equal(a, b)
