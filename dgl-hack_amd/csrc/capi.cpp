@@ -1018,9 +1018,32 @@ void gat_check_ls(const GatArgs& a, const DGLMIArray* lf, const DGLMIArray* ls) 
 // stays unbiased); t = 2^16 (p >= 1 - 2^-17, p = 1 included) keeps nothing, scale 0.
 // Caller's mask (`keep`, one uint32 word per edge id, bit h = head h kept): the kernels
 // read it through the walk's edge ids and scale kept weights by `keep_scale`.
+// torch's own draws (`draw`, DGLMIFusedGatDraw*): the kernels recompute the fused dropout
+// kernel's Philox draw of element e * H + h (internal.h dropout_draw_slot) for edge e.
+void gat_set_draw(GatArgs& a, const DGLMIDropoutDraw* d, int64_t num_edges) {
+  DGLMI_CHECK(d->vec == 1 || d->vec == 2 || d->vec == 4, "dropout draw: vec must be 1, 2 or 4");
+  DGLMI_CHECK(d->threads >= 1, "dropout draw: threads >= 1");
+  DGLMI_CHECK(d->offset % 4 == 0, "dropout draw: the generator offset is a multiple of 4");
+  DGLMI_CHECK((num_edges * a.H) % d->vec == 0, "dropout draw: E x H is not a multiple of vec");
+  DGLMI_CHECK(std::isfinite(d->keep) && d->keep >= 0.0f && d->keep <= 1.0f, "dropout draw: keep in [0, 1]");
+  DGLMI_CHECK(std::isfinite(d->scale) && d->scale >= 0.0f, "dropout draw: scale finite and >= 0");
+  a.drop = 1;
+  a.drop_rng = 1;
+  a.rng_seed = d->seed;
+  a.rng_ctr = d->offset / 4;
+  a.rng_threads = d->threads;
+  a.rng_vec = d->vec;
+  a.rng_shift = (d->threads & (d->threads - 1)) == 0 ? __builtin_ctzll(static_cast<uint64_t>(d->threads)) : -1;
+  a.rng_keep = d->keep;
+  a.drop_scale = d->scale;
+}
+
 void gat_set_dropout(GatArgs& a, float p, uint64_t seed, const void* keep = nullptr, int keep_bits = 0,
-                     float keep_scale = 0.0f, int64_t num_edges = 0, int keep_pos = 0) {
-  if (keep != nullptr || keep_bits != 0) {
+                     float keep_scale = 0.0f, int64_t num_edges = 0, int keep_pos = 0,
+                     const DGLMIDropoutDraw* draw = nullptr) {
+  if (draw != nullptr) {
+    gat_set_draw(a, draw, num_edges);
+  } else if (keep != nullptr || keep_bits != 0) {
     a.drop_pos = keep_pos != 0 ? 1 : 0;
     a.drop_off = 0;
     DGLMI_CHECK(keep_bits == 8 || keep_bits == 16 || keep_bits == 32, "keep_bits must be 8, 16 or 32");
@@ -1049,13 +1072,13 @@ int gat_forward_impl(const DGLMIGraph* graph, const DGLMIArray* feat_src, const 
                      DGLMIArray* max_out, DGLMIArray* sum_out, DGLMIArray* lf, DGLMIArray* ls,
                      void* stream, float attn_drop = 0.0f, uint64_t seed = 0,
                      const void* keep = nullptr, int keep_bits = 0, float keep_scale = 0.0f,
-                     int keep_pos = 0) {
+                     int keep_pos = 0, const DGLMIDropoutDraw* draw = nullptr) {
   API_BEGIN();
   check_graph32(graph, "fused GAT");
   DeviceGuard guard(graph->device);
   GatArgs a = gat_args(graph, feat_src, el, er, negative_slope, out, max_out, sum_out);
   gat_check_ls(a, lf, ls);
-  gat_set_dropout(a, attn_drop, seed, keep, keep_bits, keep_scale, graph->in_csr.nnz, keep_pos);
+  gat_set_dropout(a, attn_drop, seed, keep, keep_bits, keep_scale, graph->in_csr.nnz, keep_pos, draw);
   a.eids = graph->in_csr.data;
   a.lf = lf ? lf->data : nullptr;
   a.ls = ls ? ls->data : nullptr;
@@ -1162,13 +1185,13 @@ int gat_backward_impl(const DGLMIGraph* graph, const DGLMIArray* feat_src, const
                       const DGLMIArray* ls_in, const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
                       DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream, float attn_drop = 0.0f,
                       uint64_t seed = 0, const void* keep = nullptr, int keep_bits = 0,
-                      float keep_scale = 0.0f, int keep_pos = 0) {
+                      float keep_scale = 0.0f, int keep_pos = 0, const DGLMIDropoutDraw* draw = nullptr) {
   API_BEGIN();
   check_graph32(graph, "fused GAT");
   DeviceGuard guard(graph->device);
   GatArgs a = gat_args(graph, feat_src, el, er, negative_slope, const_cast<DGLMIArray*>(out),
                        const_cast<DGLMIArray*>(max_in), const_cast<DGLMIArray*>(sum_in));
-  gat_set_dropout(a, attn_drop, seed, keep, keep_bits, keep_scale, graph->in_csr.nnz, keep_pos);
+  gat_set_dropout(a, attn_drop, seed, keep, keep_bits, keep_scale, graph->in_csr.nnz, keep_pos, draw);
   // with dropout only the slope-aggregate backward (no destination-side walk) applies
   DGLMI_CHECK(!a.drop || lf_in != nullptr,
               "attention dropout needs the forward's slope aggregates (slope_feat / slope_sum)");
@@ -1396,6 +1419,49 @@ int DGLMIFusedGatKeepBackward(const DGLMIGraph* graph, const DGLMIArray* feat_sr
                            keep, keep_bits, keep_scale, keep_by_position);
 }
 
+int DGLMIFusedGatDrawForward(const DGLMIGraph* graph, const DGLMIArray* feat_src,
+                             const DGLMIArray* el, const DGLMIArray* er, float negative_slope,
+                             const DGLMIDropoutDraw* draw, DGLMIArray* out, DGLMIArray* max_out,
+                             DGLMIArray* sum_out, DGLMIArray* slope_feat, DGLMIArray* slope_sum, void* stream) {
+  if (draw == nullptr) {
+    g_last_error = "DGLMIFusedGatDrawForward: draw is required";
+    return -1;
+  }
+  return gat_forward_impl(graph, feat_src, el, er, negative_slope, out, max_out, sum_out, slope_feat,
+                          slope_sum, stream, 0.0f, 0, nullptr, 0, 0.0f, 0, draw);
+}
+
+int DGLMIFusedGatDrawBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src,
+                              const DGLMIArray* el, const DGLMIArray* er, float negative_slope,
+                              const DGLMIDropoutDraw* draw, const DGLMIArray* out, const DGLMIArray* max_in,
+                              const DGLMIArray* sum_in, const DGLMIArray* slope_feat,
+                              const DGLMIArray* slope_sum, const DGLMIArray* grad_out,
+                              DGLMIArray* grad_feat_src, DGLMIArray* grad_el, DGLMIArray* grad_er,
+                              void* stream) {
+  if (draw == nullptr) {
+    g_last_error = "DGLMIFusedGatDrawBackward: draw is required";
+    return -1;
+  }
+  return gat_backward_impl(graph, feat_src, el, er, negative_slope, out, max_in, sum_in, slope_feat,
+                           slope_sum, grad_out, grad_feat_src, grad_el, grad_er, stream, 0.0f, 0,
+                           nullptr, 0, 0.0f, 0, draw);
+}
+
+int DGLMIDropoutDrawMask(const DGLMIDropoutDraw* draw, int64_t n, uint8_t* mask, void* stream) {
+  API_BEGIN();
+  DGLMI_CHECK(draw != nullptr, "DGLMIDropoutDrawMask: draw is required");
+  DGLMI_CHECK(n >= 0 && (n == 0 || mask != nullptr), "DGLMIDropoutDrawMask: n >= 0, mask");
+  DGLMI_CHECK(draw->vec == 1 || draw->vec == 2 || draw->vec == 4, "DGLMIDropoutDrawMask: vec 1, 2 or 4");
+  DGLMI_CHECK(draw->threads >= 1 && draw->offset % 4 == 0, "DGLMIDropoutDrawMask: threads >= 1, offset % 4 == 0");
+  DGLMI_CHECK(n % draw->vec == 0, "DGLMIDropoutDrawMask: n is not a multiple of vec");
+  const int shift =
+      (draw->threads & (draw->threads - 1)) == 0 ? __builtin_ctzll(static_cast<uint64_t>(draw->threads)) : -1;
+  launch_dropout_draw_mask(draw->seed, draw->offset / 4, draw->threads, draw->vec, shift, draw->keep, n, mask,
+                           static_cast<hipStream_t>(stream));
+  check_hip(hipGetLastError(), "dropout draw mask launch");
+  API_END();
+}
+
 int DGLMIGatKeepGather(const void* keep, int keep_bits, const int32_t* index, int64_t n, void* out,
                        void* stream) {
   API_BEGIN();
@@ -1415,6 +1481,19 @@ int DGLMIGatKeepBits(const float* table, int64_t num_edges, int heads, void* bit
   DGLMI_CHECK(num_edges == 0 || (table != nullptr && bits != nullptr), "DGLMIGatKeepBits: null operand");
   launch_gat_keep_bits(table, num_edges, heads, bits, keep_bits, static_cast<hipStream_t>(stream));
   check_hip(hipGetLastError(), "keep bits launch");
+  API_END();
+}
+
+int DGLMIGatKeepBitsMask(const uint8_t* mask, int64_t num_edges, int heads, void* bits, int keep_bits,
+                         void* stream) {
+  API_BEGIN();
+  DGLMI_CHECK(keep_bits == 8 || keep_bits == 16 || keep_bits == 32, "DGLMIGatKeepBitsMask: keep_bits 8, 16 or 32");
+  DGLMI_CHECK(num_edges >= 0 && heads >= 1 && heads <= keep_bits, "DGLMIGatKeepBitsMask: 1 <= heads <= keep_bits");
+  DGLMI_CHECK(num_edges == 0 || (mask != nullptr && bits != nullptr), "DGLMIGatKeepBitsMask: null operand");
+  DGLMI_CHECK(heads != 8 || reinterpret_cast<uintptr_t>(mask) % 8 == 0,
+              "DGLMIGatKeepBitsMask: an 8-head mask must be 8-byte aligned");
+  launch_gat_keep_bits_mask(mask, num_edges, heads, bits, keep_bits, static_cast<hipStream_t>(stream));
+  check_hip(hipGetLastError(), "keep bits (mask) launch");
   API_END();
 }
 

@@ -403,8 +403,92 @@ struct GatArgs {
   // concatenated in block order) instead of at drop_bits[edge id] (a random read per edge)
   int drop_pos;
   int64_t drop_off;
+  // drop_rng = 1 (DGLMIFusedGatDraw*; drop = 1's instances): edge e, head h is kept when
+  // torch's fused dropout over the (E, H) attention tensor keeps element e * H + h --
+  // its Philox draw recomputed from (rng_seed, rng_ctr = offset / 4, rng_threads = the
+  // draw's grid x 256, rng_vec) by gat_draw_keep, kept below rng_keep = float(1 - p);
+  // rng_shift = log2(rng_threads) when that is a power of two (the capped grid), else -1
+  int drop_rng;
+  int rng_vec;
+  int rng_shift;
+  float rng_keep;
+  uint64_t rng_seed;
+  uint64_t rng_ctr;
+  int64_t rng_threads;
   const int32_t* eids;
 };
+// Philox4x32-10 (Salmon et al., SC'11 "Random123"): the generator torch draws its fused
+// dropout from on this build (hiprand / rocrand's philox4x32_10).  Counter (x, y) = the
+// draw index on top of offset / 4, (z, w) = the drawing thread's subsequence; the key is
+// the 64-bit seed, bumped by the Weyl constants between the ten rounds.
+__host__ __device__ __forceinline__ uint32_t philox_mulhi(uint32_t a, uint32_t b) {
+  return static_cast<uint32_t>((static_cast<uint64_t>(a) * b) >> 32);
+}
+struct Philox4 {
+  uint32_t x, y, z, w;
+};
+__host__ __device__ __forceinline__ Philox4 philox4x32_10(Philox4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = philox_mulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+    const uint32_t hi1 = philox_mulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+    c = Philox4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+// torch's fused dropout kernel (256-thread blocks, grid capped at CUs x 8, one uniform4
+// draw per thread per pass; scripts/philox_probe.py pins the mapping on this build) as a
+// function of the element index i: which thread t drew it, in which of that thread's
+// draws j, which component.  vec 4 (numel % 4 == 0): four consecutive elements per thread
+// and pass; vec 2: two, a fresh draw every pass (components x, y); vec 1 (the unrolled
+// scalar kernel): element i is thread i % T's, pass q = i / T, draw q / 4, component q % 4.
+struct DrawSlot {
+  int64_t t, j;
+  int comp;
+};
+__host__ __device__ __forceinline__ DrawSlot dropout_draw_slot(int64_t i, int vec, int64_t T, int shift) {
+  DrawSlot s;
+  const int64_t c = vec == 4 ? i >> 2 : vec == 2 ? i >> 1 : i;
+  int64_t q, t;
+  if (shift >= 0) {
+    q = c >> shift;
+    t = c & (T - 1);
+  } else {
+    q = c / T;
+    t = c - q * T;
+  }
+  s.t = t;
+  if (vec == 4) {
+    s.j = q;
+    s.comp = static_cast<int>(i & 3);
+  } else if (vec == 2) {
+    s.j = q;
+    s.comp = static_cast<int>(i & 1);
+  } else {
+    s.j = q >> 2;
+    s.comp = static_cast<int>(q & 3);
+  }
+  return s;
+}
+__host__ __device__ __forceinline__ Philox4 dropout_draw(uint64_t seed, uint64_t ctr, const DrawSlot& s) {
+  const uint64_t c = ctr + static_cast<uint64_t>(s.j);
+  const uint64_t t = static_cast<uint64_t>(s.t);
+  return philox4x32_10(Philox4{static_cast<uint32_t>(c), static_cast<uint32_t>(c >> 32),
+                               static_cast<uint32_t>(t), static_cast<uint32_t>(t >> 32)},
+                       static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
+}
+// rocrand's uniform: 2^-32 + v 2^-32 (exact with or without contraction: the product is a
+// power-of-two scaling), kept when below the keep probability
+__host__ __device__ __forceinline__ bool dropout_draw_kept(const Philox4& r, int comp, float keep) {
+  const uint32_t v = comp == 0 ? r.x : comp == 1 ? r.y : comp == 2 ? r.z : r.w;
+  return 2.3283064365386963e-10f + static_cast<float>(v) * 2.3283064365386963e-10f < keep;
+}
+// mask[i] = kept(i) for i < n: the draw's whole mask (DGLMIDropoutDrawMask: tests, and the
+// self-check against torch.native_dropout before the fused route trusts the mapping)
+void launch_dropout_draw_mask(uint64_t seed, uint64_t ctr, int64_t threads, int vec, int shift, float keep,
+                              int64_t n, uint8_t* mask, hipStream_t s);
 // The dropout mask's hash (mirrored in numpy by dgl.kernel.gat_dropout_keep for the
 // tests): one key per edge -- a 32-bit avalanche mix of the edge id keyed by the seed's
 // low half, xor the high half -- then, per PAIR of heads, a one-multiply finish of
@@ -438,6 +522,7 @@ bool gat_supported(int64_t H, int64_t D);
 // dropout output table (E, H) in edge-id order packed to one keep word of `width` bits
 // (8, 16 or 32) per edge (drop = 2)
 void launch_gat_keep_bits(const float* table, int64_t n, int H, void* bits, int width, hipStream_t s);
+void launch_gat_keep_bits_mask(const uint8_t* mask, int64_t n, int H, void* bits, int width, hipStream_t s);
 // out[i] = keep[index[i]], i < n, words of `width` bits: edge-id keep words into a walk's
 // position order (index = the walk CSR's edge ids)
 void launch_gat_keep_gather(const void* keep, int width, const int32_t* index, int64_t n, void* out,

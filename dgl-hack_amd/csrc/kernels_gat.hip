@@ -92,6 +92,77 @@ __device__ __forceinline__ float head_sum(float x, int d4) {
 // at 8 x 8).  The edge loop only tests a bit: a hash there (round 4 kept one for
 // H > 32, which the compiler evaluated for every edge and selected away) cost ~24 VALU
 // instructions per edge and lane.  The C entry takes H <= 32 (gat_set_dropout).
+// torch's own draws (drop_rng): the H elements e * H + h of the (E, H) draw, one Philox
+// block per run of elements that share a (thread, draw) slot -- two per edge at H = 8
+// with vec 4 -- recomputed in every walk instead of a mask read back per edge (DROP 3).
+// One 32 x 32 -> 64 multiply as a single v_mad_u64_u32 (hipcc emits v_mul_hi_u32 +
+// v_mul_lo_u32): 1.42x the Philox block rate on gfx950 (scripts/philox_rate_probe.hip:
+// 657 vs 463 G blocks/s).  The carry-out lands in an SGPR pair, unused.
+__device__ __forceinline__ void philox_mul(uint32_t m, uint32_t x, uint32_t& hi, uint32_t& lo) {
+  uint64_t r, c;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(c) : "v"(m), "v"(x));
+  hi = static_cast<uint32_t>(r >> 32);
+  lo = static_cast<uint32_t>(r);
+}
+// two independent Philox4x32-10 blocks in lockstep (the dependent chain of one block is
+// latency-bound in the staging lane; two interleave)
+__device__ __forceinline__ void philox_pair(Philox4& c0, Philox4& c1, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t h00, l00, h01, l01, h10, l10, h11, l11;
+    philox_mul(0xD2511F53u, c0.x, h00, l00);
+    philox_mul(0xD2511F53u, c1.x, h10, l10);
+    philox_mul(0xCD9E8D57u, c0.z, h01, l01);
+    philox_mul(0xCD9E8D57u, c1.z, h11, l11);
+    c0 = Philox4{h01 ^ c0.y ^ k0, l01, h00 ^ c0.w ^ k1, l00};
+    c1 = Philox4{h11 ^ c1.y ^ k0, l11, h10 ^ c1.w ^ k1, l10};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+__device__ __forceinline__ Philox4 draw_counter(const GatArgs& a, const DrawSlot& s) {
+  const uint64_t c = a.rng_ctr + static_cast<uint64_t>(s.j);
+  const uint64_t t = static_cast<uint64_t>(s.t);
+  return Philox4{static_cast<uint32_t>(c), static_cast<uint32_t>(c >> 32), static_cast<uint32_t>(t),
+                 static_cast<uint32_t>(t >> 32)};
+}
+__device__ __forceinline__ uint32_t draw_nibble(const Philox4& r, float keep) {
+  return (dropout_draw_kept(r, 0, keep) ? 1u : 0u) | (dropout_draw_kept(r, 1, keep) ? 2u : 0u) |
+         (dropout_draw_kept(r, 2, keep) ? 4u : 0u) | (dropout_draw_kept(r, 3, keep) ? 8u : 0u);
+}
+__device__ __forceinline__ uint32_t gat_draw_keep(const GatArgs& a, int32_t eid) {
+  if (a.rng_vec == 4 && (a.H & 3) == 0) {
+    // whole blocks: edge e's elements are the uniforms of draws e H / 4 + b, b < H / 4,
+    // taken two at a time (H = 8: exactly one pair)
+    const uint32_t k0 = static_cast<uint32_t>(a.rng_seed), k1 = static_cast<uint32_t>(a.rng_seed >> 32);
+    const int nb = a.H >> 2;
+    const int64_t c0 = static_cast<int64_t>(eid) * nb;
+    uint32_t kb = 0;
+    for (int b = 0; b < nb; b += 2) {
+      const int64_t ca = c0 + b, cb = c0 + (b + 1 < nb ? b + 1 : b);
+      Philox4 r0 = draw_counter(a, dropout_draw_slot(ca << 2, 4, a.rng_threads, a.rng_shift));
+      Philox4 r1 = draw_counter(a, dropout_draw_slot(cb << 2, 4, a.rng_threads, a.rng_shift));
+      philox_pair(r0, r1, k0, k1);
+      kb |= draw_nibble(r0, a.rng_keep) << (4 * b);
+      if (b + 1 < nb) kb |= draw_nibble(r1, a.rng_keep) << (4 * (b + 1));
+    }
+    return kb;
+  }
+  uint32_t kb = 0;
+  int64_t lt = -1, lj = -1;
+  Philox4 r{0u, 0u, 0u, 0u};
+  const int64_t i0 = static_cast<int64_t>(eid) * a.H;
+  for (int h = 0; h < a.H; ++h) {
+    const DrawSlot s = dropout_draw_slot(i0 + h, a.rng_vec, a.rng_threads, a.rng_shift);
+    if (s.t != lt || s.j != lj) {
+      r = dropout_draw(a.rng_seed, a.rng_ctr, s);
+      lt = s.t;
+      lj = s.j;
+    }
+    kb |= (dropout_draw_kept(r, s.comp, a.rng_keep) ? 1u : 0u) << h;
+  }
+  return kb;
+}
 __device__ __forceinline__ uint32_t gat_stage_keep(const GatArgs& a, int32_t eid) {
   const uint32_t key = gat_edge_key(a.drop_seed, static_cast<uint32_t>(eid));
   uint32_t kb = 0;
@@ -115,7 +186,8 @@ __device__ __forceinline__ uint32_t gat_keep_word(const GatArgs& a, int32_t e) {
 // ---------------------------------------------------------------------------
 // LS: also the slope aggregates lf / ls (carry record [acc F][m H][l H][lf F][ls H])
 // DROP: attention dropout (a separate instance, so the plain walk's code is untouched):
-// 1 the hashed mask, 2 the caller's keep words (GatArgs.drop_bits)
+// 1 the hashed mask, 2 the caller's keep words (GatArgs.drop_bits), 3 torch's dropout
+// draws recomputed from the generator state (GatArgs.drop_rng)
 template <int L, int NV, bool O32, bool LS, int DROP = 0>
 __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
   static_assert(L >= 1 && L <= 64, "a lane group must fit in one wavefront");
@@ -138,6 +210,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
   const int64_t CW = LS ? 2 * a.F + 3 * H : a.F + 2 * H;  // carry record, see above
   constexpr bool drop = DROP != 0;
   constexpr bool table = DROP == 2;  // the caller's keep words, else the hash
+  constexpr bool draw = DROP == 3;   // torch's dropout draws (gat_draw_keep)
   int hd[NV], fl[NV];
   bool ok4[NV], lead[NV];
 #pragma unroll
@@ -253,7 +326,10 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd(GatArgs a) {
       s_col[g][q] = nc[i];
       if constexpr (drop)
         s_keep[drop ? g : 0][drop ? q : 0] =
-            nr[i] == INT_MAX ? 0u : table ? nk[table ? i : 0] : gat_stage_keep(a, ne[drop ? i : 0]);
+            nr[i] == INT_MAX ? 0u
+            : table ? nk[table ? i : 0]
+            : draw  ? gat_draw_keep(a, ne[drop ? i : 0])
+                    : gat_stage_keep(a, ne[drop ? i : 0]);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -564,6 +640,7 @@ __device__ __forceinline__ void gat_bwd_src_body(const GatArgs& a) {
   __shared__ uint32_t s_keep[DROP ? G : 1][DROP ? B : 1];  // dropout keep bits (gat_stage_keep)
   constexpr bool drop = DROP != 0;
   constexpr bool table = DROP == 2;  // the caller's keep words, else the hash
+  constexpr bool draw = DROP == 3;   // torch's dropout draws (gat_draw_keep)
   const int g = threadIdx.x / L;
   const int lane = threadIdx.x % L;
   const int64_t chunk = (int64_t)blockIdx.x * G + g;
@@ -673,7 +750,10 @@ __device__ __forceinline__ void gat_bwd_src_body(const GatArgs& a) {
       s_col[g][q] = nc[i];
       if constexpr (drop)
         s_keep[drop ? g : 0][drop ? q : 0] =
-            nr[i] == INT_MAX ? 0u : table ? nk[table ? i : 0] : gat_stage_keep(a, ne[drop ? i : 0]);
+            nr[i] == INT_MAX ? 0u
+            : table ? nk[table ? i : 0]
+            : draw  ? gat_draw_keep(a, ne[drop ? i : 0])
+                    : gat_stage_keep(a, ne[drop ? i : 0]);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -917,6 +997,9 @@ void fwd_cfg(const GatArgs& a, hipStream_t s) {
   if (a.drop == 2) {  // dropout instances for 32-bit offsets only (checked by the C entry)
     if (ls) hipLaunchKernelGGL((k_gat_fwd<L, NV, true, true, 2>), dim3(blocks), dim3(kBlock), 0, s, a);
     else hipLaunchKernelGGL((k_gat_fwd<L, NV, true, false, 2>), dim3(blocks), dim3(kBlock), 0, s, a);
+  } else if (a.drop && a.drop_rng) {
+    if (ls) hipLaunchKernelGGL((k_gat_fwd<L, NV, true, true, 3>), dim3(blocks), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((k_gat_fwd<L, NV, true, false, 3>), dim3(blocks), dim3(kBlock), 0, s, a);
   } else if (a.drop) {
     if (ls) hipLaunchKernelGGL((k_gat_fwd<L, NV, true, true, 1>), dim3(blocks), dim3(kBlock), 0, s, a);
     else hipLaunchKernelGGL((k_gat_fwd<L, NV, true, false, 1>), dim3(blocks), dim3(kBlock), 0, s, a);
@@ -953,6 +1036,8 @@ void bwd_src_cfg(const GatArgs& a, hipStream_t s) {
   const unsigned blocks = static_cast<unsigned>((chunks + G - 1) / G);
   if (a.drop == 2)  // dropout instances for 32-bit offsets only (checked by the C entry)
     hipLaunchKernelGGL((k_gat_bwd_src<L, NV, true, 2>), dim3(blocks), dim3(kBlock), 0, s, a);
+  else if (a.drop && a.drop_rng)
+    hipLaunchKernelGGL((k_gat_bwd_src<L, NV, true, 3>), dim3(blocks), dim3(kBlock), 0, s, a);
   else if (a.drop)
     hipLaunchKernelGGL((k_gat_bwd_src<L, NV, true, 1>), dim3(blocks), dim3(kBlock), 0, s, a);
   else if (a.o32)
@@ -1026,6 +1111,50 @@ __global__ void k_gat_keep_bits(const float* __restrict__ table, int64_t n, int 
     for (int h = 0; h < H; ++h) w |= (table[e * H + h] != 0.0f ? 1u : 0u) << h;
     bits[e] = static_cast<T>(w);
   }
+}
+__global__ void k_dropout_draw_mask(uint64_t seed, uint64_t ctr, int64_t threads, int vec, int shift, float keep,
+                                    int64_t n, uint8_t* __restrict__ mask) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const DrawSlot s = dropout_draw_slot(i, vec, threads, shift);
+    mask[i] = dropout_draw_kept(dropout_draw(seed, ctr, s), s.comp, keep) ? 1 : 0;
+  }
+}
+void launch_dropout_draw_mask(uint64_t seed, uint64_t ctr, int64_t threads, int vec, int shift, float keep,
+                              int64_t n, uint8_t* mask, hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t want = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_dropout_draw_mask, dim3(static_cast<unsigned>(want < 65536 ? want : 65536)), dim3(kBlock),
+                     0, s, seed, ctr, threads, vec, shift, keep, n, mask);
+}
+// The same from the dropout's own mask (E, H) bytes, 1 = kept (torch.native_dropout's
+// second output): a quarter of the table's bytes.  H = 8 (the reference GAT's heads) reads
+// a row as one 8-byte load.
+template <typename T>
+__global__ void k_gat_keep_bits_mask(const uint8_t* __restrict__ mask, int64_t n, int H, T* __restrict__ bits) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < n; e += stride) {
+    uint32_t w = 0;
+    if (H == 8) {
+      const uint64_t v = reinterpret_cast<const uint64_t*>(mask)[e];
+#pragma unroll
+      for (int h = 0; h < 8; ++h) w |= (((v >> (8 * h)) & 0xffu) != 0 ? 1u : 0u) << h;
+    } else {
+      for (int h = 0; h < H; ++h) w |= (mask[e * H + h] != 0 ? 1u : 0u) << h;
+    }
+    bits[e] = static_cast<T>(w);
+  }
+}
+void launch_gat_keep_bits_mask(const uint8_t* mask, int64_t n, int H, void* bits, int width, hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t want = (n + kBlock - 1) / kBlock;
+  const dim3 grid(static_cast<unsigned>(want < 65536 ? want : 65536)), blk(kBlock);
+  if (width == 8)
+    hipLaunchKernelGGL(k_gat_keep_bits_mask<uint8_t>, grid, blk, 0, s, mask, n, H, static_cast<uint8_t*>(bits));
+  else if (width == 16)
+    hipLaunchKernelGGL(k_gat_keep_bits_mask<uint16_t>, grid, blk, 0, s, mask, n, H, static_cast<uint16_t*>(bits));
+  else
+    hipLaunchKernelGGL(k_gat_keep_bits_mask<uint32_t>, grid, blk, 0, s, mask, n, H, static_cast<uint32_t*>(bits));
 }
 void launch_gat_keep_bits(const float* table, int64_t n, int H, void* bits, int width, hipStream_t s) {
   if (n <= 0) return;

@@ -83,6 +83,18 @@ class Epilogue(ctypes.Structure):
     ]
 
 
+class DropoutDraw(ctypes.Structure):
+    """DGLMIDropoutDraw (include/dglmi.h): torch's fused dropout draw, as launched."""
+    _fields_ = [
+        ("seed", ctypes.c_uint64),
+        ("offset", ctypes.c_uint64),
+        ("threads", ctypes.c_int64),
+        ("vec", ctypes.c_int32),
+        ("keep", ctypes.c_float),
+        ("scale", ctypes.c_float),
+    ]
+
+
 class Array(ctypes.Structure):
     _fields_ = [
         ("data", ctypes.c_void_p),
@@ -208,10 +220,26 @@ _SIGS = {
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
         ctypes.POINTER(Array), ctypes.c_void_p]),
+    "DGLMIFusedGatDrawForward": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_float, ctypes.POINTER(DropoutDraw),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.c_void_p]),
+    "DGLMIFusedGatDrawBackward": (ctypes.c_int, [
+        ctypes.POINTER(Graph), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.c_float, ctypes.POINTER(DropoutDraw),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array), ctypes.POINTER(Array),
+        ctypes.POINTER(Array), ctypes.c_void_p]),
+    "DGLMIDropoutDrawMask": (ctypes.c_int, [
+        ctypes.POINTER(DropoutDraw), ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
     "DGLMIGatKeepGather": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
         ctypes.c_void_p]),
     "DGLMIGatKeepBits": (ctypes.c_int, [
+        ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+        ctypes.c_void_p]),
+    "DGLMIGatKeepBitsMask": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
         ctypes.c_void_p]),
     "DGLMIFusedGatKernel": (ctypes.c_int, [

@@ -486,11 +486,12 @@ class FusedGat(th.autograd.Function):
     kernels, the mask a hash of ``seed`` and the edge id, recomputed by the backward
     (DGLMIFusedGatDropout*; always with the slope aggregates).  ``keep`` (E,) keep
     words with ``keep_scale`` instead: the caller's mask (DGLMIFusedGatKeep*; GATConv's
-    own nn.Dropout draws)."""
+    own nn.Dropout draws).  ``draw`` (dgl.kernel.dropout_draw) instead: torch's own draws
+    recomputed inside the walks (DGLMIFusedGatDraw*; no mask in memory)."""
 
     @staticmethod
     def forward(ctx, gidx, feat_src, el, er, slope, attn_drop=0.0, seed=0, keep=None,
-                keep_scale=None):
+                keep_scale=None, draw=None):
         feat_src, el, er = feat_src.contiguous(), el.contiguous(), er.contiguous()
         n_dst = er.shape[0]
         H, D = feat_src.shape[1], feat_src.shape[2]
@@ -499,7 +500,7 @@ class FusedGat(th.autograd.Function):
         sm = feat_src.new_empty((n_dst, H))
         lf = ls = None
         if any(ctx.needs_input_grad[1:4]) and (
-                attn_drop > 0.0 or keep is not None
+                attn_drop > 0.0 or keep is not None or draw is not None
                 or os.environ.get("DGLMI_GAT_SLOPES", "1") != "0"):
             lf = feat_src.new_empty((n_dst, H, D))
             ls = feat_src.new_empty((n_dst, H))
@@ -516,8 +517,9 @@ class FusedGat(th.autograd.Function):
                 keep_out = K.gat_keep_walk_order(gidx, keep, feat_src, "out") if pos_out else keep
         K.fused_gat_forward(gidx, feat_src, el, er, slope, out, mx, sm, lf, ls,
                             attn_drop=attn_drop, seed=seed, keep=keep_in, keep_scale=keep_scale,
-                            keep_pos=pos_in)
+                            keep_pos=pos_in, draw=draw)
         del keep_in
+        ctx.draw = draw
         ctx.gidx, ctx.slope = gidx, slope
         ctx.attn_drop, ctx.seed = attn_drop, seed
         ctx.keep, ctx.keep_scale, ctx.keep_pos = keep_out, keep_scale, pos_out
@@ -540,12 +542,12 @@ class FusedGat(th.autograd.Function):
         K.fused_gat_backward(ctx.gidx, feat_src, el, er, ctx.slope, out, mx, sm, grad_out, g_ft,
                              g_el, g_er, lf, ls, attn_drop=ctx.attn_drop, seed=ctx.seed,
                              keep=ctx.keep, keep_scale=ctx.keep_scale,
-                             keep_pos=getattr(ctx, "keep_pos", False))
-        return None, g_ft, g_el, g_er, None, None, None, None, None
+                             keep_pos=getattr(ctx, "keep_pos", False), draw=ctx.draw)
+        return None, g_ft, g_el, g_er, None, None, None, None, None, None
 
 
 def fused_gat(graph, feat_src, el, er, slope, attn_drop=0.0, seed=None, keep=None,
-              keep_scale=None):
+              keep_scale=None, draw=None):
     """backend.py:1235 / tensor.py:415-420: softmax attention + aggregation in one kernel.
 
     ``graph`` is a DGLGraph (or an ImmutableGraphIndex); feat_src (N, H, D), el / er
@@ -556,9 +558,14 @@ def fused_gat(graph, feat_src, el, er, slope, attn_drop=0.0, seed=None, keep=Non
       caller's mask -- GATConv passes its own ``nn.Dropout``'s draws, the reference's;
     * ``attn_drop`` > 0: a hashed mask keyed by ``seed`` (default: drawn from torch's
       default generator, so ``torch.manual_seed`` reproduces it) -- no (E, H) buffer, not
-      torch's draws."""
+      torch's draws;
+    * ``draw`` (:func:`dgl.kernel.dropout_draw`, taken for the (E, H) attention tensor):
+      torch's own draws recomputed inside the kernels -- GATConv's default when
+      :func:`dgl.kernel.dropout_draw_ok`."""
     gidx = graph if hasattr(graph, "in_csr") else graph._graph.get_immutable_gidx(feat_src.device)
     attn_drop = float(attn_drop)
+    if draw is not None:
+        return FusedGat.apply(gidx, feat_src, el, er, float(slope), 0.0, 0, None, None, draw)
     if keep is not None:
         if keep_scale is None:
             raise DGLError("fused_gat: keep needs keep_scale")

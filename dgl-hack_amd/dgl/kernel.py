@@ -370,21 +370,28 @@ def gat_dropout_scale(p):
 
 
 def gat_keep_bits(table):
-    """One keep word per edge from a dropout output ``table`` (E, H[, 1]) in edge-id order:
-    bit h set where head h was kept (non-zero), in the narrowest word that holds H (uint8
-    for H <= 8, int16 for H <= 16, int32 for H <= 32) -> DGLMIGatKeepBits."""
-    t = table.reshape(table.shape[0], -1)
-    if t.dtype != th.float32 or not t.is_cuda:
-        raise DGLError("gat_keep_bits: a float32 ROCm table")
+    """One keep word per edge from a dropout output ``table`` (E, H[, 1]) float32 or the
+    dropout's boolean mask (torch.native_dropout's second output) in edge-id order: bit h
+    set where head h was kept (non-zero / True), in the narrowest word that holds H (uint8
+    for H <= 8, int16 for H <= 16, int32 for H <= 32) -> DGLMIGatKeepBits[Mask]."""
+    h = 1
+    for d in table.shape[1:]:
+        h *= int(d)
+    t = table.reshape(table.shape[0], h)
+    is_mask = t.dtype == th.bool
+    if not (is_mask or t.dtype == th.float32) or not t.is_cuda:
+        raise DGLError("gat_keep_bits: a float32 table or a bool mask on the ROCm device")
     t = t.contiguous()
     h = int(t.shape[1])
     if not 1 <= h <= 32:
         raise DGLError("gat_keep_bits: 1 <= heads <= 32")
     dt, width = (th.uint8, 8) if h <= 8 else (th.int16, 16) if h <= 16 else (th.int32, 32)
     bits = th.empty(t.shape[0], dtype=dt, device=t.device)
-    check_call(_ffi.lib().DGLMIGatKeepBits(
-        ctypes.c_void_p(t.data_ptr()), ctypes.c_int64(t.shape[0]), h,
-        ctypes.c_void_p(bits.data_ptr()), width, _stream(bits)))
+    if is_mask and h == 8 and t.data_ptr() % 8:
+        t = t.clone()  # the 8-head path reads a row as one 8-byte word
+    entry = _ffi.lib().DGLMIGatKeepBitsMask if is_mask else _ffi.lib().DGLMIGatKeepBits
+    check_call(entry(ctypes.c_void_p(t.data_ptr() if t.numel() else None), ctypes.c_int64(t.shape[0]), h,
+                     ctypes.c_void_p(bits.data_ptr() if bits.numel() else None), width, _stream(bits)))
     return bits
 
 
@@ -418,9 +425,70 @@ def gat_keep_walk_order(graph, keep, feat_src, direction):
     return out
 
 
+def dropout_draw(device, numel, p):
+    """Take torch's fused dropout draw for a contiguous float32 tensor of ``numel``
+    elements on ``device`` with drop probability 0 < ``p`` < 1, as nn.Dropout(p) would:
+    the generator's Philox offset advances by the draws per thread (the kernel's 256-thread
+    blocks, grid capped at CUs x maxThreadsPerCU / 256, four uniforms a draw), and the
+    returned DGLMIDropoutDraw lets the fused GAT kernels recompute every element's keep
+    decision (DGLMIFusedGatDraw*).  Not under stream capture (the generator's captured
+    offsets are device-side); callers check :func:`dropout_draw_ok` first."""
+    dev = th.device(device)
+    props = th.cuda.get_device_properties(dev)
+    blocks = props.multi_processor_count * (props.max_threads_per_multi_processor // 256)
+    grid = min(blocks, (numel + 255) // 256)
+    inc = ((numel - 1) // (256 * grid * 4) + 1) * 4
+    gen = th.cuda.default_generators[dev.index if dev.index is not None else th.cuda.current_device()]
+    seed, off = gen.initial_seed(), gen.get_offset()
+    gen.set_offset(off + inc)
+    vec = 4 if numel % 4 == 0 else 2 if numel % 2 == 0 else 1
+    keep = np.float32(1.0 - float(p))
+    return _ffi.DropoutDraw(seed & 0xFFFFFFFFFFFFFFFF, off, grid * 256, vec, float(keep),
+                            float(np.float32(1.0 / float(keep))))
+
+
+def dropout_draw_mask(draw, numel, device):
+    """The draw's whole keep mask (bool, ``numel``) -> DGLMIDropoutDrawMask."""
+    out = th.empty(numel, dtype=th.uint8, device=device)
+    check_call(_ffi.lib().DGLMIDropoutDrawMask(
+        ctypes.byref(draw), ctypes.c_int64(numel), ctypes.c_void_p(out.data_ptr() if numel else None),
+        _stream(out)))
+    return out.bool()
+
+
+_DRAW_OK = {}
+
+
+def dropout_draw_ok(device):
+    """Whether :func:`dropout_draw` reproduces torch.native_dropout on this device and
+    build: checked once per device against torch itself -- the masks of a vec-4 draw with
+    the grid capped, vec-2 and vec-1 draws, and the generator offset each leaves -- with
+    the generator state restored afterwards.  False under stream capture."""
+    dev = th.device(device)
+    if dev.type != "cuda" or th.cuda.is_current_stream_capturing():
+        return False
+    idx = dev.index if dev.index is not None else th.cuda.current_device()
+    if idx not in _DRAW_OK:
+        gen = th.cuda.default_generators[idx]
+        state = gen.get_state()
+        ok = True
+        try:
+            for n in ((1 << 23) + 8, 2002, 3003, 2 * ((1 << 21) + 1)):
+                gen.manual_seed(1234 + n)
+                d = dropout_draw(dev, n, 0.6)
+                after = gen.get_offset()
+                gen.manual_seed(1234 + n)
+                _, m = th.native_dropout(th.empty(n, device=dev), 0.6, True)
+                ok = ok and gen.get_offset() == after and bool(th.equal(dropout_draw_mask(d, n, dev), m))
+        finally:
+            gen.set_state(state)
+        _DRAW_OK[idx] = ok
+    return _DRAW_OK[idx]
+
+
 def fused_gat_forward(graph, feat_src, el, er, slope, out, max_out, sum_out, slope_feat=None,
                       slope_sum=None, attn_drop=0.0, seed=0, keep=None, keep_scale=None,
-                      keep_pos=False):
+                      keep_pos=False, draw=None):
     """_CAPI_DGLFusedGatKernel (binary_reduce.cc:380-396) -> DGLMIFusedGatForward, or
     with ``slope_feat`` (N, H, D) / ``slope_sum`` (N, H) DGLMIFusedGatForwardEx: the
     forward also keeps the attention's slope aggregates, so the backward needs no
@@ -428,9 +496,17 @@ def fused_gat_forward(graph, feat_src, el, er, slope, out, max_out, sum_out, slo
     attention dropout in the same pass, the mask a hash of ``seed`` and the edge id).
     ``keep`` (E,) keep words (:func:`gat_keep_bits`) with ``keep_scale``:
     DGLMIFusedGatKeepForward, the caller's mask -- by edge id, or with ``keep_pos`` in the
-    forward walk's position order (:func:`gat_keep_walk_order` "in")."""
+    forward walk's position order (:func:`gat_keep_walk_order` "in").  ``draw``
+    (:func:`dropout_draw`): DGLMIFusedGatDrawForward, torch's own draws recomputed."""
     _check_ctx(graph, [("feat_src", feat_src), ("el", el), ("er", er), ("out", out)])
     g = graph.cstruct(None, col_blocks=gat_col_blocks(graph, feat_src))
+    if draw is not None:
+        check_call(_ffi.lib().DGLMIFusedGatDrawForward(
+            ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"),
+            float(slope), ctypes.byref(draw), _arr(out, "out"), _arr(max_out, "max_out"),
+            _arr(sum_out, "sum_out"), _arr(slope_feat, "slope_feat"), _arr(slope_sum, "slope_sum"),
+            _stream(out)))
+        return out
     if keep is not None:
         kp, kb = _keep_words(keep, "keep", graph.in_csr.nnz)
         check_call(_ffi.lib().DGLMIFusedGatKeepForward(
@@ -458,13 +534,26 @@ def fused_gat_forward(graph, feat_src, el, er, slope, out, max_out, sum_out, slo
 
 def fused_gat_backward(graph, feat_src, el, er, slope, out, max_in, sum_in, grad_out,
                        grad_feat_src, grad_el, grad_er, slope_feat=None, slope_sum=None,
-                       attn_drop=0.0, seed=0, keep=None, keep_scale=None, keep_pos=False):
+                       attn_drop=0.0, seed=0, keep=None, keep_scale=None, keep_pos=False,
+                       draw=None):
     """_CAPI_DGLKernelBackwardFusedGat (binary_reduce.cc:529-549) -> DGLMIFusedGatBackward
     (or DGLMIFusedGatBackwardEx with the forward's slope aggregates; with ``attn_drop`` > 0
     DGLMIFusedGatDropoutBackward, the forward's seed; with ``keep``
     DGLMIFusedGatKeepBackward, the forward's mask -- by edge id, or with ``keep_pos`` in the
-    backward walk's position order, :func:`gat_keep_walk_order` "out")."""
+    backward walk's position order, :func:`gat_keep_walk_order` "out"; with ``draw``
+    DGLMIFusedGatDrawBackward, the forward's draw)."""
     _check_ctx(graph, [("feat_src", feat_src), ("grad_out", grad_out)])
+    if draw is not None:
+        if slope_feat is None:
+            raise DGLError("fused GAT dropout backward needs the forward's slope aggregates")
+        g = graph.cstruct(None, col_blocks=gat_col_blocks(graph, feat_src, backward=True))
+        check_call(_ffi.lib().DGLMIFusedGatDrawBackward(
+            ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"),
+            float(slope), ctypes.byref(draw), _arr(out, "out"), _arr(max_in, "max_in"),
+            _arr(sum_in, "sum_in"), _arr(slope_feat, "slope_feat"), _arr(slope_sum, "slope_sum"),
+            _arr(grad_out, "grad_out"), _arr(grad_feat_src, "grad_feat_src"), _arr(grad_el, "grad_el"),
+            _arr(grad_er, "grad_er"), _stream(grad_out)))
+        return
     if keep is not None:
         if slope_feat is None:
             raise DGLError("fused GAT dropout backward needs the forward's slope aggregates")

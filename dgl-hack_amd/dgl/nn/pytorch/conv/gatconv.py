@@ -7,10 +7,12 @@ broadcast over the head dimension (the load-balanced HIP kernel).  When the
 head size suits the fused kernel, the middle of that chain (u_add_v ..
 u_mul_e_sum) runs as ONE fused HIP kernel (``dgl.backend.fused_gat``; same math,
 max-stabilised in both forms), attention dropout in training included: by default
-the module's own ``nn.Dropout`` draws the mask on an (E, H, 1) tensor of ones in
-edge-id order -- the draws the reference's ``self.attn_drop(edge_softmax(...))``
-(gatconv.py:154) makes under the same seed -- packed to one keep word per edge that
-the fused kernels read (``attn_drop_mask = "module"``); ``attn_drop_mask =
+the module's own ``nn.Dropout`` draws over an (E, H, 1) tensor in edge-id order -- the
+draws the reference's ``self.attn_drop(edge_softmax(...))`` (gatconv.py:154) makes under
+the same seed -- recomputed inside the fused kernels from the generator state
+(``dgl.kernel.dropout_draw``; once checked against torch.native_dropout per device), or
+drawn by torch.native_dropout and packed to one keep word per edge
+(``attn_drop_mask = "module"``); ``attn_drop_mask =
 "hashed"`` opts into a mask hashed inside the kernels from a per-call seed (the same
 Bernoulli(1 - p) per edge and head, not torch's draws; no (E, H) tensors).  Set
 ``use_fused = False`` on the module to force the unfused composition.
@@ -37,6 +39,15 @@ FUSED_LEAKY = True
 # the position-space composition's backward as ONE fused pass pair (backend.GatComposition:
 # the forward unchanged, the gradients within fp32 rounding); False: step by step
 FUSED_COMPOSITION_BACKWARD = True
+# the fused route's module-mask draw: torch.native_dropout -- what nn.Dropout's forward
+# runs on a ROCm tensor with 0 < p < 1 -- on an UNINITIALISED (E, H, 1) tensor of this
+# dtype, keeping only its boolean mask: the draws depend on the generator, the element
+# count and the vector width, not on the values (scripts/dropout_draw_probe.py)
+MODULE_DRAW_DTYPE = th.float32
+# ... or, when dgl.kernel.dropout_draw_ok (checked once per device against torch itself),
+# those draws recomputed inside the fused walks from the generator state (no mask, no
+# gathers; DGLMIFusedGatDraw*)
+MODULE_DRAW_IN_KERNEL = True
 
 
 def expand_as_pair(x):
@@ -190,16 +201,28 @@ class GATConv(nn.Module):
             if self.attn_drop_mask == "hashed":
                 kw = {"attn_drop": p}
             else:
-                # this module's nn.Dropout on (E, H, 1) ones in edge-id order: the RNG
+                # this module's nn.Dropout draws on (E, H, 1) in edge-id order: the RNG
                 # draws of the reference's attn_drop(a) (same shape, same layout), packed
-                # to one keep word per edge; kept weights take torch's scale
-                # float(1 / float(1 - p)) (its fused dropout kernel's)
+                # from the dropout's boolean mask to one keep word per edge; kept weights
+                # take torch's scale float(1 / float(1 - p)) (its fused dropout kernel's)
                 gidx = graph if hasattr(graph, "in_csr") else \
                     graph._graph.get_immutable_gidx(feat_src.device)
-                ones = feat_src.new_ones((gidx.in_csr.nnz, self._num_heads, 1))
-                kw = {"keep": K.gat_keep_bits(self.attn_drop(ones)),
+                numel = gidx.in_csr.nnz * self._num_heads
+                if MODULE_DRAW_IN_KERNEL and numel > 0 and K.dropout_draw_ok(feat_src.device):
+                    # the same draws recomputed inside the walks: the generator advances
+                    # as this module's nn.Dropout would, no mask is materialised
+                    kw = {"draw": K.dropout_draw(feat_src.device, numel, p)}
+                    return self._fused_call(graph, feat_src, el, er, d, kw)
+                draw = th.empty((gidx.in_csr.nnz, self._num_heads, 1), device=feat_src.device,
+                                dtype=MODULE_DRAW_DTYPE)
+                _, keep = th.native_dropout(draw, p, True)
+                del draw
+                kw = {"keep": K.gat_keep_bits(keep),
                       "keep_scale": float(np.float32(1.0 / float(np.float32(1.0 - p))))}
-                del ones
+                del keep
+        return self._fused_call(graph, feat_src, el, er, d, kw)
+
+    def _fused_call(self, graph, feat_src, el, er, d, kw):
         if d == self._out_feats:
             return B.fused_gat(graph, feat_src, el, er, self.negative_slope, **kw)
         ft = th.nn.functional.pad(feat_src, (0, d - self._out_feats))

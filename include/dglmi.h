@@ -368,6 +368,42 @@ int DGLMIFusedGatKeepBackward(const DGLMIGraph* graph, const DGLMIArray* feat_sr
                               const DGLMIArray* slope_feat, const DGLMIArray* slope_sum,
                               const DGLMIArray* grad_out, DGLMIArray* grad_feat_src,
                               DGLMIArray* grad_el, DGLMIArray* grad_er, void* stream);
+/* torch's fused dropout draw over a contiguous (E, H) tensor, as the generator and the
+ * launch left it: seed, offset (the generator's Philox offset before the draw, a multiple
+ * of 4), threads = the dropout kernel's grid x 256 (grid = min(ceil(E H / 256), CUs x
+ * maxThreadsPerCU / 256)), vec = 4 / 2 / 1 (E H divisible by 4 / by 2 / neither), keep =
+ * float(1 - p), scale = the kept weights' factor (float(1 / float(1 - p))).  Element i is
+ * kept when the Philox4x32-10 uniform the kernel drew for it is below keep (internal.h
+ * dropout_draw_slot; scripts/philox_probe.py pins the mapping on this build). */
+typedef struct {
+  uint64_t seed;
+  uint64_t offset;
+  int64_t threads;
+  int32_t vec;
+  float keep;
+  float scale;
+} DGLMIDropoutDraw;
+/* Fused GAT with torch's own attention-dropout draws recomputed inside the walks: edge e,
+ * head h keeps its weight (scaled by draw->scale) when the draw keeps element e * H + h
+ * of the (E, H) attention tensor in edge-id order -- what nn.Dropout(p) draws on the
+ * reference's dropout(edge_softmax(...)) (gatconv.py:154) from the same generator state.
+ * No mask in memory, nothing gathered; GATConv advances the generator as the draw would.
+ * Otherwise as DGLMIFusedGatKeep*.  Extension. */
+int DGLMIFusedGatDrawForward(const DGLMIGraph* graph, const DGLMIArray* feat_src,
+                             const DGLMIArray* el, const DGLMIArray* er, float negative_slope,
+                             const DGLMIDropoutDraw* draw, DGLMIArray* out, DGLMIArray* max_out,
+                             DGLMIArray* sum_out, DGLMIArray* slope_feat, DGLMIArray* slope_sum, void* stream);
+int DGLMIFusedGatDrawBackward(const DGLMIGraph* graph, const DGLMIArray* feat_src,
+                              const DGLMIArray* el, const DGLMIArray* er, float negative_slope,
+                              const DGLMIDropoutDraw* draw, const DGLMIArray* out, const DGLMIArray* max_in,
+                              const DGLMIArray* sum_in, const DGLMIArray* slope_feat,
+                              const DGLMIArray* slope_sum, const DGLMIArray* grad_out,
+                              DGLMIArray* grad_feat_src, DGLMIArray* grad_el, DGLMIArray* grad_er,
+                              void* stream);
+/* mask[i] = 1 if the draw keeps element i, else 0, for i < n (n % vec == 0): the whole
+ * mask of the draw above (the fused route's self-check against torch.native_dropout, and
+ * the tests).  Extension. */
+int DGLMIDropoutDrawMask(const DGLMIDropoutDraw* draw, int64_t n, uint8_t* mask, void* stream);
 /* out[i] = keep[index[i]] for i < n, words of keep_bits bits (8, 16, 32): keep words in
  * edge-id order into a walk's position order (index = that CSR's edge ids, int32).
  * Device pointers; indices must lie in range.  Extension. */
@@ -378,6 +414,12 @@ int DGLMIGatKeepGather(const void* keep, int keep_bits, const int32_t* index, in
  * packed to the keep words above.  Device pointers.  Extension. */
 int DGLMIGatKeepBits(const float* table, int64_t num_edges, int heads, void* bits, int keep_bits,
                      void* stream);
+/* The same from the dropout's boolean mask (E, H) bytes, non-zero = kept -- the second
+ * output of torch.native_dropout, which nn.Dropout's fused path draws identically
+ * (GATConv's default: a quarter of the table's bytes).  heads = 8 needs mask 8-byte
+ * aligned.  Extension. */
+int DGLMIGatKeepBitsMask(const uint8_t* mask, int64_t num_edges, int heads, void* bits, int keep_bits,
+                         void* stream);
 /* The same two kernels in the reference's argument order, for a binding of the hack's
  * PackedFuncs that keeps its Python caller unchanged (tensor.py:383-420):
  *   _CAPI_DGLFusedGatKernel(G, feat_src, el, er, sum, exp, ret, slope)

@@ -181,7 +181,15 @@ def c3(dev, steps, warmup):
 
     def dfwd_bwd():
         dgat(g, x).sum().backward()
-    ms_dfb = timeit(dfwd_bwd, steps, warmup)       # the module's nn.Dropout draws (default)
+    from dgl.nn.pytorch.conv import gatconv as gatconv_mod
+    # the module's nn.Dropout draws (default: recomputed inside the walks when
+    # dgl.kernel.dropout_draw_ok; the route actually taken is recorded)
+    ms_dfb = timeit(dfwd_bwd, steps, warmup)
+    from dgl import kernel as K
+    draw_route = bool(gatconv_mod.MODULE_DRAW_IN_KERNEL and K.dropout_draw_ok(dev))
+    gatconv_mod.MODULE_DRAW_IN_KERNEL = False
+    ms_dfb_mask = timeit(dfwd_bwd, steps, warmup)  # torch's mask packed to keep words
+    gatconv_mod.MODULE_DRAW_IN_KERNEL = True
     dgat.attn_drop_mask = "hashed"
     ms_dfb_hashed = timeit(dfwd_bwd, steps, warmup)  # opt-in hashed mask
     dgat.attn_drop_mask = "module"
@@ -193,6 +201,8 @@ def c3(dev, steps, warmup):
             "fused_fwd_ms": ms_ff, "fused_fwd_bwd_ms": ms_ffb,
             "fused_fwd_Gedges_s": m / ms_ff / 1e6, "fused_fwd_bwd_Gedges_s": m / ms_ffb / 1e6,
             "attn_drop_0.6_fused_fwd_bwd_ms": ms_dfb,
+            "attn_drop_0.6_fused_draws_in_kernel": draw_route,
+            "attn_drop_0.6_fused_torch_mask_fwd_bwd_ms": ms_dfb_mask,
             "attn_drop_0.6_fused_hashed_mask_fwd_bwd_ms": ms_dfb_hashed,
             "attn_drop_0.6_unfused_fwd_bwd_ms": ms_dufb,
             "check": check}

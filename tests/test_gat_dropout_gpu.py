@@ -1,9 +1,11 @@
 """Attention dropout inside the fused GAT kernels.  GATConv in training applies
 ``nn.Dropout`` to the edge softmax (the reference's ``gatconv.py:154``).  Two fused forms:
 
-* the module's own draws (default, DGLMIFusedGatKeep*): GATConv's nn.Dropout on (E, H, 1)
-  ones in edge-id order, packed to one keep word per edge -- the fused module must agree
-  with the unfused composition (the reference's shape) under one seed;
+* the module's own draws (default): torch's fused dropout draws over (E, H, 1) in edge-id
+  order, recomputed inside the walks from the generator state (DGLMIFusedGatDraw*, once
+  checked against torch.native_dropout) or drawn by torch and packed to one keep word per
+  edge (DGLMIFusedGatKeep*) -- the fused module must agree with the unfused composition
+  (the reference's shape) under one seed, and the two routes bit for bit;
 * the hashed mask (opt-in, DGLMIFusedGatDropout*): the same Bernoulli(1 - p) per edge and
   head from a hash of a seed and the edge id, rebuilt on the host
   (``dgl.kernel.gat_dropout_keep``) for a dense fp64 restatement that applies it to the
@@ -132,14 +134,17 @@ def _graph(n_nodes, n_edges, seed):
 
 @pytest.mark.parametrize("nb,p,H,D", [(1, 0.5, 8, 8), (4, 0.5, 8, 8), (1, 0.3, 3, 16),
                                       (1, 0.6, 32, 4), (2, 0.5, 4, 8)])
-def test_gatconv_module_dropout_matches_composition(nb, p, H, D, monkeypatch):
+@pytest.mark.parametrize("in_kernel", [True, False])
+def test_gatconv_module_dropout_matches_composition(nb, p, H, D, in_kernel, monkeypatch):
     """The default fused route draws the mask with the module's nn.Dropout: under one
     torch.manual_seed the fused GATConv and the unfused composition (the reference's
     dropout(edge_softmax(...)), which draws on the (E, H, 1) attention) agree within fp32
     tolerance in the output, the input gradient and every parameter gradient -- unblocked
     and with column blocks (the kernels read the keep words through each block's edge
     ids); the route really is the fused one with the module's keep words."""
+    from dgl.nn.pytorch.conv import gatconv
     monkeypatch.setenv("DGLMI_GAT_BLOCKS", str(nb))
+    monkeypatch.setattr(gatconv, "MODULE_DRAW_IN_KERNEL", in_kernel)
     g, n = _graph(20000, 300000, 21 + nb)
     conv = GATConv(24, D, H, attn_drop=p).to(DEV).train()
     x0 = th.randn(n, 24, device=DEV, generator=th.Generator(device=DEV).manual_seed(2))
@@ -161,7 +166,7 @@ def test_gatconv_module_dropout_matches_composition(nb, p, H, D, monkeypatch):
         y.backward(go)
         res.append((y.detach(), x.grad, conv.fc.weight.grad.clone(), conv.attn_l.grad.clone(),
                     conv.attn_r.grad.clone()))
-    assert calls == [["keep", "keep_scale"]]
+    assert calls == ([["draw"]] if in_kernel else [["keep", "keep_scale"]])
     (yf, *gf), (yc, *gc) = res
     assert (yc == 0).any()  # dropout happened
     assert th.allclose(yf, yc, rtol=1e-4, atol=1e-5), float((yf - yc).abs().max())
@@ -186,6 +191,78 @@ def test_keep_bits_pack():
         m = (t.reshape(1001, h).cpu().numpy() != 0).astype(np.int64)
         want = (m << np.arange(h, dtype=np.int64)[None, :]).sum(1)
         assert np.array_equal(bits, want)
+        # the same words from the boolean mask (DGLMIGatKeepBitsMask), also from a view
+        # at an odd byte offset (the 8-head path copies it to an aligned buffer)
+        assert th.equal(K.gat_keep_bits(t != 0), kb), h
+        flat = th.cat([th.zeros(1, dtype=th.bool, device=DEV), (t != 0).reshape(-1)])
+        assert th.equal(K.gat_keep_bits(flat[1:].view(1001, h, 1)), kb), h
+    assert K.gat_keep_bits(th.zeros(0, 8, 1, dtype=th.bool, device=DEV)).numel() == 0
+
+
+@pytest.mark.parametrize("shape", [(13, 1, 1), (1001, 3, 1), (1001, 2, 1), (4099, 8, 1), (70001, 5, 1),
+                                   (3_000_001, 2, 1), (5_000_001, 3, 1), (2_000_000, 8, 1),
+                                   (1_500_001, 32, 1)])
+def test_dropout_draw_matches_native_dropout(shape):
+    """dgl.kernel.dropout_draw recomputes torch's fused dropout draw (Philox4x32-10, the
+    kernel's launch geometry, vec 4 / 2 / 1 by the element count) -- the mask of
+    DGLMIDropoutDrawMask equals torch.native_dropout's from the same generator state, bit
+    for bit, and the generator ends at the same offset; at seeds with the offset moved."""
+    n = shape[0] * shape[1]
+    gen = th.cuda.default_generators[0]
+    for seed, pre in ((0, 0), (2 ** 40 + 5, 3)):
+        for p in (0.6, 0.1):
+            th.manual_seed(seed)
+            for _ in range(pre):
+                th.native_dropout(th.empty(1000, device=DEV), 0.5, True)
+            state = gen.get_state()
+            d = K.dropout_draw(DEV, n, p)
+            off = gen.get_offset()
+            mine = K.dropout_draw_mask(d, n, DEV)
+            gen.set_state(state)
+            _, ref = th.native_dropout(th.empty(shape, device=DEV), p, True)
+            assert gen.get_offset() == off, (shape, seed, p)
+            assert th.equal(mine, ref.reshape(-1)), (shape, seed, p, int((mine != ref.reshape(-1)).sum()))
+    assert K.dropout_draw_ok(DEV)
+
+
+def test_gatconv_draw_route_bit_identical_to_mask_route(monkeypatch):
+    """The in-kernel draws and torch's own mask packed to keep words give the same fused
+    GATConv training step bit for bit (output, gradients) and leave the generator in the
+    same state -- unblocked and column-blocked, 8 and 3 heads."""
+    from dgl.nn.pytorch.conv import gatconv
+    for nb, H in ((1, 8), (4, 8), (1, 3)):
+        monkeypatch.setenv("DGLMI_GAT_BLOCKS", str(nb))
+        g, n = _graph(20000, 300001, 40 + nb)
+        conv = GATConv(24, 8, H, attn_drop=0.45).to(DEV).train()
+        x0 = th.randn(n, 24, device=DEV, generator=th.Generator(device=DEV).manual_seed(2))
+        go = th.randn(n, H, 8, device=DEV, generator=th.Generator(device=DEV).manual_seed(3))
+        res = []
+        for in_kernel in (True, False):
+            monkeypatch.setattr(gatconv, "MODULE_DRAW_IN_KERNEL", in_kernel)
+            conv.zero_grad()
+            x = x0.clone().requires_grad_()
+            th.manual_seed(5)
+            y = conv(g, x)
+            y.backward(go)
+            res.append((y.detach(), x.grad, conv.fc.weight.grad.clone(), conv.attn_l.grad.clone(),
+                        conv.attn_r.grad.clone(), th.cuda.get_rng_state()))
+        for a, b in zip(*res):
+            assert th.equal(a, b), (nb, H)
+
+
+def test_native_dropout_mask_is_module_draw():
+    """GATConv's fused route draws its mask with torch.native_dropout on an uninitialised
+    tensor (gatconv.MODULE_DRAW_DTYPE): the same mask, and the same generator state
+    after, as the module's nn.Dropout on ones -- the reference's attn_drop draws."""
+    from dgl.nn.pytorch.conv import gatconv
+    for shape in ((13, 1, 1), (1001, 3, 1), (4099, 8, 1), (70001, 5, 1)):
+        th.manual_seed(3)
+        ref = th.nn.Dropout(0.6)(th.ones(shape, device=DEV)) != 0
+        st = th.cuda.get_rng_state()
+        th.manual_seed(3)
+        _, m = th.native_dropout(th.empty(shape, device=DEV, dtype=gatconv.MODULE_DRAW_DTYPE), 0.6, True)
+        assert th.equal(m, ref), shape
+        assert th.equal(th.cuda.get_rng_state(), st), shape
 
 
 def test_fused_gatconv_ignores_attn_drop(monkeypatch):

@@ -122,8 +122,12 @@ def test_builtins_bit_identical_to_int32(case):
             assert th.equal(a, b), case
 
 
-def test_partial_pull_and_softmax_and_modules_bit_identical():
+def test_partial_pull_and_softmax_and_modules_bit_identical(monkeypatch):
     from dgl.nn.pytorch import GATConv, GraphConv, edge_softmax
+    from dgl.nn.pytorch.conv import gatconv
+    # both graphs step by step: the 64-bit graph has no fused walks, so its composition
+    # backward runs kernel by kernel; bit identity needs the same on the 32-bit graph
+    monkeypatch.setattr(gatconv, "FUSED_COMPOSITION_BACKWARD", False)
     src, dst, n = powerlaw(3000, 50000, seed=11)
     g32, g64 = _pair(src, dst, n)
     x = th.randn(n, 16, device=DEV)
