@@ -38,7 +38,7 @@ case "$mode" in
     rc=$?; echo "bench rc=$rc"; cut -c1-3000 ${out}_bench.json; [ $rc -eq 0 ] || tail -20 ${out}_bench.err
     exit $rc ;;
   stats)
-    timeout -k 10 900 rocprofv3 --kernel-trace --stats -d ${out}_prof -o run -- python3 bench.py "$@" \
+    timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d ${out}_prof -o run -- python3 bench.py "$@" \
       > ${out}_stats.log 2>&1
     rc=$?; echo "stats rc=$rc"; tail -3 ${out}_stats.log
     find ${out}_prof -name '*kernel_stats.csv' | head -3
