@@ -1193,7 +1193,10 @@ int gat_backward_impl(const DGLMIGraph* graph, const DGLMIArray* feat_src, const
                        const_cast<DGLMIArray*>(max_in), const_cast<DGLMIArray*>(sum_in));
   gat_set_dropout(a, attn_drop, seed, keep, keep_bits, keep_scale, graph->in_csr.nnz, keep_pos, draw);
   // with dropout only the slope-aggregate backward (no destination-side walk) applies
-  DGLMI_CHECK(!a.drop || lf_in != nullptr,
+  // with dropout only the slope-aggregate backward applies -- or, for the recomputed
+  // draws (drop_rng), the destination-side walks too (GATConv's composition keeps no
+  // slope aggregates); never the edge-position path
+  DGLMI_CHECK(!a.drop || lf_in != nullptr || a.drop_rng,
               "attention dropout needs the forward's slope aggregates (slope_feat / slope_sum)");
   hipStream_t s = static_cast<hipStream_t>(stream);
   a.chunk = gat_bwd_chunk_edges(std::max<int64_t>(graph->in_csr.nnz, 1));
@@ -1235,7 +1238,7 @@ int gat_backward_impl(const DGLMIGraph* graph, const DGLMIArray* feat_src, const
   // (C3, 8 blocks: 8.52 -> 9.15 ms; profiles/r03_gat_edge_pos.json).
   const bool blocks_given = graph->num_col_blocks > 1 && graph->in_col_blocks != nullptr &&
                             graph->out_col_blocks != nullptr;
-  const bool pos_path = graph->gat_edge_pos != nullptr && nb == 1 && !blocks_given &&
+  const bool pos_path = !a.drop && graph->gat_edge_pos != nullptr && nb == 1 && !blocks_given &&
                         fast_supported(FAST_COPY_EDGE, a.H, 1) && aligned16(grad_er->data);
   int64_t chunks = (in.nnz + a.chunk - 1) / a.chunk;
   for (int b = 0; b < nb && nb > 1; ++b)
@@ -1310,6 +1313,7 @@ int gat_backward_impl(const DGLMIGraph* graph, const DGLMIArray* feat_src, const
       g.indptr = c.indptr;
       g.rows = c.rows;
       g.indices = c.indices;
+      g.eids = c.data;
       g.nnz = c.nnz;
       g.num_rows = c.num_rows;
       g.chunk = gat_bwd_chunk_edges(std::max<int64_t>(c.nnz, 1));
@@ -1331,6 +1335,7 @@ int gat_backward_impl(const DGLMIGraph* graph, const DGLMIArray* feat_src, const
     return 0;
   }
   // destination side on the in-CSR
+  a.eids = in.data;
   launch_gat_backward_dst(a, s);
   check_hip(hipGetLastError(), "fused GAT backward (dst) launch");
   // source side on the out-CSR
@@ -1338,6 +1343,7 @@ int gat_backward_impl(const DGLMIGraph* graph, const DGLMIArray* feat_src, const
   b.indptr = outc.indptr;
   b.rows = outc.rows;
   b.indices = outc.indices;
+  b.eids = outc.data;
   b.nnz = outc.nnz;
   b.num_rows = outc.num_rows;
   launch_gat_backward_src(b, s);
@@ -1460,6 +1466,34 @@ int DGLMIDropoutDrawMask(const DGLMIDropoutDraw* draw, int64_t n, uint8_t* mask,
                            static_cast<hipStream_t>(stream));
   check_hip(hipGetLastError(), "dropout draw mask launch");
   API_END();
+}
+
+namespace {
+int dropout_draw_scale_impl(const DGLMIDropoutDraw* draw, int heads, const int32_t* eids, int64_t n, float* out,
+                            bool apply, void* stream) {
+  API_BEGIN();
+  DGLMI_CHECK(draw != nullptr, "DGLMIDropoutDrawScale: draw is required");
+  DGLMI_CHECK(heads >= 1 && heads <= 32, "DGLMIDropoutDrawScale: 1 <= heads <= 32");
+  DGLMI_CHECK(n >= 0 && (n == 0 || out != nullptr), "DGLMIDropoutDrawScale: n >= 0, out");
+  DGLMI_CHECK(n < (int64_t(1) << 31), "DGLMIDropoutDrawScale: positions below 2^31 (32-bit edge ids)");
+  GatArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.H = heads;
+  gat_set_draw(a, draw, n);
+  launch_dropout_draw_scale(a, eids, n, out, apply, static_cast<hipStream_t>(stream));
+  check_hip(hipGetLastError(), "dropout draw scale launch");
+  API_END();
+}
+}  // namespace
+
+int DGLMIDropoutDrawScale(const DGLMIDropoutDraw* draw, int heads, const int32_t* eids, int64_t n, float* out,
+                          void* stream) {
+  return dropout_draw_scale_impl(draw, heads, eids, n, out, false, stream);
+}
+
+int DGLMIDropoutDrawApply(const DGLMIDropoutDraw* draw, int heads, const int32_t* eids, int64_t n, float* x,
+                          void* stream) {
+  return dropout_draw_scale_impl(draw, heads, eids, n, x, true, stream);
 }
 
 int DGLMIGatKeepGather(const void* keep, int keep_bits, const int32_t* index, int64_t n, void* out,

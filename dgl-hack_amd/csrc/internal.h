@@ -489,6 +489,12 @@ __host__ __device__ __forceinline__ bool dropout_draw_kept(const Philox4& r, int
 // self-check against torch.native_dropout before the fused route trusts the mapping)
 void launch_dropout_draw_mask(uint64_t seed, uint64_t ctr, int64_t threads, int vec, int shift, float keep,
                               int64_t n, uint8_t* mask, hipStream_t s);
+// out[p H + h] = drop_scale if the draw keeps element eids[p] H + h, else 0, p < n (a.H
+// heads <= 32, a.rng_* set; eids NULL = identity): the draw's output on a tensor of ones
+// in a walk's position order (GATConv's composition: dropout(a) on the position view)
+// apply = true: out[p H + h] *= that factor instead (dropout applied in place)
+void launch_dropout_draw_scale(const GatArgs& a, const int32_t* eids, int64_t n, float* out, bool apply,
+                               hipStream_t s);
 // The dropout mask's hash (mirrored in numpy by dgl.kernel.gat_dropout_keep for the
 // tests): one key per edge -- a 32-bit avalanche mix of the edge id keyed by the seed's
 // low half, xor the high half -- then, per PAIR of heads, a one-multiply finish of

@@ -499,15 +499,20 @@ __global__ void __launch_bounds__(kBlock) k_gat_fwd_fixup(GatArgs a) {
 
 // ---------------------------------------------------------------------------
 // backward, destination side (in-CSR): grad_er, delta, packed stats
+// DROP 3: torch's dropout draws (the backward of a forward without slope aggregates:
+// GATConv's composition, backend.GatComposition): an edge's attention gradient term takes
+// its kept, rescaled <grad_out, ft>; delta = <grad_out, out> is the dropped output's.
 // ---------------------------------------------------------------------------
-template <int L, int NV, bool O32>
+template <int L, int NV, bool O32, int DROP = 0>
 __global__ void __launch_bounds__(kBlock) k_gat_bwd_dst(GatArgs a) {
   static_assert(L >= 1 && L <= 64, "a lane group must fit in one wavefront");
+  static_assert(DROP == 0 || DROP == 3, "the destination walk takes only the recomputed draws");
   constexpr int G = kBlock / L;
   constexpr int B = L > 16 ? L : 16;
   constexpr int U = NV == 1 ? 8 : 4;
   __shared__ int32_t s_row[G][B];
   __shared__ int32_t s_col[G][B];
+  __shared__ uint32_t s_keep[DROP ? G : 1][DROP ? B : 1];
   const int g = threadIdx.x / L;
   const int lane = threadIdx.x % L;
   const int64_t chunk = (int64_t)blockIdx.x * G + g;
@@ -584,6 +589,7 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_dst(GatArgs a) {
       const bool ok = p < p1;
       s_row[g][q] = ok ? a.rows[p] : INT_MAX;
       s_col[g][q] = ok ? a.indices[p] : 0;
+      if constexpr (DROP == 3) s_keep[DROP ? g : 0][DROP ? q : 0] = ok ? gat_draw_keep(a, a.eids[p]) : 0u;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -615,7 +621,9 @@ __global__ void __launch_bounds__(kBlock) k_gat_bwd_dst(GatArgs a) {
         for (int v = 0; v < NV; ++v) {
           const float pre = elv[u][v] + erv[v];
           const float att = fexp(leaky(pre, a.slope) - mv[v]) * linv[v];
-          const float ge = head_sum(dot4(gov[v], ftv[u][v]), D4);
+          float ge = head_sum(dot4(gov[v], ftv[u][v]), D4);
+          if constexpr (DROP == 3)
+            ge = gat_kept(s_keep[DROP ? g : 0][DROP ? ub + u : 0], hd[v]) ? ge * a.drop_scale : 0.0f;
           acc[v] += att * (ge - dlt[v]) * dleaky(pre, a.slope);
         }
       }
@@ -1020,7 +1028,9 @@ void bwd_dst_cfg(const GatArgs& a, hipStream_t s) {
   constexpr int G = kBlock / L;
   const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
   const unsigned blocks = static_cast<unsigned>((chunks + G - 1) / G);
-  if (a.o32)
+  if (a.drop)  // the recomputed draws only, 32-bit offsets (checked by the C entry)
+    hipLaunchKernelGGL((k_gat_bwd_dst<L, NV, true, 3>), dim3(blocks), dim3(kBlock), 0, s, a);
+  else if (a.o32)
     hipLaunchKernelGGL((k_gat_bwd_dst<L, NV, true>), dim3(blocks), dim3(kBlock), 0, s, a);
   else
     hipLaunchKernelGGL((k_gat_bwd_dst<L, NV, false>), dim3(blocks), dim3(kBlock), 0, s, a);
@@ -1126,6 +1136,26 @@ void launch_dropout_draw_mask(uint64_t seed, uint64_t ctr, int64_t threads, int 
   const int64_t want = (n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(k_dropout_draw_mask, dim3(static_cast<unsigned>(want < 65536 ? want : 65536)), dim3(kBlock),
                      0, s, seed, ctr, threads, vec, shift, keep, n, mask);
+}
+template <bool APPLY>
+__global__ void k_dropout_draw_scale(GatArgs a, const int32_t* __restrict__ eids, int64_t n, float* __restrict__ out) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t p = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; p < n; p += stride) {
+    const uint32_t kb = gat_draw_keep(a, eids != nullptr ? eids[p] : static_cast<int32_t>(p));
+    for (int h = 0; h < a.H; ++h) {
+      const float f = (kb >> h) & 1u ? a.drop_scale : 0.0f;
+      if (APPLY) out[p * a.H + h] *= f;  // x * (1 * keep * scale): the composition's order
+      else out[p * a.H + h] = f;
+    }
+  }
+}
+void launch_dropout_draw_scale(const GatArgs& a, const int32_t* eids, int64_t n, float* out, bool apply,
+                               hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t want = (n + kBlock - 1) / kBlock;
+  const dim3 grid(static_cast<unsigned>(want < 65536 ? want : 65536)), blk(kBlock);
+  if (apply) hipLaunchKernelGGL(k_dropout_draw_scale<true>, grid, blk, 0, s, a, eids, n, out);
+  else hipLaunchKernelGGL(k_dropout_draw_scale<false>, grid, blk, 0, s, a, eids, n, out);
 }
 // The same from the dropout's own mask (E, H) bytes, 1 = kept (torch.native_dropout's
 // second output): a quarter of the table's bytes.  H = 8 (the reference GAT's heads) reads

@@ -233,6 +233,12 @@ _SIGS = {
         ctypes.POINTER(Array), ctypes.c_void_p]),
     "DGLMIDropoutDrawMask": (ctypes.c_int, [
         ctypes.POINTER(DropoutDraw), ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "DGLMIDropoutDrawScale": (ctypes.c_int, [
+        ctypes.POINTER(DropoutDraw), ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+        ctypes.c_void_p]),
+    "DGLMIDropoutDrawApply": (ctypes.c_int, [
+        ctypes.POINTER(DropoutDraw), ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+        ctypes.c_void_p]),
     "DGLMIGatKeepGather": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
         ctypes.c_void_p]),

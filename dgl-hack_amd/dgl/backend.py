@@ -589,10 +589,14 @@ class GatComposition(th.autograd.Function):
     sum_e a_e (ft_u . g_v) = g_v . rst_v gives each row's correction densely, the
     attention is recomputed where it is used, and no per-edge tensor is kept from the
     forward (the attention, E x H, is freed after u_mul_e_sum).  Equal to the step-by-step
-    gradients within fp32 rounding (tests/test_nn_gpu.py)."""
+    gradients within fp32 rounding (tests/test_nn_gpu.py).  ``draw``
+    (dgl.kernel.dropout_draw over the (E, H) attention): GATConv's attention dropout with
+    the module's own draws -- the attention times nn.Dropout's output on ones, written in
+    walk order from the draws (DGLMIDropoutDrawScale), and the same draws recomputed by the
+    backward walks (DGLMIFusedGatDrawBackward without slope aggregates)."""
 
     @staticmethod
-    def forward(ctx, gidx, view, feat_src, el, er, slope):
+    def forward(ctx, gidx, view, feat_src, el, er, slope, draw=None):
         ft, el, er = feat_src.contiguous(), el.contiguous(), er.contiguous()
         n_dst = view.num_dst
         H = el.shape[1]
@@ -600,10 +604,12 @@ class GatComposition(th.autograd.Function):
         rmax = el.new_zeros((n_dst, H))
         rsum = el.new_ones((n_dst, H))
         K.edge_softmax_node_logits_forward_ex(view, el, er, slope, a, rmax, rsum)
+        if draw is not None:  # dropout(a): a * (keep * scale), torch's order of operations
+            K.dropout_draw_apply(draw, H, gidx.in_csr.data, a)
         rst = ft.new_empty((n_dst,) + tuple(ft.shape[1:]))
         K.binary_op_reduce("sum", "mul", view, SRC, EDGE, ft, a, rst)
         del a
-        ctx.gidx, ctx.slope = gidx, slope
+        ctx.gidx, ctx.slope, ctx.draw = gidx, slope, draw
         ctx.save_for_backward(ft, el, er, rst, rmax, rsum)
         return rst
 
@@ -612,8 +618,8 @@ class GatComposition(th.autograd.Function):
         ft, el, er, rst, rmax, rsum = ctx.saved_tensors
         g_ft, g_el, g_er = th.empty_like(ft), th.empty_like(el), th.empty_like(er)
         K.fused_gat_backward(ctx.gidx, ft, el, er, ctx.slope, rst, rmax, rsum, grad.contiguous(),
-                             g_ft, g_el, g_er)
-        return None, None, g_ft, g_el, g_er, None
+                             g_ft, g_el, g_er, draw=ctx.draw)
+        return None, None, g_ft, g_el, g_er, None, None
 
 
 def gat_composition_ok(gidx, feat_src, el, er):
@@ -629,10 +635,11 @@ def gat_composition_ok(gidx, feat_src, el, er):
             and K.fused_gat_supported(h, d) and K.edge_softmax_supported(h))
 
 
-def gat_composition(gidx, view, feat_src, el, er, slope):
+def gat_composition(gidx, view, feat_src, el, er, slope, draw=None):
     """rst = u_mul_e_sum(ft, edge_softmax(leaky_relu(u_add_v(el, er)))) with the fused
-    backward (:class:`GatComposition`); ``view`` = gidx.position_view("in")."""
-    return GatComposition.apply(gidx, view, feat_src, el, er, float(slope))
+    backward (:class:`GatComposition`); ``view`` = gidx.position_view("in"); ``draw``:
+    attention dropout with torch's own draws (dropout(edge_softmax(...)))."""
+    return GatComposition.apply(gidx, view, feat_src, el, er, float(slope), draw)
 
 
 # --------------------------------------------------------------------------- #

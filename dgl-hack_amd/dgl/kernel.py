@@ -456,6 +456,34 @@ def dropout_draw_mask(draw, numel, device):
     return out.bool()
 
 
+def dropout_draw_scale(draw, heads, eids, num_edges, device):
+    """(E, heads, 1) float32: the draw's output on ones -- draw.scale where kept, else 0 --
+    at position p for edge ``eids[p]`` (int32 ROCm tensor; None = identity) ->
+    DGLMIDropoutDrawScale.  The same values as ``nn.Dropout(p)(ones)[eids]`` from the
+    generator state the draw was taken at."""
+    out = th.empty((num_edges, heads, 1), dtype=th.float32, device=device)
+    if eids is not None and (eids.dtype != th.int32 or not eids.is_contiguous() or eids.numel() != num_edges):
+        raise DGLError("dropout_draw_scale: eids must be a contiguous int32 tensor of E ids")
+    check_call(_ffi.lib().DGLMIDropoutDrawScale(
+        ctypes.byref(draw), int(heads), ctypes.c_void_p(eids.data_ptr() if eids is not None and num_edges else None),
+        ctypes.c_int64(num_edges), ctypes.c_void_p(out.data_ptr() if num_edges else None), _stream(out)))
+    return out
+
+
+def dropout_draw_apply(draw, heads, eids, x):
+    """x (E, heads[, 1]) float32 contiguous, in place: x *= draw.scale where kept, else 0,
+    at position p for edge ``eids[p]`` -> DGLMIDropoutDrawApply.  Returns x."""
+    n = x.shape[0]
+    if not (x.is_cuda and x.dtype == th.float32 and x.is_contiguous() and x.numel() == n * heads):
+        raise DGLError("dropout_draw_apply: a contiguous float32 (E, heads) ROCm tensor")
+    if eids is not None and (eids.dtype != th.int32 or not eids.is_contiguous() or eids.numel() != n):
+        raise DGLError("dropout_draw_apply: eids must be a contiguous int32 tensor of E ids")
+    check_call(_ffi.lib().DGLMIDropoutDrawApply(
+        ctypes.byref(draw), int(heads), ctypes.c_void_p(eids.data_ptr() if eids is not None and n else None),
+        ctypes.c_int64(n), ctypes.c_void_p(x.data_ptr() if n else None), _stream(x)))
+    return x
+
+
 _DRAW_OK = {}
 
 
@@ -543,9 +571,7 @@ def fused_gat_backward(graph, feat_src, el, er, slope, out, max_in, sum_in, grad
     backward walk's position order, :func:`gat_keep_walk_order` "out"; with ``draw``
     DGLMIFusedGatDrawBackward, the forward's draw)."""
     _check_ctx(graph, [("feat_src", feat_src), ("grad_out", grad_out)])
-    if draw is not None:
-        if slope_feat is None:
-            raise DGLError("fused GAT dropout backward needs the forward's slope aggregates")
+    if draw is not None:  # without slope aggregates: the destination-side walks recompute too
         g = graph.cstruct(None, col_blocks=gat_col_blocks(graph, feat_src, backward=True))
         check_call(_ffi.lib().DGLMIFusedGatDrawBackward(
             ctypes.byref(g), _arr(feat_src, "feat_src"), _arr(el, "el"), _arr(er, "er"),

@@ -167,10 +167,21 @@ class GATConv(nn.Module):
         view = gidx.position_view("in")
         n_dst, m = view.num_dst, view.number_of_edges()
         if (FUSED_COMPOSITION_BACKWARD and FUSED_LEAKY and type(self.leaky_relu) is nn.LeakyReLU
-                and not self._attn_drop_active()
                 and B.gat_composition_ok(gidx, feat_src, el, er)):
-            # the same forward; the backward as the fused GAT's walks (GatComposition)
-            return B.gat_composition(gidx, view, feat_src, el, er, self.leaky_relu.negative_slope)
+            # the same forward; the backward as the fused GAT's walks (GatComposition) --
+            # with attention dropout when its draws can be recomputed in the walks
+            draw = None
+            if self._attn_drop_active():
+                p = float(self.attn_drop.p)
+                numel = m * self._num_heads
+                if (MODULE_DRAW_IN_KERNEL and 0.0 < p < 1.0 and self._num_heads <= 32 and numel > 0
+                        and K.dropout_draw_ok(feat_src.device)):
+                    draw = K.dropout_draw(feat_src.device, numel, p)
+            if draw is not None:
+                return B.gat_composition(gidx, view, feat_src, el, er, self.leaky_relu.negative_slope,
+                                         draw=draw)
+            if not self._attn_drop_active():
+                return B.gat_composition(gidx, view, feat_src, el, er, self.leaky_relu.negative_slope)
         if type(self.leaky_relu) is nn.LeakyReLU and FUSED_LEAKY:
             # u_add_v and the activation inside the softmax's passes: the logits are
             # computed where they are read, never stored (bit-identical to the three steps)
@@ -181,9 +192,19 @@ class GATConv(nn.Module):
         if self._attn_drop_active():
             # nn.Dropout's draws in edge-id order, as dropout(a) in the edge-id
             # composition: (1 * keep) * scale per edge, gathered into walk order; a times
-            # it is dropout's (a * keep) * scale bit for bit, and so is the gradient
-            scale = self.attn_drop(a.new_ones(a.shape))
-            a = a * K.gather_rows(scale, gidx.in_csr.data)
+            # it is dropout's (a * keep) * scale bit for bit, and so is the gradient.
+            # With the draws recomputable (dgl.kernel.dropout_draw_ok) the walk-order
+            # scale is written directly from them (no ones, no (E, H) draw, no gather).
+            numel = m * self._num_heads
+            p = float(self.attn_drop.p)
+            if (MODULE_DRAW_IN_KERNEL and 0.0 < p < 1.0 and self._num_heads <= 32 and numel > 0
+                    and K.dropout_draw_ok(a.device)):
+                scale = K.dropout_draw_scale(K.dropout_draw(a.device, numel, p), self._num_heads,
+                                             gidx.in_csr.data, m, a.device)
+                a = a * scale.view(a.shape)
+            else:
+                scale = self.attn_drop(a.new_ones(a.shape))
+                a = a * K.gather_rows(scale, gidx.in_csr.data)
         return B.binary_reduce("sum", "mul", view, B.SRC, B.EDGE, feat_src, a, n_dst)
 
     def _fused_dim(self):

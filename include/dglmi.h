@@ -404,6 +404,17 @@ int DGLMIFusedGatDrawBackward(const DGLMIGraph* graph, const DGLMIArray* feat_sr
  * mask of the draw above (the fused route's self-check against torch.native_dropout, and
  * the tests).  Extension. */
 int DGLMIDropoutDrawMask(const DGLMIDropoutDraw* draw, int64_t n, uint8_t* mask, void* stream);
+/* out[p * heads + h] = draw->scale if the draw keeps element eids[p] * heads + h, else 0,
+ * for p < n (eids NULL = identity; heads <= 32; n = the draw's E): nn.Dropout's output on
+ * an (E, heads) tensor of ones, in a walk's position order -- GATConv's composition on its
+ * position view multiplies the attention by it.  Extension. */
+int DGLMIDropoutDrawScale(const DGLMIDropoutDraw* draw, int heads, const int32_t* eids, int64_t n, float* out,
+                          void* stream);
+/* x[p * heads + h] *= that factor, in place: dropout(x) on a walk-ordered (E, heads) tensor
+ * with the draws of edge eids[p] (one read and one write of x instead of the factor's
+ * write plus a separate multiply).  Extension. */
+int DGLMIDropoutDrawApply(const DGLMIDropoutDraw* draw, int heads, const int32_t* eids, int64_t n, float* x,
+                          void* stream);
 /* out[i] = keep[index[i]] for i < n, words of keep_bits bits (8, 16, 32): keep words in
  * edge-id order into a walk's position order (index = that CSR's edge ids, int32).
  * Device pointers; indices must lie in range.  Extension. */

@@ -228,12 +228,17 @@ def test_dropout_draw_matches_native_dropout(shape):
 def test_gatconv_draw_route_bit_identical_to_mask_route(monkeypatch):
     """The in-kernel draws and torch's own mask packed to keep words give the same fused
     GATConv training step bit for bit (output, gradients) and leave the generator in the
-    same state -- unblocked and column-blocked, 8 and 3 heads."""
+    same state -- unblocked and column-blocked, 8 and 3 heads; and the composition's
+    walk-order scale written from the draws (DGLMIDropoutDrawScale) equals nn.Dropout on
+    ones gathered into walk order, bit for bit."""
     from dgl.nn.pytorch.conv import gatconv
-    for nb, H in ((1, 8), (4, 8), (1, 3)):
+    # the composition step by step (its fused backward is tested below)
+    monkeypatch.setattr(gatconv, "FUSED_COMPOSITION_BACKWARD", False)
+    for nb, H, fused in ((1, 8, True), (4, 8, True), (1, 3, True), (1, 8, False), (1, 3, False)):
         monkeypatch.setenv("DGLMI_GAT_BLOCKS", str(nb))
         g, n = _graph(20000, 300001, 40 + nb)
         conv = GATConv(24, 8, H, attn_drop=0.45).to(DEV).train()
+        conv.use_fused = fused
         x0 = th.randn(n, 24, device=DEV, generator=th.Generator(device=DEV).manual_seed(2))
         go = th.randn(n, H, 8, device=DEV, generator=th.Generator(device=DEV).manual_seed(3))
         res = []
@@ -247,7 +252,46 @@ def test_gatconv_draw_route_bit_identical_to_mask_route(monkeypatch):
             res.append((y.detach(), x.grad, conv.fc.weight.grad.clone(), conv.attn_l.grad.clone(),
                         conv.attn_r.grad.clone(), th.cuda.get_rng_state()))
         for a, b in zip(*res):
-            assert th.equal(a, b), (nb, H)
+            assert th.equal(a, b), (nb, H, fused)
+
+
+@pytest.mark.parametrize("nb,H", [(1, 8), (8, 8), (1, 2), (2, 4)])
+def test_composition_dropout_fused_backward(nb, H, monkeypatch):
+    """GATConv's composition with attention dropout (use_fused = False): the fused backward
+    (GatComposition with the recomputed draws: destination- and source-side walks, no
+    slope aggregates) against the step-by-step backward -- the same forward bit for bit,
+    the gradients within fp32 tolerance, the generator left in the same state --
+    unblocked and column-blocked."""
+    from dgl.nn.pytorch.conv import gatconv
+    monkeypatch.setenv("DGLMI_GAT_BLOCKS", str(nb))
+    g, n = _graph(20000, 300000, 60 + nb)
+    conv = GATConv(24, 8, H, attn_drop=0.5).to(DEV).train()
+    conv.use_fused = False
+    x0 = th.randn(n, 24, device=DEV, generator=th.Generator(device=DEV).manual_seed(2))
+    go = th.randn(n, H, 8, device=DEV, generator=th.Generator(device=DEV).manual_seed(3))
+    calls = []
+    orig = B.gat_composition
+
+    def spy(*a, **k):
+        calls.append(k.get("draw") is not None)
+        return orig(*a, **k)
+    monkeypatch.setattr(B, "gat_composition", spy)
+    res = []
+    for fused_bwd in (True, False):
+        monkeypatch.setattr(gatconv, "FUSED_COMPOSITION_BACKWARD", fused_bwd)
+        conv.zero_grad()
+        x = x0.clone().requires_grad_()
+        th.manual_seed(9)
+        y = conv(g, x)
+        y.backward(go)
+        res.append((y.detach(), x.grad, conv.fc.weight.grad.clone(), conv.attn_l.grad.clone(),
+                    conv.attn_r.grad.clone(), th.cuda.get_rng_state()))
+    assert calls == [True]
+    (yf, *gf, sf), (ys, *gs, ss) = res
+    assert th.equal(yf, ys) and th.equal(sf, ss)
+    for a, b, name in zip(gf, gs, ("x", "fc", "attn_l", "attn_r")):
+        tol = 1e-4 * float(b.abs().max()) + 1e-6
+        assert float((a - b).abs().max()) <= tol, (name, float((a - b).abs().max()), tol)
 
 
 def test_native_dropout_mask_is_module_draw():
