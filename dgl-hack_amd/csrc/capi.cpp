@@ -1705,6 +1705,9 @@ int64_t softmax_setup(const DGLMIGraph* g, const DGLMIArray* x, const char* name
   const char* owned = std::getenv("DGLMI_SOFTMAX_OWNED");
   const bool ident = (g->eid_identity & 1) != 0 && !(owned != nullptr && owned[0] == '0');
   a.eids = ident ? IdxPtr{nullptr, wide(g) ? 1 : 0} : idx(g, in.data);
+  // H <= 2 there: four values per lane (DGLMI_SOFTMAX_QUAD=0: one position per lane, for A/B)
+  const char* quad = std::getenv("DGLMI_SOFTMAX_QUAD");
+  a.quad = !(quad != nullptr && quad[0] == '0');
   a.coo_dst = (g->coo_src && g->coo_dst) ? g->coo_dst : nullptr;
   a.nnz = in.nnz;
   a.num_rows = in.num_rows;

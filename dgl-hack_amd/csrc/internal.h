@@ -274,6 +274,7 @@ struct SoftmaxArgs {
   const float* node_r;
   const int32_t* cols;     // in-CSR indices (node_l mode)
   const int32_t* coo_src;  // with coo_dst: the edge-id-order pass's source per edge
+  int quad;                // H <= 2 on the row-owned walk: four values per lane (16-B loads)
 };
 bool softmax_supported(int64_t H);
 

@@ -560,29 +560,638 @@ struct OwnedWalk {
       }
     }
   }
+  // the outputs of hub row positions [pa, pb) from the row's statistics
+  __device__ void emit_range(int64_t pa, int64_t pb, const float (&sm)[V], const float (&si)[V], int row) const {
+    for (int64_t b = pa; b < pb; b += U * L) emit<U>(b, pb, sm, si, row);
+  }
+  static constexpr int64_t W = S::W, T = S::T;
+};
+
+// ---------------------------------------------------------------------------
+// The row-owned walk with four values per lane, H <= 2 (round 6).  At H = 1 the walk
+// above loads 4 B per lane (one position), and its steps wait on one another: a step's
+// loads are issued only after the previous step's row logic, and every row end costs a
+// dependent indptr load (profiles/r06_edge_softmax_h1_pmc.json: 79 % of the cycles
+// waiting on memory).  Here
+// * lane j of a step holds the P = 4 / H positions B + P j .. B + P j + P - 1 with all
+//   their heads -- one 16-B load per lane and array, L = 64 P positions a step; every
+//   step starts at a multiple of P, so every load is aligned, and positions outside the
+//   range being walked are masked (element by element, only in a quad the range cuts);
+// * the loads of U steps are issued together whatever the rows do: the row of every
+//   position comes from a slice of the row offsets held one per lane (lane t: the start
+//   of row rb + t), so a row end needs no memory access -- only batches with more than
+//   kEnds row ends (short rows) read the row ids, and the slice is reloaded when the
+//   walk leaves it;
+// * a step that crosses a row end folds each lane's positions into lane-local segments
+//   first: a row that starts and ends inside one lane is finished there, and each lane's
+//   first and last segments take part in the segmented scan over the lanes (a lane's
+//   first segment continues the previous lane's scan);
+// * the statistics of the span's first kRows rows are kept in LDS too, so the output
+//   sweep reads them there (no fence and no L2 round trip).
+// Windows (2048 positions, as above; 1024 / 4096 measured slower), the hub threshold 2W
+// and the two carry slots per window are the walk above's scheme, so k_sm_hub serves
+// both.  32-bit row offsets only (the 64-bit layout keeps the walk above).  C3 view, H = 1
+// fwd / bwd 0.64 / 0.96 -> 0.36 / 0.44 ms (profiles/r06_edge_softmax_quad_probe.json).
+template <int H>
+struct QuadShape {
+  static_assert(H == 1 || H == 2, "four values per lane: H <= 2");
+  static constexpr int P = 4 / H;   // positions per lane
+  static constexpr int L = 64 * P;  // positions per step
+#ifndef DGLMI_SMQ_U
+#define DGLMI_SMQ_U 2
+#endif
+  static constexpr int U = DGLMI_SMQ_U;  // steps whose loads are issued together
+#ifndef DGLMI_SMQ_W
+#define DGLMI_SMQ_W 2048
+#endif
+  static constexpr int64_t W = DGLMI_SMQ_W;  // window (positions)
+  static constexpr int64_t T = 2 * W;
+  static_assert(W % L == 0, "windows of whole steps");
 };
 
 template <int H, int MODE>
+struct QuadWalk {
+  using S = QuadShape<H>;
+  static constexpr int P = S::P, L = S::L, U = S::U;
+  static constexpr int V = H, q = 0;  // every lane holds all heads (k_sm_hub's carry offsets)
+  static constexpr int W = S::W, T = S::T;
+  static constexpr int kRows = 128;  // rows of a span whose statistics stay in LDS
+  static constexpr int kEnds = 8;    // row ends per batch taken from the slice
+  static constexpr float kId = MODE == SM_STATS ? -INFINITY : 0.0f;  // identity of m
+  const SoftmaxArgs& a;
+  const int32_t* ip;  // the in-CSR's row offsets
+  int j;
+  float m[H], l[H];  // this lane's running state (MODE DOTSUM: m = sum, l unused)
+  int rb = -(1 << 30), st = 0;  // slice: lane t holds indptr[rb + t] (clamped at the last row)
+  float* cache;                 // LDS, kRows x 2H: statistics of rows c0 ..
+  int c0 = 0;
+  bool spill = false;  // a row past the cache had its statistics stored (read back from L2)
+
+  __device__ __forceinline__ QuadWalk(const SoftmaxArgs& args, int lane, float* lds = nullptr)
+      : a(args), ip(static_cast<const int32_t*>(args.indptr.p)), j(lane), cache(lds) { clear(); }
+  __device__ __forceinline__ void clear() {
+#pragma unroll
+    for (int h = 0; h < H; ++h) { m[h] = kId; l[h] = 0.0f; }
+  }
+  __device__ __forceinline__ static int first(int p) { return p - p % P; }
+  __device__ __forceinline__ static bool in(int p, int lo, int hi) { return p >= lo && p < hi; }
+
+  // ---- row offsets ----
+  __device__ __forceinline__ void slice(int r) {
+    rb = r;
+    const int t = r + j;
+    st = ip[t < a.num_rows ? t : a.num_rows];
+  }
+  // indptr[r] (r uniform), reloading the slice from r when it does not hold r
+  __device__ __forceinline__ int start_of(int r) {
+    if (r < rb || r - rb >= 64) slice(r);
+    return __shfl(st, r - rb);
+  }
+  __device__ __forceinline__ int end_of(int r) {
+    if (r < rb || r + 1 - rb >= 64) slice(r);
+    return __shfl(st, r + 1 - rb);
+  }
+  // the row holding position p (the slice holds the row's start): the last lane whose
+  // start is <= p; a.rows[p] when that is the slice's last lane
+  __device__ __forceinline__ int row_holding(int p) {
+    const int n = __popcll(__ballot(st <= p));
+    return n < 64 ? rb + n - 1 : a.rows[p];
+  }
+  // the rows of the positions of steps b + u L (u < N), cur's row ends at cur_end: from
+  // the slice when it holds the first start past the batch and at most kEnds ends fall
+  // inside it, else read (outside [lo, hi) they are not used)
+  template <int N>
+  __device__ __forceinline__ void batch_rows(int b, int lo, int hi, int cur, int (&rk)[N][P]) {
+    const int last = (b + N * L < hi ? b + N * L : hi) - 1;
+    if (cur < rb || cur + 1 - rb >= 64) slice(cur);
+    const int t0 = cur + 1 - rb;  // lane of cur's end
+    const int n = __popcll(__ballot(j >= t0 && st <= last));
+#pragma unroll
+    for (int u = 0; u < N; ++u)
+#pragma unroll
+      for (int k = 0; k < P; ++k) rk[u][k] = cur;
+    if (n <= kEnds && t0 + n < 64) {
+      for (int i = 0; i < n; ++i) {
+        const int e = __shfl(st, t0 + i);
+#pragma unroll
+        for (int u = 0; u < N; ++u)
+#pragma unroll
+          for (int k = 0; k < P; ++k) rk[u][k] += b + u * L + P * j + k >= e ? 1 : 0;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < N; ++u) ldi(a.rows, b + u * L + P * j, lo, hi, rk[u]);
+    }
+  }
+
+  // a[u] <- a[u + 1]: the next step of a batch moves to slot 0
+  template <class Tv, int N, int K>
+  __device__ __forceinline__ static void shift(Tv (&v)[N][K]) {
+#pragma unroll
+    for (int u = 0; u + 1 < N; ++u)
+#pragma unroll
+      for (int k = 0; k < K; ++k) v[u][k] = v[u + 1][k];
+  }
+
+  // ---- quads ----
+  // the 4 floats of the quad at q0 (a multiple of P) of an array of H floats per position;
+  // positions outside [lo, hi) read as `fill` (and are not loaded)
+  __device__ __forceinline__ static void ldq(const float* __restrict__ base, int q0, int lo, int hi,
+                                              float (&x)[4], float fill) {
+    if (q0 >= lo && q0 + P <= hi) {
+      const float4 t = *reinterpret_cast<const float4*>(base + (int64_t)q0 * H);
+      x[0] = t.x; x[1] = t.y; x[2] = t.z; x[3] = t.w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) x[i] = in(q0 + i / H, lo, hi) ? base[(int64_t)q0 * H + i] : fill;
+    }
+  }
+  // the P int32 of the quad at q0 (row ids, column ids); -1 outside [lo, hi)
+  __device__ __forceinline__ static void ldi(const int32_t* __restrict__ base, int q0, int lo, int hi,
+                                              int (&r)[P]) {
+    if (q0 >= lo && q0 + P <= hi) {
+      if constexpr (P == 4) {
+        const int4 t = *reinterpret_cast<const int4*>(base + q0);
+        r[0] = t.x; r[1] = t.y; r[2] = t.z; r[3] = t.w;
+      } else {
+        const int2 t = *reinterpret_cast<const int2*>(base + q0);
+        r[0] = t.x; r[1] = t.y;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < P; ++k) r[k] = in(q0 + k, lo, hi) ? base[q0 + k] : -1;
+    }
+  }
+  // store the quad at q0, only its positions inside [lo, hi)
+  __device__ __forceinline__ static void stq(float* __restrict__ base, int q0, int lo, int hi,
+                                              const float (&o)[4]) {
+    if (q0 >= lo && q0 + P <= hi) {
+      *reinterpret_cast<float4*>(base + (int64_t)q0 * H) = make_float4(o[0], o[1], o[2], o[3]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (in(q0 + i / H, lo, hi)) base[(int64_t)q0 * H + i] = o[i];
+    }
+  }
+  // the stored logits of the quad (a.s), or lhs + rhs from the nodes (a.node_l: position
+  // q0 + k in row rk[k]); kId outside [lo, hi)
+  __device__ __forceinline__ void raw(int q0, int lo, int hi, const int (&rk)[P], float (&x)[4]) const {
+    if (a.node_l != nullptr) {
+      int c[P];
+      ldi(a.cols, q0, lo, hi, c);
+#pragma unroll
+      for (int k = 0; k < P; ++k) {
+        float lv[H], rv[H];
+        if (in(q0 + k, lo, hi)) {
+          ldrow<H>(a.node_l + (int64_t)c[k] * H, lv);
+          ldrow<H>(a.node_r + (int64_t)rk[k] * H, rv);
+        }
+#pragma unroll
+        for (int h = 0; h < H; ++h) x[k * H + h] = in(q0 + k, lo, hi) ? lv[h] + rv[h] : kId;
+      }
+    } else {
+      ldq(a.s, q0, lo, hi, x, kId);
+    }
+  }
+  // the forward's values: raw logits with the fused leaky_relu on the positions inside [lo, hi)
+  __device__ __forceinline__ void logits(int q0, int lo, int hi, const int (&rk)[P], float (&x)[4]) const {
+    raw(q0, lo, hi, rk, x);
+    if (a.act) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (in(q0 + i / H, lo, hi)) x[i] = x[i] > 0.0f ? x[i] : x[i] * a.act_slope;
+    }
+  }
+  // the statistics sweep's values of the quad: forward the logits, backward a * ga
+  __device__ __forceinline__ void stat_values(int q0, int lo, int hi, const int (&rk)[P],
+                                              float (&x)[4]) const {
+    if constexpr (MODE == SM_DOTSUM) {
+      float g[4];
+      ldq(a.s, q0, lo, hi, x, 0.0f);
+      ldq(a.ga, q0, lo, hi, g, 0.0f);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) x[i] *= g[i];
+    } else {
+      logits(q0, lo, hi, rk, x);
+    }
+  }
+
+  // ---- lane and wave state ----
+  // fold one quad's values (kId where masked) into this lane's state: one rescale
+  __device__ __forceinline__ void absorb(const float (&x)[4]) {
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      if constexpr (MODE == SM_STATS) {
+        float mb = x[h];
+#pragma unroll
+        for (int k = 1; k < P; ++k) mb = fmaxf(mb, x[k * H + h]);
+        const float mn = fmaxf(m[h], mb);
+        const float ms = mn == -INFINITY ? 0.0f : mn;
+        float s = l[h] * fexp(m[h] - ms);
+#pragma unroll
+        for (int k = 0; k < P; ++k) s += fexp(x[k * H + h] - ms);
+        l[h] = s;
+        m[h] = mn;
+      } else {
+#pragma unroll
+        for (int k = 0; k < P; ++k) m[h] += x[k * H + h];
+      }
+    }
+  }
+  __device__ __forceinline__ static void fold(float& m, float& l, float x) {
+    OwnedWalk<H, MODE>::fold(m, l, x);
+  }
+  __device__ __forceinline__ static void merge_into(float& m, float& l, float m2, float l2) {
+    if constexpr (MODE == SM_STATS) merge1(m, l, m2, l2);
+    else m += m2;
+  }
+  // every lane ends with the wave's reduction (xor butterfly)
+  __device__ __forceinline__ void reduce() {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1)
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const float m2 = __shfl_xor(m[h], d);
+        const float l2 = MODE == SM_STATS ? __shfl_xor(l[h], d) : 0.0f;
+        merge_into(m[h], l[h], m2, l2);
+      }
+  }
+  // a finished row's statistics: forward (max, 1 / sum), backward sum(a ga); to the
+  // statistics arrays and, for the span's first kRows rows, to the LDS cache
+  __device__ __forceinline__ void put(int row, const float (&pm)[H], const float (&pl)[H]) {
+    const bool cached = cache != nullptr && row - c0 >= 0 && row - c0 < kRows;
+    spill |= !cached;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const float i = MODE == SM_STATS ? 1.0f / pl[h] : 0.0f;
+      a.stat0[(int64_t)row * H + h] = pm[h];
+      if constexpr (MODE == SM_STATS) a.stat1[(int64_t)row * H + h] = i;
+      if (cached) {
+        cache[(row - c0) * 2 * H + h] = pm[h];
+        cache[(row - c0) * 2 * H + H + h] = i;
+      }
+    }
+  }
+  __device__ __forceinline__ void stats_of(int row, float (&sm)[H], float (&si)[H]) const {
+    if (cache != nullptr && row - c0 >= 0 && row - c0 < kRows) {
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        sm[h] = cache[(row - c0) * 2 * H + h];
+        si[h] = cache[(row - c0) * 2 * H + H + h];
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        sm[h] = ld_fresh(a.stat0 + (int64_t)row * H + h);
+        si[h] = MODE == SM_STATS ? ld_fresh(a.stat1 + (int64_t)row * H + h) : 0.0f;
+      }
+    }
+  }
+  // the row of the step's position plast, on every lane (jl = its lane, kl = its slot)
+  __device__ __forceinline__ static int row_at(const int (&rk)[P], int b, int plast) {
+    const int jl = static_cast<int>((plast - b) / P), kl = static_cast<int>((plast - b) % P);
+    int r = rk[0];
+#pragma unroll
+    for (int k = 1; k < P; ++k) r = k == kl ? rk[k] : r;
+    return __shfl(r, jl);
+  }
+
+  // ---- the statistics sweep ----
+  // steps b + u L (u < N) inside row `row` (hub pieces, batches inside one row)
+  template <int N>
+  __device__ __forceinline__ void accumulate(int b, int lo, int hi, int row) {
+    float x[N][4];
+    int rk[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) rk[k] = row;
+#pragma unroll
+    for (int u = 0; u < N; ++u) stat_values(b + u * L + P * j, lo, hi, rk, x[u]);
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      if constexpr (MODE == SM_STATS) {
+        float mb = x[0][h];
+#pragma unroll
+        for (int u = 0; u < N; ++u)
+#pragma unroll
+          for (int k = 0; k < P; ++k) mb = fmaxf(mb, x[u][k * H + h]);
+        const float mn = fmaxf(m[h], mb);
+        const float ms = mn == -INFINITY ? 0.0f : mn;
+        float s = l[h] * fexp(m[h] - ms);
+#pragma unroll
+        for (int u = 0; u < N; ++u)
+#pragma unroll
+          for (int k = 0; k < P; ++k) s += fexp(x[u][k * H + h] - ms);
+        l[h] = s;
+        m[h] = mn;
+      } else {
+#pragma unroll
+        for (int u = 0; u < N; ++u)
+#pragma unroll
+          for (int k = 0; k < P; ++k) m[h] += x[u][k * H + h];
+      }
+    }
+  }
+  // a step [bu, bu + L) in which cur ends (at cur_end <= plast, the step's last position
+  // in the span); returns the row that continues into the next step
+  __device__ __forceinline__ int cross(int bu, int s0, int s1, int plast, const float (&x)[4],
+                                       const int (&rk)[P], int cur, int cur_end) {
+    const int q0 = bu + P * j;
+    // cur's positions (a prefix of the step) into the running state, then cur is done
+    float xc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xc[i] = in(q0 + i / H, s0, cur_end) ? x[i] : kId;
+    absorb(xc);
+    reduce();
+    if (j == 0) put(cur, m, l);
+    const int rl = row_at(rk, bu, plast);
+    // this lane's positions past cur, in lane-local segments: the first (head), the
+    // last (tail), and rows that start and end inside the lane (finished here)
+    bool has = false, multi = false, other = false;
+    int hrow = -1, trow = -1;
+    float hm[H], hl[H], tm[H], tl[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) { hm[h] = tm[h] = kId; hl[h] = tl[h] = 0.0f; }
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      if (!in(q0 + k, cur_end, s1)) continue;
+      other |= rk[k] != rl;
+      if (has && rk[k] != trow) {  // trow's segment ends inside this lane
+        if (!multi) {
+#pragma unroll
+          for (int h = 0; h < H; ++h) { hm[h] = tm[h]; hl[h] = tl[h]; }
+          hrow = trow;
+          multi = true;
+        } else {
+          put(trow, tm, tl);
+        }
+#pragma unroll
+        for (int h = 0; h < H; ++h) { tm[h] = kId; tl[h] = 0.0f; }
+      }
+      has = true;
+      trow = rk[k];
+#pragma unroll
+      for (int h = 0; h < H; ++h) fold(tm[h], tl[h], x[k * H + h]);
+    }
+    if (!multi) hrow = trow;
+    if (__ballot(other) == 0) {
+      // one new row (rl) from cur_end on: each lane keeps its own state of it
+#pragma unroll
+      for (int h = 0; h < H; ++h) { m[h] = tm[h]; l[h] = tl[h]; }
+      return rl;
+    }
+    // segmented inclusive scan of the lanes' last segments over j
+    const int rs = trow;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int r2 = __shfl_up(rs, d);
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const float m2 = __shfl_up(tm[h], d);
+        const float l2 = MODE == SM_STATS ? __shfl_up(tl[h], d) : 0.0f;
+        if (j >= d && r2 == rs) merge_into(tm[h], tl[h], m2, l2);
+      }
+    }
+    // a lane's first segment continues the previous lane's scan
+    const int rp = __shfl_up(rs, 1);
+    const int hn = __shfl_down(hrow, 1);
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const float m2 = __shfl_up(tm[h], 1);
+      const float l2 = MODE == SM_STATS ? __shfl_up(tl[h], 1) : 0.0f;
+      if (multi && j >= 1 && rp == hrow) merge_into(hm[h], hl[h], m2, l2);
+    }
+    if (multi) put(hrow, hm, hl);
+    if (has && (j == 63 || hn != rs) && rs != rl) put(rs, tm, tl);
+    clear();
+    if (j == static_cast<int>((plast - bu) / P)) {
+#pragma unroll
+      for (int h = 0; h < H; ++h) { m[h] = tm[h]; l[h] = tl[h]; }
+    }
+    return rl;
+  }
+  // statistics of the complete rows [s0, s1), cur = the row at s0
+  __device__ void sweep_stats(int s0, int s1, int cur) {
+    int cur_end = end_of(cur);
+    clear();
+    for (int b = first(s0); b < s1; b += U * L) {
+      const int last = (b + U * L < s1 ? b + U * L : s1) - 1;
+      if (cur_end > last) {  // the batch inside cur
+        accumulate<U>(b, s0, s1, cur);
+        continue;
+      }
+      int rk[U][P];
+      batch_rows<U>(b, s0, s1, cur, rk);
+      float x[U][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u) stat_values(b + u * L + P * j, s0, s1, rk[u], x[u]);
+      // one step at a time (the batch shifts down: one copy of the step logic in the code)
+#pragma unroll 1
+      for (int u = 0; u < U; ++u) {
+        const int bu = b + u * L;
+        if (bu >= s1) break;
+        const int plast = (bu + L < s1 ? bu + L : s1) - 1;
+        if (cur_end > plast) {
+          absorb(x[0]);
+        } else {
+          cur = cross(bu, s0, s1, plast, x[0], rk[0], cur, cur_end);
+          cur_end = end_of(cur);
+        }
+        shift(x);
+        shift(rk);
+      }
+    }
+    reduce();
+    if (j == 0) put(cur, m, l);
+  }
+
+  // ---- the output sweep ----
+  // the backward's leaky_relu input of the quad
+  __device__ __forceinline__ void act_input(int q0, int lo, int hi, const int (&rk)[P],
+                                            float (&x)[4]) const {
+    if (a.node_l != nullptr) raw(q0, lo, hi, rk, x);
+    else ldq(a.act_x, q0, lo, hi, x, 0.0f);
+  }
+  // the values the output sweep reads for the quad at q0
+  __device__ __forceinline__ void out_values(int q0, int lo, int hi, const int (&rk)[P], float (&x)[4],
+                                             float (&g)[4], float (&ax)[4]) const {
+    if constexpr (MODE == SM_DOTSUM) {
+      ldq(a.s, q0, lo, hi, x, 0.0f);
+      ldq(a.ga, q0, lo, hi, g, 0.0f);
+      if (a.act) act_input(q0, lo, hi, rk, ax);
+    } else {
+      logits(q0, lo, hi, rk, x);
+    }
+  }
+  // the output of one quad from its values and its positions' statistics
+  __device__ __forceinline__ void out_quad(int q0, int lo, int hi, const float (&x)[4],
+                                           const float (&g)[4], const float (&ax)[4], const float (&sm)[P][H],
+                                           const float (&si)[P][H]) const {
+    float o[4];
+#pragma unroll
+    for (int k = 0; k < P; ++k)
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const int i = k * H + h;
+        if constexpr (MODE == SM_STATS) {
+          o[i] = fexp(x[i] - sm[k][h]) * si[k][h];
+        } else {
+          o[i] = x[i] * g[i] - x[i] * sm[k][h];  // softmax.py:103-112's order
+          if (a.act) o[i] = ax[i] > 0.0f ? o[i] : o[i] * a.act_slope;
+        }
+      }
+    stq(a.out, q0, lo, hi, o);
+  }
+  __device__ __forceinline__ static void same_stats(const float (&cm)[H], const float (&ci)[H], float (&sm)[P][H],
+                                                    float (&si)[P][H]) {
+#pragma unroll
+    for (int k = 0; k < P; ++k)
+#pragma unroll
+      for (int h = 0; h < H; ++h) { sm[k][h] = cm[h]; si[k][h] = ci[h]; }
+  }
+  // the outputs of steps b + u L (u < N), every position inside [lo, hi) in row `row`
+  template <int N>
+  __device__ __forceinline__ void emit(int b, int lo, int hi, const float (&cm)[H], const float (&ci)[H],
+                                       int row) const {
+    float x[N][4], g[N][4], ax[N][4];
+    int rk[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) rk[k] = row;
+#pragma unroll
+    for (int u = 0; u < N; ++u) out_values(b + u * L + P * j, lo, hi, rk, x[u], g[u], ax[u]);
+    float sm[P][H], si[P][H];
+    same_stats(cm, ci, sm, si);
+#pragma unroll
+    for (int u = 0; u < N; ++u) out_quad(b + u * L + P * j, lo, hi, x[u], g[u], ax[u], sm, si);
+  }
+  // the outputs of the complete rows [s0, s1) (cur = the row at s0) from their statistics
+  __device__ void sweep_out(int s0, int s1, int cur) {
+    if (__ballot(spill) != 0) {
+      // statistics of rows past the cache are read back from L2: this wave's stores first
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      __builtin_amdgcn_s_waitcnt(0);
+    }
+    __builtin_amdgcn_wave_barrier();
+    int cur_end = end_of(cur);
+    float cm[H], ci[H];
+    stats_of(cur, cm, ci);
+    for (int b = first(s0); b < s1; b += U * L) {
+      const int last = (b + U * L < s1 ? b + U * L : s1) - 1;
+      if (cur_end > last) {
+        emit<U>(b, s0, s1, cm, ci, cur);
+        continue;
+      }
+      int rk[U][P];
+      batch_rows<U>(b, s0, s1, cur, rk);
+      float x[U][4], g[U][4], ax[U][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u) out_values(b + u * L + P * j, s0, s1, rk[u], x[u], g[u], ax[u]);
+#pragma unroll 1
+      for (int u = 0; u < U; ++u) {
+        const int bu = b + u * L, q0 = bu + P * j;
+        if (bu >= s1) break;
+        const int plast = (bu + L < s1 ? bu + L : s1) - 1;
+        float sm[P][H], si[P][H];
+        same_stats(cm, ci, sm, si);
+        if (cur_end <= plast) {
+#pragma unroll
+          for (int k = 0; k < P; ++k)
+            if (in(q0 + k, cur_end, s1)) stats_of(rk[0][k], sm[k], si[k]);
+        }
+        out_quad(q0, s0, s1, x[0], g[0], ax[0], sm, si);
+        if (cur_end <= plast) {
+          cur = row_at(rk[0], bu, plast);
+          cur_end = end_of(cur);
+          stats_of(cur, cm, ci);
+        }
+        shift(x);
+        shift(g);
+        shift(ax);
+        shift(rk);
+      }
+    }
+  }
+  // rows [s0, s1) complete (cur = the row at s0): statistics, then outputs
+  __device__ void span(int s0, int s1, int cur) {
+    const int rb0 = rb, st0 = st;  // the slice as the span starts (restored for the output sweep)
+    c0 = cur;
+    sweep_stats(s0, s1, cur);
+    rb = rb0;
+    st = st0;
+    sweep_out(s0, s1, cur);
+  }
+  // partial state of hub row positions [pa, pb) -> carry slot
+  __device__ void piece(int pa, int pb, float* slot, int row) {
+    clear();
+    for (int b = first(pa); b < pb; b += U * L) accumulate<U>(b, pa, pb, row);
+    reduce();
+    if (j == 0) {
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        slot[h] = m[h];
+        if constexpr (MODE == SM_STATS) slot[H + h] = l[h];
+      }
+    }
+  }
+  __device__ void emit_range(int pa, int pb, const float (&sm)[H], const float (&si)[H], int row) const {
+    for (int b = first(pa); b < pb; b += U * L) emit<U>(b, pa, pb, sm, si, row);
+  }
+};
+
+// The window prologue of the four-values-per-lane walk: the row offsets of the window's
+// first 64 rows come in as the walk's slice (one load for both ends of the first row and
+// the row the span starts with).
+template <int H, int MODE>
+__global__ void __launch_bounds__(kBlock) k_sm_owned_q(SoftmaxArgs a) {
+  using Walk = QuadWalk<H, MODE>;
+  __shared__ float lds[kBlock / 64][Walk::kRows * 2 * H];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x / 64;
+  const int w = (int)blockIdx.x * (kBlock / 64) + wv;
+  const int lo = w * Walk::W;
+  if (lo >= a.nnz) return;
+  const int hi = lo + Walk::W < a.nnz ? lo + Walk::W : a.nnz;
+  Walk walk(a, lane, lds[wv]);
+  const int r0 = a.rows[lo];
+  const int r1 = a.rows[hi - 1];
+  walk.slice(r0);
+  const int st1 = a.indptr[r1], en1 = a.indptr[r1 + 1];
+  const int st0 = walk.start_of(r0), en0 = walk.start_of(r0 + 1);
+  int s0 = lo;
+  int c = r0;
+  if (st0 < lo) {  // a row that started in an earlier window
+    if (en0 - st0 > Walk::T) walk.piece(lo, en0 < hi ? en0 : hi, a.carry + (int64_t)(2 * w) * 2 * H, r0);
+    s0 = en0;  // a shorter one belongs to the window it started in
+    if (s0 >= hi) return;
+    c = walk.row_holding(s0);
+  }
+  int s1 = en1;
+  if (en1 - st1 > Walk::T) {  // a hub row starting in this window: its first piece
+    walk.piece(st1, hi, a.carry + (int64_t)(2 * w + 1) * 2 * H, r1);
+    s1 = st1;
+  }
+  if (s1 > s0) walk.span(s0, s1, c);
+}
+
+template <int H, int MODE, class Walk>
 __global__ void __launch_bounds__(kBlock) k_sm_owned(SoftmaxArgs a) {
-  using S = OwnedShape<H, MODE>;
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
-  const int64_t lo = w * S::W;
+  const int64_t lo = w * Walk::W;
   if (lo >= a.nnz) return;
-  const int64_t hi = lo + S::W < a.nnz ? lo + S::W : a.nnz;
-  OwnedWalk<H, MODE> walk(a, lane);
+  const int64_t hi = lo + Walk::W < a.nnz ? lo + Walk::W : a.nnz;
+  Walk walk(a, lane);
   const int r0 = a.rows[lo];
   const int64_t st0 = a.indptr[r0], en0 = a.indptr[r0 + 1];
   int64_t s0 = lo;
   if (st0 < lo) {  // a row that started in an earlier window
-    if (en0 - st0 > S::T) walk.piece(lo, en0 < hi ? en0 : hi, a.carry + (2 * w) * 2 * H, r0);
+    if (en0 - st0 > Walk::T) walk.piece(lo, en0 < hi ? en0 : hi, a.carry + (2 * w) * 2 * H, r0);
     s0 = en0;  // a shorter one belongs to the window it started in
   }
   if (s0 >= hi) return;
   const int r1 = a.rows[hi - 1];
   const int64_t st1 = a.indptr[r1], en1 = a.indptr[r1 + 1];
   int64_t s1 = en1;
-  if (en1 - st1 > S::T) {  // a hub row starting in this window: its first piece
+  if (en1 - st1 > Walk::T) {  // a hub row starting in this window: its first piece
     walk.piece(st1, hi, a.carry + (2 * w + 1) * 2 * H, r1);
     s1 = st1;
   }
@@ -590,18 +1199,17 @@ __global__ void __launch_bounds__(kBlock) k_sm_owned(SoftmaxArgs a) {
 }
 
 // hub rows: merge the row's pieces in window order, then write this window's piece
-template <int H, int MODE>
+template <int H, int MODE, class Walk>
 __global__ void __launch_bounds__(kBlock) k_sm_hub(SoftmaxArgs a) {
-  using S = OwnedShape<H, MODE>;
-  constexpr int V = S::V;
+  constexpr int V = Walk::V;
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
-  const int64_t lo = w * S::W;
+  const int64_t lo = w * Walk::W;
   if (lo >= a.nnz) return;
-  const int64_t hi = lo + S::W < a.nnz ? lo + S::W : a.nnz;
-  OwnedWalk<H, MODE> walk(a, lane);
+  const int64_t hi = lo + Walk::W < a.nnz ? lo + Walk::W : a.nnz;
+  Walk walk(a, lane);
   auto finish = [&](int64_t st, int64_t en, int64_t pa, int64_t pb, int row) {
-    const int64_t wf = st / S::W, wl = (en - 1) / S::W;
+    const int64_t wf = st / Walk::W, wl = (en - 1) / Walk::W;
     float m[V], l[V];
     const float* c = a.carry + (2 * wf + 1) * 2 * H + walk.q * V;  // the first piece
 #pragma unroll
@@ -629,14 +1237,14 @@ __global__ void __launch_bounds__(kBlock) k_sm_hub(SoftmaxArgs a) {
         }
       }
     }
-    for (int64_t b = pa; b < pb; b += S::U * S::L) walk.template emit<S::U>(b, pb, m, l, row);
+    walk.emit_range(pa, pb, m, l, row);
   };
   const int r0 = a.rows[lo];
   const int64_t st0 = a.indptr[r0], en0 = a.indptr[r0 + 1];
-  if (st0 < lo && en0 - st0 > S::T) finish(st0, en0, lo, en0 < hi ? en0 : hi, r0);
+  if (st0 < lo && en0 - st0 > Walk::T) finish(st0, en0, lo, en0 < hi ? en0 : hi, r0);
   const int r1 = a.rows[hi - 1];
   const int64_t st1 = a.indptr[r1], en1 = a.indptr[r1 + 1];
-  if (st1 >= lo && en1 - st1 > S::T) finish(st1, en1, st1, hi, r1);
+  if (st1 >= lo && en1 - st1 > Walk::T) finish(st1, en1, st1, hi, r1);
 }
 
 // The chunked row pass of an edge-id walk (round 5): a wave per chunk of K positions,
@@ -665,28 +1273,54 @@ __global__ void __launch_bounds__(kBlock) k_sm_rows_v(SoftmaxArgs a) {
   walk.sweep_stats(p0, p1);
 }
 
-template <int H>
+template <int H, bool QUAD>
 void run_owned(const SoftmaxArgs& a, bool backward, hipStream_t st) {
   auto grid = [&](int64_t W) {
     const int64_t windows = (a.nnz + W - 1) / W;
     return dim3(static_cast<unsigned>((windows + kBlock / 64 - 1) / (kBlock / 64)));
   };
   const dim3 blk(kBlock);
-  if (!backward) {
-    const dim3 g = grid(OwnedShape<H, SM_STATS>::W);
-    hipLaunchKernelGGL((k_sm_owned<H, SM_STATS>), g, blk, 0, st, a);
-    hipLaunchKernelGGL((k_sm_hub<H, SM_STATS>), g, blk, 0, st, a);
+  if constexpr (QUAD) {
+    using WS = QuadWalk<H, SM_STATS>;
+    using WD = QuadWalk<H, SM_DOTSUM>;
+    if (!backward) {
+      hipLaunchKernelGGL((k_sm_owned_q<H, SM_STATS>), grid(WS::W), blk, 0, st, a);
+      hipLaunchKernelGGL((k_sm_hub<H, SM_STATS, WS>), grid(WS::W), blk, 0, st, a);
+    } else {
+      hipLaunchKernelGGL((k_sm_owned_q<H, SM_DOTSUM>), grid(WD::W), blk, 0, st, a);
+      hipLaunchKernelGGL((k_sm_hub<H, SM_DOTSUM, WD>), grid(WD::W), blk, 0, st, a);
+    }
   } else {
-    const dim3 g = grid(OwnedShape<H, SM_DOTSUM>::W);
-    hipLaunchKernelGGL((k_sm_owned<H, SM_DOTSUM>), g, blk, 0, st, a);
-    hipLaunchKernelGGL((k_sm_hub<H, SM_DOTSUM>), g, blk, 0, st, a);
+    using WS = OwnedWalk<H, SM_STATS>;
+    using WD = OwnedWalk<H, SM_DOTSUM>;
+    if (!backward) {
+      hipLaunchKernelGGL((k_sm_owned<H, SM_STATS, WS>), grid(WS::W), blk, 0, st, a);
+      hipLaunchKernelGGL((k_sm_hub<H, SM_STATS, WS>), grid(WS::W), blk, 0, st, a);
+    } else {
+      hipLaunchKernelGGL((k_sm_owned<H, SM_DOTSUM, WD>), grid(WD::W), blk, 0, st, a);
+      hipLaunchKernelGGL((k_sm_hub<H, SM_DOTSUM, WD>), grid(WD::W), blk, 0, st, a);
+    }
   }
+}
+
+// the four-values-per-lane walk: 32-bit row offsets and positions, and its 16-B loads
+// need every per-position array 16-B aligned
+bool quad_ok(const SoftmaxArgs& a) {
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
+  return a.quad && !a.indptr.wide && a.nnz < INT_MAX - 8 * 4096 && al(a.rows) && al(a.s) && al(a.out) && (a.ga == nullptr || al(a.ga)) &&
+         (a.node_l == nullptr || al(a.cols)) && (!a.act || a.node_l != nullptr || al(a.act_x));
 }
 
 template <int H>
 void run(const SoftmaxArgs& a, bool backward, hipStream_t st) {
   if (!a.eids) {
-    run_owned<H>(a, backward, st);
+    if constexpr (H <= 2) {
+      if (quad_ok(a)) {
+        run_owned<H, true>(a, backward, st);
+        return;
+      }
+    }
+    run_owned<H, false>(a, backward, st);
     return;
   }
   const int64_t chunks = (a.nnz + a.chunk - 1) / a.chunk;
@@ -722,10 +1356,10 @@ int64_t softmax_chunk_edges(int64_t nnz, int64_t H) {
 
 // the row-owned walk's carries: two slots of 2H floats per window
 int64_t softmax_owned_carry_bytes(int64_t nnz, int64_t H) {
-  int64_t W = 0;  // the smaller window of the two passes
+  int64_t W = 0;  // the smallest window of the walks
   switch (H) {
-    case 1: W = std::min(OwnedShape<1, SM_STATS>::W, OwnedShape<1, SM_DOTSUM>::W); break;
-    case 2: W = std::min(OwnedShape<2, SM_STATS>::W, OwnedShape<2, SM_DOTSUM>::W); break;
+    case 1: W = std::min({OwnedShape<1, SM_STATS>::W, OwnedShape<1, SM_DOTSUM>::W, QuadShape<1>::W}); break;
+    case 2: W = std::min({OwnedShape<2, SM_STATS>::W, OwnedShape<2, SM_DOTSUM>::W, QuadShape<2>::W}); break;
     case 4: W = std::min(OwnedShape<4, SM_STATS>::W, OwnedShape<4, SM_DOTSUM>::W); break;
     case 8: W = std::min(OwnedShape<8, SM_STATS>::W, OwnedShape<8, SM_DOTSUM>::W); break;
     default: W = std::min(OwnedShape<16, SM_STATS>::W, OwnedShape<16, SM_DOTSUM>::W); break;

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Fused edge softmax on the C3 graph (232,965 nodes / 114.6 M edges), H = 8 and
-H = 1: forward and backward HIP-event medians on the graph, on its in-CSR position
+H = 1 (--quad: H = 1 and 2 on the view, four values per lane against one): forward and backward HIP-event medians on the graph, on its in-CSR position
 view with the chunked row + edge passes, and on the view with the row-owned walk, plus a digest of every output (run against two builds of the library to
 show bit-identity)."""
 import hashlib
@@ -40,14 +40,21 @@ def main():
     # for counter passes
     pmc = "--pmc" in sys.argv
     pmc_h = 1 if "--pmc-h1" in sys.argv else 8  # --pmc --pmc-h1: the H = 1 view instead
-    for H in ((pmc_h,) if pmc else (8, 1)):
+    quad_only = "--quad" in sys.argv  # H = 1 / 2 on the view: four values per lane vs one
+    hs = (1, 2) if quad_only else ((pmc_h,) if pmc else (8, 1))
+    for H in hs:
         gen = th.Generator(device=dev).manual_seed(H)
         s = th.randn(gidx.number_of_edges(), H, 1, device=dev, generator=gen) * 3
         ga = th.randn(s.shape, device=dev, generator=gen)
         view = gidx.position_view("in")
-        routes = (("graph", gidx, "1"), ("view_chunked", view, "0"), ("view", view, "1"))
-        for name, gi, owned in (routes[1:] if pmc else routes):
+        routes = (("graph", gidx, "1", "1"), ("view_chunked", view, "0", "1"), ("view", view, "1", "1"))
+        if quad_only:
+            routes = (("view_plain", view, "1", "0"), ("view", view, "1", "1"))
+        elif pmc:
+            routes = routes[1:]
+        for name, gi, owned, quad in routes:
             os.environ["DGLMI_SOFTMAX_OWNED"] = owned  # 0: the chunked row + edge passes
+            os.environ["DGLMI_SOFTMAX_QUAD"] = quad  # 0: one position per lane at H <= 2
             out, gs = th.empty_like(s), th.empty_like(s)
             res["H%d_%s_fwd_ms" % (H, name)] = ktime(lambda: K.edge_softmax_forward(gi, s, out))
             res["H%d_%s_bwd_ms" % (H, name)] = ktime(lambda: K.edge_softmax_backward(gi, out, ga, gs))

@@ -17,16 +17,20 @@ DEV = "cuda:0"
 
 
 def _shape(H):
+    """(step, window, hub threshold) of the walk H takes: four values per lane for H <= 2
+    (QuadWalk: 4 / H positions per lane, 64 * 4 / H a step), else V = min(H, 4) heads of
+    one position per lane.  Windows are 2048 positions either way."""
     V = min(H, 4)
-    L = 64 // (H // V)
-    W = 32 * L
+    L = 64 * 4 // H if H <= 2 else 64 // (H // V)
+    W = 2048
     return L, W, 2 * W
 
 
 def _degrees(H, seed):
     L, W, T = _shape(H)
     rs = np.random.RandomState(seed)
-    edge = [0, 1, 2, 3, L - 1, L, L + 1, W - 1, W, W + 1, T - 1, T, T + 1, 3 * W + 5, 11 * W + 3]
+    edge = [0, 1, 2, 3, 4, 5, 63, 64, 65, L - 1, L, L + 1, W - 1, W, W + 1, T - 1, T, T + 1,
+            3 * W + 5, 11 * W + 3]
     tiny = list(rs.randint(0, 4, 3000))
     mid = list(rs.randint(1, 3 * L, 400))
     big = list(rs.randint(W // 2, T + 1, 60))
@@ -82,6 +86,57 @@ def test_owned_softmax_fp64_and_chunked(H, monkeypatch):
     gref = a64 * g64 - a64 * S[rows]
     assert th.allclose(g1.double(), gref, rtol=1e-4, atol=1e-6)
     assert th.allclose(g1, g0, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("mode", ["stored", "leaky", "node_logits"])
+@pytest.mark.parametrize("H", [1, 2])
+def test_quad_walk_matches_plain_walk(H, mode, monkeypatch):
+    """H <= 2 on the row-owned walk: four values per lane (QuadWalk, 16-B loads, rows that
+    start and end inside one lane's positions finished by that lane) against one position
+    per lane (DGLMI_SOFTMAX_QUAD=0) and fp64 -- stored logits, the fused leaky_relu and
+    the node logits, forward and backward, on degree sequences that end rows inside a
+    lane's positions, on step, window and hub boundaries."""
+    monkeypatch.setenv("DGLMI_SOFTMAX_OWNED", "1")
+    deg = _degrees(H, 80 + H)
+    n = len(deg)
+    gidx = _graph(deg, 81 + H)
+    view = gidx.position_view("in")
+    rows = view.in_csr.rows.long()
+    m = int(deg.sum())
+    gen = th.Generator(device=DEV).manual_seed(H + 11)
+    el = th.randn(n, H, 1, device=DEV, generator=gen) * 2
+    er = th.randn(n, H, 1, device=DEV, generator=gen) * 2
+    s = th.randn(m, H, 1, device=DEV, generator=gen) * 3
+    ga = th.randn(m, H, 1, device=DEV, generator=gen)
+    slope = 0.2
+    res = {}
+    for quad in ("1", "0"):
+        monkeypatch.setenv("DGLMI_SOFTMAX_QUAD", quad)
+        a, gs = th.empty_like(s), th.empty_like(s)
+        if mode == "stored":
+            K.edge_softmax_forward(view, s, a)
+            K.edge_softmax_backward(view, a, ga, gs)
+        elif mode == "leaky":
+            K.edge_softmax_leaky_forward(view, s, slope, a)
+            K.edge_softmax_leaky_backward(view, a, ga, s, slope, gs)
+        else:
+            K.edge_softmax_node_logits_forward(view, el, er, slope, a)
+            K.edge_softmax_node_logits_backward(view, a, ga, el, er, slope, gs)
+        res[quad] = (a, gs)
+    (a1, g1), (a0, g0) = res["1"], res["0"]
+    assert th.allclose(a1, a0, rtol=1e-5, atol=1e-7)
+    assert th.allclose(g1, g0, rtol=1e-4, atol=1e-6)
+    pre = s if mode != "node_logits" else el[view.in_csr.indices.long()] + er[rows]
+    pre = pre.reshape(m, H)
+    x = pre if mode == "stored" else th.nn.functional.leaky_relu(pre, slope)
+    ref = _fp64(rows, x, n)
+    assert th.allclose(a1.reshape(m, H).double(), ref, rtol=1e-5, atol=1e-7)
+    a64, g64 = a1.reshape(m, H).double(), ga.reshape(m, H).double()
+    S = th.zeros((n, H), dtype=th.float64, device=DEV).index_add_(0, rows, a64 * g64)
+    gref = a64 * g64 - a64 * S[rows]
+    if mode != "stored":
+        gref = th.where(pre > 0, gref, gref * slope)
+    assert th.allclose(g1.reshape(m, H).double(), gref, rtol=1e-4, atol=1e-6)
 
 
 def test_owned_softmax_deterministic(monkeypatch):
