@@ -193,6 +193,101 @@ __global__ void __launch_bounds__(kBlock) k_sm_edges(SoftmaxArgs a) {
   }
 }
 
+// k_sm_edges in edge-id order at H <= 2 (round 6): P = 4 / H consecutive edges per lane,
+// so every per-edge stream (logits or softmax output, its gradient, the leaky_relu input,
+// the COO) is one 16-B (COO at H = 2: 8-B) load or store per lane instead of P; the
+// statistics gathers stay per edge (a few MB of rows: L2).  The same operations in the
+// same order as k_sm_edges, so the same bits.  Every stream 16-B aligned (quad_edges_ok).
+template <int H, int MODE>
+__global__ void __launch_bounds__(kBlock) k_sm_edges_q(SoftmaxArgs a) {
+  constexpr int P = 4 / H;
+  const int64_t nq = (a.nnz + P - 1) / P;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  auto ld4 = [](const float* __restrict__ base, int64_t e0, int64_t n, float (&x)[4]) {
+    if (e0 + P <= n) {
+      const float4 t = *reinterpret_cast<const float4*>(base + e0 * H);
+      x[0] = t.x; x[1] = t.y; x[2] = t.z; x[3] = t.w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) x[i] = e0 + i / H < n ? base[e0 * H + i] : 0.0f;
+    }
+  };
+  auto ldP = [](const int32_t* __restrict__ base, int64_t e0, int64_t n, int (&r)[P]) {
+    if (e0 + P <= n) {
+      if constexpr (P == 4) {
+        const int4 t = *reinterpret_cast<const int4*>(base + e0);
+        r[0] = t.x; r[1] = t.y; r[2] = t.z; r[3] = t.w;
+      } else {
+        const int2 t = *reinterpret_cast<const int2*>(base + e0);
+        r[0] = t.x; r[1] = t.y;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < P; ++k) r[k] = e0 + k < n ? base[e0 + k] : 0;
+    }
+  };
+  for (int64_t qi = (int64_t)blockIdx.x * kBlock + threadIdx.x; qi < nq; qi += stride) {
+    const int64_t e0 = qi * P;
+    int v[P];
+    ldP(a.coo_dst, e0, a.nnz, v);
+    float s[4], o[4];
+    auto node_logits = [&](float (&y)[4]) {
+      int u[P];
+      ldP(a.coo_src, e0, a.nnz, u);
+#pragma unroll
+      for (int k = 0; k < P; ++k) {
+        float l[H], r[H];
+        ldrow<H>(a.node_l + (int64_t)u[k] * H, l);
+        ldrow<H>(a.node_r + (int64_t)v[k] * H, r);
+#pragma unroll
+        for (int h = 0; h < H; ++h) y[k * H + h] = l[h] + r[h];
+      }
+    };
+    if (MODE == SM_NORMALIZE && a.node_l != nullptr) node_logits(s);
+    else ld4(a.s, e0, a.nnz, s);
+    float g[4], ax[4];
+    if constexpr (MODE == SM_GRAD) {
+      ld4(a.ga, e0, a.nnz, g);
+      if (a.act) {
+        if (a.node_l != nullptr) node_logits(ax);
+        else ld4(a.act_x, e0, a.nnz, ax);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      float x[H];
+      ldrow<H>(a.stat0 + (int64_t)v[k] * H, x);
+      if constexpr (MODE == SM_NORMALIZE) {
+        float l[H], y[H];
+        ldrow<H>(a.stat1 + (int64_t)v[k] * H, l);
+#pragma unroll
+        for (int h = 0; h < H; ++h) y[h] = s[k * H + h];
+        act_fwd<H>(a, y);
+#pragma unroll
+        for (int h = 0; h < H; ++h) o[k * H + h] = expf(y[h] - x[h]) / l[h];
+      } else {
+        float y[H], axk[H];
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          const int i = k * H + h;
+          y[h] = s[i] * g[i] - s[i] * x[h];
+          axk[h] = ax[i];
+        }
+        if (a.act) act_bwd<H>(a, axk, y);
+#pragma unroll
+        for (int h = 0; h < H; ++h) o[k * H + h] = y[h];
+      }
+    }
+    if (e0 + P <= a.nnz) {
+      *reinterpret_cast<float4*>(a.out + e0 * H) = make_float4(o[0], o[1], o[2], o[3]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (e0 + i / H < a.nnz) a.out[e0 * H + i] = o[i];
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Row-owned walk (identity edge ids: a position view, or a graph whose edges came
 // sorted by destination).  The logits of a row are contiguous, so one wave can own
@@ -1311,6 +1406,13 @@ bool quad_ok(const SoftmaxArgs& a) {
          (a.node_l == nullptr || al(a.cols)) && (!a.act || a.node_l != nullptr || al(a.act_x));
 }
 
+// the edge pass in edge-id order with four values per lane: its streams 16-B aligned
+bool quad_edges_ok(const SoftmaxArgs& a) {
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
+  return a.quad && a.coo_dst != nullptr && al(a.coo_dst) && al(a.s) && al(a.out) && (a.ga == nullptr || al(a.ga)) &&
+         (a.node_l == nullptr || al(a.coo_src)) && (!a.act || a.node_l != nullptr || al(a.act_x));
+}
+
 template <int H>
 void run(const SoftmaxArgs& a, bool backward, hipStream_t st) {
   if (!a.eids) {
@@ -1329,14 +1431,21 @@ void run(const SoftmaxArgs& a, bool backward, hipStream_t st) {
   const dim3 rrb(static_cast<unsigned>((chunks + kBlock / 64 - 1) / (kBlock / 64)));
   const int64_t eb = (a.nnz + kBlock - 1) / kBlock;
   const dim3 ebl(static_cast<unsigned>(eb < 256 * 64 ? eb : 256 * 64));
+  bool quad_edges = false;  // the edge-id-order pass with P = 4 / H edges per lane
+  if constexpr (H <= 2) quad_edges = quad_edges_ok(a);
+  constexpr int64_t PQ = H <= 2 ? 4 / H : 1;  // edges per lane there
+  const int64_t qb = (a.nnz + PQ * kBlock - 1) / (PQ * kBlock);
+  const dim3 qbl(static_cast<unsigned>(qb < 256 * 64 ? qb : 256 * 64));
   if (!backward) {
     hipLaunchKernelGGL((k_sm_rows_v<H, SM_STATS>), rrb, blk, 0, st, a);
     if (chunks > 1) hipLaunchKernelGGL((k_sm_fixup<H, SM_STATS>), rb, blk, 0, st, a);
-    hipLaunchKernelGGL((k_sm_edges<H, SM_NORMALIZE>), ebl, blk, 0, st, a);
+    if (quad_edges) hipLaunchKernelGGL((k_sm_edges_q<H <= 2 ? H : 1, SM_NORMALIZE>), qbl, blk, 0, st, a);
+    else hipLaunchKernelGGL((k_sm_edges<H, SM_NORMALIZE>), ebl, blk, 0, st, a);
   } else {
     hipLaunchKernelGGL((k_sm_rows_v<H, SM_DOTSUM>), rrb, blk, 0, st, a);
     if (chunks > 1) hipLaunchKernelGGL((k_sm_fixup<H, SM_DOTSUM>), rb, blk, 0, st, a);
-    hipLaunchKernelGGL((k_sm_edges<H, SM_GRAD>), ebl, blk, 0, st, a);
+    if (quad_edges) hipLaunchKernelGGL((k_sm_edges_q<H <= 2 ? H : 1, SM_GRAD>), qbl, blk, 0, st, a);
+    else hipLaunchKernelGGL((k_sm_edges<H, SM_GRAD>), ebl, blk, 0, st, a);
   }
 }
 

@@ -49,7 +49,8 @@ def main():
         view = gidx.position_view("in")
         routes = (("graph", gidx, "1", "1"), ("view_chunked", view, "0", "1"), ("view", view, "1", "1"))
         if quad_only:
-            routes = (("view_plain", view, "1", "0"), ("view", view, "1", "1"))
+            routes = (("view_plain", view, "1", "0"), ("view", view, "1", "1"),
+                      ("graph_plain", gidx, "1", "0"), ("graph", gidx, "1", "1"))
         elif pmc:
             routes = routes[1:]
         for name, gi, owned, quad in routes:

@@ -139,6 +139,61 @@ def test_quad_walk_matches_plain_walk(H, mode, monkeypatch):
     assert th.allclose(g1.reshape(m, H).double(), gref, rtol=1e-4, atol=1e-6)
 
 
+@pytest.mark.parametrize("mode", ["stored", "leaky", "node_logits"])
+@pytest.mark.parametrize("H", [1, 2])
+def test_quad_edge_pass_bit_identical(H, mode, monkeypatch):
+    """The edge pass in edge-id order (a graph whose edges are not sorted by destination)
+    with 4 / H edges per lane (k_sm_edges_q) gives the one-edge-per-lane pass's bits,
+    forward and backward, for stored logits, the fused leaky_relu and the node logits --
+    on an edge count that is not a multiple of 4 (the last lane's partial quad) -- and
+    matches fp64."""
+    deg = _degrees(H, 90 + H)
+    deg[0] += 3 - int(deg.sum()) % 4  # nnz = 3 (mod 4)
+    n = len(deg)
+    rs = np.random.RandomState(91 + H)
+    dst = np.repeat(np.arange(n), deg)
+    src = rs.randint(0, n, len(dst))
+    perm = rs.permutation(len(dst))
+    gg = dgl.DGLGraph()
+    gg.add_nodes(n)
+    gg.add_edges(src[perm], dst[perm])
+    g = gg._graph.get_immutable_gidx(DEV)
+    assert not (g.eid_identity_bits() & 1)
+    m = len(dst)
+    assert m % 4 == 3
+    gen = th.Generator(device=DEV).manual_seed(H + 13)
+    el = th.randn(n, H, 1, device=DEV, generator=gen) * 2
+    er = th.randn(n, H, 1, device=DEV, generator=gen) * 2
+    s = th.randn(m, H, 1, device=DEV, generator=gen) * 3
+    s[7, 0, 0] = -float("inf")
+    s[m - 1, 0, 0] = float("nan")
+    ga = th.randn(m, H, 1, device=DEV, generator=gen)
+    res = {}
+    for quad in ("1", "0"):
+        monkeypatch.setenv("DGLMI_SOFTMAX_QUAD", quad)
+        a, gs = th.empty_like(s), th.empty_like(s)
+        if mode == "stored":
+            K.edge_softmax_forward(g, s, a)
+            K.edge_softmax_backward(g, a, ga, gs)
+        elif mode == "leaky":
+            K.edge_softmax_leaky_forward(g, s, 0.2, a)
+            K.edge_softmax_leaky_backward(g, a, ga, s, 0.2, gs)
+        else:
+            K.edge_softmax_node_logits_forward(g, el, er, 0.2, a)
+            K.edge_softmax_node_logits_backward(g, a, ga, el, er, 0.2, gs)
+        res[quad] = (a, gs)
+    for x, y in zip(res["1"], res["0"]):
+        assert th.equal(th.isnan(x), th.isnan(y)) and th.equal(x[~th.isnan(y)], y[~th.isnan(y)])
+    rows = th.from_numpy(dst[perm]).to(DEV)
+    pre = s.reshape(m, H) if mode != "node_logits" else (el[th.from_numpy(src[perm]).to(DEV)] + er[rows]).reshape(m, H)
+    x = pre if mode == "stored" else th.nn.functional.leaky_relu(pre, 0.2)
+    ref = _fp64(rows, x, n)
+    a1 = res["1"][0].reshape(m, H)
+    fin = ~th.isnan(ref)
+    assert th.equal(th.isnan(a1), ~fin)
+    assert th.allclose(a1[fin].double(), ref[fin], rtol=1e-5, atol=1e-7)
+
+
 def test_owned_softmax_deterministic(monkeypatch):
     monkeypatch.setenv("DGLMI_SOFTMAX_OWNED", "1")
     deg = _degrees(8, 3)
