@@ -689,13 +689,16 @@ struct OwnedWalk {
 // fwd / bwd 0.64 / 0.96 -> 0.36 / 0.44 ms (profiles/r06_edge_softmax_quad_probe.json).
 template <int H>
 struct QuadShape {
-  static_assert(H == 1 || H == 2, "four values per lane: H <= 2");
+  static_assert(H == 1 || H == 2 || H == 4, "four values per lane: H <= 4");
   static constexpr int P = 4 / H;   // positions per lane
   static constexpr int L = 64 * P;  // positions per step
 #ifndef DGLMI_SMQ_U
 #define DGLMI_SMQ_U 2
 #endif
-  static constexpr int U = DGLMI_SMQ_U;  // steps whose loads are issued together
+#ifndef DGLMI_SMQ_U4
+#define DGLMI_SMQ_U4 4
+#endif
+  static constexpr int U = H == 4 ? DGLMI_SMQ_U4 : DGLMI_SMQ_U;  // steps whose loads are issued together
 #ifndef DGLMI_SMQ_W
 #define DGLMI_SMQ_W 2048
 #endif
@@ -808,9 +811,11 @@ struct QuadWalk {
       if constexpr (P == 4) {
         const int4 t = *reinterpret_cast<const int4*>(base + q0);
         r[0] = t.x; r[1] = t.y; r[2] = t.z; r[3] = t.w;
-      } else {
+      } else if constexpr (P == 2) {
         const int2 t = *reinterpret_cast<const int2*>(base + q0);
         r[0] = t.x; r[1] = t.y;
+      } else {
+        r[0] = base[q0];
       }
     } else {
 #pragma unroll
@@ -1416,7 +1421,7 @@ bool quad_edges_ok(const SoftmaxArgs& a) {
 template <int H>
 void run(const SoftmaxArgs& a, bool backward, hipStream_t st) {
   if (!a.eids) {
-    if constexpr (H <= 2) {
+    if constexpr (H <= 4) {
       if (quad_ok(a)) {
         run_owned<H, true>(a, backward, st);
         return;

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Fused edge softmax on the C3 graph (232,965 nodes / 114.6 M edges), H = 8 and
-H = 1 (--quad: H = 1 and 2 on the view, four values per lane against one): forward and backward HIP-event medians on the graph, on its in-CSR position
+H = 1 (--quad: H = 1, 2 and 4 on the view and the graph, four values per lane against one): forward and backward HIP-event medians on the graph, on its in-CSR position
 view with the chunked row + edge passes, and on the view with the row-owned walk, plus a digest of every output (run against two builds of the library to
 show bit-identity)."""
 import hashlib
@@ -41,7 +41,7 @@ def main():
     pmc = "--pmc" in sys.argv
     pmc_h = 1 if "--pmc-h1" in sys.argv else 8  # --pmc --pmc-h1: the H = 1 view instead
     quad_only = "--quad" in sys.argv  # H = 1 / 2 on the view: four values per lane vs one
-    hs = (1, 2) if quad_only else ((pmc_h,) if pmc else (8, 1))
+    hs = (1, 2, 4) if quad_only else ((pmc_h,) if pmc else (8, 1))
     for H in hs:
         gen = th.Generator(device=dev).manual_seed(H)
         s = th.randn(gidx.number_of_edges(), H, 1, device=dev, generator=gen) * 3

@@ -17,9 +17,9 @@ DEV = "cuda:0"
 
 
 def _shape(H):
-    """(step, window, hub threshold) of the walk H takes: four values per lane for H <= 2
-    (QuadWalk: 4 / H positions per lane, 64 * 4 / H a step), else V = min(H, 4) heads of
-    one position per lane.  Windows are 2048 positions either way."""
+    """(step, window, hub threshold) of the walk H takes: four values per lane for H <= 4
+    (QuadWalk: 4 / H positions per lane, 64 * 4 / H a step), else V = 4 heads of one
+    position per lane.  Windows are 2048 positions either way."""
     V = min(H, 4)
     L = 64 * 4 // H if H <= 2 else 64 // (H // V)
     W = 2048
@@ -89,9 +89,9 @@ def test_owned_softmax_fp64_and_chunked(H, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", ["stored", "leaky", "node_logits"])
-@pytest.mark.parametrize("H", [1, 2])
+@pytest.mark.parametrize("H", [1, 2, 4])
 def test_quad_walk_matches_plain_walk(H, mode, monkeypatch):
-    """H <= 2 on the row-owned walk: four values per lane (QuadWalk, 16-B loads, rows that
+    """H <= 4 on the row-owned walk: four values per lane (QuadWalk, 16-B loads, rows that
     start and end inside one lane's positions finished by that lane) against one position
     per lane (DGLMI_SOFTMAX_QUAD=0) and fp64 -- stored logits, the fused leaky_relu and
     the node logits, forward and backward, on degree sequences that end rows inside a
