@@ -1673,18 +1673,42 @@ int DGLMIEdgeSoftmaxSupported(int64_t values_per_edge) {
   return softmax_supported(values_per_edge) ? 1 : 0;
 }
 
+namespace {
+// The edge softmax's workspace: the row statistics (max | sum, or S; unless the caller's),
+// then the chunk carries and one segmented-fixup counter per chunk (the row-owned walk's
+// carries fit in the same room), then the forward edge pass's packed row statistics
+// (edge-id order: each row's max and sum side by side, one request per edge).
+int64_t round256(int64_t b) { return (b + 255) & ~int64_t(255); }
+int64_t softmax_carry_bytes(int64_t nnz, int64_t H) {
+  const int64_t K = softmax_chunk_edges(nnz, H);
+  const int64_t chunks = (nnz + K - 1) / K;
+  const int64_t chunked = ((chunks * 2 * H * 4 + 15) & ~int64_t(15)) + chunks * 4;
+  return round256(std::max(chunked, softmax_owned_carry_bytes(nnz, H)));
+}
+}  // namespace
+
 int64_t DGLMIEdgeSoftmaxWorkspaceBytes(const DGLMICsr* in_csr, int64_t values_per_edge) {
   if (in_csr == nullptr || in_csr->nnz <= 0 || values_per_edge <= 0) return 0;
-  const int64_t K = softmax_chunk_edges(in_csr->nnz, values_per_edge);
-  const int64_t chunks = (in_csr->nnz + K - 1) / K;
-  const int64_t stats = ((2 * in_csr->num_rows * values_per_edge * 4) + 255) & ~int64_t(255);
-  // carries, then one segmented-fixup counter per chunk (the row-owned walk's carries
-  // fit in the same room)
-  const int64_t chunked = ((chunks * 2 * values_per_edge * 4 + 15) & ~int64_t(15)) + chunks * 4;
-  return stats + std::max(chunked, softmax_owned_carry_bytes(in_csr->nnz, values_per_edge));
+  const int64_t rows = in_csr->num_rows, H = values_per_edge;
+  return round256(2 * rows * H * 4) + softmax_carry_bytes(in_csr->nnz, H) + round256(2 * rows * H * 4);
 }
 
 namespace {
+// Points the softmax arguments into its workspace (DGLMIEdgeSoftmaxWorkspaceBytes's layout);
+// own_stats: the row statistics live there too (else the caller set stat0 / stat1).
+void softmax_layout(dglmi::SoftmaxArgs& a, void* ws, bool own_stats) {
+  const int64_t H = a.H;
+  char* base = static_cast<char*>(ws);
+  if (own_stats) {
+    a.stat0 = reinterpret_cast<float*>(base);
+    a.stat1 = a.stat0 + a.num_rows * H;
+  }
+  a.carry = reinterpret_cast<float*>(base + round256(2 * a.num_rows * H * 4));
+  a.seg_cnt = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(a.carry) +
+                                         ((((a.nnz + a.chunk - 1) / a.chunk) * 2 * H * 4 + 15) & ~int64_t(15)));
+  if (a.pack) a.stat_pk = reinterpret_cast<float*>(reinterpret_cast<char*>(a.carry) + softmax_carry_bytes(a.nnz, H));
+}
+
 // Shared checks of the edge-softmax entry points; returns H.
 int64_t softmax_setup(const DGLMIGraph* g, const DGLMIArray* x, const char* name,
                       dglmi::SoftmaxArgs& a) {
@@ -1708,6 +1732,10 @@ int64_t softmax_setup(const DGLMIGraph* g, const DGLMIArray* x, const char* name
   // H <= 2 there: four values per lane (DGLMI_SOFTMAX_QUAD=0: one position per lane, for A/B)
   const char* quad = std::getenv("DGLMI_SOFTMAX_QUAD");
   a.quad = !(quad != nullptr && quad[0] == '0');
+  // the forward edge pass in edge-id order reads packed row statistics (DGLMI_SOFTMAX_PACK=0:
+  // the two arrays, for A/B)
+  const char* pack = std::getenv("DGLMI_SOFTMAX_PACK");
+  a.pack = !(pack != nullptr && pack[0] == '0');
   a.coo_dst = (g->coo_src && g->coo_dst) ? g->coo_dst : nullptr;
   a.nnz = in.nnz;
   a.num_rows = in.num_rows;
@@ -1732,13 +1760,7 @@ int softmax_forward(const DGLMIGraph* graph, const DGLMIArray* logits, DGLMIArra
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (a.nnz == 0) return 0;
   Scratch ws(graph, DGLMIEdgeSoftmaxWorkspaceBytes(&graph->in_csr, H), s);
-  const int64_t stats = ((2 * a.num_rows * H * 4) + 255) & ~int64_t(255);
-  a.stat0 = static_cast<float*>(ws.ptr);
-  a.stat1 = a.stat0 + a.num_rows * H;
-  a.carry = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + stats);
-  a.seg_cnt = reinterpret_cast<int32_t*>(
-      reinterpret_cast<char*>(a.carry) +
-      ((((a.nnz + a.chunk - 1) / a.chunk) * 2 * H * 4 + 15) & ~int64_t(15)));
+  softmax_layout(a, ws.ptr, true);
   a.s = logits->data;
   a.out = out->data;
   launch_edge_softmax(a, false, s);
@@ -1770,12 +1792,7 @@ int softmax_backward(const DGLMIGraph* graph, const DGLMIArray* out, const DGLMI
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (a.nnz == 0) return 0;
   Scratch ws(graph, DGLMIEdgeSoftmaxWorkspaceBytes(&graph->in_csr, H), s);
-  const int64_t stats = ((2 * a.num_rows * H * 4) + 255) & ~int64_t(255);
-  a.stat0 = static_cast<float*>(ws.ptr);
-  a.carry = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + stats);
-  a.seg_cnt = reinterpret_cast<int32_t*>(
-      reinterpret_cast<char*>(a.carry) +
-      ((((a.nnz + a.chunk - 1) / a.chunk) * 2 * H * 4 + 15) & ~int64_t(15)));
+  softmax_layout(a, ws.ptr, true);
   a.s = out->data;
   a.ga = grad_out->data;
   a.out = grad_logits->data;
@@ -1832,13 +1849,7 @@ int DGLMIEdgeSoftmaxNodeLogitsForward(const DGLMIGraph* graph, const DGLMIArray*
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (a.nnz == 0) return 0;
   Scratch ws(graph, DGLMIEdgeSoftmaxWorkspaceBytes(&graph->in_csr, H), s);
-  const int64_t stats = ((2 * a.num_rows * H * 4) + 255) & ~int64_t(255);
-  a.stat0 = static_cast<float*>(ws.ptr);
-  a.stat1 = a.stat0 + a.num_rows * H;
-  a.carry = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + stats);
-  a.seg_cnt = reinterpret_cast<int32_t*>(
-      reinterpret_cast<char*>(a.carry) +
-      ((((a.nnz + a.chunk - 1) / a.chunk) * 2 * H * 4 + 15) & ~int64_t(15)));
+  softmax_layout(a, ws.ptr, true);
   a.s = nullptr;
   a.out = out->data;
   launch_edge_softmax(a, false, s);
@@ -1864,14 +1875,10 @@ int DGLMIEdgeSoftmaxNodeLogitsForwardEx(const DGLMIGraph* graph, const DGLMIArra
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (a.nnz == 0) return 0;
   Scratch ws(graph, DGLMIEdgeSoftmaxWorkspaceBytes(&graph->in_csr, H), s);
-  const int64_t stats = ((2 * a.num_rows * H * 4) + 255) & ~int64_t(255);
   // the row statistics straight into the caller's buffers
   a.stat0 = row_max->data;
   a.stat1 = row_sum->data;
-  a.carry = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + stats);
-  a.seg_cnt = reinterpret_cast<int32_t*>(
-      reinterpret_cast<char*>(a.carry) +
-      ((((a.nnz + a.chunk - 1) / a.chunk) * 2 * H * 4 + 15) & ~int64_t(15)));
+  softmax_layout(a, ws.ptr, false);
   a.s = nullptr;
   a.out = out->data;
   launch_edge_softmax(a, false, s);
@@ -1899,12 +1906,7 @@ int DGLMIEdgeSoftmaxNodeLogitsBackward(const DGLMIGraph* graph, const DGLMIArray
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (a.nnz == 0) return 0;
   Scratch ws(graph, DGLMIEdgeSoftmaxWorkspaceBytes(&graph->in_csr, H), s);
-  const int64_t stats = ((2 * a.num_rows * H * 4) + 255) & ~int64_t(255);
-  a.stat0 = static_cast<float*>(ws.ptr);
-  a.carry = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + stats);
-  a.seg_cnt = reinterpret_cast<int32_t*>(
-      reinterpret_cast<char*>(a.carry) +
-      ((((a.nnz + a.chunk - 1) / a.chunk) * 2 * H * 4 + 15) & ~int64_t(15)));
+  softmax_layout(a, ws.ptr, true);
   a.s = out->data;
   a.ga = grad_out->data;
   a.out = grad_logits->data;

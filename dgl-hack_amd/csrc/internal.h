@@ -274,7 +274,11 @@ struct SoftmaxArgs {
   const float* node_r;
   const int32_t* cols;     // in-CSR indices (node_l mode)
   const int32_t* coo_src;  // with coo_dst: the edge-id-order pass's source per edge
-  int quad;                // H <= 2 on the row-owned walk: four values per lane (16-B loads)
+  int quad;                // H <= 4 on the row-owned walk: four values per lane (16-B loads)
+  // the forward edge pass in edge-id order: each row's (max, sum) side by side (2H floats),
+  // packed after the row pass (one request per edge instead of two); null: stat0 / stat1
+  int pack;
+  float* stat_pk;
 };
 bool softmax_supported(int64_t H);
 

@@ -171,15 +171,21 @@ __global__ void __launch_bounds__(kBlock) k_sm_edges(SoftmaxArgs a) {
     };
     if (MODE == SM_NORMALIZE && a.node_l != nullptr) node_logits(s);
     else ldrow<H>(a.s + e * H, s);
-    ldrow<H>(a.stat0 + v * H, x);
     if constexpr (MODE == SM_NORMALIZE) {
       float l[H];
-      ldrow<H>(a.stat1 + v * H, l);
+      if (a.stat_pk != nullptr) {  // the row's max and sum side by side: one request
+        ldrow<H>(a.stat_pk + v * 2 * H, x);
+        ldrow<H>(a.stat_pk + v * 2 * H + H, l);
+      } else {
+        ldrow<H>(a.stat0 + v * H, x);
+        ldrow<H>(a.stat1 + v * H, l);
+      }
       act_fwd<H>(a, s);
 #pragma unroll
       for (int h = 0; h < H; ++h) o[h] = expf(s[h] - x[h]) / l[h];
     } else {
       float g[H], ax[H];
+      ldrow<H>(a.stat0 + v * H, x);
       ldrow<H>(a.ga + e * H, g);
       if (a.act) {
         if (a.node_l != nullptr) node_logits(ax);
@@ -190,6 +196,19 @@ __global__ void __launch_bounds__(kBlock) k_sm_edges(SoftmaxArgs a) {
       if (a.act) act_bwd<H>(a, ax, o);
     }
     strow<H>(a.out + e * H, o);
+  }
+}
+
+// The forward's row statistics packed side by side for the edge pass in edge-id order:
+// pk[r] = (max[r, 0..H), sum[r, 0..H)), so an edge's two gathers are one request.
+template <int H>
+__global__ void __launch_bounds__(kBlock) k_sm_pack(SoftmaxArgs a) {
+  const int64_t n = a.num_rows * H;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    const int64_t r = i / H, h = i % H;
+    a.stat_pk[r * 2 * H + h] = a.stat0[i];
+    a.stat_pk[r * 2 * H + H + h] = a.stat1[i];
   }
 }
 
@@ -256,10 +275,15 @@ __global__ void __launch_bounds__(kBlock) k_sm_edges_q(SoftmaxArgs a) {
 #pragma unroll
     for (int k = 0; k < P; ++k) {
       float x[H];
-      ldrow<H>(a.stat0 + (int64_t)v[k] * H, x);
       if constexpr (MODE == SM_NORMALIZE) {
         float l[H], y[H];
-        ldrow<H>(a.stat1 + (int64_t)v[k] * H, l);
+        if (a.stat_pk != nullptr) {
+          ldrow<H>(a.stat_pk + (int64_t)v[k] * 2 * H, x);
+          ldrow<H>(a.stat_pk + (int64_t)v[k] * 2 * H + H, l);
+        } else {
+          ldrow<H>(a.stat0 + (int64_t)v[k] * H, x);
+          ldrow<H>(a.stat1 + (int64_t)v[k] * H, l);
+        }
 #pragma unroll
         for (int h = 0; h < H; ++h) y[h] = s[k * H + h];
         act_fwd<H>(a, y);
@@ -267,6 +291,7 @@ __global__ void __launch_bounds__(kBlock) k_sm_edges_q(SoftmaxArgs a) {
         for (int h = 0; h < H; ++h) o[k * H + h] = expf(y[h] - x[h]) / l[h];
       } else {
         float y[H], axk[H];
+        ldrow<H>(a.stat0 + (int64_t)v[k] * H, x);
 #pragma unroll
         for (int h = 0; h < H; ++h) {
           const int i = k * H + h;
@@ -1444,8 +1469,17 @@ void run(const SoftmaxArgs& a, bool backward, hipStream_t st) {
   if (!backward) {
     hipLaunchKernelGGL((k_sm_rows_v<H, SM_STATS>), rrb, blk, 0, st, a);
     if (chunks > 1) hipLaunchKernelGGL((k_sm_fixup<H, SM_STATS>), rb, blk, 0, st, a);
-    if (quad_edges) hipLaunchKernelGGL((k_sm_edges_q<H <= 2 ? H : 1, SM_NORMALIZE>), qbl, blk, 0, st, a);
-    else hipLaunchKernelGGL((k_sm_edges<H, SM_NORMALIZE>), ebl, blk, 0, st, a);
+    // edge-id order: the rows' statistics packed for the edge pass (the rows are gathered
+    // in random order there; in-CSR order reads them in sequence and keeps the two arrays)
+    SoftmaxArgs e = a;
+    if (a.coo_dst != nullptr && a.stat_pk != nullptr) {
+      const int64_t pb = (a.num_rows * H + kBlock - 1) / kBlock;
+      hipLaunchKernelGGL((k_sm_pack<H>), dim3(static_cast<unsigned>(pb < 4096 ? pb : 4096)), blk, 0, st, a);
+    } else {
+      e.stat_pk = nullptr;
+    }
+    if (quad_edges) hipLaunchKernelGGL((k_sm_edges_q<H <= 2 ? H : 1, SM_NORMALIZE>), qbl, blk, 0, st, e);
+    else hipLaunchKernelGGL((k_sm_edges<H, SM_NORMALIZE>), ebl, blk, 0, st, e);
   } else {
     hipLaunchKernelGGL((k_sm_rows_v<H, SM_DOTSUM>), rrb, blk, 0, st, a);
     if (chunks > 1) hipLaunchKernelGGL((k_sm_fixup<H, SM_DOTSUM>), rb, blk, 0, st, a);

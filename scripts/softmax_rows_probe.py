@@ -41,7 +41,7 @@ def main():
     pmc = "--pmc" in sys.argv
     pmc_h = 1 if "--pmc-h1" in sys.argv else 8  # --pmc --pmc-h1: the H = 1 view instead
     quad_only = "--quad" in sys.argv  # H = 1 / 2 on the view: four values per lane vs one
-    hs = (1, 2, 4) if quad_only else ((pmc_h,) if pmc else (8, 1))
+    hs = (1, 2, 4) if quad_only else ((pmc_h,) if pmc else ((1, 2, 4, 8, 16) if "--pack" in sys.argv else (8, 1)))
     for H in hs:
         gen = th.Generator(device=dev).manual_seed(H)
         s = th.randn(gidx.number_of_edges(), H, 1, device=dev, generator=gen) * 3
@@ -51,11 +51,14 @@ def main():
         if quad_only:
             routes = (("view_plain", view, "1", "0"), ("view", view, "1", "1"),
                       ("graph_plain", gidx, "1", "0"), ("graph", gidx, "1", "1"))
+        elif "--pack" in sys.argv:  # the edge-id route with / without packed row statistics
+            routes = (("graph_unpacked", gidx, "1", "1", "0"), ("graph", gidx, "1", "1", "1"))
         elif pmc:
             routes = routes[1:]
-        for name, gi, owned, quad in routes:
+        for name, gi, owned, quad, *pack in routes:
             os.environ["DGLMI_SOFTMAX_OWNED"] = owned  # 0: the chunked row + edge passes
-            os.environ["DGLMI_SOFTMAX_QUAD"] = quad  # 0: one position per lane at H <= 2
+            os.environ["DGLMI_SOFTMAX_QUAD"] = quad  # 0: one position per lane at H <= 4
+            os.environ["DGLMI_SOFTMAX_PACK"] = pack[0] if pack else "1"  # 0: two statistics arrays
             out, gs = th.empty_like(s), th.empty_like(s)
             res["H%d_%s_fwd_ms" % (H, name)] = ktime(lambda: K.edge_softmax_forward(gi, s, out))
             res["H%d_%s_bwd_ms" % (H, name)] = ktime(lambda: K.edge_softmax_backward(gi, out, ga, gs))

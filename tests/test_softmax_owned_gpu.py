@@ -143,7 +143,9 @@ def test_quad_walk_matches_plain_walk(H, mode, monkeypatch):
 @pytest.mark.parametrize("H", [1, 2])
 def test_quad_edge_pass_bit_identical(H, mode, monkeypatch):
     """The edge pass in edge-id order (a graph whose edges are not sorted by destination)
-    with 4 / H edges per lane (k_sm_edges_q) gives the one-edge-per-lane pass's bits,
+    with 4 / H edges per lane (k_sm_edges_q) and with the rows' statistics packed side by
+    side (k_sm_pack; DGLMI_SOFTMAX_PACK=0: the two arrays) gives the one-edge-per-lane,
+    two-array pass's bits,
     forward and backward, for stored logits, the fused leaky_relu and the node logits --
     on an edge count that is not a multiple of 4 (the last lane's partial quad) -- and
     matches fp64."""
@@ -169,8 +171,9 @@ def test_quad_edge_pass_bit_identical(H, mode, monkeypatch):
     s[m - 1, 0, 0] = float("nan")
     ga = th.randn(m, H, 1, device=DEV, generator=gen)
     res = {}
-    for quad in ("1", "0"):
+    for quad, pack in (("1", "1"), ("0", "1"), ("1", "0"), ("0", "0")):
         monkeypatch.setenv("DGLMI_SOFTMAX_QUAD", quad)
+        monkeypatch.setenv("DGLMI_SOFTMAX_PACK", pack)
         a, gs = th.empty_like(s), th.empty_like(s)
         if mode == "stored":
             K.edge_softmax_forward(g, s, a)
@@ -181,14 +184,15 @@ def test_quad_edge_pass_bit_identical(H, mode, monkeypatch):
         else:
             K.edge_softmax_node_logits_forward(g, el, er, 0.2, a)
             K.edge_softmax_node_logits_backward(g, a, ga, el, er, 0.2, gs)
-        res[quad] = (a, gs)
-    for x, y in zip(res["1"], res["0"]):
-        assert th.equal(th.isnan(x), th.isnan(y)) and th.equal(x[~th.isnan(y)], y[~th.isnan(y)])
+        res[quad + pack] = (a, gs)
+    for key in ("01", "10", "00"):  # every form gives the same bits
+        for x, y in zip(res["11"], res[key]):
+            assert th.equal(th.isnan(x), th.isnan(y)) and th.equal(x[~th.isnan(y)], y[~th.isnan(y)])
     rows = th.from_numpy(dst[perm]).to(DEV)
     pre = s.reshape(m, H) if mode != "node_logits" else (el[th.from_numpy(src[perm]).to(DEV)] + er[rows]).reshape(m, H)
     x = pre if mode == "stored" else th.nn.functional.leaky_relu(pre, 0.2)
     ref = _fp64(rows, x, n)
-    a1 = res["1"][0].reshape(m, H)
+    a1 = res["11"][0].reshape(m, H)
     fin = ~th.isnan(ref)
     assert th.equal(th.isnan(a1), ~fin)
     assert th.allclose(a1[fin].double(), ref[fin], rtol=1e-5, atol=1e-7)
