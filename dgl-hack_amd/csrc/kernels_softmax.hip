@@ -688,7 +688,7 @@ struct OwnedWalk {
 };
 
 // ---------------------------------------------------------------------------
-// The row-owned walk with four values per lane, H <= 2 (round 6).  At H = 1 the walk
+// The row-owned walk with four values per lane, H <= 4 (round 6).  At H = 1 the walk
 // above loads 4 B per lane (one position), and its steps wait on one another: a step's
 // loads are issued only after the previous step's row logic, and every row end costs a
 // dependent indptr load (profiles/r06_edge_softmax_h1_pmc.json: 79 % of the cycles
