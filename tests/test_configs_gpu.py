@@ -133,6 +133,63 @@ def test_c3_reddit_gat_fused_vs_unfused_and_sampled_fp64():
     th.testing.assert_close(res[True][0][rows].double(), ref, rtol=1e-3, atol=1e-5)
 
 
+@pytest.mark.parametrize("H", [1, 2, 4, 8])
+def test_c3_edge_softmax_full_size(H, monkeypatch):
+    """Edge softmax on the C3 graph at full size, forward and backward: on the in-CSR
+    position view the H <= 4 four-values-per-lane walk against the one-position walk
+    (DGLMI_SOFTMAX_QUAD=0); on the graph itself (edge-id order) the packed row
+    statistics against the two arrays (DGLMI_SOFTMAX_PACK=0, the same bits); and 128
+    sampled destination rows of both recomputed in fp64."""
+    import dgl
+    from dgl import kernel as K
+    n, m = 232_965, 114_615_892
+    src, dst = _chung_lu(n, m, 0.6, 3)
+    g = dgl.DGLGraph.from_device_coo(src, dst, n)
+    del src, dst
+    gidx = g._graph.get_immutable_gidx(DEV)
+    view = gidx.position_view("in")
+    gen = th.Generator(device=DEV).manual_seed(H)
+    s = th.randn(m, H, device=DEV, generator=gen) * 3
+    ga = th.randn(m, H, device=DEV, generator=gen)
+
+    def run(gi, env):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        a, gs = th.empty_like(s), th.empty_like(s)
+        K.edge_softmax_forward(gi, s, a)
+        K.edge_softmax_backward(gi, a, ga, gs)
+        return a, gs
+    rows = th.randint(0, n, (128,), device=DEV)
+    seg, _, eids = _sample_rows(gidx, rows)
+    ip = gidx.in_csr.indptr.long()
+    pos = th.cat([th.arange(int(ip[r]), int(ip[r + 1]), device=DEV) for r in rows.tolist()])
+
+    def check(a, gs, idx, x):
+        # fp64 softmax and its backward over the sampled rows' edges (idx: where they sit)
+        e = x[idx].double()
+        emax = th.full((128, H), -1e300, dtype=th.float64, device=DEV).index_reduce(0, seg, e, "amax")
+        w = (e - emax[seg]).exp()
+        w = w / th.zeros(128, H, dtype=th.float64, device=DEV).index_add_(0, seg, w)[seg]
+        th.testing.assert_close(a[idx].double(), w, rtol=1e-5, atol=1e-7)
+        g64 = ga[idx].double()
+        S = th.zeros(128, H, dtype=th.float64, device=DEV).index_add_(0, seg, w * g64)
+        th.testing.assert_close(gs[idx].double(), w * g64 - w * S[seg], rtol=1e-4, atol=1e-6)
+
+    # position view: the logits in walk order (s is read as position-ordered there)
+    monkeypatch.setenv("DGLMI_SOFTMAX_OWNED", "1")
+    a1, g1 = run(view, {"DGLMI_SOFTMAX_QUAD": "1"})
+    a0, g0 = run(view, {"DGLMI_SOFTMAX_QUAD": "0"})
+    th.testing.assert_close(a1, a0, rtol=1e-5, atol=1e-7)
+    th.testing.assert_close(g1, g0, rtol=1e-4, atol=1e-6)
+    check(a1, g1, pos, s)
+    del a0, g0
+    # the graph in edge-id order
+    b1, h1 = run(gidx, {"DGLMI_SOFTMAX_QUAD": "1", "DGLMI_SOFTMAX_PACK": "1"})
+    b0, h0 = run(gidx, {"DGLMI_SOFTMAX_QUAD": "0", "DGLMI_SOFTMAX_PACK": "0"})
+    assert th.equal(b1, b0) and th.equal(h1, h0)
+    check(b1, h1, eids, s)
+
+
 def test_c4_rmat_copy_u_sum_and_partition():
     """C4 on one GPU: copy_u_sum over the 10 M / 200 M RMAT graph (checksum of
     checksums + 2,048 sampled rows in fp64), and the 8-way device partition:
