@@ -1936,6 +1936,65 @@ int DGLMIProject(const float* x, int64_t m, int64_t k, const float* w, int64_t w
   API_END();
 }
 
+int DGLMIGatAttnLogitsSupported(int64_t num_heads, int64_t head_dim) {
+  return dglmi::gat_logits_supported(num_heads, head_dim) ? 1 : 0;
+}
+
+int64_t DGLMIGatAttnLogitsPartials(int64_t n_src, int64_t n_dst, int64_t num_heads, int64_t head_dim) {
+  return dglmi::gat_logits_threads(n_src, n_dst, num_heads, head_dim);
+}
+
+namespace {
+int check_logits_args(const float* xs, const float* xd, int64_t ns, int64_t nd, int64_t H, int64_t D,
+                      const float* al, const float* ar) {
+  DGLMI_CHECK(dglmi::gat_logits_supported(H, D), "DGLMIGatAttnLogits: unsupported (heads, head_dim) = (" +
+                                                     std::to_string(H) + ", " + std::to_string(D) + ")");
+  DGLMI_CHECK(ns >= 0 && nd >= 0 && xs != nullptr && al != nullptr && ar != nullptr,
+              "DGLMIGatAttnLogits: null operand");
+  DGLMI_CHECK(xd != xs || ns == nd, "DGLMIGatAttnLogits: one feature table needs n_src == n_dst");
+  DGLMI_CHECK(aligned16(xs) && aligned16(xd == nullptr ? xs : xd) && aligned16(al) && aligned16(ar),
+              "DGLMIGatAttnLogits: features and attention vectors must be 16-byte aligned");
+  return 0;
+}
+}  // namespace
+
+int DGLMIGatAttnLogits(const float* feat_src, const float* feat_dst, int64_t n_src, int64_t n_dst,
+                       int64_t num_heads, int64_t head_dim, const float* attn_l, const float* attn_r,
+                       float* el, float* er, int device, void* stream) {
+  API_BEGIN();
+  const float* xd = feat_dst == nullptr ? feat_src : feat_dst;
+  check_logits_args(feat_src, xd, n_src, n_dst, num_heads, head_dim, attn_l, attn_r);
+  DGLMI_CHECK(el != nullptr && er != nullptr, "DGLMIGatAttnLogits: null output");
+  DeviceGuard guard(device);
+  dglmi::launch_gat_logits(feat_src, xd, n_src, n_dst, static_cast<int>(num_heads),
+                           static_cast<int>(head_dim), attn_l, attn_r, el, er,
+                           static_cast<hipStream_t>(stream));
+  check_hip(hipGetLastError(), "attention logits launch");
+  API_END();
+}
+
+int DGLMIGatAttnLogitsBackward(const float* feat_src, const float* feat_dst, int64_t n_src, int64_t n_dst,
+                               int64_t num_heads, int64_t head_dim, const float* attn_l,
+                               const float* attn_r, const float* grad_el, const float* grad_er,
+                               float* grad_src, float* grad_dst, float* partials, int device,
+                               void* stream) {
+  API_BEGIN();
+  const float* xd = feat_dst == nullptr ? feat_src : feat_dst;
+  check_logits_args(feat_src, xd, n_src, n_dst, num_heads, head_dim, attn_l, attn_r);
+  DGLMI_CHECK(grad_el != nullptr && grad_er != nullptr && grad_src != nullptr && partials != nullptr &&
+                  (xd == feat_src || grad_dst != nullptr),
+              "DGLMIGatAttnLogitsBackward: null operand");
+  DGLMI_CHECK(aligned16(grad_src) && aligned16(partials) && (grad_dst == nullptr || aligned16(grad_dst)),
+              "DGLMIGatAttnLogitsBackward: gradients and partials must be 16-byte aligned");
+  DeviceGuard guard(device);
+  dglmi::launch_gat_logits_bwd(feat_src, xd, n_src, n_dst, static_cast<int>(num_heads),
+                               static_cast<int>(head_dim), attn_l, attn_r, grad_el, grad_er, grad_src,
+                               xd == feat_src ? nullptr : grad_dst, partials,
+                               static_cast<hipStream_t>(stream));
+  check_hip(hipGetLastError(), "attention logits backward launch");
+  API_END();
+}
+
 int DGLMIEdgeSoftmaxLeakyBackward(const DGLMIGraph* graph, const DGLMIArray* out,
                                   const DGLMIArray* grad_out, const DGLMIArray* logits,
                                   float negative_slope, DGLMIArray* grad_logits, void* stream) {

@@ -555,6 +555,18 @@ void launch_gat_merge(const float* out_part, const float* m_part, const float* l
                       float* lf = nullptr, float* ls = nullptr);
 // l[i] = m[i] + log(l[i]) for i < n (one log-sum-exp per row and head)
 void launch_gat_fold_lse(const float* m, float* l, int64_t n, hipStream_t s);
+// GATConv's attention logits el = (xs * al).sum(-1), er = (xd * ar).sum(-1) (xs, xd (n, H,
+// D) row-major, al / ar (H, D); xd == xs: one table) and their backward (gs = gel al, gd =
+// ger ar -- one table: gs = gel al + ger ar, gd unused; part: gat_logits_threads x 8
+// floats of parameter-gradient partials).  Supported: D % 4 == 0, D / 4 a power of two
+// <= 16, H D / 4 dividing 256.
+bool gat_logits_supported(int64_t H, int64_t D);
+int64_t gat_logits_threads(int64_t ns, int64_t nd, int64_t H, int64_t D);
+void launch_gat_logits(const float* xs, const float* xd, int64_t ns, int64_t nd, int H, int D,
+                       const float* al, const float* ar, float* el, float* er, hipStream_t s);
+void launch_gat_logits_bwd(const float* xs, const float* xd, int64_t ns, int64_t nd, int H, int D,
+                           const float* al, const float* ar, const float* gel, const float* ger,
+                           float* gs, float* gd, float* part, hipStream_t s);
 
 // R-GCN C entries (hack_kernels.hip): relation-expanded ids (mode 0: etypes[eid] *
 // mul + id, mode 1: id * mul + etypes[eid]; eids NULL = position), the relation

@@ -1111,6 +1111,130 @@ void launch_gat_fold_lse(const float* m, float* l, int64_t n, hipStream_t s) {
   const unsigned blocks = static_cast<unsigned>(want < 65536 ? want : 65536);
   hipLaunchKernelGGL(k_gat_fold_lse, dim3(blocks), dim3(kBlock), 0, s, m, l, n);
 }
+
+// GATConv's attention logits (gatconv.py:137-138 of the reference: el = (ft_src *
+// attn_l).sum(-1), er = (ft_dst * attn_r).sum(-1)) in one pass over the projected
+// features instead of torch's multiply + reduce per side (two reads of the (N, H, D)
+// table and an (N, H, D) temporary each).  One thread per float4 slot of a row; the D4 =
+// D / 4 slots of a head sit on adjacent, D4-aligned lanes (F4 = H D4 slots per row, D4 a
+// power of two dividing 64), so a head's dot product is one xor butterfly over its
+// lanes.  A D4-lane group is active or inactive as a whole (the bound is a whole row), so
+// the butterfly only reads active lanes.  xs == xd (one feature table): read once.
+// Summation order: torch's (x * a).sum(-1) on this device adds the rounded products as a
+// pairwise tree of adjacent pairs ((p0 + p1) + (p2 + p3)) + ... (bit-for-bit on every
+// element for D = 4 .. 64, the head sizes taken here: scripts/sum_order_probe.py, profiles/r06_sum_order_probe.jsonl);
+// a lane's quad is the tree's first two levels and the butterfly over adjacent lanes the
+// rest, so el / er are torch's bits -- the LeakyReLU of el + er takes the same branch as
+// in the reference's composition.
+__global__ void k_gat_logits(const float* __restrict__ xs, const float* __restrict__ xd, int64_t ns,
+                             int64_t nd, int H, int D4, const float* __restrict__ al,
+                             const float* __restrict__ ar, float* __restrict__ el,
+                             float* __restrict__ er) {
+  const int64_t F4 = static_cast<int64_t>(H) * D4;
+  const int64_t rows = ns > nd ? ns : nd;
+  const int64_t total = rows * F4;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int64_t r = i / F4;
+    const int f4 = static_cast<int>(i - r * F4);
+    const float4 a = ld4g(al + 4 * f4), b = ld4g(ar + 4 * f4);
+    float sl = 0.0f, sr = 0.0f;
+    if (r < ns) {
+      const float4 x = ld4g(xs + r * F4 * 4 + 4 * f4);
+      sl = (x.x * a.x + x.y * a.y) + (x.z * a.z + x.w * a.w);
+      if (xd == xs) sr = (x.x * b.x + x.y * b.y) + (x.z * b.z + x.w * b.w);
+    }
+    if (xd != xs && r < nd) {
+      const float4 y = ld4g(xd + r * F4 * 4 + 4 * f4);
+      sr = (y.x * b.x + y.y * b.y) + (y.z * b.z + y.w * b.w);
+    }
+    for (int o = 1; o < D4; o <<= 1) {
+      sl += __shfl_xor(sl, o);
+      sr += __shfl_xor(sr, o);
+    }
+    if (f4 % D4 == 0) {
+      const int64_t hi = r * H + f4 / D4;
+      if (r < ns) el[hi] = sl;
+      if (r < nd) er[hi] = sr;
+    }
+  }
+}
+
+// Its backward: grad_xs = g_el attn_l, grad_xd = g_er attn_r (one table: their sum, one
+// write), and the parameter gradients sum_rows g_el xs / g_er xd as per-thread partials
+// part[t] = {attn_l slot (4), attn_r slot (4)} -- the grid stride is a multiple of F4, so
+// a thread's slot is fixed over its rows; the host sums the partials of each slot in
+// thread order (a fixed grid for a given shape: deterministic).
+__global__ void k_gat_logits_bwd(const float* __restrict__ xs, const float* __restrict__ xd, int64_t ns,
+                                 int64_t nd, int H, int D4, const float* __restrict__ al,
+                                 const float* __restrict__ ar, const float* __restrict__ gel,
+                                 const float* __restrict__ ger, float* __restrict__ gs,
+                                 float* __restrict__ gd, float* __restrict__ part) {
+  const int64_t F4 = static_cast<int64_t>(H) * D4;
+  const int64_t rows = ns > nd ? ns : nd;
+  const int64_t total = rows * F4;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int f4 = static_cast<int>(t % F4);
+  const float4 a = ld4g(al + 4 * f4), b = ld4g(ar + 4 * f4);
+  const int h = f4 / D4;
+  float4 pl = make_float4(0.f, 0.f, 0.f, 0.f), pr = pl;
+  const bool one = xd == xs;
+  for (int64_t i = t; i < total; i += stride) {
+    const int64_t r = i / F4;
+    const int64_t o = r * F4 * 4 + 4 * f4;
+    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < ns) {
+      const float e = gel[r * H + h];
+      const float4 x = ld4g(xs + o);
+      g = make_float4(e * a.x, e * a.y, e * a.z, e * a.w);
+      pl = make_float4(pl.x + e * x.x, pl.y + e * x.y, pl.z + e * x.z, pl.w + e * x.w);
+      if (one) {
+        const float q = ger[r * H + h];
+        g = make_float4(g.x + q * b.x, g.y + q * b.y, g.z + q * b.z, g.w + q * b.w);
+        pr = make_float4(pr.x + q * x.x, pr.y + q * x.y, pr.z + q * x.z, pr.w + q * x.w);
+      }
+      st4g(gs + o, g);
+    }
+    if (!one && r < nd) {
+      const float q = ger[r * H + h];
+      const float4 y = ld4g(xd + o);
+      st4g(gd + o, make_float4(q * b.x, q * b.y, q * b.z, q * b.w));
+      pr = make_float4(pr.x + q * y.x, pr.y + q * y.y, pr.z + q * y.z, pr.w + q * y.w);
+    }
+  }
+  st4g(part + 8 * t, pl);
+  st4g(part + 8 * t + 4, pr);
+}
+
+bool gat_logits_supported(int64_t H, int64_t D) {
+  if (H < 1 || D < 4 || D % 4 != 0) return false;
+  const int64_t D4 = D / 4, F4 = H * D4;
+  // D <= 64: where torch's summation order was checked bit for bit (the header above)
+  return (D4 & (D4 - 1)) == 0 && D4 <= 16 && F4 <= kBlock && kBlock % F4 == 0;
+}
+// threads of the logits kernels: whole blocks, at most 1024 of them (fixed for a shape)
+int64_t gat_logits_threads(int64_t ns, int64_t nd, int64_t H, int64_t D) {
+  const int64_t total = (ns > nd ? ns : nd) * H * (D / 4);
+  int64_t blocks = (total + kBlock - 1) / kBlock;
+  if (blocks > 1024) blocks = 1024;
+  if (blocks < 1) blocks = 1;
+  return blocks * kBlock;
+}
+void launch_gat_logits(const float* xs, const float* xd, int64_t ns, int64_t nd, int H, int D,
+                       const float* al, const float* ar, float* el, float* er, hipStream_t s) {
+  if (ns <= 0 && nd <= 0) return;
+  const unsigned blocks = static_cast<unsigned>(gat_logits_threads(ns, nd, H, D) / kBlock);
+  hipLaunchKernelGGL(k_gat_logits, dim3(blocks), dim3(kBlock), 0, s, xs, xd, ns, nd, H, D / 4, al, ar,
+                     el, er);
+}
+void launch_gat_logits_bwd(const float* xs, const float* xd, int64_t ns, int64_t nd, int H, int D,
+                           const float* al, const float* ar, const float* gel, const float* ger,
+                           float* gs, float* gd, float* part, hipStream_t s) {
+  const unsigned blocks = static_cast<unsigned>(gat_logits_threads(ns, nd, H, D) / kBlock);
+  hipLaunchKernelGGL(k_gat_logits_bwd, dim3(blocks), dim3(kBlock), 0, s, xs, xd, ns, nd, H, D / 4, al,
+                     ar, gel, ger, gs, gd, part);
+}
 // One keep word per edge from a dropout output (E, H) in edge-id order: the lanes of a
 // wave read 64 consecutive rows, every byte of the span used over the H loads.
 template <typename T>

@@ -576,6 +576,39 @@ def fused_gat(graph, feat_src, el, er, slope, attn_drop=0.0, seed=None, keep=Non
     return FusedGat.apply(gidx, feat_src, el, er, float(slope), attn_drop, int(seed or 0))
 
 
+class _AttnLogits(th.autograd.Function):
+    """GATConv's el = (ft_src * attn_l).sum(-1), er = (ft_dst * attn_r).sum(-1)
+    (gatconv.py:137-138) as one pass over the features each way (DGLMIGatAttnLogits /
+    Backward) instead of a multiply and a reduction per side and, backward, a multiply,
+    a multiply-reduce and an add per side.  ``feat_dst`` None: one table for both."""
+
+    @staticmethod
+    def forward(ctx, feat_src, attn_l, attn_r, feat_dst):
+        el, er = K.attn_logits(feat_src, feat_dst, attn_l, attn_r)
+        ctx.one = feat_dst is None
+        ctx.save_for_backward(feat_src, attn_l, attn_r, feat_dst)
+        return el, er
+
+    @staticmethod
+    def backward(ctx, g_el, g_er):
+        feat_src, attn_l, attn_r, feat_dst = ctx.saved_tensors
+        if g_el is None:
+            g_el = feat_src.new_zeros(feat_src.shape[:2] + (1,))
+        if g_er is None:
+            n = feat_src.shape[0] if ctx.one else feat_dst.shape[0]
+            g_er = feat_src.new_zeros((n, feat_src.shape[1], 1))
+        gs, gd, gl, gr = K.attn_logits_backward(feat_src, None if ctx.one else feat_dst, attn_l,
+                                                attn_r, g_el, g_er)
+        return gs, gl, gr, gd
+
+
+def attn_logits(feat_src, feat_dst, attn_l, attn_r):
+    """(el, er), each (N, H, 1): GATConv's attention logits on the device
+    (:class:`_AttnLogits`); ``feat_dst is feat_src``: one pass over one table."""
+    one = feat_dst is feat_src
+    return _AttnLogits.apply(feat_src, attn_l, attn_r, None if one else feat_dst)
+
+
 class GatComposition(th.autograd.Function):
     """GATConv's unfused composition (gatconv.py:151-157: u_add_v, leaky_relu, edge_softmax,
     u_mul_e_sum) on the in-CSR position view, forward step by step -- the node-logit edge

@@ -721,6 +721,70 @@ def project_mfma(x2, w, bias=None):
     return y
 
 
+def attn_logits_ok(feat_src, feat_dst, attn_l, attn_r):
+    """Whether GATConv's el / er (gatconv.py:137-138) can take DGLMIGatAttnLogits: fp32
+    contiguous (N, H, D) features on one ROCm device (16-B aligned) and (1, H, D) attention
+    vectors there, (H, D) a supported shape."""
+    if not (feat_src.is_cuda and feat_src.dim() == 3 and feat_src.dtype == th.float32):
+        return False
+    _, h, d = feat_src.shape
+    for t in (feat_src, feat_dst):
+        if not (t.dim() == 3 and t.shape[1:] == (h, d) and t.dtype == th.float32
+                and t.device == feat_src.device and t.is_contiguous() and t.data_ptr() % 16 == 0):
+            return False
+    for a in (attn_l, attn_r):
+        if not (a.shape == (1, h, d) and a.dtype == th.float32 and a.device == feat_src.device):
+            return False
+    return bool(_ffi.lib().DGLMIGatAttnLogitsSupported(int(h), int(d)))
+
+
+def _aligned(t):
+    t = t.contiguous()
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
+def attn_logits(feat_src, feat_dst, attn_l, attn_r):
+    """(el, er) of shape (N, H, 1) -> DGLMIGatAttnLogits; ``feat_dst`` None: one table."""
+    ns, h, d = feat_src.shape
+    nd = ns if feat_dst is None else feat_dst.shape[0]
+    el = feat_src.new_empty((ns, h, 1))
+    er = feat_src.new_empty((nd, h, 1))
+    al, ar = _aligned(attn_l), _aligned(attn_r)
+    check_call(_ffi.lib().DGLMIGatAttnLogits(
+        ctypes.c_void_p(feat_src.data_ptr()),
+        ctypes.c_void_p(None if feat_dst is None else feat_dst.data_ptr()),
+        ctypes.c_int64(ns), ctypes.c_int64(nd), ctypes.c_int64(h), ctypes.c_int64(d),
+        ctypes.c_void_p(al.data_ptr()), ctypes.c_void_p(ar.data_ptr()),
+        ctypes.c_void_p(el.data_ptr()), ctypes.c_void_p(er.data_ptr()),
+        int(feat_src.device.index or 0), _stream(el)))
+    return el, er
+
+
+def attn_logits_backward(feat_src, feat_dst, attn_l, attn_r, grad_el, grad_er):
+    """-> (grad_src, grad_dst or None, grad_attn_l, grad_attn_r) through
+    DGLMIGatAttnLogitsBackward; the parameter gradients sum the per-thread partials of
+    each slot in thread order (a fixed grid per shape: deterministic)."""
+    ns, h, d = feat_src.shape
+    nd = ns if feat_dst is None else feat_dst.shape[0]
+    al, ar = _aligned(attn_l), _aligned(attn_r)
+    gel, ger = grad_el.contiguous(), grad_er.contiguous()
+    gs = th.empty_like(feat_src)
+    gd = None if feat_dst is None else th.empty_like(feat_dst)
+    nt = int(_ffi.lib().DGLMIGatAttnLogitsPartials(ns, nd, h, d))
+    part = feat_src.new_empty((nt, 8))
+    check_call(_ffi.lib().DGLMIGatAttnLogitsBackward(
+        ctypes.c_void_p(feat_src.data_ptr()),
+        ctypes.c_void_p(None if feat_dst is None else feat_dst.data_ptr()),
+        ctypes.c_int64(ns), ctypes.c_int64(nd), ctypes.c_int64(h), ctypes.c_int64(d),
+        ctypes.c_void_p(al.data_ptr()), ctypes.c_void_p(ar.data_ptr()),
+        ctypes.c_void_p(gel.data_ptr()), ctypes.c_void_p(ger.data_ptr()),
+        ctypes.c_void_p(gs.data_ptr()), ctypes.c_void_p(None if gd is None else gd.data_ptr()),
+        ctypes.c_void_p(part.data_ptr()), int(feat_src.device.index or 0), _stream(gs)))
+    f4 = h * d // 4
+    p = part.view(nt // f4, f4, 2, 4).sum(0)  # (slot, {l, r}, 4)
+    return gs, gd, p[:, 0, :].reshape(1, h, d), p[:, 1, :].reshape(1, h, d)
+
+
 def gather_rows(src, index, check=False):
     """src[index] for a contiguous fp32 device tensor and an int32 / int64 index on its
     device -> DGLMIGatherRows (one random row read per output row, rows written in

@@ -48,6 +48,10 @@ MODULE_DRAW_DTYPE = th.float32
 # those draws recomputed inside the fused walks from the generator state (no mask, no
 # gathers; DGLMIFusedGatDraw*)
 MODULE_DRAW_IN_KERNEL = True
+# the fused route's el / er (gatconv.py:137-138) as one pass over the features each way
+# (dgl.backend.attn_logits; equal to torch's multiply + sum within fp32 rounding); the
+# composition routes keep torch's, as the reference
+FUSED_ATTN_LOGITS = True
 
 
 def expand_as_pair(x):
@@ -271,9 +275,14 @@ class GATConv(nn.Module):
         else:
             h_src = h_dst = self.feat_drop(feat)
             feat_src = feat_dst = B.project(h_src, self.fc.weight.t()).view(-1, self._num_heads, self._out_feats)
-        el = (feat_src * self.attn_l).sum(dim=-1).unsqueeze(-1)
-        er = (feat_dst * self.attn_r).sum(dim=-1).unsqueeze(-1)
-        if self._fused_route(graph, max(feat_src.shape[0], feat_dst.shape[0])):
+        fused = self._fused_route(graph, max(feat_src.shape[0], feat_dst.shape[0]))
+        if fused and FUSED_ATTN_LOGITS and K.attn_logits_ok(feat_src, feat_dst, self.attn_l,
+                                                            self.attn_r):
+            el, er = B.attn_logits(feat_src, feat_dst, self.attn_l, self.attn_r)
+        else:
+            el = (feat_src * self.attn_l).sum(dim=-1).unsqueeze(-1)
+            er = (feat_dst * self.attn_r).sum(dim=-1).unsqueeze(-1)
+        if fused:
             rst = self._fused(graph, feat_src, el, er)
         elif not isinstance(feat, tuple) and self._position_space(graph, feat_src):
             rst = self._composed_in_positions(graph, feat_src, el, er)

@@ -511,6 +511,28 @@ int DGLMIProjectSupported(int64_t k, int64_t n);
 int DGLMIProject(const float* x, int64_t m, int64_t k, const float* w, int64_t w_rows,
                  int64_t w_stride_k, int64_t w_stride_n, int64_t n, const float* bias, float* y,
                  int device, void* stream);
+/* GATConv's attention logits (the reference's gatconv.py:137-138, two torch multiply +
+ * sum pairs): el[i, h] = sum_d feat_src[i, h, d] attn_l[h, d] for i < n_src, er[i, h] =
+ * sum_d feat_dst[i, h, d] attn_r[h, d] for i < n_dst, in one pass; feat_dst NULL = the same
+ * table as feat_src (n_dst == n_src).  Row-major fp32 device pointers, the inputs 16-byte
+ * aligned.  The backward writes grad_src = grad_el attn_l (+ grad_er attn_r for one table)
+ * and grad_dst = grad_er attn_r (two tables), and per-thread partials of the parameter
+ * gradients: DGLMIGatAttnLogitsPartials(...) records of 8 floats, record t = {sum over its
+ * rows of grad_el feat_src at slot t mod (H D / 4) (4 floats), the same of grad_er
+ * feat_dst (4)}; summing the records of each slot in record order gives grad attn_l and
+ * grad attn_r.  el / er are bit-identical to torch's (x * a).sum(-1) on MI355X (its
+ * pairwise order).  DGLMIGatAttnLogitsSupported: head_dim in {4, 8, 16, 32, 64}, heads *
+ * head_dim / 4 dividing 256 (extension). */
+int DGLMIGatAttnLogitsSupported(int64_t num_heads, int64_t head_dim);
+int64_t DGLMIGatAttnLogitsPartials(int64_t n_src, int64_t n_dst, int64_t num_heads, int64_t head_dim);
+int DGLMIGatAttnLogits(const float* feat_src, const float* feat_dst, int64_t n_src, int64_t n_dst,
+                       int64_t num_heads, int64_t head_dim, const float* attn_l, const float* attn_r,
+                       float* el, float* er, int device, void* stream);
+int DGLMIGatAttnLogitsBackward(const float* feat_src, const float* feat_dst, int64_t n_src,
+                               int64_t n_dst, int64_t num_heads, int64_t head_dim,
+                               const float* attn_l, const float* attn_r, const float* grad_el,
+                               const float* grad_er, float* grad_src, float* grad_dst,
+                               float* partials, int device, void* stream);
 /* out[i, :] = src[index[i], :] for i < n, rows of row_floats floats; index int32
  * (index_bits 32) or int64 (64), device pointers.  Indices are NOT bound-checked: each
  * must lie in [0, rows of src) (dgl.kernel.gather_rows(check=True) verifies on the host

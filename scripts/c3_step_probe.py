@@ -3,7 +3,9 @@
 Reddit-size graph, repeated --steps times after --warmup: run it under
 `rocprofv3 --kernel-trace --stats` to see where the step's time goes kernel by kernel
 (the walks against the projections, el / er, torch elementwise work and allocations).
---composition: GATConv with use_fused = False (the reference's composition) instead."""
+--composition: GATConv with use_fused = False (the reference's composition) instead.
+--ab-logits: alternate the fused route's device el / er (gatconv.FUSED_ATTN_LOGITS) with
+torch's multiply + sum, three rounds each, and print both series."""
 import argparse
 import json
 import os
@@ -26,6 +28,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--composition", action="store_true")
+    ap.add_argument("--ab-logits", action="store_true")
     args = ap.parse_args()
     dev = "cuda:0"
     g = chung_lu(232965, 114615892, 0.4, 3, dev)
@@ -36,16 +39,26 @@ def main():
 
     def step():
         gat(g, x).sum().backward()
-    for _ in range(args.warmup):
-        step()
-    th.cuda.synchronize()
-    t = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    th.cuda.synchronize()
-    ms = (time.perf_counter() - t) * 1000 / args.steps
+    def timed():
+        for _ in range(args.warmup):
+            step()
+        th.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        th.cuda.synchronize()
+        return (time.perf_counter() - t) * 1000 / args.steps
+    if args.ab_logits:
+        from dgl.nn.pytorch.conv import gatconv
+        series = {"device_logits": [], "torch_logits": []}
+        for _ in range(3):
+            for flag, key in ((True, "device_logits"), (False, "torch_logits")):
+                gatconv.FUSED_ATTN_LOGITS = flag
+                series[key].append(timed())
+        print(json.dumps({"route": "fused", "steps": args.steps, "ms_per_step": series}), flush=True)
+        return
     print(json.dumps({"route": "composition" if args.composition else "fused", "steps": args.steps,
-                      "ms_per_step": ms}), flush=True)
+                      "ms_per_step": timed()}), flush=True)
 
 
 if __name__ == "__main__":

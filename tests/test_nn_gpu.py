@@ -581,3 +581,107 @@ def test_gat_composition_fused_backward(H, D, blocks, owned, monkeypatch):
     for a, b in zip(res[0][1:], res[1][1:]):
         tol = 1e-4 * float(b.abs().max()) + 1e-7
         assert float((a - b).abs().max()) <= tol, (float((a - b).abs().max()), tol)
+
+
+@pytest.mark.parametrize("h,d", [(8, 8), (1, 4), (4, 16), (2, 32), (16, 4), (64, 4), (4, 64), (32, 8)])
+@pytest.mark.parametrize("two", [False, True])
+def test_attn_logits_kernel(h, d, two):
+    """DGLMIGatAttnLogits / Backward (GATConv's el / er, gatconv.py:137-138) against fp64:
+    one feature table and two (bipartite, n_src != n_dst, both larger), every head layout
+    the kernel takes (D / 4 lanes per head: 1 .. 16; H D / 4 slots per row dividing 256),
+    row counts off the grid; the parameter gradients from the per-thread partials."""
+    from dgl import backend as B
+    from dgl import kernel as K
+    g = th.Generator(device=DEV).manual_seed(7 * h + d + two)
+    ns = 70001
+    nd = 50003 if two else ns
+    xs = th.randn(ns, h, d, device=DEV, generator=g).requires_grad_()
+    xd = th.randn(nd, h, d, device=DEV, generator=g).requires_grad_() if two else xs
+    al = th.randn(1, h, d, device=DEV, generator=g).requires_grad_()
+    ar = th.randn(1, h, d, device=DEV, generator=g).requires_grad_()
+    assert K.attn_logits_ok(xs, xd, al, ar)
+    el, er = B.attn_logits(xs, xd, al, ar)
+    assert el.shape == (ns, h, 1) and er.shape == (nd, h, 1)
+    rl = (xs.double() * al.double()).sum(-1, keepdim=True)
+    rr = (xd.double() * ar.double()).sum(-1, keepdim=True)
+    ml = (xs.double().abs() * al.double().abs()).sum(-1, keepdim=True)
+    mr = (xd.double().abs() * ar.double().abs()).sum(-1, keepdim=True)
+    assert bool(((el.double() - rl).abs() <= 1e-6 * ml + 1e-7).all())
+    assert bool(((er.double() - rr).abs() <= 1e-6 * mr + 1e-7).all())
+    # torch's own fp32 bits (its pairwise summation order; the LeakyReLU branch of
+    # el + er is then the reference composition's)
+    with th.no_grad():
+        assert th.equal(el, (xs * al).sum(-1, keepdim=True))
+        assert th.equal(er, (xd * ar).sum(-1, keepdim=True))
+    gl = th.randn(ns, h, 1, device=DEV, generator=g)
+    gr = th.randn(nd, h, 1, device=DEV, generator=g)
+    ins = [xs, al, ar] + ([xd] if two else [])
+    got = th.autograd.grad((el, er), ins, (gl, gr))
+    ins64 = [t.detach().double().requires_grad_() for t in ins]
+    xs64, al64, ar64 = ins64[:3]
+    xd64 = ins64[3] if two else xs64
+    ref = th.autograd.grad(((xs64 * al64).sum(-1, keepdim=True), (xd64 * ar64).sum(-1, keepdim=True)),
+                           ins64, (gl.double(), gr.double()))
+    for a, r, t in zip(got, ref, ins):
+        # magnitude bound of each gradient: the same sums over |terms|
+        scale = r.abs().amax().item() + 1.0
+        tol = 1e-6 * scale * (1.0 if t.dim() == 3 and t.shape[0] > 1 else np.sqrt(ns))
+        assert a.shape == t.shape
+        assert (a.double() - r).abs().max().item() <= tol
+
+
+def test_attn_logits_unsupported_and_deterministic():
+    """Shapes the kernel does not take stay on torch (head size not a multiple of 4, a
+    non-power-of-two D / 4, H D / 4 not dividing 256, D > 64, a strided feature view), and the
+    parameter gradients are bit-identical run to run (fixed partial order)."""
+    from dgl import backend as B
+    from dgl import kernel as K
+    for h, d in ((8, 6), (4, 12), (3, 20), (65, 4), (3, 8), (1, 128), (2, 256)):
+        x = th.randn(100, h, d, device=DEV)
+        a = th.randn(1, h, d, device=DEV)
+        assert not K.attn_logits_ok(x, x, a, a)
+    x = th.randn(100, 8, 16, device=DEV)[:, :, :8]
+    a = th.randn(1, 8, 8, device=DEV)
+    assert not K.attn_logits_ok(x, x, a, a)
+    x = th.randn(300001, 8, 8, device=DEV).requires_grad_()
+    al = th.randn(1, 8, 8, device=DEV).requires_grad_()
+    ar = th.randn(1, 8, 8, device=DEV).requires_grad_()
+    gl, gr = th.randn(300001, 8, 1, device=DEV), th.randn(300001, 8, 1, device=DEV)
+    runs = []
+    for _ in range(2):
+        el, er = B.attn_logits(x, x, al, ar)
+        runs.append((el, er) + th.autograd.grad((el, er), (x, al, ar), (gl, gr)))
+    for u, v in zip(*runs):
+        assert th.equal(u, v)
+
+
+@pytest.mark.parametrize("drop", [0.0, 0.6])
+def test_gatconv_attn_logits_route(monkeypatch, drop):
+    """GATConv's fused route with the device el / er against torch's multiply + sum
+    (FUSED_ATTN_LOGITS off): the same output bits, every gradient (x, fc, attn_l, attn_r,
+    bias) within fp32 rounding, in training with attention dropout under one seed too."""
+    from dgl.nn.pytorch.conv import gatconv
+    from graphs import powerlaw
+    src, dst, n = powerlaw(20000, 400000, seed=5)
+    g = dgl.DGLGraph()
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    x = th.randn(n, 48, device=DEV)
+    res = []
+    for flag in (True, False):
+        monkeypatch.setattr(gatconv, "FUSED_ATTN_LOGITS", flag)
+        th.manual_seed(0)
+        conv = nn.GATConv(48, 8, 8, attn_drop=drop).to(DEV)
+        conv.train()
+        xr = x.clone().requires_grad_()
+        th.manual_seed(1)
+        y = conv(g, xr)
+        gy = th.randn_like(y)
+        grads = th.autograd.grad((y * gy).sum(), [xr] + list(conv.parameters()), allow_unused=True)
+        res.append((y,) + tuple(grads))
+    assert th.equal(res[0][0], res[1][0])  # el / er are torch's bits: the same forward
+    for a, b in zip(*res):
+        if a is None:
+            assert b is None
+            continue
+        th.testing.assert_close(a, b, rtol=2e-4, atol=2e-5)
