@@ -928,8 +928,15 @@ class DistGATConv(th.nn.Module):
         c = self.conv
         H, D = c._num_heads, c._out_feats
         ft = B.project(feat, c.fc.weight.t()).view(-1, H, D)
-        el = (ft * c.attn_l).sum(dim=-1)
-        er = (ft * c.attn_r).sum(dim=-1).unsqueeze(-1)
+        from . import kernel as K
+        from .nn.pytorch.conv import gatconv
+        if gatconv.FUSED_ATTN_LOGITS and K.attn_logits_ok(ft, ft, c.attn_l, c.attn_r):
+            # one pass over the owned rows, torch's bits (DGLMIGatAttnLogits)
+            el, er = B.attn_logits(ft, ft, c.attn_l, c.attn_r)
+            el = el.squeeze(-1)
+        else:
+            el = (ft * c.attn_l).sum(dim=-1)
+            er = (ft * c.attn_r).sum(dim=-1).unsqueeze(-1)
         full = halo_exchange(th.cat([ft.reshape(-1, H * D), el], 1), part, group)
         ft_full = full[:, :H * D].reshape(-1, H, D)
         el_full = full[:, H * D:].reshape(-1, H, 1)
