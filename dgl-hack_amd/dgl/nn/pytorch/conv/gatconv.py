@@ -48,9 +48,9 @@ MODULE_DRAW_DTYPE = th.float32
 # those draws recomputed inside the fused walks from the generator state (no mask, no
 # gathers; DGLMIFusedGatDraw*)
 MODULE_DRAW_IN_KERNEL = True
-# the fused route's el / er (gatconv.py:137-138) as one pass over the features each way
-# (dgl.backend.attn_logits; equal to torch's multiply + sum within fp32 rounding); the
-# composition routes keep torch's, as the reference
+# el / er (gatconv.py:137-138) as one pass over the features each way on every route
+# (dgl.backend.attn_logits: torch's bits -- the same pairwise summation order -- so the
+# composition's forward keeps the reference's bits; the gradients within fp32 rounding)
 FUSED_ATTN_LOGITS = True
 
 
@@ -276,8 +276,7 @@ class GATConv(nn.Module):
             h_src = h_dst = self.feat_drop(feat)
             feat_src = feat_dst = B.project(h_src, self.fc.weight.t()).view(-1, self._num_heads, self._out_feats)
         fused = self._fused_route(graph, max(feat_src.shape[0], feat_dst.shape[0]))
-        if fused and FUSED_ATTN_LOGITS and K.attn_logits_ok(feat_src, feat_dst, self.attn_l,
-                                                            self.attn_r):
+        if FUSED_ATTN_LOGITS and K.attn_logits_ok(feat_src, feat_dst, self.attn_l, self.attn_r):
             el, er = B.attn_logits(feat_src, feat_dst, self.attn_l, self.attn_r)
         else:
             el = (feat_src * self.attn_l).sum(dim=-1).unsqueeze(-1)
